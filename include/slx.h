@@ -1,0 +1,177 @@
+/*
+ * slx.h — C-ABI of libslx_hip.so, the MI355X (gfx950) kernels behind the SimLingo VLA hot path.
+ *
+ * Conventions (SURVEY.md §8b "Ownership"/"Error convention"):
+ *   - Plain pointers + sizes + element strides; no framework types. bf16 tensors are uint16 bit
+ *     patterns, f32 tensors are float. Caller allocates every buffer; kernels never allocate.
+ *   - Every call takes the HIP stream it is enqueued on (slx_stream_t == hipStream_t).
+ *   - Every call returns 0 on success, a negative code on failure (-22 = bad argument,
+ *     <= -1000 = HIP launch error); slx_last_error() returns a thread-local message.
+ *   - Calls are asynchronous and reentrant per stream; the library holds no global mutable state.
+ *
+ * Each entry point names the reference interface it replaces (file:line under the reference
+ * repository TimS-ml/simlingo, or the third-party kernel it stands for).
+ */
+#ifndef SLX_H_
+#define SLX_H_
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* slx_stream_t;
+
+/* ---- library ------------------------------------------------------------------------------ */
+const char* slx_last_error(void);
+int slx_abi_version(void);
+int slx_device_sync(void);
+
+/* ---- GEMM ---------------------------------------------------------------------------------
+ * C[M,N] = alpha * sum_k A(m,k) B(k,n)   (+ epilogue), bf16 operands, f32 accumulation (MFMA).
+ * Replaces cuBLAS behind every nn.Linear of InternViT / mlp1 / Qwen2+LoRA / LM head
+ * (simlingo_training/models/encoder/internvl2_model.py:114 -> remote InternVisionModel;
+ *  simlingo_training/models/driving.py:217 -> Qwen2ForCausalLM; llm.py:106-119 LoRA).       */
+enum {
+  SLX_GEMM_NT = 0, /* A [M][K] (lda), B [N][K] (ldb): Y = X W^T          (forward Linear)  */
+  SLX_GEMM_NN = 1, /* A [M][K],       B [K][N]:       dX = dY W            (data grad)     */
+  SLX_GEMM_TN = 2, /* A [K][M],       B [K][N]:       dW = dY^T X          (weight grad)   */
+  SLX_GEMM_TT = 3  /* A [K][M],       B [N][K]                                              */
+};
+enum {
+  SLX_EPI_STORE = 0,      /* C (+)= alpha*acc + bias[n]                                       */
+  SLX_EPI_GELU = 1,       /* aux_out = h = alpha*acc + bias; C = gelu_erf(h)   (bf16)          */
+  SLX_EPI_RESID_LS = 2,   /* y = alpha*acc + bias; aux_out = y (bf16, optional);
+                             C(f32) = resid + ls[n]*y   (InternViT layer-scale residual)      */
+  SLX_EPI_GELU_BWD = 3,   /* C = alpha*acc * gelu_erf'(aux[m,n])                              */
+  SLX_EPI_SWIGLU_BWD = 4, /* aux=[g|u] (ld ldaux, width 2N): C[m,n]=d*u*silu'(g), C[m,N+n]=d*silu(g) */
+  SLX_EPI_DROPMASK = 5    /* C (+)= alpha*acc * keep(seed, m*ldmask+n)/(1-p)   (LoRA dropout bwd) */
+};
+typedef struct slx_gemm_desc {
+  int layout, epilogue, out_f32;
+  int M, N, K, batch;
+  const void* A; int64_t lda; int64_t sA;
+  const void* B; int64_t ldb; int64_t sB;
+  void* C; int64_t ldc; int64_t sC;
+  float alpha;
+  const float* bias;   /* [N] f32 or NULL */
+  const float* ls;     /* [N] f32 (RESID_LS) */
+  const void* aux; int64_t ldaux;       /* bf16 epilogue input */
+  void* aux_out; int64_t ldaux_out;     /* bf16 epilogue output */
+  const float* resid; int64_t ldr;      /* f32 residual (RESID_LS) */
+  int accumulate;
+  uint64_t seed; float drop_p; int64_t ldmask;
+} slx_gemm_desc;
+int slx_gemm_bf16(const slx_gemm_desc* d, slx_stream_t stream);
+
+/* ---- Attention (head_dim 64) ----------------------------------------------------------------
+ * Replaces flash-attn 2.7.0.post2 (README.md:67-68) inside the InternVL2-1B remote code:
+ * InternViT non-causal MHA (internvl2_model.py:114 -> extract_feature) and Qwen2 causal GQA with
+ * key padding (driving.py:217-223, attention_mask = inputs_mask, valid-first layout).
+ * q/k/v/o: token-major rows [B*S, ld], head h at columns h*64..h*64+63.                       */
+typedef struct slx_attn_desc {
+  int B, S, Hq, Hkv, head_dim, causal;
+  const void* q; int64_t ldq;
+  const void* k; int64_t ldk;
+  const void* v; int64_t ldv;
+  void* o; int64_t ldo;
+  float* lse;           /* [B, Hq, S] f32, log2 domain (written by fwd, read by bwd)        */
+  const int* seqlens;   /* [B] valid keys per sequence (key-padding mask) or NULL           */
+  float scale;          /* softmax scale (1/sqrt(64))                                       */
+} slx_attn_desc;
+typedef struct slx_attn_bwd_desc {
+  const void* dout; int64_t lddo;
+  void* dq; int64_t lddq;
+  void* dk; int64_t lddk;
+  void* dv; int64_t lddv;
+  float* delta_ws;              /* [B, Hq, S]                                            */
+  float* dq_acc;                /* [B*S, Hq*64] f32 workspace                            */
+  float* dk_acc; float* dv_acc; /* [B*S, Hkv*64] f32 workspaces (GQA only)               */
+  const float* rope_cos; const float* rope_sin; /* [S, 32] tables: apply RoPE^T to dq/dk */
+} slx_attn_bwd_desc;
+int slx_attn_fwd(const slx_attn_desc* d, slx_stream_t stream);
+int slx_attn_bwd(const slx_attn_desc* d, const slx_attn_bwd_desc* g, slx_stream_t stream);
+/* Qwen2 rotary embedding, rotate_half convention, theta baked into the [S,32] cos/sin tables
+ * (HF Qwen2RotaryEmbedding, rope_theta 1e6; position_ids=None -> arange, driving.py:207).    */
+int slx_rope(void* x, int64_t ldx, int64_t ntok, int S, int nheads, const float* cos_tab,
+             const float* sin_tab, int inverse, slx_stream_t stream);
+
+/* ---- LayerNorm / RMSNorm ---------------------------------------------------------------------
+ * InternViT norm1/norm2 (eps 1e-6), mlp1 LayerNorm(4096, eps 1e-5) with the pixel_shuffle(0.5)
+ * gather fused in (pixel_shuffle_grid = 32, tokens_per_image = 1025), Qwen2RMSNorm (eps 1e-6).
+ * x: f32 rows, y: bf16 rows. D % 4 == 0, D <= 4096.                                           */
+typedef struct slx_norm_desc {
+  int rms;
+  const float* x; int64_t ldx;
+  const float* gamma; const float* beta;
+  void* y; int64_t ldy;
+  float* mean; float* rstd;   /* [rows] saved statistics */
+  int64_t rows; int D; float eps;
+  int pixel_shuffle_grid; int tokens_per_image;
+} slx_norm_desc;
+int slx_norm_fwd(const slx_norm_desc* d, slx_stream_t stream);
+int slx_norm_bwd(const slx_norm_desc* d, const float* dy, int64_t lddy, float* dx, int64_t lddx,
+                 int dx_accumulate, float* dgamma, float* dbeta, int param_accumulate,
+                 float* partial_ws, slx_stream_t stream);
+int slx_norm_partial_ws_floats(int D);
+
+/* ---- glue kernels ----------------------------------------------------------------------------- */
+/* InternViT patch embedding Conv2d(3,1024,k14,s14) as im2col (K padded to kpad) + GEMM.      */
+int slx_im2col_patch(const float* pix, int N, int H, int W, int P, int kpad, void* out, slx_stream_t s);
+/* x0 = [cls; patches] + pos_embed   (InternVisionEmbeddings; no interpolation at 448)        */
+int slx_vit_embed_fwd(const float* patch, const float* cls, const float* pos, float* out, int N, int T, int D, slx_stream_t s);
+int slx_vit_embed_bwd(const float* dx, int N, int T, int D, float* dpos, float* dcls, void* dpatch, slx_stream_t s);
+/* Qwen2MLP act: silu(gate) * up, gu = [gate | up] (fused gate/up GEMM output)                  */
+int slx_swiglu_fwd(const void* gu, int64_t ldgu, void* out, int64_t ldo, int64_t M, int F, slx_stream_t s);
+/* bias gradients: out[c] (+)= sum_r x[r,c]; mode 0 bf16 x, 1 f32 x                              */
+int slx_colsum(int mode, const void* x, int64_t ldx, int64_t M, int N, float* out, int accumulate, float* ws, slx_stream_t s);
+int slx_colsum_ws_floats(int N);
+/* InternViT layer-scale branch backward: g = dres*ls (bf16), dls = sum dres*y, dbias = sum g   */
+int slx_ls_branch_bwd(const float* dres, int64_t ldr, const float* ls, const void* y, int64_t ldy, void* g, int64_t ldg,
+                      int64_t M, int N, float* dls, float* dbias, int accumulate, float* ws, slx_stream_t s);
+/* LLM input assembly (AdaptorList.forward adaptors.py:301-331 + replace_placeholder_tokens
+ * internvl2_model.py:44-142 restated as one gather): code = kind<<28 | index,
+ * kind 0 token (embed_tokens, ids clamped to V-1), 1 image row, 2 wp_encoder row, 3 query.    */
+int slx_assemble_tokens(const int* code, int64_t n, int D, const void* embed, int V, const void* img, const float* wp,
+                        const float* query, float* out, slx_stream_t s);
+int slx_gather_rows(const float* src, int64_t lds, const int* idx, int64_t n, int D, void* dst, int64_t ldd, int dst_bf16, slx_stream_t s);
+int slx_gather_rows_bf16(const void* src, int64_t lds, const int* idx, int64_t n, int D, void* dst, int64_t ldd, slx_stream_t s);
+int slx_gather_sum(const float* src, int64_t lds, const int* pos, int B, int nq, int D, float* out, int accumulate, slx_stream_t s);
+/* peft LoRA dropout (lora_dropout, llm.py:113) with a counter-hash mask regenerated in backward */
+int slx_dropout(const void* src, int64_t lds, void* dst, int64_t ldd, int64_t M, int N, uint64_t seed, float p, int64_t ldmask, slx_stream_t s);
+
+/* small strided f32 GEMM (driving heads adaptors.py:113-132, WaypointInputAdaptor :80)        */
+enum { SLX_ACT_NONE = 0, SLX_ACT_RELU = 1, SLX_ACT_SILU = 2 };
+typedef struct slx_sgemm_desc {
+  int M, N, K, act, accumulate;
+  const float* A; int64_t sam, sak;
+  const float* B; int64_t sbk, sbn;
+  float* C; int64_t scm, scn;
+  const float* bias;
+  float* pre; int64_t ldpre;   /* optional pre-activation output [M][ldpre] */
+  float alpha;
+} slx_sgemm_desc;
+int slx_sgemm(const slx_sgemm_desc* d, slx_stream_t s);
+int slx_act_bwd(const float* dact, const float* pre, float* dpre, int64_t n, int act, slx_stream_t s);
+
+/* ---- losses ---------------------------------------------------------------------------------
+ * LanguageAdaptor.compute_loss (adaptors.py:259-274) on the gathered loss rows only,
+ * DrivingAdaptor.compute_loss (adaptors.py:183-221: cumsum + smooth_l1(beta 1).sum(-1)),
+ * summarise_losses (models/utils.py:7-41).                                                      */
+int slx_ce_fwd(const float* logits, int64_t ld, const int* labels, int64_t R, int V, float* loss, float* lse, slx_stream_t s);
+int slx_ce_bwd(const float* logits, int64_t ld, const int* labels, const float* lse, int64_t R, int V, const float* gscale,
+               void* dlogits, int64_t ldd, slx_stream_t s);
+int slx_wp_loss_fwd(const float* out, const float* label, int B, int n, int dims, float* pred, float* loss, slx_stream_t s);
+int slx_wp_loss_bwd(const float* pred, const float* label, int B, int n, int dims, const float* gscale, float* dout, slx_stream_t s);
+int slx_loss_finalize(const float* lang, int nl, const float* route, int nr, const float* speed, int ns, float* out, slx_stream_t s);
+int slx_loss_gscale(const float* dtotal, int nl, int nr, int ns, float* gs, slx_stream_t s);
+
+/* ---- optimizer (torch.optim.AdamW semantics, driving.py:718-724; clip_grad_norm 0.3, train.py:206) */
+int slx_sumsq(const float* g, int64_t n, float* out, int zero_first, slx_stream_t s);
+int slx_adamw(float* p, const float* g, float* m, float* v, void* p_bf16, int64_t n, float lr, float beta1, float beta2,
+              float eps, float weight_decay, int step, const float* sumsq, float max_norm, slx_stream_t s);
+int slx_cast_f32_bf16(const float* src, void* dst, int64_t n, slx_stream_t s);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SLX_H_ */

@@ -1,0 +1,583 @@
+// Memory-bound glue of the SimLingo VLA step, each kernel fused to one pass over HBM:
+// patch im2col, InternViT embeddings, SwiGLU, column reductions (bias / layer-scale grads),
+// LLM token assembly (the sync-free restatement of AdaptorList.forward + replace_placeholder_tokens),
+// row gathers, LoRA dropout, small strided GEMMs for the driving heads / waypoint encoder,
+// cross-entropy over the 151655-way vocabulary, waypoint cumsum + smooth-L1, and the fused
+// clip + AdamW optimizer step.
+#include "common.h"
+#include "../../include/slx.h"
+
+namespace slx {
+
+// ---------------------------------------------------------------------------------------------
+// im2col for Conv2d(3, D, k=P, s=P): out[n*Np + p, k] = pix[n, c, py*P+ky, px*P+kx], k = c*P*P+ky*P+kx,
+// zero for k >= 3*P*P (K padded to kpad so the GEMM gets 16-B aligned rows).
+__global__ void im2col_kernel(const float* pix, int N, int H, int W, int P, int kpad, bf16* out) {
+  const int gw = W / P, gh = H / P, np = gw * gh;
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long total = (long)N * np * (kpad / 8);
+  if (idx >= total) return;
+  const int kc = (idx % (kpad / 8)) * 8;
+  const long rowi = idx / (kpad / 8);
+  const int n = rowi / np, p = rowi % np, py = p / gw, px = p % gw;
+  bf16x8 v;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int k = kc + j;
+    float x = 0.f;
+    if (k < 3 * P * P) {
+      const int c = k / (P * P), r = k % (P * P), ky = r / P, kx = r % P;
+      x = pix[(((long)n * 3 + c) * H + py * P + ky) * W + px * P + kx];
+    }
+    v[j] = (bf16)x;
+  }
+  *reinterpret_cast<bf16x8*>(out + rowi * kpad + kc) = v;
+}
+
+// x0[n, 0] = cls + pos[0]; x0[n, 1+p] = patch[n*Np+p] + pos[1+p]
+__global__ void vit_embed_fwd_kernel(const float* patch, const float* cls, const float* pos, float* out, int N, int T, int D) {
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long total = (long)N * T * (D / 4);
+  if (idx >= total) return;
+  const int c = (idx % (D / 4)) * 4;
+  const long row = idx / (D / 4);
+  const int n = row / T, t = row % T;
+  float4 p4 = *reinterpret_cast<const float4*>(pos + (long)t * D + c);
+  float4 s4 = t == 0 ? *reinterpret_cast<const float4*>(cls + c)
+                     : *reinterpret_cast<const float4*>(patch + ((long)n * (T - 1) + t - 1) * D + c);
+  float4 o = {s4.x + p4.x, s4.y + p4.y, s4.z + p4.z, s4.w + p4.w};
+  *reinterpret_cast<float4*>(out + row * D + c) = o;
+}
+
+// dpos[t] = sum_n dx[n,t]; dcls = dpos[0]; dpatch[n*Np+p] = bf16(dx[n, 1+p])
+__global__ void vit_embed_bwd_kernel(const float* dx, int N, int T, int D, float* dpos, float* dcls, bf16* dpatch) {
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (long)T * D) return;
+  const int t = idx / D, c = idx % D;
+  float s = 0.f;
+  for (int n = 0; n < N; ++n) {
+    const float g = dx[((long)n * T + t) * D + c];
+    s += g;
+    if (t > 0) dpatch[((long)n * (T - 1) + t - 1) * D + c] = (bf16)g;
+  }
+  dpos[idx] = s;
+  if (t == 0) dcls[c] = s;
+}
+
+// out[m, f] = silu(gu[m, f]) * gu[m, F + f]
+__global__ void swiglu_fwd_kernel(const bf16* gu, long ldgu, bf16* out, long ldo, long M, int F) {
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= M * (F / 8)) return;
+  const long m = idx / (F / 8);
+  const int f = (idx % (F / 8)) * 8;
+  const bf16x8 g = *reinterpret_cast<const bf16x8*>(gu + m * ldgu + f);
+  const bf16x8 u = *reinterpret_cast<const bf16x8*>(gu + m * ldgu + F + f);
+  bf16x8 o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = (bf16)(silu((float)g[j]) * (float)u[j]);
+  *reinterpret_cast<bf16x8*>(out + m * ldo + f) = o;
+}
+
+// Column partial sums over a strided set of rows: partial[blk, c] = sum_rows x[r, c] (* ls[c])
+// mode 0: x bf16 ; mode 1: x f32 ; mode 2 (layer-scale grad): x = dres f32, y bf16 ->
+//   g = bf16(dres*ls) written, partial[blk, c] = sum dres*y, partial[blk, N + c] = sum dres*ls
+template <int MODE>
+__global__ __launch_bounds__(256) void colsum_kernel(const void* xv, long ldx, long M, int N, float* partial,
+                                                     const float* ls, const bf16* y, long ldy, bf16* g, long ldg) {
+  const int c0 = (blockIdx.y * 256 + threadIdx.x) * 4;
+  if (c0 >= N) return;
+  float s[4] = {0, 0, 0, 0}, s2[4] = {0, 0, 0, 0};
+  float lsv[4] = {1, 1, 1, 1};
+  if (MODE == 2) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) lsv[e] = ls[c0 + e];
+  }
+  for (long r = blockIdx.x; r < M; r += gridDim.x) {
+    float v[4];
+    if (MODE == 0) {
+      const bf16x4 t = *reinterpret_cast<const bf16x4*>((const bf16*)xv + r * ldx + c0);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = (float)t[e];
+    } else {
+      const float4 t = *reinterpret_cast<const float4*>((const float*)xv + r * ldx + c0);
+      v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+    }
+    if (MODE == 2) {
+      const bf16x4 yy = *reinterpret_cast<const bf16x4*>(y + r * ldy + c0);
+      bf16x4 go;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        s2[e] += v[e] * (float)yy[e];
+        const float gv = v[e] * lsv[e];
+        go[e] = (bf16)gv;
+        s[e] += gv;
+      }
+      *reinterpret_cast<bf16x4*>(g + r * ldg + c0) = go;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) s[e] += v[e];
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    partial[(long)blockIdx.x * 2 * N + c0 + e] = (MODE == 2) ? s2[e] : s[e];
+    if (MODE == 2) partial[(long)blockIdx.x * 2 * N + N + c0 + e] = s[e];
+  }
+}
+
+__global__ void colreduce2_kernel(const float* partial, int nblk, int N, float* out, int accumulate, int off) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= N) return;
+  float s = 0.f;
+  for (int b = 0; b < nblk; ++b) s += partial[(long)b * 2 * N + off + c];
+  out[c] = accumulate ? out[c] + s : s;
+}
+
+// LLM input assembly: out[i, :] (f32) from code[i] = (kind << 28) | index
+//   kind 0: token  -> embed[min(index, V-1)] (bf16 table; ids clamped like adaptors.py:256)
+//   kind 1: image  -> img[index] (bf16, mlp1 output rows)
+//   kind 2: waypoint encoder row -> wp[index] (f32)
+//   kind 3: driving query -> query[index] (f32)
+__global__ void assemble_kernel(const int* code, long n, int D, const bf16* embed, int V, const bf16* img,
+                                const float* wp, const float* query, float* out) {
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= n * (D / 4)) return;
+  const long i = idx / (D / 4);
+  const int c = (idx % (D / 4)) * 4;
+  const int cd = code[i];
+  const int kind = (cd >> 28) & 0xF, ix = cd & 0x0FFFFFFF;
+  float4 o;
+  if (kind == 0 || kind == 1) {
+    const bf16* src = kind == 0 ? embed + (long)min(ix, V - 1) * D : img + (long)ix * D;
+    const bf16x4 t = *reinterpret_cast<const bf16x4*>(src + c);
+    o = {(float)t[0], (float)t[1], (float)t[2], (float)t[3]};
+  } else {
+    const float* src = (kind == 2 ? wp : query) + (long)ix * D;
+    o = *reinterpret_cast<const float4*>(src + c);
+  }
+  *reinterpret_cast<float4*>(out + i * D + c) = o;
+}
+
+// dst[i, :] = src[idx[i], :]  (f32 -> f32 or bf16), D % 4 == 0
+template <typename OutT>
+__global__ void gather_rows_kernel(const float* src, long lds, const int* idx, long n, int D, OutT* dst, long ldd) {
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n * (D / 4)) return;
+  const long i = t / (D / 4);
+  const int c = (t % (D / 4)) * 4;
+  const float4 v = *reinterpret_cast<const float4*>(src + (long)idx[i] * lds + c);
+  OutT* d = dst + i * ldd + c;
+  d[0] = (OutT)v.x; d[1] = (OutT)v.y; d[2] = (OutT)v.z; d[3] = (OutT)v.w;
+}
+
+// bf16 rows -> f32 rows gather (features for the heads / loss rows)
+__global__ void gather_rows_bf16_kernel(const bf16* src, long lds, const int* idx, long n, int D, bf16* dst, long ldd) {
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n * (D / 8)) return;
+  const long i = t / (D / 8);
+  const int c = (t % (D / 8)) * 8;
+  *reinterpret_cast<bf16x8*>(dst + i * ldd + c) = *reinterpret_cast<const bf16x8*>(src + (long)idx[i] * lds + c);
+}
+
+// out[j, c] (+)= sum_b src[pos[b*nq + j], c]
+__global__ void gather_sum_kernel(const float* src, long lds, const int* pos, int B, int nq, int D, float* out, int accumulate) {
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (long)nq * D) return;
+  const int j = t / D, c = t % D;
+  float s = 0.f;
+  for (int b = 0; b < B; ++b) s += src[(long)pos[b * nq + j] * lds + c];
+  out[t] = accumulate ? out[t] + s : s;
+}
+
+// dst = src * keep(seed, m*ldmask + n) / (1-p)  (LoRA dropout; same mask as the GEMM DROPMASK epilogue)
+__global__ void dropout_kernel(const bf16* src, long lds, bf16* dst, long ldd, long M, int N, unsigned long long seed,
+                               float p, long ldmask) {
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= M * (N / 8)) return;
+  const long m = t / (N / 8);
+  const int n0 = (t % (N / 8)) * 8;
+  const bf16x8 x = *reinterpret_cast<const bf16x8*>(src + m * lds + n0);
+  bf16x8 o;
+  const float sc = 1.0f / (1.0f - p);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float keep = uniform01(seed, (unsigned long long)m * ldmask + n0 + j) >= p ? sc : 0.f;
+    o[j] = (bf16)((float)x[j] * keep);
+  }
+  *reinterpret_cast<bf16x8*>(dst + m * ldd + n0) = o;
+}
+
+// Small strided f32 GEMM for the driving heads / waypoint encoder (M <= a few hundred rows):
+// C[m,n] (+)= act(alpha * sum_k A[m*sam + k*sak] * B[k*sbk + n*sbn] + bias[n]); pre-act optional.
+__global__ __launch_bounds__(256) void sgemm_kernel(slx_sgemm_desc d) {
+  __shared__ float As[16][17], Bs[16][17];
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  const int m = blockIdx.y * 16 + ty, n = blockIdx.x * 16 + tx;
+  float acc = 0.f;
+  for (int k0 = 0; k0 < d.K; k0 += 16) {
+    const int ka = k0 + tx, kb = k0 + ty;
+    const int am = blockIdx.y * 16 + ty, bn = blockIdx.x * 16 + tx;
+    As[ty][tx] = (am < d.M && ka < d.K) ? d.A[(long)am * d.sam + (long)ka * d.sak] : 0.f;
+    Bs[ty][tx] = (bn < d.N && kb < d.K) ? d.B[(long)kb * d.sbk + (long)bn * d.sbn] : 0.f;
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < 16; ++kk) acc += As[ty][kk] * Bs[kk][tx];
+    __syncthreads();
+  }
+  if (m >= d.M || n >= d.N) return;
+  float v = acc * d.alpha;
+  if (d.bias) v += d.bias[n];
+  const long ci = (long)m * d.scm + (long)n * d.scn;
+  if (d.pre) d.pre[(long)m * d.ldpre + n] = v;
+  if (d.act == SLX_ACT_RELU) v = fmaxf(v, 0.f);
+  else if (d.act == SLX_ACT_SILU) v = silu(v);
+  if (d.accumulate) v += d.C[ci];
+  d.C[ci] = v;
+}
+
+// d_pre = d_act * act'(pre)
+__global__ void act_bwd_kernel(const float* dact, const float* pre, float* dpre, long n, int act) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float x = pre[i];
+  const float g = act == SLX_ACT_RELU ? (x > 0.f ? 1.f : 0.f) : act == SLX_ACT_SILU ? silu_grad(x) : 1.f;
+  dpre[i] = dact[i] * g;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Cross-entropy over the vocabulary for the gathered loss rows (adaptors.py:259-274).
+// fwd: loss[r] = logsumexp(logits[r]) - logits[r, label[r]]; lse[r] kept for bwd.
+__global__ __launch_bounds__(1024) void ce_fwd_kernel(const float* logits, long ld, const int* labels, int V, float* loss, float* lse) {
+  __shared__ float sh[16];
+  const long r = blockIdx.x;
+  const float* x = logits + r * ld;
+  float mx = -INFINITY;
+  for (int i = threadIdx.x; i < V; i += blockDim.x) mx = fmaxf(mx, x[i]);
+  mx = warp_max(mx);
+  {
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = mx;
+    __syncthreads();
+    float t = -INFINITY;
+    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) t = fmaxf(t, sh[i]);
+    mx = t;
+  }
+  float s = 0.f;
+  for (int i = threadIdx.x; i < V; i += blockDim.x) s += __expf(x[i] - mx);
+  s = block_sum(s, sh);
+  if (threadIdx.x == 0) {
+    const float l = mx + __logf(s);
+    lse[r] = l;
+    loss[r] = l - x[labels[r]];
+  }
+}
+// bwd: dlogits[r, v] = (softmax - onehot) * (*gscale); padded columns [V, ldd) zeroed.
+__global__ void ce_bwd_kernel(const float* logits, long ld, const int* labels, const float* lse, int V, const float* gscale,
+                              bf16* dlogits, long ldd) {
+  const long r = blockIdx.y;
+  const float g = *gscale, l = lse[r];
+  const int lab = labels[r];
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < ldd; i += gridDim.x * blockDim.x) {
+    float v = 0.f;
+    if (i < V) v = (__expf(logits[r * ld + i] - l) - (i == lab ? 1.f : 0.f)) * g;
+    dlogits[r * ldd + i] = (bf16)v;
+  }
+}
+
+// Driving heads (adaptors.py:183-221): pred[b, i] = sum_{j<=i} out[b, j]  (cumsum over points),
+// loss[b, i] = sum_xy smooth_l1(pred - label, beta=1). Backward: d_out = reverse-cumsum of
+// d_pred, d_pred = smooth_l1'(pred - label) * gscale.
+__global__ void wp_loss_fwd_kernel(const float* out, const float* label, int B, int n, int dims, float* pred, float* loss) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  float run[4] = {0, 0, 0, 0};
+  for (int i = 0; i < n; ++i) {
+    float l = 0.f;
+    for (int c = 0; c < dims; ++c) {
+      run[c] += out[((long)b * n + i) * dims + c];
+      pred[((long)b * n + i) * dims + c] = run[c];
+      const float d = run[c] - label[((long)b * n + i) * dims + c];
+      const float ad = fabsf(d);
+      l += ad < 1.f ? 0.5f * d * d : ad - 0.5f;
+    }
+    loss[(long)b * n + i] = l;
+  }
+}
+__global__ void wp_loss_bwd_kernel(const float* pred, const float* label, int B, int n, int dims, const float* gscale, float* dout) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const float g = *gscale;
+  float run[4] = {0, 0, 0, 0};
+  for (int i = n - 1; i >= 0; --i) {
+    for (int c = 0; c < dims; ++c) {
+      const long k = ((long)b * n + i) * dims + c;
+      const float d = pred[k] - label[k];
+      const float gd = (fabsf(d) < 1.f ? d : (d > 0.f ? 1.f : -1.f)) * g;
+      run[c] += gd;
+      dout[k] = run[c];
+    }
+  }
+}
+
+// summarise_losses (simlingo_training/models/utils.py:7-41) on device:
+// out[0] = total, out[1..3] = lang, route, speed averages; gs[0..2] = d(total)/d(per-item) scales
+// given the upstream gradient dtotal (device scalar, may be NULL in forward).
+__global__ void loss_finalize_kernel(const float* lang, int nl, const float* route, int nr, const float* speed, int ns, float* out) {
+  __shared__ float sh[16];
+  float a = 0.f, b = 0.f, c = 0.f;
+  for (int i = threadIdx.x; i < nl; i += blockDim.x) a += lang[i];
+  for (int i = threadIdx.x; i < nr; i += blockDim.x) b += route[i];
+  for (int i = threadIdx.x; i < ns; i += blockDim.x) c += speed[i];
+  a = block_sum(a, sh);
+  b = block_sum(b, sh);
+  c = block_sum(c, sh);
+  if (threadIdx.x == 0) {
+    const float la = nl > 0 ? a / nl : 0.f, ra = nr > 0 ? b / nr : 0.f, sa = ns > 0 ? c / ns : 0.f;
+    out[0] = la + ra + sa;
+    out[1] = la; out[2] = ra; out[3] = sa;
+  }
+}
+__global__ void loss_gscale_kernel(const float* dtotal, int nl, int nr, int ns, float* gs) {
+  const float g = dtotal ? *dtotal : 1.f;
+  gs[0] = nl > 0 ? g / nl : 0.f;
+  gs[1] = nr > 0 ? g / nr : 0.f;
+  gs[2] = ns > 0 ? g / ns : 0.f;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Optimizer: global grad-norm (sum of squares, partials + atomics) and fused clip + AdamW
+// (torch.optim.AdamW semantics, decoupled weight decay; driving.py:718-724, clip train.py:206).
+__global__ __launch_bounds__(256) void sumsq_kernel(const float* g, long n, float* out) {
+  __shared__ float sh[16];
+  float s = 0.f;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n / 4; i += (long)gridDim.x * blockDim.x) {
+    const float4 v = reinterpret_cast<const float4*>(g)[i];
+    s += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+  }
+  if (blockIdx.x == 0)
+    for (long i = (n / 4) * 4 + threadIdx.x; i < n; i += blockDim.x) s += g[i] * g[i];
+  s = block_sum(s, sh);
+  if (threadIdx.x == 0) atomicAdd(out, s);
+}
+
+__global__ __launch_bounds__(256) void adamw_kernel(float* p, const float* g, float* m, float* v, bf16* pbf, long n,
+                                                    float lr, float b1, float b2, float eps, float wd, float bc1,
+                                                    float bc2s, const float* sumsq, float max_norm) {
+  float coef = 1.f;
+  if (sumsq && max_norm > 0.f) {
+    const float tn = sqrtf(*sumsq);
+    coef = fminf(1.f, max_norm / (tn + 1e-6f));
+  }
+  const float step = lr / bc1;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const float gi = g[i] * coef;
+    float pi = p[i] * (1.f - lr * wd);
+    const float mi = m[i] + (1.f - b1) * (gi - m[i]);
+    const float vi = v[i] * b2 + (1.f - b2) * gi * gi;
+    const float den = sqrtf(vi) / bc2s + eps;
+    pi -= step * mi / den;
+    p[i] = pi; m[i] = mi; v[i] = vi;
+    if (pbf) pbf[i] = (bf16)pi;
+  }
+}
+
+__global__ void cast_kernel(const float* src, bf16* dst, long n) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) dst[i] = (bf16)src[i];
+}
+
+}  // namespace slx
+
+using namespace slx;
+
+static inline dim3 g1(long n, int bs = 256) { return dim3((unsigned)((n + bs - 1) / bs)); }
+
+extern "C" {
+
+int slx_im2col_patch(const float* pix, int N, int H, int W, int P, int kpad, void* out, slx_stream_t s) {
+  SLX_CHECK_ARG(kpad % 8 == 0 && kpad >= 3 * P * P && H % P == 0 && W % P == 0, "slx_im2col_patch: bad shape");
+  const long total = (long)N * (H / P) * (W / P) * (kpad / 8);
+  if (!total) return 0;
+  hipLaunchKernelGGL(im2col_kernel, g1(total), dim3(256), 0, (hipStream_t)s, pix, N, H, W, P, kpad, (bf16*)out);
+  SLX_LAUNCH_CHECK("slx_im2col_patch");
+  return 0;
+}
+
+int slx_vit_embed_fwd(const float* patch, const float* cls, const float* pos, float* out, int N, int T, int D, slx_stream_t s) {
+  SLX_CHECK_ARG(D % 4 == 0, "slx_vit_embed_fwd: D %% 4");
+  const long total = (long)N * T * (D / 4);
+  hipLaunchKernelGGL(vit_embed_fwd_kernel, g1(total), dim3(256), 0, (hipStream_t)s, patch, cls, pos, out, N, T, D);
+  SLX_LAUNCH_CHECK("slx_vit_embed_fwd");
+  return 0;
+}
+
+int slx_vit_embed_bwd(const float* dx, int N, int T, int D, float* dpos, float* dcls, void* dpatch, slx_stream_t s) {
+  hipLaunchKernelGGL(vit_embed_bwd_kernel, g1((long)T * D), dim3(256), 0, (hipStream_t)s, dx, N, T, D, dpos, dcls, (bf16*)dpatch);
+  SLX_LAUNCH_CHECK("slx_vit_embed_bwd");
+  return 0;
+}
+
+int slx_swiglu_fwd(const void* gu, int64_t ldgu, void* out, int64_t ldo, int64_t M, int F, slx_stream_t s) {
+  SLX_CHECK_ARG(F % 8 == 0 && ldgu % 8 == 0 && ldo % 8 == 0, "slx_swiglu_fwd: F/ld must be multiples of 8");
+  hipLaunchKernelGGL(swiglu_fwd_kernel, g1(M * (F / 8)), dim3(256), 0, (hipStream_t)s, (const bf16*)gu, ldgu, (bf16*)out, ldo, M, F);
+  SLX_LAUNCH_CHECK("slx_swiglu_fwd");
+  return 0;
+}
+
+int slx_colsum_ws_floats(int N) { return 256 * 2 * N; }
+
+// mode 0: x bf16, 1: x f32 -> out[c] (+)= sum_r x[r,c]
+int slx_colsum(int mode, const void* x, int64_t ldx, int64_t M, int N, float* out, int accumulate, float* ws, slx_stream_t s) {
+  SLX_CHECK_ARG(N % 4 == 0 && (mode == 0 || mode == 1), "slx_colsum: N %% 4 / mode");
+  const int nblk = (int)(M < 256 ? (M > 0 ? M : 1) : 256);
+  dim3 grid(nblk, (N / 4 + 255) / 256);
+  hipStream_t st = (hipStream_t)s;
+  if (mode == 0) hipLaunchKernelGGL((colsum_kernel<0>), grid, dim3(256), 0, st, x, ldx, M, N, ws, nullptr, nullptr, 0L, nullptr, 0L);
+  else hipLaunchKernelGGL((colsum_kernel<1>), grid, dim3(256), 0, st, x, ldx, M, N, ws, nullptr, nullptr, 0L, nullptr, 0L);
+  hipLaunchKernelGGL(colreduce2_kernel, g1(N), dim3(256), 0, st, ws, nblk, N, out, accumulate, 0);
+  SLX_LAUNCH_CHECK("slx_colsum");
+  return 0;
+}
+
+// Layer-scale residual branch backward: g = bf16(dres*ls), dls = sum dres*y, dbias = sum g
+int slx_ls_branch_bwd(const float* dres, int64_t ldr, const float* ls, const void* y, int64_t ldy, void* g, int64_t ldg,
+                      int64_t M, int N, float* dls, float* dbias, int accumulate, float* ws, slx_stream_t s) {
+  SLX_CHECK_ARG(N % 4 == 0, "slx_ls_branch_bwd: N %% 4");
+  const int nblk = (int)(M < 256 ? (M > 0 ? M : 1) : 256);
+  dim3 grid(nblk, (N / 4 + 255) / 256);
+  hipStream_t st = (hipStream_t)s;
+  hipLaunchKernelGGL((colsum_kernel<2>), grid, dim3(256), 0, st, (const void*)dres, ldr, M, N, ws, ls, (const bf16*)y, ldy, (bf16*)g, ldg);
+  hipLaunchKernelGGL(colreduce2_kernel, g1(N), dim3(256), 0, st, ws, nblk, N, dls, accumulate, 0);
+  hipLaunchKernelGGL(colreduce2_kernel, g1(N), dim3(256), 0, st, ws, nblk, N, dbias, accumulate, N);
+  SLX_LAUNCH_CHECK("slx_ls_branch_bwd");
+  return 0;
+}
+
+int slx_assemble_tokens(const int* code, int64_t n, int D, const void* embed, int V, const void* img, const float* wp,
+                        const float* query, float* out, slx_stream_t s) {
+  SLX_CHECK_ARG(D % 4 == 0, "slx_assemble_tokens: D %% 4");
+  hipLaunchKernelGGL(assemble_kernel, g1(n * (D / 4)), dim3(256), 0, (hipStream_t)s, code, n, D, (const bf16*)embed, V,
+                     (const bf16*)img, wp, query, out);
+  SLX_LAUNCH_CHECK("slx_assemble_tokens");
+  return 0;
+}
+
+int slx_gather_rows(const float* src, int64_t lds, const int* idx, int64_t n, int D, void* dst, int64_t ldd, int dst_bf16, slx_stream_t s) {
+  SLX_CHECK_ARG(D % 4 == 0, "slx_gather_rows: D %% 4");
+  if (!n) return 0;
+  if (dst_bf16) hipLaunchKernelGGL(gather_rows_kernel<bf16>, g1(n * (D / 4)), dim3(256), 0, (hipStream_t)s, src, lds, idx, n, D, (bf16*)dst, ldd);
+  else hipLaunchKernelGGL(gather_rows_kernel<float>, g1(n * (D / 4)), dim3(256), 0, (hipStream_t)s, src, lds, idx, n, D, (float*)dst, ldd);
+  SLX_LAUNCH_CHECK("slx_gather_rows");
+  return 0;
+}
+
+int slx_gather_rows_bf16(const void* src, int64_t lds, const int* idx, int64_t n, int D, void* dst, int64_t ldd, slx_stream_t s) {
+  SLX_CHECK_ARG(D % 8 == 0 && lds % 8 == 0 && ldd % 8 == 0, "slx_gather_rows_bf16: D/ld %% 8");
+  if (!n) return 0;
+  hipLaunchKernelGGL(gather_rows_bf16_kernel, g1(n * (D / 8)), dim3(256), 0, (hipStream_t)s, (const bf16*)src, lds, idx, n, D, (bf16*)dst, ldd);
+  SLX_LAUNCH_CHECK("slx_gather_rows_bf16");
+  return 0;
+}
+
+int slx_gather_sum(const float* src, int64_t lds, const int* pos, int B, int nq, int D, float* out, int accumulate, slx_stream_t s) {
+  hipLaunchKernelGGL(gather_sum_kernel, g1((long)nq * D), dim3(256), 0, (hipStream_t)s, src, lds, pos, B, nq, D, out, accumulate);
+  SLX_LAUNCH_CHECK("slx_gather_sum");
+  return 0;
+}
+
+int slx_dropout(const void* src, int64_t lds, void* dst, int64_t ldd, int64_t M, int N, uint64_t seed, float p, int64_t ldmask, slx_stream_t s) {
+  SLX_CHECK_ARG(N % 8 == 0 && p >= 0.f && p < 1.f, "slx_dropout: N %% 8, 0 <= p < 1");
+  hipLaunchKernelGGL(dropout_kernel, g1(M * (N / 8)), dim3(256), 0, (hipStream_t)s, (const bf16*)src, lds, (bf16*)dst, ldd, M, N, seed, p, ldmask);
+  SLX_LAUNCH_CHECK("slx_dropout");
+  return 0;
+}
+
+int slx_sgemm(const slx_sgemm_desc* d, slx_stream_t s) {
+  if (d->M == 0 || d->N == 0) return 0;
+  dim3 grid((d->N + 15) / 16, (d->M + 15) / 16);
+  hipLaunchKernelGGL(sgemm_kernel, grid, dim3(256), 0, (hipStream_t)s, *d);
+  SLX_LAUNCH_CHECK("slx_sgemm");
+  return 0;
+}
+
+int slx_act_bwd(const float* dact, const float* pre, float* dpre, int64_t n, int act, slx_stream_t s) {
+  hipLaunchKernelGGL(act_bwd_kernel, g1(n), dim3(256), 0, (hipStream_t)s, dact, pre, dpre, n, act);
+  SLX_LAUNCH_CHECK("slx_act_bwd");
+  return 0;
+}
+
+int slx_ce_fwd(const float* logits, int64_t ld, const int* labels, int64_t R, int V, float* loss, float* lse, slx_stream_t s) {
+  if (!R) return 0;
+  hipLaunchKernelGGL(ce_fwd_kernel, dim3((unsigned)R), dim3(1024), 0, (hipStream_t)s, logits, ld, labels, V, loss, lse);
+  SLX_LAUNCH_CHECK("slx_ce_fwd");
+  return 0;
+}
+
+int slx_ce_bwd(const float* logits, int64_t ld, const int* labels, const float* lse, int64_t R, int V, const float* gscale,
+               void* dlogits, int64_t ldd, slx_stream_t s) {
+  if (!R) return 0;
+  dim3 grid((unsigned)((ldd + 1023) / 1024 < 64 ? (ldd + 1023) / 1024 : 64), (unsigned)R);
+  hipLaunchKernelGGL(ce_bwd_kernel, grid, dim3(1024), 0, (hipStream_t)s, logits, ld, labels, lse, V, gscale, (bf16*)dlogits, ldd);
+  SLX_LAUNCH_CHECK("slx_ce_bwd");
+  return 0;
+}
+
+int slx_wp_loss_fwd(const float* out, const float* label, int B, int n, int dims, float* pred, float* loss, slx_stream_t s) {
+  SLX_CHECK_ARG(dims <= 4, "slx_wp_loss_fwd: dims <= 4");
+  hipLaunchKernelGGL(wp_loss_fwd_kernel, g1(B, 64), dim3(64), 0, (hipStream_t)s, out, label, B, n, dims, pred, loss);
+  SLX_LAUNCH_CHECK("slx_wp_loss_fwd");
+  return 0;
+}
+
+int slx_wp_loss_bwd(const float* pred, const float* label, int B, int n, int dims, const float* gscale, float* dout, slx_stream_t s) {
+  hipLaunchKernelGGL(wp_loss_bwd_kernel, g1(B, 64), dim3(64), 0, (hipStream_t)s, pred, label, B, n, dims, gscale, dout);
+  SLX_LAUNCH_CHECK("slx_wp_loss_bwd");
+  return 0;
+}
+
+int slx_loss_finalize(const float* lang, int nl, const float* route, int nr, const float* speed, int ns, float* out, slx_stream_t s) {
+  hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(256), 0, (hipStream_t)s, lang, nl, route, nr, speed, ns, out);
+  SLX_LAUNCH_CHECK("slx_loss_finalize");
+  return 0;
+}
+
+int slx_loss_gscale(const float* dtotal, int nl, int nr, int ns, float* gs, slx_stream_t s) {
+  hipLaunchKernelGGL(loss_gscale_kernel, dim3(1), dim3(1), 0, (hipStream_t)s, dtotal, nl, nr, ns, gs);
+  SLX_LAUNCH_CHECK("slx_loss_gscale");
+  return 0;
+}
+
+int slx_sumsq(const float* g, int64_t n, float* out, int zero_first, slx_stream_t s) {
+  hipStream_t st = (hipStream_t)s;
+  if (zero_first) hipMemsetAsync(out, 0, sizeof(float), st);
+  if (!n) return 0;
+  long blocks = (n / 4 + 255) / 256;
+  if (blocks > 2048) blocks = 2048;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(sumsq_kernel, dim3((unsigned)blocks), dim3(256), 0, st, g, n, out);
+  SLX_LAUNCH_CHECK("slx_sumsq");
+  return 0;
+}
+
+int slx_adamw(float* p, const float* g, float* m, float* v, void* p_bf16, int64_t n, float lr, float beta1, float beta2,
+              float eps, float weight_decay, int step, const float* sumsq, float max_norm, slx_stream_t s) {
+  SLX_CHECK_ARG(step >= 1, "slx_adamw: step >= 1");
+  if (!n) return 0;
+  const float bc1 = 1.f - powf(beta1, (float)step);
+  const float bc2s = sqrtf(1.f - powf(beta2, (float)step));
+  long blocks = (n + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(adamw_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)s, p, g, m, v, (bf16*)p_bf16, n, lr,
+                     beta1, beta2, eps, weight_decay, bc1, bc2s, sumsq, max_norm);
+  SLX_LAUNCH_CHECK("slx_adamw");
+  return 0;
+}
+
+int slx_cast_f32_bf16(const float* src, void* dst, int64_t n, slx_stream_t s) {
+  if (!n) return 0;
+  hipLaunchKernelGGL(cast_kernel, g1(n), dim3(256), 0, (hipStream_t)s, src, (bf16*)dst, n);
+  SLX_LAUNCH_CHECK("slx_cast_f32_bf16");
+  return 0;
+}
+
+}  // extern "C"

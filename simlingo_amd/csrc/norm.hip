@@ -1,0 +1,240 @@
+// LayerNorm (InternViT blocks eps 1e-6, mlp1 eps 1e-5) and RMSNorm (Qwen2, eps 1e-6), fwd + bwd.
+// One workgroup per row in the forward (wave64 shuffle + LDS reduction); the backward walks a
+// strided set of rows per workgroup so the gamma/beta column partials stay in registers, then a
+// second pass reduces the partials. The mlp1 LayerNorm can gather its input through InternVL's
+// pixel_shuffle(0.5, ps_version v2) (remote `extract_feature`, called at
+// simlingo_training/models/encoder/internvl2_model.py:114), so the shuffled tensor never exists.
+#include "common.h"
+#include "../../include/slx.h"
+
+namespace slx {
+
+// Source row of pixel-shuffle output row `r`, chunk `c4` (0..3) of C channels.
+// out[n, i2*G/2 + j2, c4*C + c] = x[n, 1 + (2*i2 + c4/2)*G + 2*j2 + c4%2, c]   (CLS token skipped)
+__device__ __forceinline__ long ps_src_row(long r, int c4, int G, int tok_per_img) {
+  const int half = G / 2;
+  const long n = r / (half * half);
+  const int t = r % (half * half);
+  const int i2 = t / half, j2 = t % half;
+  return n * tok_per_img + 1 + (long)(2 * i2 + (c4 >> 1)) * G + 2 * j2 + (c4 & 1);
+}
+
+struct NormArgs {
+  const float* x; long ldx;
+  const float* gamma; const float* beta;
+  bf16* y; long ldy;
+  float* mean; float* rstd;
+  long rows; int D; float eps;
+  int ps; int G; int C; int tok_per_img;  // pixel-shuffle gather
+  // bwd
+  const float* dy; long lddy;
+  float* dx; long lddx; int dx_accumulate;
+  float* partial;   // [nblk, 2, D] (dgamma | dbeta)
+};
+
+template <int VPT, bool RMS>
+__global__ __launch_bounds__(256) void norm_fwd_kernel(NormArgs a) {
+  __shared__ float sh[16];
+  const long row = blockIdx.x;
+  const int tid = threadIdx.x;
+  float v[VPT];
+#pragma unroll
+  for (int i = 0; i < VPT / 4; ++i) {
+    const int col = (tid + i * 256) * 4;
+    if (col >= a.D) { v[4 * i] = v[4 * i + 1] = v[4 * i + 2] = v[4 * i + 3] = 0.f; continue; }
+    const float* src;
+    if (a.ps) {
+      const int c4 = col / a.C;
+      src = a.x + ps_src_row(row, c4, a.G, a.tok_per_img) * a.ldx + (col % a.C);
+    } else {
+      src = a.x + row * a.ldx + col;
+    }
+    const float4 t = *reinterpret_cast<const float4*>(src);
+    v[4 * i] = t.x; v[4 * i + 1] = t.y; v[4 * i + 2] = t.z; v[4 * i + 3] = t.w;
+  }
+  float mu = 0.f;
+  if (!RMS) {
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) s += v[i];
+    mu = block_sum(s, sh) / a.D;
+  }
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const float d = ((tid + (i / 4) * 256) * 4 < a.D) ? v[i] - mu : 0.f;
+    ss += d * d;
+  }
+  const float var = block_sum(ss, sh) / a.D;
+  const float rs = rsqrtf(var + a.eps);
+  if (tid == 0) {
+    if (a.mean) a.mean[row] = mu;
+    a.rstd[row] = rs;
+  }
+#pragma unroll
+  for (int i = 0; i < VPT / 4; ++i) {
+    const int col = (tid + i * 256) * 4;
+    if (col >= a.D) continue;
+    bf16x4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float xh = (v[4 * i + e] - mu) * rs;
+      float yv;
+      if (RMS) yv = (float)(bf16)xh * a.gamma[col + e];  // Qwen2: weight * hs.to(input_dtype)
+      else yv = xh * a.gamma[col + e] + a.beta[col + e];
+      o[e] = (bf16)yv;
+    }
+    *reinterpret_cast<bf16x4*>(a.y + row * a.ldy + col) = o;
+  }
+}
+
+// Backward. dx = rstd * (g*dy - mean(g*dy) - xhat * mean(g*dy*xhat))      (LayerNorm)
+//           dx = rstd * (g*dy - xhat * mean(g*dy*xhat))                     (RMSNorm)
+// dgamma = sum dy*xhat, dbeta = sum dy -> per-block partials.
+template <int VPT, bool RMS>
+__global__ __launch_bounds__(256) void norm_bwd_kernel(NormArgs a) {
+  __shared__ float sh[16];
+  const int tid = threadIdx.x;
+  float pg[VPT], pb[VPT];
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) { pg[i] = 0.f; pb[i] = 0.f; }
+  for (long row = blockIdx.x; row < a.rows; row += gridDim.x) {
+    const float mu = RMS ? 0.f : a.mean[row];
+    const float rs = a.rstd[row];
+    float xh[VPT], gd[VPT];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < VPT / 4; ++i) {
+      const int col = (tid + i * 256) * 4;
+      if (col >= a.D) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { xh[4 * i + e] = 0.f; gd[4 * i + e] = 0.f; }
+        continue;
+      }
+      const float* src;
+      if (a.ps) src = a.x + ps_src_row(row, col / a.C, a.G, a.tok_per_img) * a.ldx + (col % a.C);
+      else src = a.x + row * a.ldx + col;
+      const float4 t = *reinterpret_cast<const float4*>(src);
+      const float4 d = *reinterpret_cast<const float4*>(a.dy + row * a.lddy + col);
+      const float tv[4] = {t.x, t.y, t.z, t.w}, dv[4] = {d.x, d.y, d.z, d.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int k = 4 * i + e;
+        xh[k] = (tv[e] - mu) * rs;
+        gd[k] = dv[e] * a.gamma[col + e];
+        s1 += gd[k];
+        s2 += gd[k] * xh[k];
+        pg[k] += dv[e] * (RMS ? (float)(bf16)xh[k] : xh[k]);
+        pb[k] += dv[e];
+      }
+    }
+    const float m1 = RMS ? 0.f : block_sum(s1, sh) / a.D;
+    const float m2 = block_sum(s2, sh) / a.D;
+#pragma unroll
+    for (int i = 0; i < VPT / 4; ++i) {
+      const int col = (tid + i * 256) * 4;
+      if (col >= a.D) continue;
+      float* dst;
+      if (a.ps) dst = a.dx + ps_src_row(row, col / a.C, a.G, a.tok_per_img) * a.lddx + (col % a.C);
+      else dst = a.dx + row * a.lddx + col;
+      float4 o;
+      float ov[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int k = 4 * i + e;
+        ov[e] = rs * (gd[k] - m1 - xh[k] * m2);
+      }
+      if (a.dx_accumulate) {
+        const float4 p = *reinterpret_cast<const float4*>(dst);
+        ov[0] += p.x; ov[1] += p.y; ov[2] += p.z; ov[3] += p.w;
+      }
+      o.x = ov[0]; o.y = ov[1]; o.z = ov[2]; o.w = ov[3];
+      *reinterpret_cast<float4*>(dst) = o;
+    }
+  }
+  if (a.partial) {
+#pragma unroll
+    for (int i = 0; i < VPT / 4; ++i) {
+      const int col = (tid + i * 256) * 4;
+      if (col >= a.D) continue;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        a.partial[(long)blockIdx.x * 2 * a.D + col + e] = pg[4 * i + e];
+        a.partial[(long)blockIdx.x * 2 * a.D + a.D + col + e] = pb[4 * i + e];
+      }
+    }
+  }
+}
+
+// out[c] (+)= sum_b partial[b, c]   for c < ncols  (column reduction of [nblk, ncols] partials)
+__global__ void colreduce_kernel(const float* partial, int nblk, int ncols, long ldp, float* out, int accumulate) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= ncols) return;
+  float s = 0.f;
+  for (int b = 0; b < nblk; ++b) s += partial[(long)b * ldp + c];
+  out[c] = accumulate ? out[c] + s : s;
+}
+
+}  // namespace slx
+
+using namespace slx;
+
+static constexpr int kBwdBlocks = 512;
+
+template <bool RMS>
+static int norm_fwd(NormArgs& a, hipStream_t st) {
+  SLX_CHECK_ARG(a.D % 4 == 0 && a.D <= 4096, "norm fwd: D=%d must be a multiple of 4 and <= 4096", a.D);
+  if (a.D <= 1024) hipLaunchKernelGGL((norm_fwd_kernel<4, RMS>), dim3(a.rows), dim3(256), 0, st, a);
+  else if (a.D <= 2048) hipLaunchKernelGGL((norm_fwd_kernel<8, RMS>), dim3(a.rows), dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((norm_fwd_kernel<16, RMS>), dim3(a.rows), dim3(256), 0, st, a);
+  SLX_LAUNCH_CHECK("slx_norm_fwd");
+  return 0;
+}
+
+template <bool RMS>
+static int norm_bwd(NormArgs& a, float* dgamma, float* dbeta, int accumulate, hipStream_t st) {
+  const int nblk = (int)(a.rows < kBwdBlocks ? a.rows : kBwdBlocks);
+  SLX_CHECK_ARG(a.D % 4 == 0 && a.D <= 4096, "norm bwd: D=%d must be a multiple of 4 and <= 4096", a.D);
+  if (a.D <= 1024) hipLaunchKernelGGL((norm_bwd_kernel<4, RMS>), dim3(nblk), dim3(256), 0, st, a);
+  else if (a.D <= 2048) hipLaunchKernelGGL((norm_bwd_kernel<8, RMS>), dim3(nblk), dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((norm_bwd_kernel<16, RMS>), dim3(nblk), dim3(256), 0, st, a);
+  SLX_LAUNCH_CHECK("slx_norm_bwd");
+  if (a.partial) {
+    if (dgamma) hipLaunchKernelGGL(colreduce_kernel, dim3((a.D + 255) / 256), dim3(256), 0, st, a.partial, nblk, a.D, (long)2 * a.D, dgamma, accumulate);
+    if (dbeta) hipLaunchKernelGGL(colreduce_kernel, dim3((a.D + 255) / 256), dim3(256), 0, st, a.partial + a.D, nblk, a.D, (long)2 * a.D, dbeta, accumulate);
+    SLX_LAUNCH_CHECK("slx_norm_bwd(reduce)");
+  }
+  return 0;
+}
+
+static void fill(NormArgs& a, const slx_norm_desc* d) {
+  memset(&a, 0, sizeof(a));
+  a.x = d->x; a.ldx = d->ldx; a.gamma = d->gamma; a.beta = d->beta;
+  a.y = (bf16*)d->y; a.ldy = d->ldy; a.mean = d->mean; a.rstd = d->rstd;
+  a.rows = d->rows; a.D = d->D; a.eps = d->eps;
+  a.ps = d->pixel_shuffle_grid > 0; a.G = d->pixel_shuffle_grid; a.C = d->pixel_shuffle_grid > 0 ? d->D / 4 : d->D;
+  a.tok_per_img = d->tokens_per_image;
+}
+
+extern "C" int slx_norm_fwd(const slx_norm_desc* d, slx_stream_t stream) {
+  if (d->rows == 0) return 0;
+  NormArgs a;
+  fill(a, d);
+  SLX_CHECK_ARG(d->ldx % 4 == 0 && d->ldy % 4 == 0, "slx_norm_fwd: strides must be multiples of 4");
+  return d->rms ? norm_fwd<true>(a, (hipStream_t)stream) : norm_fwd<false>(a, (hipStream_t)stream);
+}
+
+extern "C" int slx_norm_bwd(const slx_norm_desc* d, const float* dy, int64_t lddy, float* dx, int64_t lddx,
+                            int dx_accumulate, float* dgamma, float* dbeta, int param_accumulate, float* partial_ws,
+                            slx_stream_t stream) {
+  if (d->rows == 0) return 0;
+  NormArgs a;
+  fill(a, d);
+  a.dy = dy; a.lddy = lddy; a.dx = dx; a.lddx = lddx; a.dx_accumulate = dx_accumulate;
+  a.partial = (dgamma || dbeta) ? partial_ws : nullptr;
+  SLX_CHECK_ARG(!(dgamma || dbeta) || partial_ws, "slx_norm_bwd: partial_ws required for dgamma/dbeta");
+  return d->rms ? norm_bwd<true>(a, dgamma, dbeta, param_accumulate, (hipStream_t)stream)
+                : norm_bwd<false>(a, dgamma, dbeta, param_accumulate, (hipStream_t)stream);
+}
+
+extern "C" int slx_norm_partial_ws_floats(int D) { return kBwdBlocks * 2 * D; }

@@ -1,0 +1,334 @@
+"""ctypes binding of libslx_hip.so (include/slx.h).
+
+PyTorch supplies device memory and the current HIP stream; every computation happens in the HIP
+library. There is deliberately no fallback: if the library is missing or a call fails, a
+RuntimeError is raised (a silent eager/CPU path would void every parity claim).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+
+import torch
+
+_LIB_PATH = Path(__file__).resolve().parent / "csrc" / "libslx_hip.so"
+_lib = None
+
+c_int, c_i64, c_u64, c_float, c_vp = ctypes.c_int, ctypes.c_int64, ctypes.c_uint64, ctypes.c_float, ctypes.c_void_p
+
+# ---- enums (mirror include/slx.h) --------------------------------------------------------------
+GEMM_NT, GEMM_NN, GEMM_TN, GEMM_TT = 0, 1, 2, 3
+EPI_STORE, EPI_GELU, EPI_RESID_LS, EPI_GELU_BWD, EPI_SWIGLU_BWD, EPI_DROPMASK = 0, 1, 2, 3, 4, 5
+
+
+class GemmDesc(ctypes.Structure):
+    _fields_ = [
+        ("layout", c_int), ("epilogue", c_int), ("out_f32", c_int),
+        ("M", c_int), ("N", c_int), ("K", c_int), ("batch", c_int),
+        ("A", c_vp), ("lda", c_i64), ("sA", c_i64),
+        ("B", c_vp), ("ldb", c_i64), ("sB", c_i64),
+        ("C", c_vp), ("ldc", c_i64), ("sC", c_i64),
+        ("alpha", c_float),
+        ("bias", c_vp), ("ls", c_vp),
+        ("aux", c_vp), ("ldaux", c_i64),
+        ("aux_out", c_vp), ("ldaux_out", c_i64),
+        ("resid", c_vp), ("ldr", c_i64),
+        ("accumulate", c_int),
+        ("seed", c_u64), ("drop_p", c_float), ("ldmask", c_i64),
+    ]
+
+
+# name -> argtypes (restype int unless listed in _RESTYPE)
+_SIGS: dict[str, list] = {
+    "slx_abi_version": [],
+    "slx_device_sync": [],
+    "slx_gemm_bf16": [ctypes.POINTER(GemmDesc), c_vp],
+}
+_RESTYPE = {"slx_last_error": ctypes.c_char_p}
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not _LIB_PATH.exists():
+            raise RuntimeError(
+                f"{_LIB_PATH} is not built: run `python -m simlingo_amd.build` (hipcc, gfx950). "
+                "There is no CPU/eager fallback for the SimLingo MI355X kernels.")
+        _lib = ctypes.CDLL(str(_LIB_PATH))
+        _lib.slx_last_error.restype = ctypes.c_char_p
+        _lib.slx_last_error.argtypes = []
+        for name, args in _SIGS.items():
+            f = getattr(_lib, name)
+            f.argtypes = args
+            f.restype = c_int
+    return _lib
+
+
+def register(name: str, argtypes: list):
+    """Declare a C-ABI entry point (used by modules that add bindings)."""
+    _SIGS[name] = argtypes
+    if _lib is not None:
+        f = getattr(_lib, name)
+        f.argtypes = argtypes
+        f.restype = c_int
+
+
+def exported_symbols() -> list[str]:
+    return ["slx_last_error"] + list(_SIGS)
+
+
+def check(rc: int, name: str):
+    if rc != 0:
+        msg = lib().slx_last_error().decode(errors="replace")
+        raise RuntimeError(f"{name} failed (rc={rc}): {msg}")
+
+
+def call(name: str, *args):
+    check(getattr(lib(), name)(*args), name)
+
+
+def stream_ptr() -> c_vp:
+    return c_vp(torch.cuda.current_stream().cuda_stream)
+
+
+def P(t: torch.Tensor | None) -> c_vp:
+    """Raw device pointer of a tensor (None -> NULL)."""
+    if t is None:
+        return c_vp(0)
+    return c_vp(t.data_ptr())
+
+
+def _require_cuda(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError("SimLingo MI355X kernels need device tensors (no CPU fallback)")
+
+
+# ------------------------------------------------------------------------------------------------
+# GEMM
+# ------------------------------------------------------------------------------------------------
+def gemm(A, B, C, M, N, K, layout, lda, ldb, ldc, *, epi=EPI_STORE, alpha=1.0, bias=None, ls=None,
+         aux=None, ldaux=0, aux_out=None, ldaux_out=0, resid=None, ldr=0, accumulate=False,
+         seed=0, drop_p=0.0, ldmask=0, batch=1, sA=0, sB=0, sC=0):
+    _require_cuda(A, B, C)
+    d = GemmDesc()
+    d.layout, d.epilogue = layout, epi
+    d.out_f32 = 1 if C.dtype == torch.float32 else 0
+    d.M, d.N, d.K, d.batch = int(M), int(N), int(K), int(batch)
+    d.A, d.lda, d.sA = A.data_ptr(), int(lda), int(sA)
+    d.B, d.ldb, d.sB = B.data_ptr(), int(ldb), int(sB)
+    d.C, d.ldc, d.sC = C.data_ptr(), int(ldc), int(sC)
+    d.alpha = float(alpha)
+    d.bias = bias.data_ptr() if bias is not None else 0
+    d.ls = ls.data_ptr() if ls is not None else 0
+    d.aux = aux.data_ptr() if aux is not None else 0
+    d.ldaux = int(ldaux)
+    d.aux_out = aux_out.data_ptr() if aux_out is not None else 0
+    d.ldaux_out = int(ldaux_out)
+    d.resid = resid.data_ptr() if resid is not None else 0
+    d.ldr = int(ldr)
+    d.accumulate = 1 if accumulate else 0
+    d.seed, d.drop_p, d.ldmask = int(seed) & ((1 << 64) - 1), float(drop_p), int(ldmask)
+    check(lib().slx_gemm_bf16(ctypes.byref(d), stream_ptr()), "slx_gemm_bf16")
+
+
+def linear(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor, bias=None, **kw):
+    """out[M,N] = x[M,K] @ w[N,K]^T (+bias) — 2-D row-major views with unit inner stride."""
+    M, K = x.shape
+    N = w.shape[0]
+    gemm(x, w, out, M, N, K, GEMM_NT, x.stride(0), w.stride(0), out.stride(0), bias=bias, **kw)
+    return out
+
+
+def dgrad(dy: torch.Tensor, w: torch.Tensor, out: torch.Tensor, **kw):
+    """out[M,K] = dy[M,N] @ w[N,K]."""
+    M, N = dy.shape
+    K = w.shape[1]
+    gemm(dy, w, out, M, K, N, GEMM_NN, dy.stride(0), w.stride(0), out.stride(0), **kw)
+    return out
+
+
+def wgrad(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor, **kw):
+    """out[N,K] = dy[M,N]^T @ x[M,K]."""
+    M, N = dy.shape
+    K = x.shape[1]
+    gemm(dy, x, out, N, K, M, GEMM_TN, dy.stride(0), x.stride(0), out.stride(0), **kw)
+    return out
+
+
+# ------------------------------------------------------------------------------------------------
+# Attention
+# ------------------------------------------------------------------------------------------------
+class AttnDesc(ctypes.Structure):
+    _fields_ = [
+        ("B", c_int), ("S", c_int), ("Hq", c_int), ("Hkv", c_int), ("head_dim", c_int), ("causal", c_int),
+        ("q", c_vp), ("ldq", c_i64), ("k", c_vp), ("ldk", c_i64), ("v", c_vp), ("ldv", c_i64),
+        ("o", c_vp), ("ldo", c_i64), ("lse", c_vp), ("seqlens", c_vp), ("scale", c_float),
+    ]
+
+
+class AttnBwdDesc(ctypes.Structure):
+    _fields_ = [
+        ("dout", c_vp), ("lddo", c_i64), ("dq", c_vp), ("lddq", c_i64), ("dk", c_vp), ("lddk", c_i64),
+        ("dv", c_vp), ("lddv", c_i64), ("delta_ws", c_vp), ("dq_acc", c_vp), ("dk_acc", c_vp), ("dv_acc", c_vp),
+        ("rope_cos", c_vp), ("rope_sin", c_vp),
+    ]
+
+
+class NormDesc(ctypes.Structure):
+    _fields_ = [
+        ("rms", c_int), ("x", c_vp), ("ldx", c_i64), ("gamma", c_vp), ("beta", c_vp), ("y", c_vp), ("ldy", c_i64),
+        ("mean", c_vp), ("rstd", c_vp), ("rows", c_i64), ("D", c_int), ("eps", c_float),
+        ("pixel_shuffle_grid", c_int), ("tokens_per_image", c_int),
+    ]
+
+
+ACT_NONE, ACT_RELU, ACT_SILU = 0, 1, 2
+
+
+class SgemmDesc(ctypes.Structure):
+    _fields_ = [
+        ("M", c_int), ("N", c_int), ("K", c_int), ("act", c_int), ("accumulate", c_int),
+        ("A", c_vp), ("sam", c_i64), ("sak", c_i64), ("B", c_vp), ("sbk", c_i64), ("sbn", c_i64),
+        ("C", c_vp), ("scm", c_i64), ("scn", c_i64), ("bias", c_vp), ("pre", c_vp), ("ldpre", c_i64),
+        ("alpha", c_float),
+    ]
+
+
+_vp, _i, _I, _f = c_vp, c_int, c_i64, c_float
+for _n, _a in {
+    "slx_attn_fwd": [ctypes.POINTER(AttnDesc), _vp],
+    "slx_attn_bwd": [ctypes.POINTER(AttnDesc), ctypes.POINTER(AttnBwdDesc), _vp],
+    "slx_rope": [_vp, _I, _I, _i, _i, _vp, _vp, _i, _vp],
+    "slx_norm_fwd": [ctypes.POINTER(NormDesc), _vp],
+    "slx_norm_bwd": [ctypes.POINTER(NormDesc), _vp, _I, _vp, _I, _i, _vp, _vp, _i, _vp, _vp],
+    "slx_norm_partial_ws_floats": [_i],
+    "slx_im2col_patch": [_vp, _i, _i, _i, _i, _i, _vp, _vp],
+    "slx_vit_embed_fwd": [_vp, _vp, _vp, _vp, _i, _i, _i, _vp],
+    "slx_vit_embed_bwd": [_vp, _i, _i, _i, _vp, _vp, _vp, _vp],
+    "slx_swiglu_fwd": [_vp, _I, _vp, _I, _I, _i, _vp],
+    "slx_colsum": [_i, _vp, _I, _I, _i, _vp, _i, _vp, _vp],
+    "slx_colsum_ws_floats": [_i],
+    "slx_ls_branch_bwd": [_vp, _I, _vp, _vp, _I, _vp, _I, _I, _i, _vp, _vp, _i, _vp, _vp],
+    "slx_assemble_tokens": [_vp, _I, _i, _vp, _i, _vp, _vp, _vp, _vp, _vp],
+    "slx_gather_rows": [_vp, _I, _vp, _I, _i, _vp, _I, _i, _vp],
+    "slx_gather_rows_bf16": [_vp, _I, _vp, _I, _i, _vp, _I, _vp],
+    "slx_gather_sum": [_vp, _I, _vp, _i, _i, _i, _vp, _i, _vp],
+    "slx_dropout": [_vp, _I, _vp, _I, _I, _i, c_u64, _f, _I, _vp],
+    "slx_sgemm": [ctypes.POINTER(SgemmDesc), _vp],
+    "slx_act_bwd": [_vp, _vp, _vp, _I, _i, _vp],
+    "slx_ce_fwd": [_vp, _I, _vp, _I, _i, _vp, _vp, _vp],
+    "slx_ce_bwd": [_vp, _I, _vp, _vp, _I, _i, _vp, _vp, _I, _vp],
+    "slx_wp_loss_fwd": [_vp, _vp, _i, _i, _i, _vp, _vp, _vp],
+    "slx_wp_loss_bwd": [_vp, _vp, _i, _i, _i, _vp, _vp, _vp],
+    "slx_loss_finalize": [_vp, _i, _vp, _i, _vp, _i, _vp, _vp],
+    "slx_loss_gscale": [_vp, _i, _i, _i, _vp, _vp],
+    "slx_sumsq": [_vp, _I, _vp, _i, _vp],
+    "slx_adamw": [_vp, _vp, _vp, _vp, _vp, _I, _f, _f, _f, _f, _f, _i, _vp, _f, _vp],
+    "slx_cast_f32_bf16": [_vp, _vp, _I, _vp],
+}.items():
+    register(_n, _a)
+
+
+def attn_desc(q, k, v, o, lse, *, B, S, Hq, Hkv, causal=False, seqlens=None, scale=0.125):
+    d = AttnDesc()
+    d.B, d.S, d.Hq, d.Hkv, d.head_dim, d.causal = B, S, Hq, Hkv, 64, int(bool(causal))
+    d.q, d.ldq = q.data_ptr(), q.stride(0)
+    d.k, d.ldk = k.data_ptr(), k.stride(0)
+    d.v, d.ldv = v.data_ptr(), v.stride(0)
+    d.o, d.ldo = o.data_ptr(), o.stride(0)
+    d.lse = lse.data_ptr() if lse is not None else 0
+    d.seqlens = seqlens.data_ptr() if seqlens is not None else 0
+    d.scale = float(scale)
+    return d
+
+
+def attn_fwd(q, k, v, o, lse, **kw):
+    """q/k/v/o: 2-D token-major views [B*S, >= H*64] (column slices allowed)."""
+    _require_cuda(q, k, v, o)
+    d = attn_desc(q, k, v, o, lse, **kw)
+    check(lib().slx_attn_fwd(ctypes.byref(d), stream_ptr()), "slx_attn_fwd")
+
+
+def attn_bwd(q, k, v, o, lse, dout, dq, dk, dv, ws, *, rope_cos=None, rope_sin=None, **kw):
+    """ws: dict with 'delta' [B*Hq*S], 'dq_acc' [B*S*Hq*64], ('dk_acc','dv_acc' for GQA) f32 buffers."""
+    d = attn_desc(q, k, v, o, lse, **kw)
+    g = AttnBwdDesc()
+    g.dout, g.lddo = dout.data_ptr(), dout.stride(0)
+    g.dq, g.lddq = dq.data_ptr(), dq.stride(0)
+    g.dk, g.lddk = dk.data_ptr(), dk.stride(0)
+    g.dv, g.lddv = dv.data_ptr(), dv.stride(0)
+    g.delta_ws = ws["delta"].data_ptr()
+    g.dq_acc = ws["dq_acc"].data_ptr()
+    g.dk_acc = ws["dk_acc"].data_ptr() if "dk_acc" in ws else 0
+    g.dv_acc = ws["dv_acc"].data_ptr() if "dv_acc" in ws else 0
+    g.rope_cos = rope_cos.data_ptr() if rope_cos is not None else 0
+    g.rope_sin = rope_sin.data_ptr() if rope_sin is not None else 0
+    check(lib().slx_attn_bwd(ctypes.byref(d), ctypes.byref(g), stream_ptr()), "slx_attn_bwd")
+
+
+def attn_ws(B, S, Hq, Hkv, device):
+    ws = {"delta": torch.empty(B * Hq * S, device=device), "dq_acc": torch.empty(B * S * Hq * 64, device=device)}
+    if Hq != Hkv:
+        ws["dk_acc"] = torch.empty(B * S * Hkv * 64, device=device)
+        ws["dv_acc"] = torch.empty(B * S * Hkv * 64, device=device)
+    return ws
+
+
+def rope(x, ntok, S, nheads, cos, sin, inverse=False):
+    call("slx_rope", P(x), x.stride(0), ntok, S, nheads, P(cos), P(sin), int(inverse), stream_ptr())
+
+
+def rope_tables(S, theta, device, head_dim=64):
+    """HF Qwen2RotaryEmbedding: inv_freq[i] = theta^(-2i/d); tables [S, d/2] f32."""
+    inv = 1.0 / (theta ** (torch.arange(0, head_dim, 2, dtype=torch.int64).float() / head_dim))
+    t = torch.arange(S, dtype=torch.int64).float()
+    fr = torch.outer(t, inv)
+    return fr.cos().to(device).contiguous(), fr.sin().to(device).contiguous()
+
+
+# ------------------------------------------------------------------------------------------------
+# Norms
+# ------------------------------------------------------------------------------------------------
+def norm_desc(x, gamma, beta, y, mean, rstd, rows, D, eps, rms=False, ps_grid=0, tok_per_img=0, ldx=None):
+    d = NormDesc()
+    d.rms = int(rms)
+    d.x, d.ldx = x.data_ptr(), ldx if ldx is not None else x.stride(0)
+    d.gamma = gamma.data_ptr()
+    d.beta = beta.data_ptr() if beta is not None else 0
+    d.y, d.ldy = (y.data_ptr(), y.stride(0)) if y is not None else (0, 0)
+    d.mean = mean.data_ptr() if mean is not None else 0
+    d.rstd = rstd.data_ptr()
+    d.rows, d.D, d.eps = int(rows), int(D), float(eps)
+    d.pixel_shuffle_grid, d.tokens_per_image = int(ps_grid), int(tok_per_img)
+    return d
+
+
+def norm_fwd(d: NormDesc):
+    check(lib().slx_norm_fwd(ctypes.byref(d), stream_ptr()), "slx_norm_fwd")
+
+
+def norm_bwd(d: NormDesc, dy, dx, *, dx_accumulate=False, dgamma=None, dbeta=None, param_accumulate=False, ws=None,
+             lddx=None):
+    check(lib().slx_norm_bwd(ctypes.byref(d), P(dy), dy.stride(0), P(dx), lddx if lddx is not None else dx.stride(0),
+                             int(dx_accumulate), P(dgamma), P(dbeta), int(param_accumulate), P(ws), stream_ptr()),
+          "slx_norm_bwd")
+
+
+def norm_ws_floats(D):
+    return lib().slx_norm_partial_ws_floats(D)
+
+
+def sgemm(A, sam, sak, B, sbk, sbn, C, scm, scn, M, N, Kd, *, bias=None, act=ACT_NONE, pre=None, ldpre=0,
+          accumulate=False, alpha=1.0):
+    d = SgemmDesc()
+    d.M, d.N, d.K, d.act, d.accumulate = int(M), int(N), int(Kd), int(act), int(accumulate)
+    d.A, d.sam, d.sak = A.data_ptr(), sam, sak
+    d.B, d.sbk, d.sbn = B.data_ptr(), sbk, sbn
+    d.C, d.scm, d.scn = C.data_ptr(), scm, scn
+    d.bias = bias.data_ptr() if bias is not None else 0
+    d.pre = pre.data_ptr() if pre is not None else 0
+    d.ldpre = ldpre
+    d.alpha = alpha
+    check(lib().slx_sgemm(ctypes.byref(d), stream_ptr()), "slx_sgemm")

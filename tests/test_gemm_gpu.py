@@ -1,0 +1,71 @@
+"""GEMM parity: HIP bf16 MFMA GEMM vs a plain PyTorch fp32 matmul of the same bf16 operands."""
+import pytest
+import torch
+
+from simlingo_amd import kernels as K
+
+pytestmark = pytest.mark.gpu
+
+SHAPES = [(128, 128, 64), (200, 136, 72), (1000, 520, 1032), (33, 8, 8), (16400 // 8, 3072 // 4, 1024)]
+
+
+def _ref(a, b):
+    return a.float() @ b.float()
+
+
+@pytest.mark.parametrize("M,N,Kd", SHAPES)
+@pytest.mark.parametrize("layout", [K.GEMM_NT, K.GEMM_NN, K.GEMM_TN, K.GEMM_TT])
+@pytest.mark.parametrize("out_f32", [True, False])
+def test_gemm_layouts(dev, M, N, Kd, layout, out_f32):
+    a_contig = Kd if layout in (K.GEMM_NT, K.GEMM_NN) else M
+    b_contig = Kd if layout in (K.GEMM_NT, K.GEMM_TT) else N
+    if a_contig % 8 or b_contig % 8:
+        with pytest.raises(RuntimeError, match="multiple of 8"):
+            A = torch.zeros(8, 8, device=dev, dtype=torch.bfloat16)
+            K.gemm(A, A, A, M, N, Kd, layout, 8, 8, 8)
+        return
+    g = torch.Generator(device=dev).manual_seed(M * 7 + N + Kd + layout)
+    a = torch.randn(M, Kd, device=dev, generator=g).bfloat16()
+    b = torch.randn(Kd, N, device=dev, generator=g).bfloat16()
+    # materialise the storage each layout expects
+    A = a if layout in (K.GEMM_NT, K.GEMM_NN) else a.t().contiguous()
+    B = b.t().contiguous() if layout in (K.GEMM_NT, K.GEMM_TT) else b
+    C = torch.empty(M, N, device=dev, dtype=torch.float32 if out_f32 else torch.bfloat16)
+    K.gemm(A, B, C, M, N, Kd, layout, A.stride(0), B.stride(0), C.stride(0))
+    ref = _ref(a, b)
+    tol = 2e-3 * Kd ** 0.5 + (0 if out_f32 else 1e-2 * ref.abs().max().item())
+    assert (C.float() - ref).abs().max().item() < tol
+
+
+def test_gemm_epilogues(dev):
+    M, N, Kd = 300, 256, 192
+    g = torch.Generator(device=dev).manual_seed(0)
+    x = torch.randn(M, Kd, device=dev, generator=g).bfloat16()
+    w = torch.randn(N, Kd, device=dev, generator=g).bfloat16() * 0.1
+    bias = torch.randn(N, device=dev, generator=g)
+    ref = x.float() @ w.float().t() + bias
+    # bias + alpha + accumulate
+    C = torch.ones(M, N, device=dev)
+    K.linear(x, w, C, bias=bias, alpha=1.0, accumulate=True)
+    torch.testing.assert_close(C, ref + 1, atol=2e-3, rtol=2e-3)
+    # gelu with pre-activation aux
+    h = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    y = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    K.linear(x, w, y, bias=bias, epi=K.EPI_GELU, aux_out=h, ldaux_out=N)
+    torch.testing.assert_close(h.float(), ref, atol=3e-2, rtol=1e-2)
+    torch.testing.assert_close(y.float(), torch.nn.functional.gelu(h.float()), atol=3e-2, rtol=1e-2)
+    # residual + layer scale
+    resid = torch.randn(M, N, device=dev, generator=g)
+    ls = torch.rand(N, device=dev, generator=g)
+    out = torch.empty(M, N, device=dev)
+    yb = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    K.linear(x, w, out, bias=bias, epi=K.EPI_RESID_LS, resid=resid, ldr=N, ls=ls, aux_out=yb, ldaux_out=N)
+    torch.testing.assert_close(out, resid + ls * ref, atol=3e-3, rtol=3e-3)
+    # gelu backward
+    dy = torch.randn(M, Kd, device=dev, generator=g).bfloat16()
+    w2 = torch.randn(Kd, N, device=dev, generator=g).bfloat16()  # "weight" [Nout=Kd][Kin=N]
+    dh = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    K.dgrad(dy, w2, dh, epi=K.EPI_GELU_BWD, aux=h, ldaux=N)
+    hh = h.float().requires_grad_()
+    torch.nn.functional.gelu(hh).backward(dy.float() @ w2.float())
+    torch.testing.assert_close(dh.float(), hh.grad, atol=5e-2, rtol=2e-2)

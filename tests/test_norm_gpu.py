@@ -1,0 +1,76 @@
+"""LayerNorm / RMSNorm (+ pixel-shuffle gather) parity vs PyTorch fp32."""
+import pytest
+import torch
+
+from simlingo_amd import kernels as K
+
+pytestmark = pytest.mark.gpu
+
+
+def pixel_shuffle_v2(x, scale=0.5):
+    # InternVL extract_feature pixel_shuffle (ps_version v2), x: [n, w, h, c]
+    n, w, h, c = x.size()
+    x = x.view(n, w, int(h * scale), int(c / scale))
+    x = x.permute(0, 2, 1, 3).contiguous()
+    x = x.view(n, int(h * scale), int(w * scale), int(c / (scale * scale)))
+    return x.permute(0, 2, 1, 3).contiguous()
+
+
+@pytest.mark.parametrize("D,rms", [(1024, False), (896, True), (4096, False), (512, True)])
+def test_norm(dev, D, rms):
+    torch.manual_seed(D)
+    rows = 777
+    x = torch.randn(rows, D, device=dev) * 2 + 0.5
+    g = torch.rand(D, device=dev) + 0.5
+    b = torch.randn(D, device=dev)
+    y = torch.empty(rows, D, device=dev, dtype=torch.bfloat16)
+    mean = torch.empty(rows, device=dev)
+    rstd = torch.empty(rows, device=dev)
+    d = K.norm_desc(x, g, None if rms else b, y, None if rms else mean, rstd, rows, D, 1e-6, rms=rms)
+    K.norm_fwd(d)
+    xr = x.clone().requires_grad_()
+    gr = g.clone().requires_grad_()
+    br = b.clone().requires_grad_()
+    if rms:
+        xh = xr * torch.rsqrt(xr.pow(2).mean(-1, keepdim=True) + 1e-6)
+        # Qwen2RMSNorm: weight * hs.to(input_dtype) -> the weight sees the bf16-rounded xhat
+        ref = gr * (xh + (xh.bfloat16().float() - xh).detach())
+    else:
+        ref = torch.nn.functional.layer_norm(xr, (D,), gr, br, 1e-6)
+    assert (y.float() - ref).abs().max().item() < 3e-2
+    dy = torch.randn(rows, D, device=dev)
+    ref.backward(dy)
+    dx = torch.ones(rows, D, device=dev)
+    dg = torch.empty(D, device=dev)
+    db = torch.empty(D, device=dev)
+    ws = torch.empty(K.norm_ws_floats(D), device=dev)
+    K.norm_bwd(d, dy, dx, dx_accumulate=True, dgamma=dg, dbeta=None if rms else db, ws=ws)
+    torch.testing.assert_close(dx - 1, xr.grad, atol=2e-3, rtol=2e-3)
+    torch.testing.assert_close(dg, gr.grad, atol=5e-2, rtol=1e-2)
+    if not rms:
+        torch.testing.assert_close(db, br.grad, atol=2e-3, rtol=1e-3)
+
+
+def test_layernorm_pixel_shuffle_gather(dev):
+    torch.manual_seed(1)
+    n, G, C = 3, 8, 64
+    T = 1 + G * G
+    xv = torch.randn(n * T, C, device=dev)
+    D = 4 * C
+    rows = n * (G // 2) ** 2
+    g = torch.rand(D, device=dev) + 0.5
+    b = torch.randn(D, device=dev)
+    y = torch.empty(rows, D, device=dev, dtype=torch.bfloat16)
+    mean = torch.empty(rows, device=dev)
+    rstd = torch.empty(rows, device=dev)
+    d = K.norm_desc(xv, g, b, y, mean, rstd, rows, D, 1e-5, ps_grid=G, tok_per_img=T)
+    K.norm_fwd(d)
+    xr = xv.clone().requires_grad_()
+    sh = pixel_shuffle_v2(xr.view(n, T, C)[:, 1:].reshape(n, G, G, C)).reshape(rows, D)
+    ref = torch.nn.functional.layer_norm(sh, (D,), g, b, 1e-5)
+    assert (y.float() - ref).abs().max().item() < 3e-2
+    dy = torch.randn(rows, D, device=dev)
+    ref.backward(dy)
+    dx = torch.zeros(n * T, C, device=dev)
+    K.norm_bwd(d, dy, dx, lddx=C)
+    torch.testing.assert_close(dx, xr.grad, atol=2e-3, rtol=2e-3)
