@@ -163,12 +163,20 @@ int slx_ce_bwd(const float* logits, int64_t ld, const int* labels, const float* 
 int slx_wp_loss_fwd(const float* out, const float* label, int B, int n, int dims, float* pred, float* loss, slx_stream_t s);
 int slx_wp_loss_bwd(const float* pred, const float* label, int B, int n, int dims, const float* gscale, float* dout, slx_stream_t s);
 int slx_loss_finalize(const float* lang, int nl, const float* route, int nr, const float* speed, int ns, float* out, slx_stream_t s);
-int slx_loss_gscale(const float* dtotal, int nl, int nr, int ns, float* gs, slx_stream_t s);
+/* gs[0..2] = (dl[0] + dl[1+i]) / n_i : per-item gradient scales from the upstream grads of
+ * [total, lang, route, speed] (dl may be NULL -> d total = 1).                                 */
+int slx_loss_gscale(const float* dl, int nl, int nr, int ns, float* gs, slx_stream_t s);
+int slx_scatter_rows(const float* src, int64_t lds, const int* idx, int64_t n, int D, float* dst, int64_t ldd, int accumulate, slx_stream_t s);
+int slx_gather_rows_b2f(const void* src, int64_t lds, const int* idx, int64_t n, int D, float* dst, int64_t ldd, slx_stream_t s);
+/* SwiGLU backward from f32 d(act) (used when LoRA adds to d(act) before the activation backward) */
+int slx_swiglu_bwd(const float* dact, int64_t ldd, const void* gu, int64_t ldgu, void* dgu, int64_t lddgu, int64_t M, int F, slx_stream_t s);
+int slx_cast_rows(const float* src, int64_t lds, void* dst, int64_t ldd, int64_t M, int N, slx_stream_t s);
 
 /* ---- optimizer (torch.optim.AdamW semantics, driving.py:718-724; clip_grad_norm 0.3, train.py:206) */
 int slx_sumsq(const float* g, int64_t n, float* out, int zero_first, slx_stream_t s);
+/* grad_scale multiplies the gradient (1/world after a SUM all-reduce); clipping uses the scaled norm */
 int slx_adamw(float* p, const float* g, float* m, float* v, void* p_bf16, int64_t n, float lr, float beta1, float beta2,
-              float eps, float weight_decay, int step, const float* sumsq, float max_norm, slx_stream_t s);
+              float eps, float weight_decay, int step, const float* sumsq, float max_norm, float grad_scale, slx_stream_t s);
 int slx_cast_f32_bf16(const float* src, void* dst, int64_t n, slx_stream_t s);
 
 #ifdef __cplusplus

@@ -337,11 +337,12 @@ __global__ void loss_finalize_kernel(const float* lang, int nl, const float* rou
     out[1] = la; out[2] = ra; out[3] = sa;
   }
 }
-__global__ void loss_gscale_kernel(const float* dtotal, int nl, int nr, int ns, float* gs) {
-  const float g = dtotal ? *dtotal : 1.f;
-  gs[0] = nl > 0 ? g / nl : 0.f;
-  gs[1] = nr > 0 ? g / nr : 0.f;
-  gs[2] = ns > 0 ? g / ns : 0.f;
+__global__ void loss_gscale_kernel(const float* dl, int nl, int nr, int ns, float* gs) {
+  // dl = d(out)/d[total, lang, route, speed]; every average feeds the total with weight 1
+  const float t = dl ? dl[0] : 1.f;
+  gs[0] = nl > 0 ? (t + (dl ? dl[1] : 0.f)) / nl : 0.f;
+  gs[1] = nr > 0 ? (t + (dl ? dl[2] : 0.f)) / nr : 0.f;
+  gs[2] = ns > 0 ? (t + (dl ? dl[3] : 0.f)) / ns : 0.f;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -362,11 +363,12 @@ __global__ __launch_bounds__(256) void sumsq_kernel(const float* g, long n, floa
 
 __global__ __launch_bounds__(256) void adamw_kernel(float* p, const float* g, float* m, float* v, bf16* pbf, long n,
                                                     float lr, float b1, float b2, float eps, float wd, float bc1,
-                                                    float bc2s, const float* sumsq, float max_norm) {
-  float coef = 1.f;
+                                                    float bc2s, const float* sumsq, float max_norm, float gscale) {
+  // gscale: 1/world for summed data-parallel gradients; clip on the averaged gradient's norm
+  float coef = gscale;
   if (sumsq && max_norm > 0.f) {
-    const float tn = sqrtf(*sumsq);
-    coef = fminf(1.f, max_norm / (tn + 1e-6f));
+    const float tn = sqrtf(*sumsq) * gscale;
+    coef = gscale * fminf(1.f, max_norm / (tn + 1e-6f));
   }
   const float step = lr / bc1;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
@@ -379,6 +381,59 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* p, const float* g, fl
     p[i] = pi; m[i] = mi; v[i] = vi;
     if (pbf) pbf[i] = (bf16)pi;
   }
+}
+
+// dst[idx[i], :] (+)= src[i, :]   (f32 rows; idx unique)
+__global__ void scatter_rows_kernel(const float* src, long lds, const int* idx, long n, int D, float* dst, long ldd, int accumulate) {
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n * (D / 4)) return;
+  const long i = t / (D / 4);
+  const int c = (t % (D / 4)) * 4;
+  const float4 v = *reinterpret_cast<const float4*>(src + i * lds + c);
+  float4* d = reinterpret_cast<float4*>(dst + (long)idx[i] * ldd + c);
+  if (accumulate) { const float4 o = *d; *d = {o.x + v.x, o.y + v.y, o.z + v.z, o.w + v.w}; }
+  else *d = v;
+}
+
+// bf16 rows gathered into f32 rows
+__global__ void gather_rows_b2f_kernel(const bf16* src, long lds, const int* idx, long n, int D, float* dst, long ldd) {
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n * (D / 8)) return;
+  const long i = t / (D / 8);
+  const int c = (t % (D / 8)) * 8;
+  const bf16x8 v = *reinterpret_cast<const bf16x8*>(src + (long)idx[i] * lds + c);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) dst[i * ldd + c + j] = (float)v[j];
+}
+
+// SwiGLU backward from an f32 d(act): dgu[m, f] = d*u*silu'(g), dgu[m, F+f] = d*silu(g)
+__global__ void swiglu_bwd_kernel(const float* dact, long ldd, const bf16* gu, long ldgu, bf16* dgu, long lddgu, long M, int F) {
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= M * (F / 8)) return;
+  const long m = idx / (F / 8);
+  const int f = (idx % (F / 8)) * 8;
+  const bf16x8 g = *reinterpret_cast<const bf16x8*>(gu + m * ldgu + f);
+  const bf16x8 u = *reinterpret_cast<const bf16x8*>(gu + m * ldgu + F + f);
+  bf16x8 og, ou;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float d = dact[m * ldd + f + j], gv = (float)g[j], uv = (float)u[j];
+    og[j] = (bf16)(d * uv * silu_grad(gv));
+    ou[j] = (bf16)(d * silu(gv));
+  }
+  *reinterpret_cast<bf16x8*>(dgu + m * lddgu + f) = og;
+  *reinterpret_cast<bf16x8*>(dgu + m * lddgu + F + f) = ou;
+}
+
+// f32 rows -> bf16 rows (row strides), cols % 4 == 0
+__global__ void cast_rows_kernel(const float* src, long lds, bf16* dst, long ldd, long M, int N) {
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= M * (N / 4)) return;
+  const long m = t / (N / 4);
+  const int c = (t % (N / 4)) * 4;
+  const float4 v = *reinterpret_cast<const float4*>(src + m * lds + c);
+  bf16x4 o = {(bf16)v.x, (bf16)v.y, (bf16)v.z, (bf16)v.w};
+  *reinterpret_cast<bf16x4*>(dst + m * ldd + c) = o;
 }
 
 __global__ void cast_kernel(const float* src, bf16* dst, long n) {
@@ -547,7 +602,7 @@ int slx_loss_gscale(const float* dtotal, int nl, int nr, int ns, float* gs, slx_
   return 0;
 }
 
-int slx_sumsq(const float* g, int64_t n, float* out, int zero_first, slx_stream_t s) {
+int slx_sumsq(const float* g, int64_t n, float* out, int zero_first, slx_stream_t s) {  // out (+)= sum g^2
   hipStream_t st = (hipStream_t)s;
   if (zero_first) hipMemsetAsync(out, 0, sizeof(float), st);
   if (!n) return 0;
@@ -560,7 +615,7 @@ int slx_sumsq(const float* g, int64_t n, float* out, int zero_first, slx_stream_
 }
 
 int slx_adamw(float* p, const float* g, float* m, float* v, void* p_bf16, int64_t n, float lr, float beta1, float beta2,
-              float eps, float weight_decay, int step, const float* sumsq, float max_norm, slx_stream_t s) {
+              float eps, float weight_decay, int step, const float* sumsq, float max_norm, float grad_scale, slx_stream_t s) {
   SLX_CHECK_ARG(step >= 1, "slx_adamw: step >= 1");
   if (!n) return 0;
   const float bc1 = 1.f - powf(beta1, (float)step);
@@ -568,8 +623,39 @@ int slx_adamw(float* p, const float* g, float* m, float* v, void* p_bf16, int64_
   long blocks = (n + 255) / 256;
   if (blocks > 8192) blocks = 8192;
   hipLaunchKernelGGL(adamw_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)s, p, g, m, v, (bf16*)p_bf16, n, lr,
-                     beta1, beta2, eps, weight_decay, bc1, bc2s, sumsq, max_norm);
+                     beta1, beta2, eps, weight_decay, bc1, bc2s, sumsq, max_norm, grad_scale);
   SLX_LAUNCH_CHECK("slx_adamw");
+  return 0;
+}
+
+int slx_scatter_rows(const float* src, int64_t lds, const int* idx, int64_t n, int D, float* dst, int64_t ldd, int accumulate, slx_stream_t s) {
+  SLX_CHECK_ARG(D % 4 == 0, "slx_scatter_rows: D %% 4");
+  if (!n) return 0;
+  hipLaunchKernelGGL(scatter_rows_kernel, g1(n * (D / 4)), dim3(256), 0, (hipStream_t)s, src, lds, idx, n, D, dst, ldd, accumulate);
+  SLX_LAUNCH_CHECK("slx_scatter_rows");
+  return 0;
+}
+
+int slx_gather_rows_b2f(const void* src, int64_t lds, const int* idx, int64_t n, int D, float* dst, int64_t ldd, slx_stream_t s) {
+  SLX_CHECK_ARG(D % 8 == 0 && lds % 8 == 0, "slx_gather_rows_b2f: D/lds %% 8");
+  if (!n) return 0;
+  hipLaunchKernelGGL(gather_rows_b2f_kernel, g1(n * (D / 8)), dim3(256), 0, (hipStream_t)s, (const bf16*)src, lds, idx, n, D, dst, ldd);
+  SLX_LAUNCH_CHECK("slx_gather_rows_b2f");
+  return 0;
+}
+
+int slx_swiglu_bwd(const float* dact, int64_t ldd, const void* gu, int64_t ldgu, void* dgu, int64_t lddgu, int64_t M, int F, slx_stream_t s) {
+  SLX_CHECK_ARG(F % 8 == 0 && ldgu % 8 == 0 && lddgu % 8 == 0, "slx_swiglu_bwd: F/ld %% 8");
+  hipLaunchKernelGGL(swiglu_bwd_kernel, g1(M * (F / 8)), dim3(256), 0, (hipStream_t)s, dact, ldd, (const bf16*)gu, ldgu, (bf16*)dgu, lddgu, M, F);
+  SLX_LAUNCH_CHECK("slx_swiglu_bwd");
+  return 0;
+}
+
+int slx_cast_rows(const float* src, int64_t lds, void* dst, int64_t ldd, int64_t M, int N, slx_stream_t s) {
+  SLX_CHECK_ARG(N % 4 == 0 && lds % 4 == 0 && ldd % 4 == 0, "slx_cast_rows: N/ld %% 4");
+  if (!M) return 0;
+  hipLaunchKernelGGL(cast_rows_kernel, g1(M * (N / 4)), dim3(256), 0, (hipStream_t)s, src, lds, (bf16*)dst, ldd, M, N);
+  SLX_LAUNCH_CHECK("slx_cast_rows");
   return 0;
 }
 

@@ -1,0 +1,207 @@
+"""Drop-in DrivingModel for the SimLingo VLA hot path on MI355X.
+
+Mirrors simlingo_training.models.driving.DrivingModel (simlingo_training/models/driving.py:40-732):
+same constructor (cfg_data_module, processor, cache_dir, **cfg with the Hydra keys of
+DrivingModelConfig, config.py:75-104), same methods forward_loss / training_step / forward /
+configure_optimizers, same TrainingOutput. The arithmetic of forward_loss + backward is one
+VLAEngine step (HIP kernels); autograd sees a single node so `loss.backward()` from Lightning (or a
+plain loop) runs the hand-written backward, which also launches the bucketed RCCL all-reduce.
+Subclasses pytorch_lightning.LightningModule when Lightning is installed, nn.Module otherwise.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+from torch import nn
+
+from .config import VLAConfig, full_config, tiny_config
+from .plan import plan_from_example
+from .types import TrainingOutput
+
+try:  # Lightning is optional (absent in this image); the surface is the same either way
+    import pytorch_lightning as _pl
+    _Base = _pl.LightningModule
+except Exception:  # pragma: no cover - depends on the environment
+    _Base = nn.Module
+
+
+def _get(obj, key, default=None):
+    if obj is None:
+        return default
+    if isinstance(obj, dict):
+        return obj.get(key, default)
+    return getattr(obj, key, default)
+
+
+def geometry_for(variant: str, **overrides) -> VLAConfig:
+    """InternVL2 variant string (config.py:42,65) -> kernel geometry."""
+    v = (variant or "").lower()
+    if "internvl2-1b" in v:
+        return full_config(**overrides)
+    if v in ("tiny", "simlingo-tiny"):
+        return tiny_config(**overrides)
+    raise ValueError(f"Unknown variant {variant}")  # same error type as vlm.py:24-25 / llm.py:94-95
+
+
+class _VLAStep(torch.autograd.Function):
+    """One autograd node for the whole hot path: forward = VLAEngine.forward, backward = VLAEngine.backward."""
+
+    @staticmethod
+    def forward(ctx, anchor, model, example, plan, dplan):
+        eng = model.engine
+        dev = eng.device
+        di, lab = example.driving_input, example.driving_label
+        out4, rp, sp = eng.forward(di.camera_images.to(dev, non_blocking=True), plan, dplan,
+                                   lab.path.to(dev, non_blocking=True), lab.waypoints.to(dev, non_blocking=True),
+                                   training=model.training)
+        ctx.model = model
+        model._last_predictions = {"route": rp, "speed_wps": sp}
+        return out4
+
+    @staticmethod
+    def backward(ctx, dout4):
+        ctx.model.engine.backward(dout4)
+        return None, None, None, None, None
+
+
+class DrivingModel(_Base):
+    def __init__(self, cfg_data_module=None, processor=None, cache_dir=None, **cfg):
+        super().__init__()
+        for key, value in cfg.items():   # driving.py:51-52
+            setattr(self, key, value)
+        self.cfg_data_module = cfg_data_module
+        self.processor = processor
+        self.cache_dir = cache_dir
+        vm = cfg.get("vision_model", {"variant": "OpenGVLab/InternVL2-1B"})
+        lm = cfg.get("language_model", {"variant": "OpenGVLab/InternVL2-1B"})
+        if _get(vm, "freeze", False):
+            raise NotImplementedError("vision_model.freeze=True is not on the MI355X hot path yet")
+        if _get(cfg, "speed_wps_mode", "2d") != "2d" or not _get(cfg, "predict_route_as_wps", True):
+            raise NotImplementedError("MI355X hot path implements speed_wps_mode='2d', predict_route_as_wps=True")
+        over = dict(lora=bool(_get(lm, "lora", True)), lora_r=int(_get(lm, "lora_r", 32)),
+                    lora_alpha=int(_get(lm, "lora_alpha", 64)), lora_dropout=float(_get(lm, "lora_dropout", 0.1)),
+                    lr=float(cfg.get("lr", 3e-5)), weight_decay=float(cfg.get("weight_decay", 0.1)),
+                    betas=tuple(cfg.get("betas", (0.9, 0.999))), pct_start=float(cfg.get("pct_start", 0.05)))
+        if "grad_clip" in cfg:
+            over["grad_clip"] = float(cfg["grad_clip"])
+        self.vla_cfg = geometry_for(_get(lm, "variant", "OpenGVLab/InternVL2-1B"), **over)
+        self.seed = int(cfg.get("seed", 0))
+        self._init_params = cfg.get("init_params")  # optional {name: tensor} (tests, checkpoints)
+        self.anchor = nn.Parameter(torch.zeros(()))  # autograd anchor of the fused step
+        self.engine = None
+        self.hidden_size = self.vla_cfg.llm_dim
+        self._last_predictions = None
+
+    # ---- device placement ----------------------------------------------------------------------
+    def build_engine(self, device=None):
+        from .engine import VLAEngine
+        if self.engine is None:
+            dev = torch.device(device) if device is not None else (
+                torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu"))
+            self.engine = VLAEngine(self.vla_cfg, dev, params=self._init_params, seed=self.seed)
+            self._maybe_distributed()
+        return self.engine
+
+    def _maybe_distributed(self):
+        import torch.distributed as dist
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            dist.broadcast(self.engine.master, src=0)
+            self.engine.wbf.copy_(self.engine.master.to(torch.bfloat16))
+            self.engine._refresh_derived()
+            self.engine.set_distributed(None, dist.get_world_size())
+
+    # ---- reference surface ----------------------------------------------------------------------
+    def forward_loss(self, example, per_sample: bool = False):
+        """driving.py:236-261 -> (TrainingOutput, loss_logs) or (loss_dict, pred_labels)."""
+        eng = self.build_engine()
+        plan = plan_from_example(self.vla_cfg, example)
+        dplan = plan.to_device(eng.device)
+        out4 = _VLAStep.apply(self.anchor, self, example, plan, dplan)
+        sv_counts = {"language_loss": torch.full((1,), plan.loss_pos.shape[0]),
+                     "route_loss": torch.full((1,), plan.B * self.vla_cfg.n_route),
+                     "speed_wps_loss": torch.full((1,), plan.B * self.vla_cfg.n_speed)}
+        averages = {"language_loss": out4[1], "route_loss": out4[2], "speed_wps_loss": out4[3]}
+        preds = self._last_predictions
+        if per_sample:
+            return averages, {"route_prediction": preds["route"], "speed_wps_prediction": preds["speed_wps"]}
+        out = TrainingOutput(loss=out4[0], loss_averages=averages, loss_values=averages, loss_counts=sv_counts)
+        return out, {}
+
+    def training_step(self, batch, _batch_idx: int = 0):
+        """driving.py:263-271 (logging through Lightning when present; sync_dist scalars dropped)."""
+        output, _ = self.forward_loss(batch)
+        if _Base is not nn.Module:
+            self.log("train/loss", output.loss.detach(), on_step=True, prog_bar=True, logger=True)
+        return {"loss": output.loss, "outputs": output}
+
+    @torch.no_grad()
+    def forward(self, example, return_language: Optional[bool] = None, prompt_ids=None):
+        """driving.py:104-187 with predict_language=False: one forward, driving predictions only.
+        Returns (speed_wps [B,10,2], route [B,20,2], language=[]). (Greedy text decode: next row.)"""
+        eng = self.build_engine()
+        plan = plan_from_example(self.vla_cfg, example, inference=True)
+        dplan = plan.to_device(eng.device)
+        di = example.driving_input if hasattr(example, "driving_input") else example
+        B = di.camera_images.shape[0]
+        lab = getattr(example, "driving_label", None)
+        zeros_p = torch.zeros(B, self.vla_cfg.n_route, 2, device=eng.device)
+        zeros_s = torch.zeros(B, self.vla_cfg.n_speed, self.vla_cfg.speed_dims, device=eng.device)
+        path = lab.path.to(eng.device) if lab is not None else zeros_p
+        wps = lab.waypoints.to(eng.device) if lab is not None else zeros_s
+        _, rp, sp = eng.forward(di.camera_images.to(eng.device), plan, dplan, path, wps, training=False)
+        eng.saved = None
+        return sp, rp, []
+
+    def configure_optimizers(self):
+        """driving.py:718-732: AdamW(lr, weight_decay, betas) + OneCycleLR(interval='step')."""
+        eng = self.build_engine()
+        opt = FusedAdamW(self, lr=self.vla_cfg.lr, betas=self.vla_cfg.betas, weight_decay=self.vla_cfg.weight_decay,
+                         eps=self.vla_cfg.eps, max_norm=self.vla_cfg.grad_clip)
+        trainer = getattr(self, "_trainer", None)
+        max_steps = getattr(self, "max_steps", None) or (
+            getattr(trainer, "max_steps", -1) if trainer is not None else -1)
+        if max_steps is None or max_steps <= 0:
+            max_steps = int(getattr(trainer, "estimated_stepping_batches", 10000) or 10000) if trainer is not None else 10000
+        sched = torch.optim.lr_scheduler.OneCycleLR(opt, max_lr=self.vla_cfg.lr, total_steps=int(max_steps),
+                                                    pct_start=self.vla_cfg.pct_start)
+        return {"optimizer": opt, "lr_scheduler": {"scheduler": sched, "frequency": 1, "interval": "step"}}
+
+    # ---- parameters (reference key names) ------------------------------------------------------
+    def vla_state_dict(self):
+        """{internal name: fp32/bf16 tensor} of the engine's parameters."""
+        eng = self.build_engine()
+        out = {k: v for k, v in eng.P.items()}
+        for k, v in eng.W.items():
+            if k not in out:
+                out[k] = v
+        return out
+
+
+class FusedAdamW(torch.optim.Optimizer):
+    """torch.optim.AdamW semantics (decoupled weight decay on every parameter, as driving.py:719 uses
+    self.parameters()) + global-norm clipping (train.py:206 gradient_clip_val=0.3), executed as one
+    HIP kernel over the engine's flat fp32 master buffer. param_groups carry lr/betas so
+    OneCycleLR (with its beta1 cycling) drives it exactly like the reference's optimizer."""
+
+    def __init__(self, model: DrivingModel, lr=3e-5, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.1, max_norm=0.3):
+        super().__init__([model.anchor], dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
+        self.model = model
+        self.max_norm = max_norm
+        self.step_count = 0
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        g = self.param_groups[0]
+        self.step_count += 1
+        self.model.engine.adamw_step(g["lr"], self.step_count, betas=g["betas"], eps=g["eps"],
+                                     weight_decay=g["weight_decay"], max_norm=self.max_norm)
+        return loss
+
+    def zero_grad(self, set_to_none: bool = True):
+        # gradients are overwritten by every backward (no accumulation across steps)
+        self.model.anchor.grad = None

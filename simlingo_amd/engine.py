@@ -1,0 +1,637 @@
+"""VLA training-step engine: the SimLingo hot path as an explicit sequence of gfx950 HIP kernels.
+
+One step = InternViT (24 blocks) -> pixel_shuffle + mlp1 -> token assembly -> Qwen2 (24 blocks, LoRA)
+-> final RMSNorm -> LM head on the loss rows + driving heads -> losses, then the hand-written backward.
+It replaces, as one unit, DrivingModel.forward_loss (simlingo_training/models/driving.py:236-261)
+and the autograd backward Lightning/DeepSpeed run after it.
+
+Memory layout (sized for 288 GB HBM3E; no activation recompute):
+  * trainable parameters live in ONE flat f32 master buffer in backward-completion order
+    (param_specs), mirrored by a flat bf16 working copy (GEMM operands) and a flat f32 gradient
+    buffer, so the optimizer is a single kernel and gradient buckets are contiguous ranges;
+  * frozen Qwen2 weights are bf16 only (q/k/v and gate/up stored fused), 1-D frozen params f32;
+  * residual streams are f32, GEMM operands and saved activations bf16, token-major everywhere
+    (attention reads the fused QKV GEMM output in place).
+All arithmetic is in libslx_hip.so; torch only allocates and supplies the stream.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+from . import kernels as K
+from .config import VLAConfig
+from .params import LORA_SITES, lora_io, param_specs
+from .plan import Plan
+
+BF16, F32 = torch.bfloat16, torch.float32
+ALIGN = 64  # elements; keeps every parameter view 256-B aligned
+
+
+def _pad8(n):
+    return (n + 7) // 8 * 8
+
+
+@dataclass
+class Bucket:
+    start: int
+    end: int
+    groups: list
+    handle: object = None
+
+
+class VLAEngine:
+    def __init__(self, cfg: VLAConfig, device, params: dict[str, torch.Tensor] | None = None, seed: int = 0,
+                 bucket_bytes: int = 32 << 20):
+        from .params import init_params
+        self.cfg = cfg
+        self.device = torch.device(device)
+        if self.device.type != "cuda":
+            raise RuntimeError("VLAEngine runs on the MI355X (HIP) only; there is no CPU path")
+        K.lib()  # fail loudly if the HIP library is missing
+        params = params if params is not None else init_params(cfg, seed)
+        self.specs = param_specs(cfg)
+        # ---- flat trainable storage ----
+        offs, off = {}, 0
+        for s in self.specs:
+            if s.trainable:
+                offs[s.name] = off
+                off += (math.prod(s.shape) + ALIGN - 1) // ALIGN * ALIGN
+        self.n_flat = off
+        dev = self.device
+        self.master = torch.zeros(off, dtype=F32, device=dev)
+        self.grad = torch.zeros(off, dtype=F32, device=dev)
+        self.wbf = torch.zeros(off, dtype=BF16, device=dev)
+        self.P, self.G, self.W = {}, {}, {}
+        self.offsets = offs
+        for s in self.specs:
+            n = math.prod(s.shape)
+            if s.trainable:
+                o = offs[s.name]
+                self.P[s.name] = self.master[o:o + n].view(s.shape)
+                self.G[s.name] = self.grad[o:o + n].view(s.shape)
+                self.W[s.name] = self.wbf[o:o + n].view(s.shape)
+                self.P[s.name].copy_(params[s.name].to(dev))
+            else:
+                t = params[s.name].to(dev)
+                if len(s.shape) == 1:
+                    self.P[s.name] = t.float().contiguous()
+                else:
+                    self.W[s.name] = t.to(BF16).contiguous()
+        self.wbf.copy_(self.master.to(BF16))
+        # LM head padded to a multiple of 8 rows (its dgrad GEMM reads K = V rows as [K][N])
+        V, d = cfg.vocab, cfg.llm_dim
+        self.Vp = _pad8(V)
+        if self.Vp != V:
+            lm = torch.zeros(self.Vp, d, dtype=BF16, device=dev)
+            lm[:V].copy_(self.W["llm.lm_head"])
+            self.W["llm.lm_head"] = lm
+        # patch-embedding weight padded to K = kpad columns for the im2col GEMM
+        self.wpatch = torch.zeros(cfg.vit_dim, cfg.patch_kpad, dtype=BF16, device=dev)
+        self._refresh_derived()
+        self.ones_d = torch.ones(d, dtype=F32, device=dev)
+        # contiguity needed by the assembly kernel: the 30 query rows are one [30, d] block
+        qr, qs = offs["drv.query_route"], offs["drv.query_speed"]
+        assert qs == qr + cfg.n_route * d, "query parameters must be adjacent"
+        # ---- gradient buckets (contiguous ranges, backward-completion order) ----
+        self.group_ranges = {}
+        for s in self.specs:
+            if not s.trainable:
+                continue
+            o = offs[s.name]
+            e = o + (math.prod(s.shape) + ALIGN - 1) // ALIGN * ALIGN
+            a, b = self.group_ranges.get(s.group, (o, e))
+            self.group_ranges[s.group] = (min(a, o), max(b, e))
+        order = sorted(self.group_ranges, key=lambda g: self.group_ranges[g][0])
+        self.buckets: list[Bucket] = []
+        cur = None
+        for g in order:
+            a, b = self.group_ranges[g]
+            if cur is None or (cur.end - cur.start) * 4 >= bucket_bytes or cur.end != a:
+                cur = Bucket(a, b, [g])
+                self.buckets.append(cur)
+            else:
+                cur.end = b
+                cur.groups.append(g)
+        self.group_bucket = {g: bk for bk in self.buckets for g in bk.groups}
+        self.dist_pg = None
+        self.world = 1
+        self.step_seed = 0
+        self.saved = None
+        self._cos_sin = {}
+        self.probe_site = None     # name of a call site to bracket with HIP events (bench roofline)
+        self.probe_events = []
+
+    def _probe(self, site):
+        """Context manager: HIP events around one call site on the current stream (bench.py)."""
+        eng = self
+
+        class _P:
+            def __enter__(self):
+                if eng.probe_site == site:
+                    self.e0 = torch.cuda.Event(enable_timing=True)
+                    self.e0.record()
+                return self
+
+            def __exit__(self, *a):
+                if eng.probe_site == site:
+                    e1 = torch.cuda.Event(enable_timing=True)
+                    e1.record()
+                    eng.probe_events.append((self.e0, e1))
+                return False
+        return _P()
+
+    # ------------------------------------------------------------------------------------------
+    def _refresh_derived(self):
+        """bf16 views that are not plain slices of the flat buffer (after every optimizer step)."""
+        cfg = self.cfg
+        self.wpatch[:, : cfg.patch_k].copy_(self.W["vit.patch.w"])
+
+    def set_distributed(self, pg=None, world: int = 1):
+        self.dist_pg = pg
+        self.world = world
+
+    def _group_done(self, g):
+        if self.world <= 1:
+            return
+        bk = self.group_bucket[g]
+        bk.groups_done = getattr(bk, "groups_done", 0) + 1
+        if bk.groups_done == len(bk.groups):
+            import torch.distributed as dist
+            bk.handle = dist.all_reduce(self.grad[bk.start:bk.end], group=self.dist_pg, async_op=True)
+
+    def wait_grads(self):
+        for bk in self.buckets:
+            if bk.handle is not None:
+                bk.handle.wait()
+                bk.handle = None
+            bk.groups_done = 0
+
+    def rope_tables(self, S):
+        if S not in self._cos_sin:
+            self._cos_sin[S] = K.rope_tables(S, self.cfg.rope_theta, self.device)
+        return self._cos_sin[S]
+
+    # ------------------------------------------------------------------------------------------
+    # helpers
+    def _e(self, *shape, dtype=BF16):
+        return torch.empty(*shape, dtype=dtype, device=self.device)
+
+    def _z(self, *shape, dtype=F32):
+        return torch.zeros(*shape, dtype=dtype, device=self.device)
+
+    def _norm(self, x, gamma, beta, rows, D, eps, rms=False, ps=0, tpi=0, ldx=None):
+        y = self._e(rows, D)
+        mean = None if rms else self._e(rows, dtype=F32)
+        rstd = self._e(rows, dtype=F32)
+        d = K.norm_desc(x, gamma, beta, y, mean, rstd, rows, D, eps, rms=rms, ps_grid=ps, tok_per_img=tpi, ldx=ldx)
+        K.norm_fwd(d)
+        return y, d
+
+    def _ws(self, nfloats):
+        if getattr(self, "_wsbuf", None) is None or self._wsbuf.numel() < nfloats:
+            self._wsbuf = self._e(max(nfloats, 1 << 20), dtype=F32)
+        return self._wsbuf
+
+    def _colsum(self, x, out, mode):
+        M, N = x.shape
+        ws = self._ws(K.lib().slx_colsum_ws_floats(N))
+        K.call("slx_colsum", mode, K.P(x), x.stride(0), M, N, K.P(out), 0, K.P(ws), K.stream_ptr())
+
+    # ==========================================================================================
+    # forward
+    def forward(self, pix: torch.Tensor, plan: Plan, dplan: dict, path: torch.Tensor, waypoints: torch.Tensor,
+                training: bool = True):
+        cfg = self.cfg
+        sv = {}
+        B = plan.B
+        pix = pix.reshape(-1, 3, cfg.img_size, cfg.img_size)
+        if pix.dtype != F32 or not pix.is_contiguous():
+            pix = pix.float().contiguous()
+        N = pix.shape[0]
+        self.step_seed += 1
+        sv["seed"] = self.step_seed * 1000003
+        sv["drop"] = cfg.lora_dropout if (training and cfg.lora) else 0.0
+        sv["N"], sv["B"] = N, B
+        # ---------------- InternViT ----------------
+        D, T, F_, H = cfg.vit_dim, cfg.vit_tokens, cfg.vit_ffn, cfg.vit_heads
+        g = cfg.vit_grid
+        Mv = N * T
+        col = self._e(N * g * g, cfg.patch_kpad)
+        K.call("slx_im2col_patch", K.P(pix), N, cfg.img_size, cfg.img_size, cfg.patch, cfg.patch_kpad, K.P(col), K.stream_ptr())
+        pe = self._e(N * g * g, D, dtype=F32)
+        K.mm(col, self.wpatch, pe, bias=self.P["vit.patch.b"])
+        x = self._e(Mv, D, dtype=F32)
+        K.call("slx_vit_embed_fwd", K.P(pe), K.P(self.P["vit.cls"]), K.P(self.P["vit.pos"]), K.P(x), N, T, D, K.stream_ptr())
+        sv["col"] = col
+        vit_saved = []
+        for i in range(cfg.vit_layers):
+            p = f"vit.{i}."
+            h1, n1 = self._norm(x, self.P[p + "ln1.w"], self.P[p + "ln1.b"], Mv, D, cfg.vit_eps)
+            qkv = self._e(Mv, 3 * D)
+            K.mm(h1, self.W[p + "qkv.w"], qkv, bias=self.P[p + "qkv.b"])
+            o = self._e(Mv, D)
+            lse = self._e(N * H * T, dtype=F32)
+            with self._probe("vit.attn"):
+                K.attn_fwd(qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], o, lse, B=N, S=T, Hq=H, Hkv=H, causal=False)
+            xm = self._e(Mv, D, dtype=F32)
+            y1 = self._e(Mv, D)
+            K.mm(o, self.W[p + "proj.w"], xm, bias=self.P[p + "proj.b"], epi=K.EPI_RESID_LS, resid=x, ldr=D,
+                 ls=self.P[p + "ls1"], aux_out=y1, ldaux_out=D)
+            h2, n2 = self._norm(xm, self.P[p + "ln2.w"], self.P[p + "ln2.b"], Mv, D, cfg.vit_eps)
+            hpre = self._e(Mv, F_)
+            hact = self._e(Mv, F_)
+            with self._probe("vit.fc1"):
+                K.mm(h2, self.W[p + "fc1.w"], hact, bias=self.P[p + "fc1.b"], epi=K.EPI_GELU, aux_out=hpre, ldaux_out=F_)
+            xo = self._e(Mv, D, dtype=F32)
+            y2 = self._e(Mv, D)
+            K.mm(hact, self.W[p + "fc2.w"], xo, bias=self.P[p + "fc2.b"], epi=K.EPI_RESID_LS, resid=xm, ldr=D,
+                 ls=self.P[p + "ls2"], aux_out=y2, ldaux_out=D)
+            vit_saved.append(dict(x=x, h1=h1, n1=n1, qkv=qkv, o=o, lse=lse, y1=y1, xm=xm, h2=h2, n2=n2, hpre=hpre,
+                                  hact=hact, y2=y2))
+            x = xo
+        sv["vit"] = vit_saved
+        sv["vit_out"] = x
+        # ---------------- pixel_shuffle + mlp1 ----------------
+        d = cfg.llm_dim
+        Mi = N * cfg.img_tokens_per_tile
+        z, nz = self._norm(x, self.P["proj.ln.w"], self.P["proj.ln.b"], Mi, 4 * D, cfg.proj_eps, ps=g, tpi=T, ldx=D)
+        a1pre = self._e(Mi, d)
+        a1 = self._e(Mi, d)
+        K.mm(z, self.W["proj.fc1.w"], a1, bias=self.P["proj.fc1.b"], epi=K.EPI_GELU, aux_out=a1pre, ldaux_out=d)
+        img = self._e(Mi, d)
+        K.mm(a1, self.W["proj.fc2.w"], img, bias=self.P["proj.fc2.b"])
+        sv.update(z=z, nz=nz, a1pre=a1pre, a1=a1)
+        # ---------------- waypoint encoder (placeholder coords) ----------------
+        nwp = plan.wp_coords.shape[0]
+        wp_out = self._e(max(nwp, 1), d, dtype=F32)
+        if nwp:
+            c = dplan["wp_coords"]
+            w1pre = self._e(nwp, cfg.wp_hidden, dtype=F32)
+            w1 = self._e(nwp, cfg.wp_hidden, dtype=F32)
+            K.sgemm(c, 2, 1, self.P["wp.0.w"], 1, 2, w1, cfg.wp_hidden, 1, nwp, cfg.wp_hidden, 2, bias=self.P["wp.0.b"],
+                    act=K.ACT_RELU, pre=w1pre, ldpre=cfg.wp_hidden)
+            w2pre = self._e(nwp, cfg.wp_hidden2, dtype=F32)
+            w2 = self._e(nwp, cfg.wp_hidden2, dtype=F32)
+            K.sgemm(w1, cfg.wp_hidden, 1, self.P["wp.1.w"], 1, cfg.wp_hidden, w2, cfg.wp_hidden2, 1, nwp, cfg.wp_hidden2,
+                    cfg.wp_hidden, bias=self.P["wp.1.b"], act=K.ACT_RELU, pre=w2pre, ldpre=cfg.wp_hidden2)
+            K.sgemm(w2, cfg.wp_hidden2, 1, self.P["wp.2.w"], 1, cfg.wp_hidden2, wp_out, d, 1, nwp, d, cfg.wp_hidden2,
+                    bias=self.P["wp.2.b"])
+            sv.update(w1pre=w1pre, w1=w1, w2pre=w2pre, w2=w2)
+        # ---------------- token assembly ----------------
+        S = plan.S
+        Ml = B * S
+        X = self._e(Ml, d, dtype=F32)
+        K.call("slx_assemble_tokens", K.P(dplan["code"]), Ml, d, K.P(self.W["llm.embed"]), cfg.vocab, K.P(img),
+               K.P(wp_out), K.P(self.P["drv.query_route"]), K.P(X), K.stream_ptr())
+        # ---------------- Qwen2 + LoRA ----------------
+        Hq, Hk, Fl = cfg.llm_heads, cfg.llm_kv_heads, cfg.llm_ffn
+        qn, kn = Hq * 64, Hk * 64
+        nqkv = qn + 2 * kn
+        cos, sin = self.rope_tables(S)
+        seql = dplan["seqlens"]
+        llm_saved = []
+        for i in range(cfg.llm_layers):
+            p = f"llm.{i}."
+            L = {}
+            h, nrm1 = self._norm(X, self.P[p + "ln1"], None, Ml, d, cfg.rms_eps, rms=True)
+            qkv = self._e(Ml, nqkv)
+            K.mm(h, self.W[p + "qkv_w"], qkv, bias=self.P[p + "qkv_b"])
+            if cfg.lora:
+                for site, c0, c1 in (("q", 0, qn), ("k", qn, qn + kn), ("v", qn + kn, nqkv)):
+                    L[site] = self._lora_fwd(h, i, site, qkv[:, c0:c1], sv, d)
+            K.rope(qkv, Ml, S, Hq + Hk, cos, sin)  # q and k heads are the first Hq+Hk head slots
+            o = self._e(Ml, qn)
+            lse = self._e(B * Hq * S, dtype=F32)
+            K.attn_fwd(qkv[:, :qn], qkv[:, qn:qn + kn], qkv[:, qn + kn:], o, lse, B=B, S=S, Hq=Hq, Hkv=Hk, causal=True,
+                       seqlens=seql)
+            Xm = self._e(Ml, d, dtype=F32)
+            K.mm(o, self.W[p + "o_w"], Xm, epi=K.EPI_RESID_LS, resid=X, ldr=d, ls=self.ones_d)
+            if cfg.lora:
+                L["o"] = self._lora_fwd(o, i, "o", Xm, sv, qn)
+            h2, nrm2 = self._norm(Xm, self.P[p + "ln2"], None, Ml, d, cfg.rms_eps, rms=True)
+            gu = self._e(Ml, 2 * Fl)
+            K.mm(h2, self.W[p + "gate_up_w"], gu)
+            if cfg.lora:
+                L["gate"] = self._lora_fwd(h2, i, "gate", gu[:, :Fl], sv, d)
+                L["up"] = self._lora_fwd(h2, i, "up", gu[:, Fl:], sv, d)
+            act = self._e(Ml, Fl)
+            K.call("slx_swiglu_fwd", K.P(gu), gu.stride(0), K.P(act), act.stride(0), Ml, Fl, K.stream_ptr())
+            Xo = self._e(Ml, d, dtype=F32)
+            K.mm(act, self.W[p + "down_w"], Xo, epi=K.EPI_RESID_LS, resid=Xm, ldr=d, ls=self.ones_d)
+            if cfg.lora:
+                L["down"] = self._lora_fwd(act, i, "down", Xo, sv, Fl)
+            llm_saved.append(dict(X=X, h=h, n1=nrm1, qkv=qkv, o=o, lse=lse, Xm=Xm, h2=h2, n2=nrm2, gu=gu, act=act,
+                                  lora=L))
+            X = Xo
+        sv["llm"] = llm_saved
+        feat, nf = self._norm(X, self.P["llm.norm"], None, Ml, d, cfg.rms_eps, rms=True)
+        sv.update(X_last=X, feat=feat, nf=nf)
+        # ---------------- language loss rows ----------------
+        R = plan.loss_pos.shape[0]
+        ce_loss = self._e(max(R, 1), dtype=F32)
+        if R:
+            fl = self._e(R, d)
+            K.call("slx_gather_rows_bf16", K.P(feat), d, K.P(dplan["loss_pos"]), R, d, K.P(fl), d, K.stream_ptr())
+            logits = self._e(R, self.Vp, dtype=F32)
+            K.mm(fl, self.W["llm.lm_head"][: cfg.vocab], logits)
+            lse_ce = self._e(R, dtype=F32)
+            K.call("slx_ce_fwd", K.P(logits), self.Vp, K.P(dplan["loss_labels"]), R, cfg.vocab, K.P(ce_loss),
+                   K.P(lse_ce), K.stream_ptr())
+            sv.update(fl=fl, logits=logits, lse_ce=lse_ce)
+        # ---------------- driving heads ----------------
+        nr, ns = cfg.n_route, cfg.n_speed
+        qpos = dplan["query_pos"].view(B, cfg.n_queries)
+        rpos = qpos[:, :nr].contiguous().view(-1)
+        spos = qpos[:, nr:].contiguous().view(-1)
+        m = cfg.head_mlp
+        fr = self._e(B * nr, d, dtype=F32)
+        fs = self._e(B * ns, d, dtype=F32)
+        K.call("slx_gather_rows_b2f", K.P(feat), d, K.P(rpos), B * nr, d, K.P(fr), d, K.stream_ptr())
+        K.call("slx_gather_rows_b2f", K.P(feat), d, K.P(spos), B * ns, d, K.P(fs), d, K.stream_ptr())
+        hd = self._mlp_fwd(fr, [("route.0", 2 * m, K.ACT_SILU), ("route.1", m, K.ACT_SILU), ("route.2", 2, K.ACT_NONE)])
+        sd_ = self._mlp_fwd(fs, [("speed.0", m, K.ACT_SILU), ("speed.1", cfg.speed_dims, K.ACT_NONE)])
+        route_pred = self._e(B, nr, 2, dtype=F32)
+        route_loss = self._e(B * nr, dtype=F32)
+        lab_r = path.float().contiguous()
+        lab_s = waypoints[:, : nr + 1].float().contiguous()
+        K.call("slx_wp_loss_fwd", K.P(hd[0][0]), K.P(lab_r), B, nr, 2, K.P(route_pred), K.P(route_loss), K.stream_ptr())
+        speed_pred = self._e(B, ns, cfg.speed_dims, dtype=F32)
+        speed_loss = self._e(B * ns, dtype=F32)
+        K.call("slx_wp_loss_fwd", K.P(sd_[0][0]), K.P(lab_s), B, ns, cfg.speed_dims, K.P(speed_pred), K.P(speed_loss),
+               K.stream_ptr())
+        out4 = self._e(4, dtype=F32)
+        K.call("slx_loss_finalize", K.P(ce_loss), R, K.P(route_loss), B * nr, K.P(speed_loss), B * ns, K.P(out4),
+               K.stream_ptr())
+        sv.update(plan=plan, dplan=dplan, rpos=rpos, spos=spos, fr=fr, fs=fs, hd=hd, sd=sd_, lab_r=lab_r, lab_s=lab_s,
+                  route_pred=route_pred, speed_pred=speed_pred, R=R, nwp=nwp, S=S, Ml=Ml, Mi=Mi, Mv=Mv,
+                  ce_loss=ce_loss, route_loss=route_loss, speed_loss=speed_loss)
+        self.saved = sv
+        return out4, route_pred, speed_pred
+
+    def _lora_fwd(self, x, i, site, out, sv, kin):
+        """out (+)= s * (drop(x) A^T) B^T; returns saved (t, xd, seed)."""
+        cfg = self.cfg
+        p = f"llm.{i}.lora.{site}."
+        M = x.shape[0]
+        seed = sv["seed"] + 131 * i + 7 * LORA_SITES.index(site) + 1
+        xd = x
+        if sv["drop"] > 0:
+            xd = self._e(M, kin)
+            K.call("slx_dropout", K.P(x), x.stride(0), K.P(xd), kin, M, kin, seed, sv["drop"], kin, K.stream_ptr())
+        t = self._e(M, cfg.lora_r)
+        K.mm(xd, self.W[p + "a"], t)
+        K.mm(t, self.W[p + "b"], out, alpha=cfg.lora_scale, accumulate=True)
+        return (t, xd, seed)
+
+    def _mlp_fwd(self, x, layers):
+        """driving head: list of (prefix, out_dim, act) -> saved [(out, pre, in)]"""
+        saved = []
+        h = x
+        M = x.shape[0]
+        for pre_name, n, act in layers:
+            kin = h.shape[1]
+            out = self._e(M, n, dtype=F32)
+            pre = self._e(M, n, dtype=F32) if act != K.ACT_NONE else None
+            bias = self.P.get(pre_name + ".b")
+            K.sgemm(h, kin, 1, self.P[pre_name + ".w"], 1, kin, out, n, 1, M, n, kin, bias=bias, act=act, pre=pre,
+                    ldpre=n)
+            saved.append((out, pre, h, pre_name, act))
+            h = out
+        saved.reverse()
+        return saved
+
+    # ==========================================================================================
+    # backward
+    def backward(self, dlosses: torch.Tensor | None = None):
+        cfg = self.cfg
+        sv = self.saved
+        assert sv is not None, "backward() without forward()"
+        B, S, Ml, Mv, Mi, R = sv["B"], sv["S"], sv["Ml"], sv["Mv"], sv["Mi"], sv["R"]
+        d, D = cfg.llm_dim, cfg.vit_dim
+        nr, ns = cfg.n_route, cfg.n_speed
+        dplan = sv["dplan"]
+        gs = self._e(3, dtype=F32)
+        if dlosses is not None:
+            dlosses = dlosses.float().contiguous()
+        K.call("slx_loss_gscale", K.P(dlosses), R, B * nr, B * ns, K.P(gs), K.stream_ptr())
+        # ---------------- driving heads ----------------
+        dfeat = self._z(Ml + 1, d)  # + one zero row for unreferenced gathers
+        for tag, npts, dims, saved, lab, pos in (("route", nr, 2, sv["hd"], sv["lab_r"], sv["rpos"]),
+                                                 ("speed", ns, cfg.speed_dims, sv["sd"], sv["lab_s"], sv["spos"])):
+            dout = self._e(B * npts, dims, dtype=F32)
+            pred = sv["route_pred"] if tag == "route" else sv["speed_pred"]
+            K.call("slx_wp_loss_bwd", K.P(pred), K.P(lab), B, npts, dims, K.P(gs[1:2] if tag == "route" else gs[2:3]),
+                   K.P(dout), K.stream_ptr())
+            dx = self._mlp_bwd(dout, saved)
+            K.call("slx_scatter_rows", K.P(dx), d, K.P(pos), B * npts, d, K.P(dfeat), d, 1, K.stream_ptr())
+        self._group_done("heads")
+        # ---------------- language loss ----------------
+        if R:
+            dlog = self._e(R, self.Vp)
+            K.call("slx_ce_bwd", K.P(sv["logits"]), self.Vp, K.P(dplan["loss_labels"]), K.P(sv["lse_ce"]), R,
+                   cfg.vocab, K.P(gs[0:1]), K.P(dlog), self.Vp, K.stream_ptr())
+            dfl = self._e(R, d, dtype=F32)
+            K.mm(dlog, self.W["llm.lm_head"], dfl, tb=False)  # [R,Vp] @ [Vp,d]
+            K.call("slx_scatter_rows", K.P(dfl), d, K.P(dplan["loss_pos"]), R, d, K.P(dfeat), d, 1, K.stream_ptr())
+        # ---------------- final RMSNorm ----------------
+        dX = self._z(Ml + 1, d)
+        K.norm_bwd(sv["nf"], dfeat, dX)
+        # ---------------- Qwen2 layers ----------------
+        Hq, Hk, Fl = cfg.llm_heads, cfg.llm_kv_heads, cfg.llm_ffn
+        qn, kn = Hq * 64, Hk * 64
+        nqkv = qn + 2 * kn
+        cos, sin = self.rope_tables(S)
+        ws = K.attn_ws(B, S, Hq, Hk, self.device)
+        dxb = self._e(Ml, d)
+        for i in reversed(range(cfg.llm_layers)):
+            p = f"llm.{i}."
+            Ls = sv["llm"][i]
+            L = Ls["lora"]
+            # down projection (+LoRA): Xo = Xm + act Wd^T + s t_d B_d^T
+            K.call("slx_cast_rows", K.P(dX), d, K.P(dxb), d, Ml, d, K.stream_ptr())
+            dact = self._e(Ml, Fl, dtype=F32)
+            K.mm(dxb, self.W[p + "down_w"], dact, tb=False)
+            if cfg.lora:
+                self._lora_bwd(dxb, L["down"], i, "down", dact, sv)
+            dgu = self._e(Ml, 2 * Fl)
+            K.call("slx_swiglu_bwd", K.P(dact), Fl, K.P(Ls["gu"]), 2 * Fl, K.P(dgu), 2 * Fl, Ml, Fl, K.stream_ptr())
+            del dact
+            dh2 = self._e(Ml, d, dtype=F32)
+            K.mm(dgu, self.W[p + "gate_up_w"], dh2, tb=False)
+            if cfg.lora:
+                self._lora_bwd(dgu[:, :Fl], L["gate"], i, "gate", dh2, sv)
+                self._lora_bwd(dgu[:, Fl:], L["up"], i, "up", dh2, sv)
+            del dgu
+            K.norm_bwd(Ls["n2"], dh2, dX, dx_accumulate=True)
+            # o projection (+LoRA)
+            K.call("slx_cast_rows", K.P(dX), d, K.P(dxb), d, Ml, d, K.stream_ptr())
+            do = self._e(Ml, qn, dtype=F32)
+            K.mm(dxb, self.W[p + "o_w"], do, tb=False)
+            if cfg.lora:
+                self._lora_bwd(dxb, L["o"], i, "o", do, sv)
+            dob = self._e(Ml, qn)
+            K.call("slx_cast_rows", K.P(do), qn, K.P(dob), qn, Ml, qn, K.stream_ptr())
+            del do
+            qkv = Ls["qkv"]
+            dqkv = self._e(Ml, nqkv)
+            K.attn_bwd(qkv[:, :qn], qkv[:, qn:qn + kn], qkv[:, qn + kn:], Ls["o"], Ls["lse"], dob,
+                       dqkv[:, :qn], dqkv[:, qn:qn + kn], dqkv[:, qn + kn:], ws, rope_cos=cos, rope_sin=sin,
+                       B=B, S=S, Hq=Hq, Hkv=Hk, causal=True, seqlens=dplan["seqlens"])
+            dh = self._e(Ml, d, dtype=F32)
+            K.mm(dqkv, self.W[p + "qkv_w"], dh, tb=False)
+            if cfg.lora:
+                for site, c0, c1 in (("q", 0, qn), ("k", qn, qn + kn), ("v", qn + kn, nqkv)):
+                    self._lora_bwd(dqkv[:, c0:c1], L[site], i, site, dh, sv)
+            K.norm_bwd(Ls["n1"], dh, dX, dx_accumulate=True)
+            del dqkv, dh, dh2
+            if cfg.lora:
+                self._group_done(f"llm{i}")
+        # ---------------- token assembly backward ----------------
+        qg = self.G["drv.query_route"]  # [20, d] followed by [10, d] (adjacent)
+        K.call("slx_gather_sum", K.P(dX), d, K.P(dplan["query_pos"]), B, cfg.n_queries, d, K.P(qg), 0, K.stream_ptr())
+        nwp = sv["nwp"]
+        if nwp:
+            dwp = self._e(nwp, d, dtype=F32)
+            K.call("slx_gather_rows", K.P(dX), d, K.P(dplan["wp_pos"]), nwp, d, K.P(dwp), d, 0, K.stream_ptr())
+            saved = [(None, None, sv["w2"], "wp.2", K.ACT_NONE), (sv["w2"], sv["w2pre"], sv["w1"], "wp.1", K.ACT_RELU),
+                     (sv["w1"], sv["w1pre"], dplan["wp_coords"], "wp.0", K.ACT_RELU)]
+            self._mlp_bwd(dwp, saved, need_dx=False)
+        else:
+            for n in ("wp.0.w", "wp.0.b", "wp.1.w", "wp.1.b", "wp.2.w", "wp.2.b"):
+                self.G[n].zero_()
+        self._group_done("assembly")
+        dimg = self._e(Mi, d)
+        K.call("slx_gather_rows", K.P(dX), d, K.P(dplan["img_pos"]), Mi, d, K.P(dimg), d, 1, K.stream_ptr())
+        del dX, dfeat
+        # ---------------- mlp1 backward ----------------
+        K.mm(dimg, sv["a1"], self.G["proj.fc2.w"], ta=True, tb=False)
+        self._colsum(dimg, self.G["proj.fc2.b"], 0)
+        da1 = self._e(Mi, d)
+        K.mm(dimg, self.W["proj.fc2.w"], da1, tb=False, epi=K.EPI_GELU_BWD, aux=sv["a1pre"], ldaux=d)
+        K.mm(da1, sv["z"], self.G["proj.fc1.w"], ta=True, tb=False)
+        self._colsum(da1, self.G["proj.fc1.b"], 0)
+        dz = self._e(Mi, 4 * D, dtype=F32)
+        K.mm(da1, self.W["proj.fc1.w"], dz, tb=False)
+        T = cfg.vit_tokens
+        dxv = self._z(Mv, D)
+        ws_n = self._ws(K.norm_ws_floats(4 * D))
+        K.norm_bwd(sv["nz"], dz, dxv, dgamma=self.G["proj.ln.w"], dbeta=self.G["proj.ln.b"], ws=ws_n, lddx=D)
+        del dz, da1, dimg
+        self._group_done("proj")
+        # ---------------- InternViT layers ----------------
+        F_, H, N = cfg.vit_ffn, cfg.vit_heads, sv["N"]
+        vws = K.attn_ws(N, T, H, H, self.device)
+        g = self._e(Mv, D)
+        lnws = self._ws(max(K.norm_ws_floats(D), K.lib().slx_colsum_ws_floats(F_) + 0))
+        for i in reversed(range(cfg.vit_layers)):
+            p = f"vit.{i}."
+            Ls = sv["vit"][i]
+            # x_out = x_mid + ls2 * (fc2(gelu(fc1(ln2(x_mid)))) )
+            K.call("slx_ls_branch_bwd", K.P(dxv), D, K.P(self.P[p + "ls2"]), K.P(Ls["y2"]), D, K.P(g), D, Mv, D,
+                   K.P(self.G[p + "ls2"]), K.P(self.G[p + "fc2.b"]), 0, K.P(self._ws(2 * 256 * D)), K.stream_ptr())
+            K.mm(g, Ls["hact"], self.G[p + "fc2.w"], ta=True, tb=False)
+            dh = self._e(Mv, F_)
+            K.mm(g, self.W[p + "fc2.w"], dh, tb=False, epi=K.EPI_GELU_BWD, aux=Ls["hpre"], ldaux=F_)
+            K.mm(dh, Ls["h2"], self.G[p + "fc1.w"], ta=True, tb=False)
+            self._colsum(dh, self.G[p + "fc1.b"], 0)
+            dh2 = self._e(Mv, D, dtype=F32)
+            K.mm(dh, self.W[p + "fc1.w"], dh2, tb=False)
+            del dh
+            K.norm_bwd(Ls["n2"], dh2, dxv, dx_accumulate=True, dgamma=self.G[p + "ln2.w"], dbeta=self.G[p + "ln2.b"],
+                       ws=self._ws(K.norm_ws_floats(D)))
+            # x_mid = x_in + ls1 * proj(attn(ln1(x_in)))
+            K.call("slx_ls_branch_bwd", K.P(dxv), D, K.P(self.P[p + "ls1"]), K.P(Ls["y1"]), D, K.P(g), D, Mv, D,
+                   K.P(self.G[p + "ls1"]), K.P(self.G[p + "proj.b"]), 0, K.P(self._ws(2 * 256 * D)), K.stream_ptr())
+            K.mm(g, Ls["o"], self.G[p + "proj.w"], ta=True, tb=False)
+            do = self._e(Mv, D)
+            K.mm(g, self.W[p + "proj.w"], do, tb=False)
+            qkv = Ls["qkv"]
+            dqkv = self._e(Mv, 3 * D)
+            K.attn_bwd(qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], Ls["o"], Ls["lse"], do,
+                       dqkv[:, :D], dqkv[:, D:2 * D], dqkv[:, 2 * D:], vws, B=N, S=T, Hq=H, Hkv=H, causal=False)
+            del do
+            K.mm(dqkv, Ls["h1"], self.G[p + "qkv.w"], ta=True, tb=False)
+            self._colsum(dqkv, self.G[p + "qkv.b"], 0)
+            K.mm(dqkv, self.W[p + "qkv.w"], dh2, tb=False)
+            del dqkv
+            K.norm_bwd(Ls["n1"], dh2, dxv, dx_accumulate=True, dgamma=self.G[p + "ln1.w"], dbeta=self.G[p + "ln1.b"],
+                       ws=self._ws(K.norm_ws_floats(D)))
+            del dh2
+            self._group_done(f"vit{i}")
+        # ---------------- embeddings ----------------
+        g_ = cfg.vit_grid
+        dpatch = self._e(N * g_ * g_, D)
+        K.call("slx_vit_embed_bwd", K.P(dxv), N, T, D, K.P(self.G["vit.pos"]), K.P(self.G["vit.cls"]), K.P(dpatch),
+               K.stream_ptr())
+        dwp = self._e(D, cfg.patch_kpad, dtype=F32)
+        K.mm(dpatch, sv["col"], dwp, ta=True, tb=False)
+        self.G["vit.patch.w"].copy_(dwp[:, : cfg.patch_k])
+        self._colsum(dpatch, self.G["vit.patch.b"], 0)
+        self._group_done("vit_embed")
+        self.saved = None
+
+    def _lora_bwd(self, dy, saved, i, site, dx, sv):
+        """dy: bf16 [M, out] (view); dx: f32 [M, in] accumulated."""
+        cfg = self.cfg
+        t, xd, seed = saved
+        p = f"llm.{i}.lora.{site}."
+        s = cfg.lora_scale
+        M = dy.shape[0]
+        K.mm(dy, t, self.G[p + "b"], ta=True, tb=False, alpha=s)            # dB = s dy^T t
+        dt = self._e(M, cfg.lora_r)
+        K.mm(dy, self.W[p + "b"], dt, tb=False, alpha=s)                    # dt = s dy B
+        K.mm(dt, xd, self.G[p + "a"], ta=True, tb=False)                    # dA = dt^T drop(x)
+        kin = xd.shape[1]
+        if sv["drop"] > 0:
+            K.mm(dt, self.W[p + "a"], dx, tb=False, epi=K.EPI_DROPMASK, accumulate=True, seed=seed, drop_p=sv["drop"],
+                 ldmask=kin)
+        else:
+            K.mm(dt, self.W[p + "a"], dx, tb=False, accumulate=True)      # dx += dt A
+
+    def _mlp_bwd(self, dout, saved, need_dx=True):
+        """saved: [(out, pre, in, prefix, act)] from last layer to first; dout: grad of the last output."""
+        g = dout
+        for (out, pre, inp, name, act) in saved:
+            M, n = g.shape
+            kin = inp.shape[1]
+            if act != K.ACT_NONE:
+                gp = self._e(M, n, dtype=F32)
+                K.call("slx_act_bwd", K.P(g), K.P(pre), K.P(gp), M * n, act, K.stream_ptr())
+                g = gp
+            # dW[n, kin] = g^T inp ; db = colsum(g) ; dinp = g W
+            K.sgemm(g, 1, n, inp, kin, 1, self.G[name + ".w"], kin, 1, n, kin, M)
+            if name + ".b" in self.G:
+                K.sgemm(g, 1, n, self.ones_col(M), 1, 1, self.G[name + ".b"], 1, 1, n, 1, M)
+            if inp is saved[-1][2] and not need_dx:
+                break
+            dinp = self._e(M, kin, dtype=F32)
+            K.sgemm(g, n, 1, self.P[name + ".w"], kin, 1, dinp, kin, 1, M, kin, n)
+            g = dinp
+        return g
+
+    def ones_col(self, M):
+        if getattr(self, "_ones", None) is None or self._ones.numel() < M:
+            self._ones = torch.ones(max(M, 1024), dtype=F32, device=self.device)
+        return self._ones
+
+    # ==========================================================================================
+    # optimizer
+    def adamw_step(self, lr, step, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.1, max_norm=0.3):
+        self.wait_grads()
+        if not hasattr(self, "m_state"):
+            self.m_state = torch.zeros_like(self.master)
+            self.v_state = torch.zeros_like(self.master)
+            self.sumsq = torch.zeros(1, dtype=F32, device=self.device)
+        K.call("slx_sumsq", K.P(self.grad), self.n_flat, K.P(self.sumsq), 1, K.stream_ptr())
+        K.call("slx_adamw", K.P(self.master), K.P(self.grad), K.P(self.m_state), K.P(self.v_state), K.P(self.wbf),
+               self.n_flat, float(lr), float(betas[0]), float(betas[1]), float(eps), float(weight_decay), int(step),
+               K.P(self.sumsq), float(max_norm if max_norm else 0.0), 1.0 / self.world, K.stream_ptr())
+        self._refresh_derived()
+
+    def grad_norm(self):
+        """L2 norm of the (averaged) gradient — diagnostic (syncs)."""
+        return float(torch.linalg.vector_norm(self.grad).item()) / self.world

@@ -225,7 +225,11 @@ for _n, _a in {
     "slx_loss_finalize": [_vp, _i, _vp, _i, _vp, _i, _vp, _vp],
     "slx_loss_gscale": [_vp, _i, _i, _i, _vp, _vp],
     "slx_sumsq": [_vp, _I, _vp, _i, _vp],
-    "slx_adamw": [_vp, _vp, _vp, _vp, _vp, _I, _f, _f, _f, _f, _f, _i, _vp, _f, _vp],
+    "slx_adamw": [_vp, _vp, _vp, _vp, _vp, _I, _f, _f, _f, _f, _f, _i, _vp, _f, _f, _vp],
+    "slx_scatter_rows": [_vp, _I, _vp, _I, _i, _vp, _I, _i, _vp],
+    "slx_gather_rows_b2f": [_vp, _I, _vp, _I, _i, _vp, _I, _vp],
+    "slx_swiglu_bwd": [_vp, _I, _vp, _I, _vp, _I, _I, _i, _vp],
+    "slx_cast_rows": [_vp, _I, _vp, _I, _I, _i, _vp],
     "slx_cast_f32_bf16": [_vp, _vp, _I, _vp],
 }.items():
     register(_n, _a)
@@ -233,6 +237,7 @@ for _n, _a in {
 
 def attn_desc(q, k, v, o, lse, *, B, S, Hq, Hkv, causal=False, seqlens=None, scale=0.125):
     d = AttnDesc()
+    d._keep = (q, k, v, o, lse, seqlens)
     d.B, d.S, d.Hq, d.Hkv, d.head_dim, d.causal = B, S, Hq, Hkv, 64, int(bool(causal))
     d.q, d.ldq = q.data_ptr(), q.stride(0)
     d.k, d.ldk = k.data_ptr(), k.stride(0)
@@ -292,7 +297,10 @@ def rope_tables(S, theta, device, head_dim=64):
 # Norms
 # ------------------------------------------------------------------------------------------------
 def norm_desc(x, gamma, beta, y, mean, rstd, rows, D, eps, rms=False, ps_grid=0, tok_per_img=0, ldx=None):
+    """The descriptor keeps references to every tensor it points to (ctypes holds raw pointers only;
+    without this the caching allocator could recycle the saved statistics before the backward)."""
     d = NormDesc()
+    d._keep = (x, gamma, beta, y, mean, rstd)
     d.rms = int(rms)
     d.x, d.ldx = x.data_ptr(), ldx if ldx is not None else x.stride(0)
     d.gamma = gamma.data_ptr()
@@ -332,3 +340,17 @@ def sgemm(A, sam, sak, B, sbk, sbn, C, scm, scn, M, N, Kd, *, bias=None, act=ACT
     d.ldpre = ldpre
     d.alpha = alpha
     check(lib().slx_sgemm(ctypes.byref(d), stream_ptr()), "slx_sgemm")
+
+
+def mm(A, B, C, *, ta=False, tb=True, **kw):
+    """C = op(A) @ op(B). A is stored [M,K] (ta=False) or [K,M] (ta=True); B is stored [K,N] (tb=False)
+    or [N,K] (tb=True). All operands are 2-D views with unit inner stride (column slices allowed)."""
+    if ta:
+        Kd, M = A.shape
+    else:
+        M, Kd = A.shape
+    N = B.shape[0] if tb else B.shape[1]
+    layout = {(False, True): GEMM_NT, (False, False): GEMM_NN, (True, False): GEMM_TN, (True, True): GEMM_TT}[(ta, tb)]
+    assert C.shape[0] >= M and C.shape[1] >= N, (C.shape, M, N)
+    gemm(A, B, C, M, N, Kd, layout, A.stride(0), B.stride(0), C.stride(0), **kw)
+    return C

@@ -37,9 +37,7 @@ def param_specs(cfg: VLAConfig) -> list[PSpec]:
     d = cfg.llm_dim
     out: list[PSpec] = []
     a = out.append
-    # driving heads + queries (adaptors.py:110-136)
-    a(PSpec("drv.query_route", (cfg.n_route, d), True, "query", "heads"))
-    a(PSpec("drv.query_speed", (cfg.n_speed, d), True, "query", "heads"))
+    # driving heads (adaptors.py:110-136)
     m = cfg.head_mlp
     for nm, shp, init in (("route.0.w", (2 * m, d), "normal"), ("route.0.b", (2 * m,), "zeros"),
                           ("route.1.w", (m, 2 * m), "normal"), ("route.1.b", (m,), "zeros"),
@@ -67,13 +65,15 @@ def param_specs(cfg: VLAConfig) -> list[PSpec]:
                 a(PSpec(p + f"lora.{s}.a", (cfg.lora_r, fin), True, "lora_a", f"llm{i}"))
                 a(PSpec(p + f"lora.{s}.b", (fout, cfg.lora_r), True, "lora_b", f"llm{i}"))
     a(PSpec("llm.embed", (V, d), False, "normal", "llm_frozen"))
-    # wp_encoder (driving.py:91-96, adaptors.py:64-93)
-    a(PSpec("wp.0.w", (cfg.wp_hidden, 2), True, "normal", "wp"))
-    a(PSpec("wp.0.b", (cfg.wp_hidden,), True, "zeros", "wp"))
-    a(PSpec("wp.1.w", (cfg.wp_hidden2, cfg.wp_hidden), True, "normal", "wp"))
-    a(PSpec("wp.1.b", (cfg.wp_hidden2,), True, "zeros", "wp"))
-    a(PSpec("wp.2.w", (d, cfg.wp_hidden2), True, "normal", "wp"))
-    a(PSpec("wp.2.b", (d,), True, "zeros", "wp"))
+    # token assembly inputs: driving queries (adjacent, [30, d]) and wp_encoder (driving.py:91-96)
+    a(PSpec("drv.query_route", (cfg.n_route, d), True, "query", "assembly"))
+    a(PSpec("drv.query_speed", (cfg.n_speed, d), True, "query", "assembly"))
+    a(PSpec("wp.0.w", (cfg.wp_hidden, 2), True, "normal", "assembly"))
+    a(PSpec("wp.0.b", (cfg.wp_hidden,), True, "zeros", "assembly"))
+    a(PSpec("wp.1.w", (cfg.wp_hidden2, cfg.wp_hidden), True, "normal", "assembly"))
+    a(PSpec("wp.1.b", (cfg.wp_hidden2,), True, "zeros", "assembly"))
+    a(PSpec("wp.2.w", (d, cfg.wp_hidden2), True, "normal", "assembly"))
+    a(PSpec("wp.2.b", (d,), True, "zeros", "assembly"))
     # mlp1 projector
     a(PSpec("proj.ln.w", (4 * D,), True, "ones", "proj"))
     a(PSpec("proj.ln.b", (4 * D,), True, "zeros", "proj"))
@@ -100,31 +100,35 @@ def param_specs(cfg: VLAConfig) -> list[PSpec]:
     return out
 
 
-def init_params(cfg: VLAConfig, seed: int = 0, lora_b_std: float = 0.02, std: float = 0.02) -> dict[str, torch.Tensor]:
+def init_params(cfg: VLAConfig, seed: int = 0, lora_b_std: float = 0.02, std: float = 0.02,
+                device="cpu") -> dict[str, torch.Tensor]:
     """Seeded fp32 CPU initialisation. Weights N(0, std) (HF default initializer_range 0.02), biases 0,
     norms 1, layer scale ls_init (InternViT), queries 0.02*randn (adaptors.py:112,129),
     LoRA A kaiming-uniform(a=sqrt(5)) as peft; LoRA B N(0, lora_b_std) (peft inits B = 0; a non-zero
     B exercises the LoRA path in parity runs)."""
-    g = torch.Generator().manual_seed(seed)
+    import zlib
     out = {}
     for s in param_specs(cfg):
+        # one generator per parameter: values do not depend on the order of the spec list
+        g = torch.Generator(device=device).manual_seed(seed * 1000003 + zlib.crc32(s.name.encode()))
+        kw = dict(generator=g, device=device)
         if s.init == "normal":
-            t = torch.randn(s.shape, generator=g) * std
+            t = torch.randn(s.shape, **kw) * std
         elif s.init == "normal_small":
-            t = torch.randn(s.shape, generator=g) * std
+            t = torch.randn(s.shape, **kw) * std
         elif s.init == "zeros":
-            t = torch.zeros(s.shape)
+            t = torch.zeros(s.shape, device=device)
         elif s.init == "ones":
-            t = torch.ones(s.shape)
+            t = torch.ones(s.shape, device=device)
         elif s.init == "ls":
-            t = torch.full(s.shape, cfg.ls_init)
+            t = torch.full(s.shape, cfg.ls_init, device=device)
         elif s.init == "query":
-            t = 0.02 * torch.randn(s.shape, generator=g)
+            t = 0.02 * torch.randn(s.shape, **kw)
         elif s.init == "lora_a":
             bound = 1.0 / math.sqrt(s.shape[1])  # kaiming_uniform(a=sqrt(5)) on fan_in
-            t = (torch.rand(s.shape, generator=g) * 2 - 1) * bound
+            t = (torch.rand(s.shape, **kw) * 2 - 1) * bound
         elif s.init == "lora_b":
-            t = torch.randn(s.shape, generator=g) * lora_b_std
+            t = torch.randn(s.shape, **kw) * lora_b_std
         else:
             raise ValueError(s.init)
         out[s.name] = t.float().contiguous()
