@@ -60,6 +60,7 @@ typedef struct slx_gemm_desc {
   const float* resid; int64_t ldr;      /* f32 residual (RESID_LS) */
   int accumulate;
   uint64_t seed; float drop_p; int64_t ldmask;
+  int ksplit_max;   /* 0 = automatic split-K for under-filled f32 STORE GEMMs, < 0 = never, > 0 = cap */
 } slx_gemm_desc;
 int slx_gemm_bf16(const slx_gemm_desc* d, slx_stream_t stream);
 

@@ -49,6 +49,8 @@ struct GemmArgs {
   float drop_p;
   long ldmask;
   int tilesM, tilesN;
+  int ksplit;        // > 1: split-K, f32 atomic accumulation into a pre-zeroed / accumulating C
+  int kchunk;        // K range per split (multiple of BK)
 };
 
 template <bool KC>
@@ -126,6 +128,11 @@ __device__ __forceinline__ void epilogue_elem(const GemmArgs& p, OutT* __restric
   float v = acc * p.alpha;
   const long ci = (long)m * p.ldc + n;
   if constexpr (EPI == EPI_STORE) {
+    if (p.ksplit > 1) {  // split-K: every split adds its partial; split 0 adds the bias
+      if (p.bias && blockIdx.y == 0) v += p.bias[n];
+      atomicAdd(reinterpret_cast<float*>(C) + ci, v);
+      return;
+    }
     if (p.bias) v += p.bias[n];
     if (p.accumulate) v += (float)C[ci];
     C[ci] = (OutT)v;
@@ -187,14 +194,19 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs p) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = (p.K + BK - 1) / BK;
+  int kbeg = 0, kend = p.K;
+  if (p.ksplit > 1) {
+    kbeg = blockIdx.y * p.kchunk;
+    kend = min(p.K, kbeg + p.kchunk);
+  }
+  const int nk = (kend - kbeg + BK - 1) / BK;
   char* As0 = smem;
   char* Bs0 = smem + BM * BK * 2;
   constexpr int STAGE = BM * BK * 2 + BN * BK * 2;
 
   uint4 ra[4], rb[4];
-  load_tile<AK>(A, p.lda, m0, p.M, 0, p.K, ra);
-  load_tile<BKc>(B, p.ldb, n0, p.N, 0, p.K, rb);
+  load_tile<AK>(A, p.lda, m0, p.M, kbeg, kend, ra);
+  load_tile<BKc>(B, p.ldb, n0, p.N, kbeg, kend, rb);
   store_tile<AK>(As0, ra);
   store_tile<BKc>(Bs0, rb);
   __syncthreads();
@@ -204,8 +216,8 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs p) {
     const char* As = As0 + cur * STAGE;
     const char* Bs = Bs0 + cur * STAGE;
     if (kt + 1 < nk) {
-      load_tile<AK>(A, p.lda, m0, p.M, (kt + 1) * BK, p.K, ra);
-      load_tile<BKc>(B, p.ldb, n0, p.N, (kt + 1) * BK, p.K, rb);
+      load_tile<AK>(A, p.lda, m0, p.M, kbeg + (kt + 1) * BK, kend, ra);
+      load_tile<BKc>(B, p.ldb, n0, p.N, kbeg + (kt + 1) * BK, kend, rb);
     }
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -241,7 +253,7 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs p) {
 
 template <bool AK, bool BKc, int EPI, typename OutT>
 static int launch(GemmArgs& a, int batch, hipStream_t st) {
-  dim3 grid(a.tilesM * a.tilesN, 1, batch);
+  dim3 grid(a.tilesM * a.tilesN, a.ksplit > 1 ? a.ksplit : 1, batch);
   hipLaunchKernelGGL((gemm_bf16_kernel<AK, BKc, EPI, OutT>), grid, dim3(NT), 0, st, a);
   SLX_LAUNCH_CHECK("slx_gemm_bf16");
   return 0;
@@ -293,6 +305,30 @@ extern "C" int slx_gemm_bf16(const slx_gemm_desc* d, slx_stream_t stream) {
   a.tilesN = (d->N + BN - 1) / BN;
   const int batch = d->batch < 1 ? 1 : d->batch;
   hipStream_t st = (hipStream_t)stream;
+  a.ksplit = 1;
+  a.kchunk = d->K;
+  {  // split-K for under-filled grids (weight gradients of skinny / LoRA GEMMs): >= 4 K-steps per split
+    const int tiles = a.tilesM * a.tilesN * batch;
+    const int ksteps = (d->K + BK - 1) / BK;
+    if (d->epilogue == SLX_EPI_STORE && d->out_f32 && tiles < 256 && ksteps >= 8) {
+      int want = (512 + tiles - 1) / tiles;
+      int maxs = ksteps / 4;
+      int sp = want < maxs ? want : maxs;
+      if (d->ksplit_max > 0 && sp > d->ksplit_max) sp = d->ksplit_max;
+      if (d->ksplit_max < 0) sp = 1;
+      if (sp > 1) {
+        const int per = ((ksteps + sp - 1) / sp) * BK;
+        sp = (d->K + per - 1) / per;
+        a.ksplit = sp;
+        a.kchunk = per;
+        if (!d->accumulate) {
+          hipError_t e = hipMemset2DAsync(d->C, d->ldc * sizeof(float), 0, (size_t)d->N * sizeof(float), d->M, st);
+          if (e != hipSuccess) { set_error("slx_gemm_bf16: memset2D failed: %s", hipGetErrorString(e)); return -1000 - (int)e; }
+        }
+        SLX_CHECK_ARG(batch == 1, "slx_gemm_bf16: split-K with batch > 1 unsupported");
+      }
+    }
+  }
   switch (d->epilogue) {
     case SLX_EPI_STORE:
       return d->out_f32 ? dispatch_layout<EPI_STORE, float>(d->layout, a, batch, st)

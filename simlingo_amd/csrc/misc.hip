@@ -125,13 +125,9 @@ __global__ __launch_bounds__(256) void colsum_kernel(const void* xv, long ldx, l
   }
 }
 
-__global__ void colreduce2_kernel(const float* partial, int nblk, int N, float* out, int accumulate, int off) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= N) return;
-  float s = 0.f;
-  for (int b = 0; b < nblk; ++b) s += partial[(long)b * 2 * N + off + c];
-  out[c] = accumulate ? out[c] + s : s;
-}
+}  // namespace slx
+#include "colreduce.h"
+namespace slx {
 
 // LLM input assembly: out[i, :] (f32) from code[i] = (kind << 28) | index
 //   kind 0: token  -> embed[min(index, V-1)] (bf16 table; ids clamped like adaptors.py:256)
@@ -489,7 +485,7 @@ int slx_colsum(int mode, const void* x, int64_t ldx, int64_t M, int N, float* ou
   hipStream_t st = (hipStream_t)s;
   if (mode == 0) hipLaunchKernelGGL((colsum_kernel<0>), grid, dim3(256), 0, st, x, ldx, M, N, ws, nullptr, nullptr, 0L, nullptr, 0L);
   else hipLaunchKernelGGL((colsum_kernel<1>), grid, dim3(256), 0, st, x, ldx, M, N, ws, nullptr, nullptr, 0L, nullptr, 0L);
-  hipLaunchKernelGGL(colreduce2_kernel, g1(N), dim3(256), 0, st, ws, nblk, N, out, accumulate, 0);
+  launch_colreduce(ws, nblk, N, 2L * N, out, accumulate, st);
   SLX_LAUNCH_CHECK("slx_colsum");
   return 0;
 }
@@ -502,8 +498,8 @@ int slx_ls_branch_bwd(const float* dres, int64_t ldr, const float* ls, const voi
   dim3 grid(nblk, (N / 4 + 255) / 256);
   hipStream_t st = (hipStream_t)s;
   hipLaunchKernelGGL((colsum_kernel<2>), grid, dim3(256), 0, st, (const void*)dres, ldr, M, N, ws, ls, (const bf16*)y, ldy, (bf16*)g, ldg);
-  hipLaunchKernelGGL(colreduce2_kernel, g1(N), dim3(256), 0, st, ws, nblk, N, dls, accumulate, 0);
-  hipLaunchKernelGGL(colreduce2_kernel, g1(N), dim3(256), 0, st, ws, nblk, N, dbias, accumulate, N);
+  launch_colreduce(ws, nblk, N, 2L * N, dls, accumulate, st);
+  launch_colreduce(ws + N, nblk, N, 2L * N, dbias, accumulate, st);
   SLX_LAUNCH_CHECK("slx_ls_branch_bwd");
   return 0;
 }

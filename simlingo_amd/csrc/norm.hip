@@ -166,20 +166,15 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(NormArgs a) {
   }
 }
 
-// out[c] (+)= sum_b partial[b, c]   for c < ncols  (column reduction of [nblk, ncols] partials)
-__global__ void colreduce_kernel(const float* partial, int nblk, int ncols, long ldp, float* out, int accumulate) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= ncols) return;
-  float s = 0.f;
-  for (int b = 0; b < nblk; ++b) s += partial[(long)b * ldp + c];
-  out[c] = accumulate ? out[c] + s : s;
-}
+}  // namespace slx
+#include "colreduce.h"
+namespace slx {
 
 }  // namespace slx
 
 using namespace slx;
 
-static constexpr int kBwdBlocks = 512;
+static constexpr int kBwdBlocks = 256;
 
 template <bool RMS>
 static int norm_fwd(NormArgs& a, hipStream_t st) {
@@ -200,8 +195,8 @@ static int norm_bwd(NormArgs& a, float* dgamma, float* dbeta, int accumulate, hi
   else hipLaunchKernelGGL((norm_bwd_kernel<16, RMS>), dim3(nblk), dim3(256), 0, st, a);
   SLX_LAUNCH_CHECK("slx_norm_bwd");
   if (a.partial) {
-    if (dgamma) hipLaunchKernelGGL(colreduce_kernel, dim3((a.D + 255) / 256), dim3(256), 0, st, a.partial, nblk, a.D, (long)2 * a.D, dgamma, accumulate);
-    if (dbeta) hipLaunchKernelGGL(colreduce_kernel, dim3((a.D + 255) / 256), dim3(256), 0, st, a.partial + a.D, nblk, a.D, (long)2 * a.D, dbeta, accumulate);
+    if (dgamma) launch_colreduce(a.partial, nblk, a.D, (long)2 * a.D, dgamma, accumulate, st);
+    if (dbeta) launch_colreduce(a.partial + a.D, nblk, a.D, (long)2 * a.D, dbeta, accumulate, st);
     SLX_LAUNCH_CHECK("slx_norm_bwd(reduce)");
   }
   return 0;

@@ -36,6 +36,7 @@ class GemmDesc(ctypes.Structure):
         ("resid", c_vp), ("ldr", c_i64),
         ("accumulate", c_int),
         ("seed", c_u64), ("drop_p", c_float), ("ldmask", c_i64),
+        ("ksplit_max", c_int),
     ]
 
 
@@ -110,7 +111,7 @@ def _require_cuda(*ts):
 # ------------------------------------------------------------------------------------------------
 def gemm(A, B, C, M, N, K, layout, lda, ldb, ldc, *, epi=EPI_STORE, alpha=1.0, bias=None, ls=None,
          aux=None, ldaux=0, aux_out=None, ldaux_out=0, resid=None, ldr=0, accumulate=False,
-         seed=0, drop_p=0.0, ldmask=0, batch=1, sA=0, sB=0, sC=0):
+         seed=0, drop_p=0.0, ldmask=0, batch=1, sA=0, sB=0, sC=0, ksplit_max=0):
     _require_cuda(A, B, C)
     d = GemmDesc()
     d.layout, d.epilogue = layout, epi
@@ -130,6 +131,7 @@ def gemm(A, B, C, M, N, K, layout, lda, ldb, ldc, *, epi=EPI_STORE, alpha=1.0, b
     d.ldr = int(ldr)
     d.accumulate = 1 if accumulate else 0
     d.seed, d.drop_p, d.ldmask = int(seed) & ((1 << 64) - 1), float(drop_p), int(ldmask)
+    d.ksplit_max = int(ksplit_max)
     check(lib().slx_gemm_bf16(ctypes.byref(d), stream_ptr()), "slx_gemm_bf16")
 
 

@@ -69,3 +69,22 @@ def test_gemm_epilogues(dev):
     hh = h.float().requires_grad_()
     torch.nn.functional.gelu(hh).backward(dy.float() @ w2.float())
     torch.testing.assert_close(dh.float(), hh.grad, atol=5e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("M,N,Kd,layout", [(896, 32, 6384, K.GEMM_TN), (32, 4864, 6384, K.GEMM_TN),
+                                            (1024, 1024, 16400, K.GEMM_TN), (128, 96, 2048, K.GEMM_NT)])
+@pytest.mark.parametrize("accumulate", [False, True])
+def test_gemm_split_k(dev, M, N, Kd, layout, accumulate):
+    """Under-filled f32 GEMMs take the split-K path (f32 atomics); compare with an fp32 reference."""
+    g = torch.Generator(device=dev).manual_seed(M + N)
+    a = torch.randn(M, Kd, device=dev, generator=g).bfloat16()
+    b = torch.randn(Kd, N, device=dev, generator=g).bfloat16()
+    A = a if layout in (K.GEMM_NT, K.GEMM_NN) else a.t().contiguous()
+    B = b.t().contiguous() if layout in (K.GEMM_NT, K.GEMM_TT) else b
+    C0 = torch.randn(M, N, device=dev, generator=g)
+    C = C0.clone()
+    bias = torch.randn(N, device=dev, generator=g)
+    K.gemm(A, B, C, M, N, Kd, layout, A.stride(0), B.stride(0), C.stride(0), bias=bias, alpha=0.5,
+           accumulate=accumulate)
+    ref = 0.5 * (a.float() @ b.float()) + bias + (C0 if accumulate else 0)
+    assert (C - ref).abs().max().item() < 2e-3 * Kd ** 0.5
