@@ -24,6 +24,7 @@ import torch
 
 from . import kernels as K
 from .config import VLAConfig
+from .ddp import GradBucketer
 from .params import LORA_SITES, lora_io, param_specs
 from .plan import Plan
 
@@ -33,14 +34,6 @@ ALIGN = 64  # elements; keeps every parameter view 256-B aligned
 
 def _pad8(n):
     return (n + 7) // 8 * 8
-
-
-@dataclass
-class Bucket:
-    start: int
-    end: int
-    groups: list
-    handle: object = None
 
 
 class VLAEngine:
@@ -105,19 +98,7 @@ class VLAEngine:
             e = o + (math.prod(s.shape) + ALIGN - 1) // ALIGN * ALIGN
             a, b = self.group_ranges.get(s.group, (o, e))
             self.group_ranges[s.group] = (min(a, o), max(b, e))
-        order = sorted(self.group_ranges, key=lambda g: self.group_ranges[g][0])
-        self.buckets: list[Bucket] = []
-        cur = None
-        for g in order:
-            a, b = self.group_ranges[g]
-            if cur is None or (cur.end - cur.start) * 4 >= bucket_bytes or cur.end != a:
-                cur = Bucket(a, b, [g])
-                self.buckets.append(cur)
-            else:
-                cur.end = b
-                cur.groups.append(g)
-        self.group_bucket = {g: bk for bk in self.buckets for g in bk.groups}
-        self.dist_pg = None
+        self.bucketer = GradBucketer(self.grad, self.group_ranges, bucket_bytes)
         self.world = 1
         self.step_seed = 0
         self.saved = None
@@ -151,24 +132,14 @@ class VLAEngine:
         self.wpatch[:, : cfg.patch_k].copy_(self.W["vit.patch.w"])
 
     def set_distributed(self, pg=None, world: int = 1):
-        self.dist_pg = pg
         self.world = world
+        self.bucketer.set_distributed(pg, world)
 
     def _group_done(self, g):
-        if self.world <= 1:
-            return
-        bk = self.group_bucket[g]
-        bk.groups_done = getattr(bk, "groups_done", 0) + 1
-        if bk.groups_done == len(bk.groups):
-            import torch.distributed as dist
-            bk.handle = dist.all_reduce(self.grad[bk.start:bk.end], group=self.dist_pg, async_op=True)
+        self.bucketer.group_done(g)
 
     def wait_grads(self):
-        for bk in self.buckets:
-            if bk.handle is not None:
-                bk.handle.wait()
-                bk.handle = None
-            bk.groups_done = 0
+        self.bucketer.wait()
 
     def rope_tables(self, S):
         if S not in self._cos_sin:

@@ -1,0 +1,72 @@
+"""Data-parallel gradient exchange on CPU with gloo, world_size 2 (the N>1 path of bench.py)."""
+import math
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from simlingo_amd.config import full_config, tiny_config
+from simlingo_amd.ddp import GradBucketer
+from simlingo_amd.params import param_specs
+
+
+def group_ranges(cfg, align=64):
+    off, ranges = 0, {}
+    for s in param_specs(cfg):
+        if not s.trainable:
+            continue
+        n = (math.prod(s.shape) + align - 1) // align * align
+        a, b = ranges.get(s.group, (off, off + n))
+        ranges[s.group] = (min(a, off), max(b, off + n))
+        off += n
+    return ranges, off
+
+
+def test_buckets_cover_flat_buffer_in_backward_order():
+    cfg = full_config()
+    ranges, n = group_ranges(cfg)
+    bk = GradBucketer(torch.zeros(n), ranges, bucket_bytes=32 << 20)
+    spans = bk.summary()
+    assert spans[0][0] == 0 and spans[-1][1] == n
+    for (a0, b0, _), (a1, b1, _) in zip(spans, spans[1:]):
+        assert b0 == a1  # contiguous, no overlap
+    # backward order: heads first, LoRA layers last->first, assembly, projector, ViT last->first, embeddings
+    order = [g for b in bk.buckets for g in b.groups]
+    assert order[0] == "heads" and order[-1] == "vit_embed"
+    assert order.index("llm23") < order.index("llm0") < order.index("assembly") < order.index("proj")
+    assert order.index("vit23") < order.index("vit0")
+    # ViT layers (12.6 M params = 50 MB f32) are their own buckets; LoRA layers are merged
+    assert any(b.groups == ["vit12"] for b in bk.buckets)
+    assert sum(1 for b in bk.buckets if any(g.startswith("llm") for g in b.groups)) < cfg.llm_layers
+
+
+def _worker(rank, world, port, n, ranges, ret):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    g = torch.arange(n, dtype=torch.float32) * (rank + 1)
+    bk = GradBucketer(g, ranges, bucket_bytes=4096)
+    bk.set_distributed(None, world)
+    order = sorted(ranges, key=lambda k: ranges[k][0])
+    for name in order:  # the backward signals groups in layout order
+        bk.group_done(name)
+    bk.wait()
+    ret[rank] = g.clone()
+    dist.destroy_process_group()
+
+
+def test_bucketed_allreduce_gloo_world2():
+    cfg = tiny_config()
+    ranges, n = group_ranges(cfg)
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    mgr = mp.Manager()
+    ret = mgr.dict()
+    mp.spawn(_worker, args=(2, port, n, ranges, ret), nprocs=2, join=True)
+    want = torch.arange(n, dtype=torch.float32) * 3  # sum over ranks (1x + 2x); AdamW applies 1/world
+    for r in range(2):
+        torch.testing.assert_close(ret[r], want)
