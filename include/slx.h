@@ -61,6 +61,9 @@ typedef struct slx_gemm_desc {
   int accumulate;
   uint64_t seed; float drop_p; int64_t ldmask;
   int ksplit_max;   /* 0 = automatic split-K for under-filled f32 STORE GEMMs, < 0 = never, > 0 = cap */
+  int variant;      /* 0 = automatic main-loop choice (tuning/testing hook; see gemm.hip)         */
+  int drop_operand; /* 0 none; 1/2: LoRA dropout applied to A/B while loading, mask index =
+                       storage_row*ldmask + storage_col, hash of slx_dropout (seed, drop_p)      */
 } slx_gemm_desc;
 int slx_gemm_bf16(const slx_gemm_desc* d, slx_stream_t stream);
 
@@ -86,7 +89,7 @@ typedef struct slx_attn_bwd_desc {
   void* dv; int64_t lddv;
   float* delta_ws;              /* [B, Hq, S]                                            */
   float* dq_acc;                /* [B*S, Hq*64] f32 workspace                            */
-  float* dk_acc; float* dv_acc; /* [B*S, Hkv*64] f32 workspaces (GQA only)               */
+  float* dk_acc; float* dv_acc; /* [B*S, Hq*64] f32 per-q-head partial workspaces (GQA only) */
   const float* rope_cos; const float* rope_sin; /* [S, 32] tables: apply RoPE^T to dq/dk */
 } slx_attn_bwd_desc;
 int slx_attn_fwd(const slx_attn_desc* d, slx_stream_t stream);
@@ -179,6 +182,9 @@ int slx_sumsq(const float* g, int64_t n, float* out, int zero_first, slx_stream_
 int slx_adamw(float* p, const float* g, float* m, float* v, void* p_bf16, int64_t n, float lr, float beta1, float beta2,
               float eps, float weight_decay, int step, const float* sumsq, float max_norm, float grad_scale, slx_stream_t s);
 int slx_cast_f32_bf16(const float* src, void* dst, int64_t n, slx_stream_t s);
+/* table: n device-resident entries {src f32*, lds, dst bf16*, ldd, rows, cols, float-bits scale}:
+ * dst = bf16(src * scale). Packs LoRA B (scaled by lora_alpha/r) into the fused [W | s*B] operands. */
+int slx_pack_scaled(const int64_t* table, int n, slx_stream_t s);
 
 #ifdef __cplusplus
 }

@@ -17,9 +17,9 @@
 // Backward: one workgroup = 4 waves = 128 keys of one (b, h); loops over 64-query chunks;
 // S and dP are recomputed with the key on the lane (their accumulators are the B operands of the
 // dV^T and dK^T products), dS^T goes through LDS once for dQ, which is accumulated with f32
-// atomics (2 x 128-B row segments per wave-instruction). For GQA the dK/dV partials of the q-heads
-// in a group are also combined with f32 atomics; a finalize kernel converts to bf16 and applies
-// the RoPE transpose.
+// atomics (2 x 128-B row segments per wave-instruction). For GQA each q-head's dK/dV partial is
+// stored with plain 16-B stores and a finalize kernel sums the group, applies the RoPE transpose
+// and converts to bf16 (row-scattered f32 atomics ran ~17x below the atomic rate here).
 #include "common.h"
 #include "../../include/slx.h"
 
@@ -73,7 +73,7 @@ struct AttnArgs {
   const bf16* dout; long lddo;
   const float* delta;
   float* dq_acc;               // [B*S, Hq*64] f32 (zeroed)
-  float* dk_acc; float* dv_acc;  // [B*S, Hkv*64] f32 (zeroed) when kv_atomic
+  float* dk_acc; float* dv_acc;  // [B*S, Hq*64] f32 per-q-head partials when kv_atomic (GQA)
   bf16* dk; bf16* dv; long lddk, lddv;  // direct bf16 outputs when !kv_atomic
   int kv_atomic;
 };
@@ -397,15 +397,13 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kernel(AttnArgs a) {
   for (int g = 0; g < 4; ++g) {
     const int d = 8 * g + 4 * hl;
     if (a.kv_atomic) {
-      float* kp = a.dk_acc + ((long)b * S + mykey) * (a.Hkv * 64) + hk * 64;
-      float* vp = a.dv_acc + ((long)b * S + mykey) * (a.Hkv * 64) + hk * 64;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        atomicAdd(kp + d + e, dk0[4 * g + e] * a.scale);
-        atomicAdd(kp + 32 + d + e, dk1[4 * g + e] * a.scale);
-        atomicAdd(vp + d + e, dv0[4 * g + e]);
-        atomicAdd(vp + 32 + d + e, dv1[4 * g + e]);
-      }
+      // GQA: per-q-head partials with plain 16-B stores; slx_attn_bwd's finalize sums the group
+      float* kp = a.dk_acc + ((long)b * S + mykey) * (a.Hq * 64) + h * 64;
+      float* vp = a.dv_acc + ((long)b * S + mykey) * (a.Hq * 64) + h * 64;
+      *reinterpret_cast<float4*>(kp + d) = make_float4(dk0[4 * g] * a.scale, dk0[4 * g + 1] * a.scale, dk0[4 * g + 2] * a.scale, dk0[4 * g + 3] * a.scale);
+      *reinterpret_cast<float4*>(kp + 32 + d) = make_float4(dk1[4 * g] * a.scale, dk1[4 * g + 1] * a.scale, dk1[4 * g + 2] * a.scale, dk1[4 * g + 3] * a.scale);
+      *reinterpret_cast<float4*>(vp + d) = make_float4(dv0[4 * g], dv0[4 * g + 1], dv0[4 * g + 2], dv0[4 * g + 3]);
+      *reinterpret_cast<float4*>(vp + 32 + d) = make_float4(dv1[4 * g], dv1[4 * g + 1], dv1[4 * g + 2], dv1[4 * g + 3]);
     } else {
       bf16* kp = a.dk + ((long)b * S + mykey) * a.lddk + hk * 64;
       bf16* vp = a.dv + ((long)b * S + mykey) * a.lddv + hk * 64;
@@ -475,6 +473,43 @@ __global__ void rope_kernel(RopeArgs r) {
   *reinterpret_cast<bf16x8*>(x + 32 + i0) = ob;
 }
 
+// GQA finalize: dst[t, hk, :] = sum_{j<G} src[t, hk*G + j, :] (f32 per-q-head partials, row stride
+// Hq*64) -> optional RoPE^T -> bf16. One thread per (token, kv head, quarter of the pairs).
+__global__ void gqa_reduce_kernel(const float* src, int Hq, int Hkv, bf16* dst, long ldd, long ntok, int S, const float* cos,
+                                  const float* sin) {
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= ntok * Hkv * 4) return;
+  const int part = idx & 3;
+  const long th = idx >> 2;
+  const int hk = th % Hkv;
+  const long tok = th / Hkv;
+  const int G = Hq / Hkv, i0 = part * 8;
+  float v0[8], v1[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { v0[j] = 0.f; v1[j] = 0.f; }
+  for (int g = 0; g < G; ++g) {
+    const float* sp = src + tok * (long)Hq * 64 + (hk * G + g) * 64;
+#pragma unroll
+    for (int j = 0; j < 8; j += 4) {
+      const float4 a = *reinterpret_cast<const float4*>(sp + i0 + j);
+      const float4 c = *reinterpret_cast<const float4*>(sp + 32 + i0 + j);
+      v0[j] += a.x; v0[j + 1] += a.y; v0[j + 2] += a.z; v0[j + 3] += a.w;
+      v1[j] += c.x; v1[j + 1] += c.y; v1[j + 2] += c.z; v1[j + 3] += c.w;
+    }
+  }
+  bf16x8 oa, ob;
+  const int pos = tok % S;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    if (cos) rope_pair(v0[j], v1[j], cos[(long)pos * 32 + i0 + j], sin[(long)pos * 32 + i0 + j], true);
+    oa[j] = (bf16)v0[j];
+    ob[j] = (bf16)v1[j];
+  }
+  bf16* dp = dst + tok * ldd + hk * 64;
+  *reinterpret_cast<bf16x8*>(dp + i0) = oa;
+  *reinterpret_cast<bf16x8*>(dp + 32 + i0) = ob;
+}
+
 // f32 [ntok, ncols] -> bf16 rows (ld) (no rope)
 __global__ void f32_to_bf16_rows_kernel(const float* src, long lds, bf16* dst, long ldd, long ntok, int ncols) {
   const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -532,8 +567,7 @@ extern "C" int slx_attn_bwd(const slx_attn_desc* d, const slx_attn_bwd_desc* g, 
   const long ntok = (long)a.B * a.S;
   hipMemsetAsync(a.dq_acc, 0, ntok * a.Hq * 64 * sizeof(float), st);
   if (a.kv_atomic) {
-    hipMemsetAsync(a.dk_acc, 0, ntok * a.Hkv * 64 * sizeof(float), st);
-    hipMemsetAsync(a.dv_acc, 0, ntok * a.Hkv * 64 * sizeof(float), st);
+    // per-q-head partials, fully overwritten by the kernel (no memset)
   } else {
     a.dk = (bf16*)g->dk; a.dv = (bf16*)g->dv; a.lddk = g->lddk; a.lddv = g->lddv;
   }
@@ -563,8 +597,12 @@ extern "C" int slx_attn_bwd(const slx_attn_desc* d, const slx_attn_bwd_desc* g, 
   };
   if ((rc = conv(a.dq_acc, a.Hq, (bf16*)g->dq, g->lddq, true))) return rc;
   if (a.kv_atomic) {
-    if ((rc = conv(a.dk_acc, a.Hkv, (bf16*)g->dk, g->lddk, true))) return rc;
-    if ((rc = conv(a.dv_acc, a.Hkv, (bf16*)g->dv, g->lddv, false))) return rc;
+    const long total = ntok * a.Hkv * 4;
+    hipLaunchKernelGGL(gqa_reduce_kernel, dim3((total + 255) / 256), dim3(256), 0, st, a.dk_acc, a.Hq, a.Hkv, (bf16*)g->dk,
+                       (long)g->lddk, ntok, a.S, r.cos, r.sin);
+    hipLaunchKernelGGL(gqa_reduce_kernel, dim3((total + 255) / 256), dim3(256), 0, st, a.dv_acc, a.Hq, a.Hkv, (bf16*)g->dv,
+                       (long)g->lddv, ntok, a.S, (const float*)nullptr, (const float*)nullptr);
+    SLX_LAUNCH_CHECK("slx_attn_bwd(gqa reduce)");
   } else if (r.cos) {
     // direct bf16 dK still needs the RoPE transpose (in place)
     r.x = (bf16*)g->dk; r.ldx = g->lddk; r.nheads = a.Hkv; r.src_f32 = nullptr;

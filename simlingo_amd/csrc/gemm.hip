@@ -51,11 +51,30 @@ struct GemmArgs {
   int tilesM, tilesN;
   int ksplit;        // > 1: split-K, f32 atomic accumulation into a pre-zeroed / accumulating C
   int kchunk;        // K range per split (multiple of BK)
+  int vec_ok;        // 16-B aligned rows for C / aux / resid -> vectorised epilogue
+  int drop_operand;  // 0 none, 1 = dropout on A while loading, 2 = on B (v1 main loop only)
 };
+
+// Dropout applied while loading an operand (LoRA dropout, regenerated bit-exactly in backward):
+// element at STORAGE coordinates (srow, scol) is kept with probability 1-p and scaled by 1/(1-p),
+// keep = uniform01(seed, srow*ldmask + scol) >= p  (same hash as slx_dropout / EPI_DROPMASK).
+struct LoadMask {
+  unsigned long long seed;
+  float p;
+  long ldmask;
+};
+
+__device__ __forceinline__ uint4 mask8(uint4 v, const LoadMask& mk, long base) {
+  bf16x8 x = __builtin_bit_cast(bf16x8, v);
+  const float sc = 1.0f / (1.0f - mk.p);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) x[j] = (bf16)((float)x[j] * (uniform01(mk.seed, (unsigned long long)(base + j)) >= mk.p ? sc : 0.f));
+  return __builtin_bit_cast(uint4, x);
+}
 
 template <bool KC>
 __device__ __forceinline__ void load_tile(const bf16* __restrict__ X, long ld, int row0, int rows_total, int k0,
-                                          int K, uint4 (&r)[4]) {
+                                          int K, uint4 (&r)[4], const LoadMask* mk = nullptr) {
   const int tid = threadIdx.x;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -72,6 +91,7 @@ __device__ __forceinline__ void load_tile(const bf16* __restrict__ X, long ld, i
     if (grow < rows_total && gk < K) {
       const bf16* ptr = KC ? X + (long)grow * ld + gk : X + (long)gk * ld + grow;
       r[i] = *reinterpret_cast<const uint4*>(ptr);
+      if (mk) r[i] = mask8(r[i], *mk, KC ? (long)grow * mk->ldmask + gk : (long)gk * mk->ldmask + grow);
     } else {
       r[i] = make_uint4(0u, 0u, 0u, 0u);
     }
@@ -162,6 +182,105 @@ __device__ __forceinline__ void epilogue_elem(const GemmArgs& p, OutT* __restric
   }
 }
 
+
+// 8 consecutive columns n..n+7 of row m (vector path: caller guarantees n+8 <= N and 16-B alignment)
+template <typename T>
+__device__ __forceinline__ void ld8(const T* p, float (&v)[8]) {
+  if constexpr (sizeof(T) == 2) {
+    const bf16x8 x = *reinterpret_cast<const bf16x8*>(p);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = (float)x[e];
+  } else {
+    const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  }
+}
+template <typename T>
+__device__ __forceinline__ void st8(T* p, const float (&v)[8]) {
+  if constexpr (sizeof(T) == 2) {
+    bf16x8 x;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) x[e] = (bf16)v[e];
+    *reinterpret_cast<bf16x8*>(p) = x;
+  } else {
+    *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+    *reinterpret_cast<float4*>(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
+  }
+}
+
+template <int EPI, typename OutT>
+__device__ __forceinline__ void epilogue_vec8(const GemmArgs& p, OutT* __restrict__ C, int m, int n, float (&v)[8]) {
+  const long ci = (long)m * p.ldc + n;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] *= p.alpha;
+  if constexpr (EPI == EPI_STORE) {
+    if (p.ksplit > 1) {
+      if (p.bias && blockIdx.y == 0) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += p.bias[n + e];
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) atomicAdd(reinterpret_cast<float*>(C) + ci + e, v[e]);
+      return;
+    }
+    if (p.bias) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += p.bias[n + e];
+    }
+    if (p.accumulate) {
+      float c[8];
+      ld8(C + ci, c);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += c[e];
+    }
+    st8(C + ci, v);
+  } else if constexpr (EPI == EPI_GELU) {
+    float h[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) h[e] = (float)(bf16)(v[e] + (p.bias ? p.bias[n + e] : 0.f));
+    st8(p.aux_out + (long)m * p.ldaux_out + n, h);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) h[e] = gelu_erf(h[e]);
+    st8(C + ci, h);
+  } else if constexpr (EPI == EPI_RESID_LS) {
+    if (p.bias) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += p.bias[n + e];
+    }
+    if (p.aux_out) st8(p.aux_out + (long)m * p.ldaux_out + n, v);
+    float r[8];
+    ld8(p.resid + (long)m * p.ldr + n, r);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) r[e] += p.ls[n + e] * v[e];
+    st8(C + ci, r);
+  } else if constexpr (EPI == EPI_GELU_BWD) {
+    float h[8];
+    ld8(p.aux + (long)m * p.ldaux + n, h);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] *= gelu_erf_grad(h[e]);
+    st8(C + ci, v);
+  } else if constexpr (EPI == EPI_SWIGLU_BWD) {
+    float g[8], u[8], o[8];
+    ld8(p.aux + (long)m * p.ldaux + n, g);
+    ld8(p.aux + (long)m * p.ldaux + p.N + n, u);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { o[e] = v[e] * u[e] * silu_grad(g[e]); u[e] = v[e] * silu(g[e]); }
+    st8(C + ci, o);
+    st8(C + ci + p.N, u);
+  } else if constexpr (EPI == EPI_DROPMASK) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      v[e] *= uniform01(p.seed, (unsigned long long)m * p.ldmask + n + e) >= p.drop_p ? 1.0f / (1.0f - p.drop_p) : 0.0f;
+    if (p.accumulate) {
+      float c[8];
+      ld8(C + ci, c);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += c[e];
+    }
+    st8(C + ci, v);
+  }
+}
+
 template <bool AK, bool BKc, int EPI, typename OutT>
 __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs p) {
   __shared__ __attribute__((aligned(16))) char smem[2 * (BM * BK * 2 + BN * BK * 2)];
@@ -205,8 +324,11 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs p) {
   constexpr int STAGE = BM * BK * 2 + BN * BK * 2;
 
   uint4 ra[4], rb[4];
-  load_tile<AK>(A, p.lda, m0, p.M, kbeg, kend, ra);
-  load_tile<BKc>(B, p.ldb, n0, p.N, kbeg, kend, rb);
+  LoadMask mk{p.seed, p.drop_p, p.ldmask};
+  const LoadMask* mka = p.drop_operand == 1 ? &mk : nullptr;
+  const LoadMask* mkb = p.drop_operand == 2 ? &mk : nullptr;
+  load_tile<AK>(A, p.lda, m0, p.M, kbeg, kend, ra, mka);
+  load_tile<BKc>(B, p.ldb, n0, p.N, kbeg, kend, rb, mkb);
   store_tile<AK>(As0, ra);
   store_tile<BKc>(Bs0, rb);
   __syncthreads();
@@ -216,8 +338,8 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs p) {
     const char* As = As0 + cur * STAGE;
     const char* Bs = Bs0 + cur * STAGE;
     if (kt + 1 < nk) {
-      load_tile<AK>(A, p.lda, m0, p.M, kbeg + (kt + 1) * BK, kend, ra);
-      load_tile<BKc>(B, p.ldb, n0, p.N, kbeg + (kt + 1) * BK, kend, rb);
+      load_tile<AK>(A, p.lda, m0, p.M, kbeg + (kt + 1) * BK, kend, ra, mka);
+      load_tile<BKc>(B, p.ldb, n0, p.N, kbeg + (kt + 1) * BK, kend, rb, mkb);
     }
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -251,6 +373,224 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs p) {
       }
 }
 
+// ---------------------------------------------------------------------------------------------
+// v2 main loop: LDS-DMA (buffer_load_dwordx4 ... lds) ring of NS stages, counted vmcnt, one raw
+// s_barrier per K-step. Each wave-instruction writes 1 KiB of LDS lane-linearly, so the XOR
+// swizzles of v1 are applied to the per-lane SOURCE address (the LDS images are identical to v1's,
+// and so are the fragment reads). Rows outside the matrix get a sentinel offset beyond the buffer
+// descriptor's num_records -> the hardware returns zeros. Tile BM x 128 (BM = 128 or 256), waves
+// (BM/64) x 2, each 64x64. Requirements: K-contiguous operands need K % 64 == 0 (else v1).
+constexpr unsigned kSent = 0x7FFFFFF0u;
+constexpr int EP_LD = 68;  // epilogue staging row stride (floats)
+
+template <bool KC, int ROWS>
+struct DmaOperand {
+  // per-lane precomputed element offsets of the LOADS this wave issues for one stage
+  static constexpr int BYTES = ROWS * BK * 2;       // per stage
+  static constexpr int INSTR = BYTES / 1024;         // wave-instructions per stage (whole block)
+};
+
+template <bool KC, int ROWS, int NW>
+__device__ __forceinline__ void dma_setup(int lane, int wave, int r0, int rows_total, long ld, long (&base)[ROWS * BK * 2 / 1024 / NW],
+                                          int (&kr)[ROWS * BK * 2 / 1024 / NW], bool (&ok)[ROWS * BK * 2 / 1024 / NW]) {
+  constexpr int PER = ROWS * BK * 2 / 1024 / NW;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int o = (wave * PER + i) * 1024 + lane * 16;
+    if (KC) {
+      const int row = o >> 7, pc = (o >> 4) & 7;
+      const int c = pc ^ ((row >> 1) & 7);
+      ok[i] = r0 + row < rows_total;
+      base[i] = (long)(r0 + row) * ld + 8 * c;
+      kr[i] = 0;
+    } else {
+      const int panel = o >> 14, o2 = o & 16383;
+      const int k = o2 >> 8, pc = (o2 >> 4) & 15;
+      const int x = (k & 3) | (((k >> 3) & 1) << 2);
+      const int c = pc ^ (2 * x);
+      const int col = r0 + panel * 128 + 8 * c;
+      ok[i] = col < rows_total;
+      base[i] = (long)k * ld + col;
+      kr[i] = k;
+    }
+  }
+}
+
+template <bool KC, int ROWS, int NW>
+__device__ __forceinline__ void dma_issue(__amdgpu_buffer_rsrc_t rs, char* lds_tile, int wave, int k0, int K, long ld,
+                                          const long (&base)[ROWS * BK * 2 / 1024 / NW],
+                                          const int (&kr)[ROWS * BK * 2 / 1024 / NW],
+                                          const bool (&ok)[ROWS * BK * 2 / 1024 / NW]) {
+  constexpr int PER = ROWS * BK * 2 / 1024 / NW;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    unsigned off;
+    if (KC) off = ok[i] ? (unsigned)((base[i] + k0) * 2) : kSent;
+    else off = (ok[i] && k0 + kr[i] < K) ? (unsigned)((base[i] + (long)k0 * ld) * 2) : kSent;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(lds_tile + (wave * PER + i) * 1024),
+                                             16, off, 0, 0, 0);
+  }
+}
+
+// fragment read from a tile made of 128-row panels
+template <bool KC>
+__device__ __forceinline__ bf16x8 read_frag_p(const char* lds, int rb, int s, int lane) {
+  if (KC) return read_frag<true>(lds, rb, s, lane);
+  return read_frag<false>(lds + (rb >> 7) * 16384, rb & 127, s, lane);
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if constexpr (N == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+  else if constexpr (N == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  else if constexpr (N == 18) asm volatile("s_waitcnt vmcnt(18)" ::: "memory");
+  else if constexpr (N == 24) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+  else static_assert(N < 0, "unsupported vmcnt");
+}
+
+template <bool AK, bool BKc, int EPI, typename OutT, int BMv, int NS>
+__global__ __launch_bounds__(BMv * 2, 1) void gemm_bf16_dma_kernel(GemmArgs p) {
+  constexpr int NW = BMv / 32;                 // waves: (BM/64) x 2
+  constexpr int A_BYTES = BMv * BK * 2, B_BYTES = BN * BK * 2;
+  constexpr int STAGE = A_BYTES + B_BYTES;
+  constexpr int LPW = (A_BYTES + B_BYTES) / 1024 / NW;   // DMA instructions per wave per stage
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tilesM = p.tilesM, tilesN = p.tilesN;
+  const int nwg = tilesM * tilesN;
+  int bid = blockIdx.x;
+  {
+    const int q = nwg >> 3, r = nwg & 7, xcd = bid & 7;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  }
+  constexpr int GROUP = 8;
+  const int npg = GROUP * tilesN;
+  const int gid = bid / npg;
+  const int fm = gid * GROUP;
+  const int gs = min(tilesM - fm, GROUP);
+  const int tm = fm + (bid % npg) % gs;
+  const int tn = (bid % npg) / gs;
+  const int m0 = tm * BMv, n0 = tn * BN;
+  const long z = blockIdx.z;
+  const bf16* A = p.A + z * p.sA;
+  const bf16* B = p.B + z * p.sB;
+  OutT* __restrict__ C = reinterpret_cast<OutT*>(p.C) + z * p.sC;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+
+  int kbeg = 0, kend = p.K;
+  if (p.ksplit > 1) {
+    kbeg = blockIdx.y * p.kchunk;
+    kend = min(p.K, kbeg + p.kchunk);
+  }
+  const int nk = (kend - kbeg + BK - 1) / BK;
+  // buffer descriptors over each operand's exact extent (OOB -> 0)
+  const long extA = AK ? ((long)(p.M - 1) * p.lda + p.K) : ((long)(p.K - 1) * p.lda + p.M);
+  const long extB = BKc ? ((long)(p.N - 1) * p.ldb + p.K) : ((long)(p.K - 1) * p.ldb + p.N);
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)A, (short)0, (int)(extA * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)B, (short)0, (int)(extB * 2), 0x00020000);
+  constexpr int PA = A_BYTES / 1024 / NW, PB = B_BYTES / 1024 / NW;
+  long baseA[PA], baseB[PB];
+  int krA[PA], krB[PB];
+  bool okA[PA], okB[PB];
+  dma_setup<AK, BMv, NW>(lane, wave, m0, p.M, p.lda, baseA, krA, okA);
+  dma_setup<BKc, BN, NW>(lane, wave, n0, p.N, p.ldb, baseB, krB, okB);
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int st = 0; st < NS - 1; ++st) {
+    if (st < nk) {
+      char* sl = smem + st * STAGE;
+      dma_issue<AK, BMv, NW>(ra, sl, wave, kbeg + st * BK, kend, p.lda, baseA, krA, okA);
+      dma_issue<BKc, BN, NW>(rb, sl + A_BYTES, wave, kbeg + st * BK, kend, p.ldb, baseB, krB, okB);
+    }
+  }
+  for (int kt = 0; kt < nk; ++kt) {
+    // stage kt landed for this wave: newer stages may stay in flight
+    const int newer = min(NS - 2, nk - 1 - kt);
+    if constexpr (NS >= 3) {
+      if (newer >= 1) wait_vm<LPW * (NS - 2)>();
+      else wait_vm<0>();
+    } else {
+      wait_vm<0>();
+    }
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (kt + NS - 1 < nk) {
+      char* sl = smem + ((kt + NS - 1) % NS) * STAGE;
+      dma_issue<AK, BMv, NW>(ra, sl, wave, kbeg + (kt + NS - 1) * BK, kend, p.lda, baseA, krA, okA);
+      dma_issue<BKc, BN, NW>(rb, sl + A_BYTES, wave, kbeg + (kt + NS - 1) * BK, kend, p.ldb, baseB, krB, okB);
+    }
+    const char* As = smem + (kt % NS) * STAGE;
+    const char* Bs = As + A_BYTES;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8 af[4], bfr[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = read_frag_p<AK>(As, wm * 64 + i * 16, s, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bfr[j] = read_frag_p<BKc>(Bs, wn * 64 + j * 16, s, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  // ---- epilogue: stage the wave's 64x64 f32 tile in LDS (row stride 68 floats: conflict-free
+  // writes), then every lane finishes 8 consecutive columns of a row with 16-B loads/stores.
+  __syncthreads();
+  float* ep = reinterpret_cast<float*>(smem) + wave * (64 * EP_LD);
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) ep[(i * 16 + (lane >> 4) * 4 + r) * EP_LD + j * 16 + (lane & 15)] = acc[i][j][r];
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS writes done (wave-private region)
+  if constexpr (EPI == EPI_STORE) {
+    if (p.ksplit > 1) {  // split-K partials: one 64-float row (256 contiguous bytes) per atomic wave-instruction
+      const int n1 = n0 + wn * 64 + lane;
+      const float bv = (p.bias && blockIdx.y == 0 && n1 < p.N) ? p.bias[n1] : 0.f;
+      float* Cf = reinterpret_cast<float*>(C);
+      for (int row = 0; row < 64; ++row) {
+        const int m = m0 + wm * 64 + row;
+        if (m < p.M && n1 < p.N) atomicAdd(Cf + (long)m * p.ldc + n1, ep[row * EP_LD + lane] * p.alpha + bv);
+      }
+      return;
+    }
+  }
+  const int cc = (lane & 7) * 8;
+  const int n = n0 + wn * 64 + cc;
+  const bool vec_ok = p.vec_ok && n + 8 <= p.N;
+#pragma unroll 2
+  for (int pass = 0; pass < 8; ++pass) {
+    const int row = pass * 8 + (lane >> 3);
+    const int m = m0 + wm * 64 + row;
+    if (m >= p.M) continue;
+    float v[8];
+    const float4 a0 = *reinterpret_cast<const float4*>(ep + row * EP_LD + cc);
+    const float4 a1 = *reinterpret_cast<const float4*>(ep + row * EP_LD + cc + 4);
+    v[0] = a0.x; v[1] = a0.y; v[2] = a0.z; v[3] = a0.w; v[4] = a1.x; v[5] = a1.y; v[6] = a1.z; v[7] = a1.w;
+    if (vec_ok) {
+      epilogue_vec8<EPI, OutT>(p, C, m, n, v);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (n + e < p.N) epilogue_elem<EPI, OutT>(p, C, m, n + e, v[e]);
+    }
+  }
+}
+
 template <bool AK, bool BKc, int EPI, typename OutT>
 static int launch(GemmArgs& a, int batch, hipStream_t st) {
   dim3 grid(a.tilesM * a.tilesN, a.ksplit > 1 ? a.ksplit : 1, batch);
@@ -259,13 +599,49 @@ static int launch(GemmArgs& a, int batch, hipStream_t st) {
   return 0;
 }
 
+template <bool AK, bool BKc, int EPI, typename OutT, int BMv, int NS>
+static int launch_v2(GemmArgs a, int batch, hipStream_t st) {
+  constexpr int LDS_RING = NS * (BMv * BK * 2 + BN * BK * 2);
+  constexpr int LDS_EP = (BMv / 32) * 64 * EP_LD * 4;
+  constexpr int LDS = LDS_RING > LDS_EP ? LDS_RING : LDS_EP;
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)gemm_bf16_dma_kernel<AK, BKc, EPI, OutT, BMv, NS>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    attr = true;
+  }
+  a.tilesM = (a.M + BMv - 1) / BMv;
+  dim3 grid(a.tilesM * a.tilesN, a.ksplit > 1 ? a.ksplit : 1, batch);
+  hipLaunchKernelGGL((gemm_bf16_dma_kernel<AK, BKc, EPI, OutT, BMv, NS>), grid, dim3(BMv * 2), LDS, st, a);
+  SLX_LAUNCH_CHECK("slx_gemm_bf16(dma)");
+  return 0;
+}
+
+// variant: 1 = v1 register-staged 128x128; 2 = DMA 128x128 NS2; 3 = DMA 128x128 NS3; 4 = DMA 128x128 NS4;
+//          5 = DMA 256x128 NS2; 6 = DMA 256x128 NS3; 0 = automatic
+template <bool AK, bool BKc, int EPI, typename OutT>
+static int launch_any(GemmArgs& a, int batch, hipStream_t st, int variant) {
+  const bool dma_ok = (!AK || a.K % BK == 0) && (!BKc || a.K % BK == 0) && (a.ksplit <= 1 || a.kchunk % BK == 0) &&
+                      a.drop_operand == 0;
+  if (variant == 0) variant = dma_ok ? 2 : 1;
+  if (variant != 1 && !dma_ok) variant = 1;
+  switch (variant) {
+    case 2: return launch_v2<AK, BKc, EPI, OutT, 128, 2>(a, batch, st);
+    case 3: return launch_v2<AK, BKc, EPI, OutT, 128, 3>(a, batch, st);
+    case 4: return launch_v2<AK, BKc, EPI, OutT, 128, 4>(a, batch, st);
+    case 5: return launch_v2<AK, BKc, EPI, OutT, 256, 2>(a, batch, st);
+    case 6: return launch_v2<AK, BKc, EPI, OutT, 256, 3>(a, batch, st);
+    default: return launch<AK, BKc, EPI, OutT>(a, batch, st);
+  }
+}
+
 template <int EPI, typename OutT>
-static int dispatch_layout(int layout, GemmArgs& a, int batch, hipStream_t st) {
+static int dispatch_layout(int layout, GemmArgs& a, int batch, hipStream_t st, int variant) {
   switch (layout) {
-    case SLX_GEMM_NT: return launch<true, true, EPI, OutT>(a, batch, st);
-    case SLX_GEMM_NN: return launch<true, false, EPI, OutT>(a, batch, st);
-    case SLX_GEMM_TN: return launch<false, false, EPI, OutT>(a, batch, st);
-    case SLX_GEMM_TT: return launch<false, true, EPI, OutT>(a, batch, st);
+    case SLX_GEMM_NT: return launch_any<true, true, EPI, OutT>(a, batch, st, variant);
+    case SLX_GEMM_NN: return launch_any<true, false, EPI, OutT>(a, batch, st, variant);
+    case SLX_GEMM_TN: return launch_any<false, false, EPI, OutT>(a, batch, st, variant);
+    case SLX_GEMM_TT: return launch_any<false, true, EPI, OutT>(a, batch, st, variant);
   }
   set_error("slx_gemm_bf16: bad layout %d", layout);
   return -22;
@@ -301,8 +677,21 @@ extern "C" int slx_gemm_bf16(const slx_gemm_desc* d, slx_stream_t stream) {
   a.resid = d->resid; a.ldr = d->ldr;
   a.accumulate = d->accumulate;
   a.seed = d->seed; a.drop_p = d->drop_p; a.ldmask = d->ldmask;
+  a.drop_operand = d->drop_operand;
+  SLX_CHECK_ARG(d->drop_operand == 0 || (d->epilogue == SLX_EPI_STORE && d->drop_p >= 0.f && d->drop_p < 1.f),
+                "slx_gemm_bf16: operand dropout needs EPI_STORE and 0 <= p < 1");
   a.tilesM = (d->M + BM - 1) / BM;
   a.tilesN = (d->N + BN - 1) / BN;
+  {
+    const int esz = d->out_f32 ? 4 : 2;
+    bool ok = d->ldc % 8 == 0 && ((uintptr_t)d->C % 16) == 0 && (d->batch <= 1 || d->sC % 8 == 0);
+    (void)esz;
+    if (d->aux) ok = ok && d->ldaux % 8 == 0 && ((uintptr_t)d->aux % 16) == 0;
+    if (d->aux_out) ok = ok && d->ldaux_out % 8 == 0 && ((uintptr_t)d->aux_out % 16) == 0;
+    if (d->resid) ok = ok && d->ldr % 8 == 0 && ((uintptr_t)d->resid % 16) == 0;
+    if (d->epilogue == SLX_EPI_SWIGLU_BWD) ok = ok && d->N % 8 == 0;
+    a.vec_ok = ok ? 1 : 0;
+  }
   const int batch = d->batch < 1 ? 1 : d->batch;
   hipStream_t st = (hipStream_t)stream;
   a.ksplit = 1;
@@ -329,25 +718,26 @@ extern "C" int slx_gemm_bf16(const slx_gemm_desc* d, slx_stream_t stream) {
       }
     }
   }
+  const int v = d->variant;
   switch (d->epilogue) {
     case SLX_EPI_STORE:
-      return d->out_f32 ? dispatch_layout<EPI_STORE, float>(d->layout, a, batch, st)
-                        : dispatch_layout<EPI_STORE, bf16>(d->layout, a, batch, st);
+      return d->out_f32 ? dispatch_layout<EPI_STORE, float>(d->layout, a, batch, st, v)
+                        : dispatch_layout<EPI_STORE, bf16>(d->layout, a, batch, st, v);
     case SLX_EPI_GELU:
       SLX_CHECK_ARG(!d->out_f32 && d->layout == SLX_GEMM_NT && d->aux_out, "slx_gemm_bf16: GELU needs NT, bf16 out, aux_out");
-      return launch<true, true, EPI_GELU, bf16>(a, batch, st);
+      return launch_any<true, true, EPI_GELU, bf16>(a, batch, st, v);
     case SLX_EPI_RESID_LS:
       SLX_CHECK_ARG(d->out_f32 && d->layout == SLX_GEMM_NT && d->resid && d->ls, "slx_gemm_bf16: RESID_LS needs NT, f32 out, resid, ls");
-      return launch<true, true, EPI_RESID_LS, float>(a, batch, st);
+      return launch_any<true, true, EPI_RESID_LS, float>(a, batch, st, v);
     case SLX_EPI_GELU_BWD:
       SLX_CHECK_ARG(!d->out_f32 && d->layout == SLX_GEMM_NN && d->aux, "slx_gemm_bf16: GELU_BWD needs NN, bf16 out, aux");
-      return launch<true, false, EPI_GELU_BWD, bf16>(a, batch, st);
+      return launch_any<true, false, EPI_GELU_BWD, bf16>(a, batch, st, v);
     case SLX_EPI_SWIGLU_BWD:
       SLX_CHECK_ARG(!d->out_f32 && d->layout == SLX_GEMM_NN && d->aux, "slx_gemm_bf16: SWIGLU_BWD needs NN, bf16 out, aux");
-      return launch<true, false, EPI_SWIGLU_BWD, bf16>(a, batch, st);
+      return launch_any<true, false, EPI_SWIGLU_BWD, bf16>(a, batch, st, v);
     case SLX_EPI_DROPMASK:
       SLX_CHECK_ARG(d->out_f32 && d->layout == SLX_GEMM_NN, "slx_gemm_bf16: DROPMASK needs NN, f32 out");
-      return launch<true, false, EPI_DROPMASK, float>(a, batch, st);
+      return launch_any<true, false, EPI_DROPMASK, float>(a, batch, st, v);
   }
   set_error("slx_gemm_bf16: bad epilogue %d", d->epilogue);
   return -22;

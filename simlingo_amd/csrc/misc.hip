@@ -78,21 +78,23 @@ __global__ void swiglu_fwd_kernel(const bf16* gu, long ldgu, bf16* out, long ldo
   *reinterpret_cast<bf16x8*>(out + m * ldo + f) = o;
 }
 
-// Column partial sums over a strided set of rows: partial[blk, c] = sum_rows x[r, c] (* ls[c])
-// mode 0: x bf16 ; mode 1: x f32 ; mode 2 (layer-scale grad): x = dres f32, y bf16 ->
-//   g = bf16(dres*ls) written, partial[blk, c] = sum dres*y, partial[blk, N + c] = sum dres*ls
+// Column sums over a strided set of rows, accumulated into the outputs with f32 atomics
+// (outputs pre-zeroed by the host wrapper unless accumulating):
+// mode 0: out0[c] += sum_r x[r,c] (x bf16) ; mode 1: same with x f32 ;
+// mode 2 (layer-scale branch backward): x = dres f32, y bf16 -> g = bf16(dres*ls) written,
+//   out0[c] += sum dres*y (d ls), out1[c] += sum dres*ls (d bias)
 template <int MODE>
-__global__ __launch_bounds__(256) void colsum_kernel(const void* xv, long ldx, long M, int N, float* partial,
+__global__ __launch_bounds__(256) void colsum_kernel(const void* xv, long ldx, long M, int N, float* out0, float* out1,
                                                      const float* ls, const bf16* y, long ldy, bf16* g, long ldg) {
   const int c0 = (blockIdx.y * 256 + threadIdx.x) * 4;
-  if (c0 >= N) return;
+  const bool live = c0 < N;
   float s[4] = {0, 0, 0, 0}, s2[4] = {0, 0, 0, 0};
   float lsv[4] = {1, 1, 1, 1};
-  if (MODE == 2) {
+  if (MODE == 2 && live) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) lsv[e] = ls[c0 + e];
   }
-  for (long r = blockIdx.x; r < M; r += gridDim.x) {
+  for (long r = blockIdx.x; live && r < M; r += gridDim.x) {
     float v[4];
     if (MODE == 0) {
       const bf16x4 t = *reinterpret_cast<const bf16x4*>((const bf16*)xv + r * ldx + c0);
@@ -118,16 +120,23 @@ __global__ __launch_bounds__(256) void colsum_kernel(const void* xv, long ldx, l
       for (int e = 0; e < 4; ++e) s[e] += v[e];
     }
   }
+  // transpose through LDS: each atomic wave-instruction then covers 256 contiguous bytes
+  __shared__ float cs[2][1024];
+  const int lc = threadIdx.x * 4;
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
-    partial[(long)blockIdx.x * 2 * N + c0 + e] = (MODE == 2) ? s2[e] : s[e];
-    if (MODE == 2) partial[(long)blockIdx.x * 2 * N + N + c0 + e] = s[e];
+    cs[0][lc + e] = (MODE == 2) ? s2[e] : s[e];
+    if (MODE == 2) cs[1][lc + e] = s[e];
+  }
+  __syncthreads();
+  const int cb = blockIdx.y * 1024;
+  for (int c = threadIdx.x; c < 1024 && cb + c < N; c += 256) {
+    atomicAdd(out0 + cb + c, cs[0][c]);
+    if (MODE == 2) atomicAdd(out1 + cb + c, cs[1][c]);
   }
 }
 
-}  // namespace slx
-#include "colreduce.h"
-namespace slx {
+
 
 // LLM input assembly: out[i, :] (f32) from code[i] = (kind << 28) | index
 //   kind 0: token  -> embed[min(index, V-1)] (bf16 table; ids clamped like adaptors.py:256)
@@ -432,6 +441,23 @@ __global__ void cast_rows_kernel(const float* src, long lds, bf16* dst, long ldd
   *reinterpret_cast<bf16x4*>(dst + m * ldd + c) = o;
 }
 
+// Batched 2-D scaled copy f32 -> bf16: entry e of `tab` = {src, lds, dst, ldd, rows, cols, scale(bits)}.
+// Packs every LoRA B (times alpha/r) into the fused [W | s*B] GEMM operands in one launch.
+__global__ void pack_scaled_kernel(const long long* tab, int n) {
+  const int e = blockIdx.x;
+  const long long* t = tab + 7 * (long)e;
+  const float* src = reinterpret_cast<const float*>(t[0]);
+  const long lds = t[1];
+  bf16* dst = reinterpret_cast<bf16*>(t[2]);
+  const long ldd = t[3];
+  const long rows = t[4], cols = t[5];
+  const float sc = __int_as_float((int)t[6]);
+  for (long i = (long)blockIdx.y * blockDim.x + threadIdx.x; i < rows * cols; i += (long)gridDim.y * blockDim.x) {
+    const long r = i / cols, c = i % cols;
+    dst[r * ldd + c] = (bf16)(src[r * lds + c] * sc);
+  }
+}
+
 __global__ void cast_kernel(const float* src, bf16* dst, long n) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) dst[i] = (bf16)src[i];
@@ -480,12 +506,13 @@ int slx_colsum_ws_floats(int N) { return 256 * 2 * N; }
 // mode 0: x bf16, 1: x f32 -> out[c] (+)= sum_r x[r,c]
 int slx_colsum(int mode, const void* x, int64_t ldx, int64_t M, int N, float* out, int accumulate, float* ws, slx_stream_t s) {
   SLX_CHECK_ARG(N % 4 == 0 && (mode == 0 || mode == 1), "slx_colsum: N %% 4 / mode");
-  const int nblk = (int)(M < 256 ? (M > 0 ? M : 1) : 256);
-  dim3 grid(nblk, (N / 4 + 255) / 256);
+  (void)ws;
   hipStream_t st = (hipStream_t)s;
-  if (mode == 0) hipLaunchKernelGGL((colsum_kernel<0>), grid, dim3(256), 0, st, x, ldx, M, N, ws, nullptr, nullptr, 0L, nullptr, 0L);
-  else hipLaunchKernelGGL((colsum_kernel<1>), grid, dim3(256), 0, st, x, ldx, M, N, ws, nullptr, nullptr, 0L, nullptr, 0L);
-  launch_colreduce(ws, nblk, N, 2L * N, out, accumulate, st);
+  if (!accumulate) hipMemsetAsync(out, 0, (size_t)N * sizeof(float), st);
+  const int nblk = (int)(M < 512 ? (M > 0 ? M : 1) : 512);
+  dim3 grid(nblk, (N / 4 + 255) / 256);
+  if (mode == 0) hipLaunchKernelGGL((colsum_kernel<0>), grid, dim3(256), 0, st, x, ldx, M, N, out, (float*)nullptr, nullptr, nullptr, 0L, nullptr, 0L);
+  else hipLaunchKernelGGL((colsum_kernel<1>), grid, dim3(256), 0, st, x, ldx, M, N, out, (float*)nullptr, nullptr, nullptr, 0L, nullptr, 0L);
   SLX_LAUNCH_CHECK("slx_colsum");
   return 0;
 }
@@ -494,12 +521,15 @@ int slx_colsum(int mode, const void* x, int64_t ldx, int64_t M, int N, float* ou
 int slx_ls_branch_bwd(const float* dres, int64_t ldr, const float* ls, const void* y, int64_t ldy, void* g, int64_t ldg,
                       int64_t M, int N, float* dls, float* dbias, int accumulate, float* ws, slx_stream_t s) {
   SLX_CHECK_ARG(N % 4 == 0, "slx_ls_branch_bwd: N %% 4");
-  const int nblk = (int)(M < 256 ? (M > 0 ? M : 1) : 256);
-  dim3 grid(nblk, (N / 4 + 255) / 256);
+  (void)ws;
   hipStream_t st = (hipStream_t)s;
-  hipLaunchKernelGGL((colsum_kernel<2>), grid, dim3(256), 0, st, (const void*)dres, ldr, M, N, ws, ls, (const bf16*)y, ldy, (bf16*)g, ldg);
-  launch_colreduce(ws, nblk, N, 2L * N, dls, accumulate, st);
-  launch_colreduce(ws + N, nblk, N, 2L * N, dbias, accumulate, st);
+  if (!accumulate) {
+    hipMemsetAsync(dls, 0, (size_t)N * sizeof(float), st);
+    hipMemsetAsync(dbias, 0, (size_t)N * sizeof(float), st);
+  }
+  const int nblk = (int)(M < 512 ? (M > 0 ? M : 1) : 512);
+  dim3 grid(nblk, (N / 4 + 255) / 256);
+  hipLaunchKernelGGL((colsum_kernel<2>), grid, dim3(256), 0, st, (const void*)dres, ldr, M, N, dls, dbias, ls, (const bf16*)y, ldy, (bf16*)g, ldg);
   SLX_LAUNCH_CHECK("slx_ls_branch_bwd");
   return 0;
 }
@@ -652,6 +682,13 @@ int slx_cast_rows(const float* src, int64_t lds, void* dst, int64_t ldd, int64_t
   if (!M) return 0;
   hipLaunchKernelGGL(cast_rows_kernel, g1(M * (N / 4)), dim3(256), 0, (hipStream_t)s, src, lds, (bf16*)dst, ldd, M, N);
   SLX_LAUNCH_CHECK("slx_cast_rows");
+  return 0;
+}
+
+int slx_pack_scaled(const int64_t* table, int n, slx_stream_t s) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(pack_scaled_kernel, dim3(n, 32), dim3(256), 0, (hipStream_t)s, (const long long*)table, n);
+  SLX_LAUNCH_CHECK("slx_pack_scaled");
   return 0;
 }
 

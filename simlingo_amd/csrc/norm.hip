@@ -29,7 +29,8 @@ struct NormArgs {
   // bwd
   const float* dy; long lddy;
   float* dx; long lddx; int dx_accumulate;
-  float* partial;   // [nblk, 2, D] (dgamma | dbeta)
+  float* partial;   // unused (kept for ABI workspace sizing)
+  float* dgamma; float* dbeta;
 };
 
 template <int VPT, bool RMS>
@@ -152,29 +153,34 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(NormArgs a) {
       *reinterpret_cast<float4*>(dst) = o;
     }
   }
-  if (a.partial) {
+  // column partials -> dgamma / dbeta (pre-zeroed or accumulating) with f32 atomics, transposed
+  // through LDS so that each atomic wave-instruction covers 256 contiguous bytes
+  if (a.dgamma || a.dbeta) {
+    __shared__ float cs[2][VPT * 256];
 #pragma unroll
     for (int i = 0; i < VPT / 4; ++i) {
       const int col = (tid + i * 256) * 4;
-      if (col >= a.D) continue;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        a.partial[(long)blockIdx.x * 2 * a.D + col + e] = pg[4 * i + e];
-        a.partial[(long)blockIdx.x * 2 * a.D + a.D + col + e] = pb[4 * i + e];
+        cs[0][col + e] = pg[4 * i + e];
+        cs[1][col + e] = pb[4 * i + e];
       }
+    }
+    __syncthreads();
+    for (int c = tid; c < a.D; c += 256) {
+      if (a.dgamma) atomicAdd(a.dgamma + c, cs[0][c]);
+      if (a.dbeta) atomicAdd(a.dbeta + c, cs[1][c]);
     }
   }
 }
 
-}  // namespace slx
-#include "colreduce.h"
-namespace slx {
+
 
 }  // namespace slx
 
 using namespace slx;
 
-static constexpr int kBwdBlocks = 256;
+static constexpr int kBwdBlocks = 512;
 
 template <bool RMS>
 static int norm_fwd(NormArgs& a, hipStream_t st) {
@@ -190,15 +196,16 @@ template <bool RMS>
 static int norm_bwd(NormArgs& a, float* dgamma, float* dbeta, int accumulate, hipStream_t st) {
   const int nblk = (int)(a.rows < kBwdBlocks ? a.rows : kBwdBlocks);
   SLX_CHECK_ARG(a.D % 4 == 0 && a.D <= 4096, "norm bwd: D=%d must be a multiple of 4 and <= 4096", a.D);
+  a.dgamma = dgamma;
+  a.dbeta = dbeta;
+  if (!accumulate) {
+    if (dgamma) hipMemsetAsync(dgamma, 0, a.D * sizeof(float), st);
+    if (dbeta) hipMemsetAsync(dbeta, 0, a.D * sizeof(float), st);
+  }
   if (a.D <= 1024) hipLaunchKernelGGL((norm_bwd_kernel<4, RMS>), dim3(nblk), dim3(256), 0, st, a);
   else if (a.D <= 2048) hipLaunchKernelGGL((norm_bwd_kernel<8, RMS>), dim3(nblk), dim3(256), 0, st, a);
   else hipLaunchKernelGGL((norm_bwd_kernel<16, RMS>), dim3(nblk), dim3(256), 0, st, a);
   SLX_LAUNCH_CHECK("slx_norm_bwd");
-  if (a.partial) {
-    if (dgamma) launch_colreduce(a.partial, nblk, a.D, (long)2 * a.D, dgamma, accumulate, st);
-    if (dbeta) launch_colreduce(a.partial + a.D, nblk, a.D, (long)2 * a.D, dbeta, accumulate, st);
-    SLX_LAUNCH_CHECK("slx_norm_bwd(reduce)");
-  }
   return 0;
 }
 
@@ -227,7 +234,7 @@ extern "C" int slx_norm_bwd(const slx_norm_desc* d, const float* dy, int64_t ldd
   fill(a, d);
   a.dy = dy; a.lddy = lddy; a.dx = dx; a.lddx = lddx; a.dx_accumulate = dx_accumulate;
   a.partial = (dgamma || dbeta) ? partial_ws : nullptr;
-  SLX_CHECK_ARG(!(dgamma || dbeta) || partial_ws, "slx_norm_bwd: partial_ws required for dgamma/dbeta");
+
   return d->rms ? norm_bwd<true>(a, dgamma, dbeta, param_accumulate, (hipStream_t)stream)
                 : norm_bwd<false>(a, dgamma, dbeta, param_accumulate, (hipStream_t)stream);
 }

@@ -36,6 +36,10 @@ def _pad8(n):
     return (n + 7) // 8 * 8
 
 
+def _pad64(n):
+    return (n + 63) // 64 * 64
+
+
 class VLAEngine:
     def __init__(self, cfg: VLAConfig, device, params: dict[str, torch.Tensor] | None = None, seed: int = 0,
                  bucket_bytes: int = 32 << 20):
@@ -77,7 +81,7 @@ class VLAEngine:
         self.wbf.copy_(self.master.to(BF16))
         # LM head padded to a multiple of 8 rows (its dgrad GEMM reads K = V rows as [K][N])
         V, d = cfg.vocab, cfg.llm_dim
-        self.Vp = _pad8(V)
+        self.Vp = _pad64(V)
         if self.Vp != V:
             lm = torch.zeros(self.Vp, d, dtype=BF16, device=dev)
             lm[:V].copy_(self.W["llm.lm_head"])
@@ -103,6 +107,7 @@ class VLAEngine:
         self.step_seed = 0
         self.saved = None
         self._cos_sin = {}
+        self._build_lora_cat()
         self.probe_site = None     # name of a call site to bracket with HIP events (bench roofline)
         self.probe_events = []
 
@@ -130,6 +135,51 @@ class VLAEngine:
         """bf16 views that are not plain slices of the flat buffer (after every optimizer step)."""
         cfg = self.cfg
         self.wpatch[:, : cfg.patch_k].copy_(self.W["vit.patch.w"])
+        if getattr(self, "_pack_tab", None) is not None:
+            K.call("slx_pack_scaled", K.P(self._pack_tab), self._pack_n, K.stream_ptr())
+
+    # LoRA folded into the frozen GEMMs by K-concatenation: y = [x | t] . [W | s*B_blockdiag]^T with
+    # t = drop(x) A^T written into the extra columns of the activation buffer. Per layer and group:
+    #   qkv  : x = RMSNorm1(X) [M, d]   -> W_cat [d + 2kv, d + 128]   (t_q, t_k, t_v, pad)
+    #   o    : x = attention out [M, d] -> W_cat [d, d + 64]         (t_o, pad)
+    #   gu   : x = RMSNorm2 [M, d]      -> W_cat [2F, d + 64]        (t_gate, t_up)
+    #   down : x = SwiGLU act [M, F]    -> W_cat [d, F + 64]         (t_down, pad)
+    # The dgrad GEMM dy . W_cat then returns [dx_base | s * dy_s B_s] = [dx_base | dt] in one pass.
+    LORA_GROUPS = (("qkv", ("q", "k", "v"), 128), ("o", ("o",), 64), ("gu", ("gate", "up"), 64), ("down", ("down",), 64))
+
+    def _build_lora_cat(self):
+        cfg = self.cfg
+        self.cat = []
+        self._pack_tab = None
+        if not cfg.lora:
+            return
+        d, F = cfg.llm_dim, cfg.llm_ffn
+        qn, kn = cfg.llm_heads * 64, cfg.llm_kv_heads * 64
+        s = float(cfg.lora_scale)
+        entries = []
+        r = cfg.lora_r
+        for i in range(cfg.llm_layers):
+            p = f"llm.{i}."
+            cats = {}
+            for g, sites, pad in self.LORA_GROUPS:
+                base = {"qkv": self.W[p + "qkv_w"], "o": self.W[p + "o_w"], "gu": self.W[p + "gate_up_w"],
+                        "down": self.W[p + "down_w"]}[g]
+                N, Kin = base.shape
+                w = torch.zeros(N, Kin + pad, dtype=BF16, device=self.device)
+                w[:, :Kin].copy_(base)
+                row = 0
+                for j, site in enumerate(sites):
+                    out_s = lora_io(cfg, site)[1]
+                    b = self.P[p + f"lora.{site}.b"]  # [out_s, r] f32 master
+                    dst = w[row:row + out_s, Kin + r * j: Kin + r * (j + 1)]
+                    entries.append([b.data_ptr(), b.stride(0), dst.data_ptr(), dst.stride(0), out_s, r,
+                                    int(np.float32(s).view(np.int32))])
+                    row += out_s
+                cats[g] = w
+            self.cat.append(cats)
+        self._pack_tab = torch.tensor(entries, dtype=torch.int64, device=self.device)
+        self._pack_n = len(entries)
+        K.call("slx_pack_scaled", K.P(self._pack_tab), self._pack_n, K.stream_ptr())
 
     def set_distributed(self, pg=None, world: int = 1):
         self.world = world
@@ -154,8 +204,8 @@ class VLAEngine:
     def _z(self, *shape, dtype=F32):
         return torch.zeros(*shape, dtype=dtype, device=self.device)
 
-    def _norm(self, x, gamma, beta, rows, D, eps, rms=False, ps=0, tpi=0, ldx=None):
-        y = self._e(rows, D)
+    def _norm(self, x, gamma, beta, rows, D, eps, rms=False, ps=0, tpi=0, ldx=None, out=None):
+        y = self._e(rows, D) if out is None else out
         mean = None if rms else self._e(rows, dtype=F32)
         rstd = self._e(rows, dtype=F32)
         d = K.norm_desc(x, gamma, beta, y, mean, rstd, rows, D, eps, rms=rms, ps_grid=ps, tok_per_img=tpi, ldx=ldx)
@@ -170,7 +220,7 @@ class VLAEngine:
     def _colsum(self, x, out, mode):
         M, N = x.shape
         ws = self._ws(K.lib().slx_colsum_ws_floats(N))
-        K.call("slx_colsum", mode, K.P(x), x.stride(0), M, N, K.P(out), 0, K.P(ws), K.stream_ptr())
+        K.call("slx_colsum", mode, K.P(x), x.stride(0), M, N, K.P(out), 1, K.P(ws), K.stream_ptr())
 
     # ==========================================================================================
     # forward
@@ -265,37 +315,46 @@ class VLAEngine:
         cos, sin = self.rope_tables(S)
         seql = dplan["seqlens"]
         llm_saved = []
+        lora = cfg.lora
+        r = cfg.lora_r
         for i in range(cfg.llm_layers):
             p = f"llm.{i}."
             L = {}
-            h, nrm1 = self._norm(X, self.P[p + "ln1"], None, Ml, d, cfg.rms_eps, rms=True)
+            cat = self.cat[i] if lora else None
+            Pq, Po, Pg, Pd = (128, 64, 64, 64) if lora else (0, 0, 0, 0)
+            hx = (self._z if lora else self._e)(Ml, d + Pq, dtype=BF16)
+            h, nrm1 = self._norm(X, self.P[p + "ln1"], None, Ml, d, cfg.rms_eps, rms=True, out=hx[:, :d])
+            if lora:
+                for j, site in enumerate(("q", "k", "v")):
+                    L[site] = self._lora_down(hx[:, :d], i, site, hx[:, d + r * j: d + r * (j + 1)], sv)
             qkv = self._e(Ml, nqkv)
-            K.mm(h, self.W[p + "qkv_w"], qkv, bias=self.P[p + "qkv_b"])
-            if cfg.lora:
-                for site, c0, c1 in (("q", 0, qn), ("k", qn, qn + kn), ("v", qn + kn, nqkv)):
-                    L[site] = self._lora_fwd(h, i, site, qkv[:, c0:c1], sv, d)
+            K.mm(hx, cat["qkv"] if lora else self.W[p + "qkv_w"], qkv, bias=self.P[p + "qkv_b"])
             K.rope(qkv, Ml, S, Hq + Hk, cos, sin)  # q and k heads are the first Hq+Hk head slots
-            o = self._e(Ml, qn)
+            ox = (self._z if lora else self._e)(Ml, qn + Po, dtype=BF16)
+            o = ox[:, :qn]
             lse = self._e(B * Hq * S, dtype=F32)
             K.attn_fwd(qkv[:, :qn], qkv[:, qn:qn + kn], qkv[:, qn + kn:], o, lse, B=B, S=S, Hq=Hq, Hkv=Hk, causal=True,
                        seqlens=seql)
+            if lora:
+                L["o"] = self._lora_down(o, i, "o", ox[:, qn:qn + r], sv)
             Xm = self._e(Ml, d, dtype=F32)
-            K.mm(o, self.W[p + "o_w"], Xm, epi=K.EPI_RESID_LS, resid=X, ldr=d, ls=self.ones_d)
-            if cfg.lora:
-                L["o"] = self._lora_fwd(o, i, "o", Xm, sv, qn)
-            h2, nrm2 = self._norm(Xm, self.P[p + "ln2"], None, Ml, d, cfg.rms_eps, rms=True)
+            K.mm(ox, cat["o"] if lora else self.W[p + "o_w"], Xm, epi=K.EPI_RESID_LS, resid=X, ldr=d, ls=self.ones_d)
+            h2x = (self._z if lora else self._e)(Ml, d + Pg, dtype=BF16)
+            h2, nrm2 = self._norm(Xm, self.P[p + "ln2"], None, Ml, d, cfg.rms_eps, rms=True, out=h2x[:, :d])
+            if lora:
+                L["gate"] = self._lora_down(h2, i, "gate", h2x[:, d:d + r], sv)
+                L["up"] = self._lora_down(h2, i, "up", h2x[:, d + r:d + 2 * r], sv)
             gu = self._e(Ml, 2 * Fl)
-            K.mm(h2, self.W[p + "gate_up_w"], gu)
-            if cfg.lora:
-                L["gate"] = self._lora_fwd(h2, i, "gate", gu[:, :Fl], sv, d)
-                L["up"] = self._lora_fwd(h2, i, "up", gu[:, Fl:], sv, d)
-            act = self._e(Ml, Fl)
+            K.mm(h2x, cat["gu"] if lora else self.W[p + "gate_up_w"], gu)
+            ax = (self._z if lora else self._e)(Ml, Fl + Pd, dtype=BF16)
+            act = ax[:, :Fl]
             K.call("slx_swiglu_fwd", K.P(gu), gu.stride(0), K.P(act), act.stride(0), Ml, Fl, K.stream_ptr())
+            if lora:
+                L["down"] = self._lora_down(act, i, "down", ax[:, Fl:Fl + r], sv)
             Xo = self._e(Ml, d, dtype=F32)
-            K.mm(act, self.W[p + "down_w"], Xo, epi=K.EPI_RESID_LS, resid=Xm, ldr=d, ls=self.ones_d)
-            if cfg.lora:
-                L["down"] = self._lora_fwd(act, i, "down", Xo, sv, Fl)
-            llm_saved.append(dict(X=X, h=h, n1=nrm1, qkv=qkv, o=o, lse=lse, Xm=Xm, h2=h2, n2=nrm2, gu=gu, act=act,
+            K.mm(ax, cat["down"] if lora else self.W[p + "down_w"], Xo, epi=K.EPI_RESID_LS, resid=Xm, ldr=d,
+                 ls=self.ones_d)
+            llm_saved.append(dict(X=X, hx=hx, n1=nrm1, qkv=qkv, ox=ox, lse=lse, Xm=Xm, h2x=h2x, n2=nrm2, gu=gu, ax=ax,
                                   lora=L))
             X = Xo
         sv["llm"] = llm_saved
@@ -343,20 +402,16 @@ class VLAEngine:
         self.saved = sv
         return out4, route_pred, speed_pred
 
-    def _lora_fwd(self, x, i, site, out, sv, kin):
-        """out (+)= s * (drop(x) A^T) B^T; returns saved (t, xd, seed)."""
+    def _lora_down(self, x, i, site, t_out, sv):
+        """t_out = drop(x) A^T (bf16, written into the extra columns of the activation buffer).
+        Dropout is applied while loading x (hash mask, regenerated in backward). Returns the seed."""
         cfg = self.cfg
-        p = f"llm.{i}.lora.{site}."
-        M = x.shape[0]
         seed = sv["seed"] + 131 * i + 7 * LORA_SITES.index(site) + 1
-        xd = x
-        if sv["drop"] > 0:
-            xd = self._e(M, kin)
-            K.call("slx_dropout", K.P(x), x.stride(0), K.P(xd), kin, M, kin, seed, sv["drop"], kin, K.stream_ptr())
-        t = self._e(M, cfg.lora_r)
-        K.mm(xd, self.W[p + "a"], t)
-        K.mm(t, self.W[p + "b"], out, alpha=cfg.lora_scale, accumulate=True)
-        return (t, xd, seed)
+        kin = x.shape[1]
+        drop = sv["drop"]
+        K.mm(x, self.W[f"llm.{i}.lora.{site}.a"], t_out, drop_operand=1 if drop > 0 else 0, seed=seed, drop_p=drop,
+             ldmask=kin)
+        return seed
 
     def _mlp_fwd(self, x, layers):
         """driving head: list of (prefix, out_dim, act) -> saved [(out, pre, in)]"""
@@ -385,6 +440,7 @@ class VLAEngine:
         d, D = cfg.llm_dim, cfg.vit_dim
         nr, ns = cfg.n_route, cfg.n_speed
         dplan = sv["dplan"]
+        self.grad.zero_()  # one memset per step; every gradient producer below accumulates
         gs = self._e(3, dtype=F32)
         if dlosses is not None:
             dlosses = dlosses.float().contiguous()
@@ -418,48 +474,55 @@ class VLAEngine:
         cos, sin = self.rope_tables(S)
         ws = K.attn_ws(B, S, Hq, Hk, self.device)
         dxb = self._e(Ml, d)
+        lora = cfg.lora
+        r = cfg.lora_r
         for i in reversed(range(cfg.llm_layers)):
             p = f"llm.{i}."
             Ls = sv["llm"][i]
-            L = Ls["lora"]
-            # down projection (+LoRA): Xo = Xm + act Wd^T + s t_d B_d^T
+            cat = self.cat[i] if lora else None
+            Pq, Po, Pg, Pd = (128, 64, 64, 64) if lora else (0, 0, 0, 0)
+            hx, ox, h2x, ax = Ls["hx"], Ls["ox"], Ls["h2x"], Ls["ax"]
+            # down projection: Xo = Xm + [act | t_d] . [Wd | s B_d]^T
             K.call("slx_cast_rows", K.P(dX), d, K.P(dxb), d, Ml, d, K.stream_ptr())
-            dact = self._e(Ml, Fl, dtype=F32)
-            K.mm(dxb, self.W[p + "down_w"], dact, tb=False)
-            if cfg.lora:
-                self._lora_bwd(dxb, L["down"], i, "down", dact, sv)
+            dax = self._e(Ml, Fl + Pd, dtype=F32)
+            K.mm(dxb, cat["down"] if lora else self.W[p + "down_w"], dax, tb=False)
+            if lora:
+                self._lora_bwd(dxb, ax[:, Fl:Fl + r], ax[:, :Fl], dax[:, Fl:Fl + r], dax[:, :Fl], i, "down", sv)
             dgu = self._e(Ml, 2 * Fl)
-            K.call("slx_swiglu_bwd", K.P(dact), Fl, K.P(Ls["gu"]), 2 * Fl, K.P(dgu), 2 * Fl, Ml, Fl, K.stream_ptr())
-            del dact
-            dh2 = self._e(Ml, d, dtype=F32)
-            K.mm(dgu, self.W[p + "gate_up_w"], dh2, tb=False)
-            if cfg.lora:
-                self._lora_bwd(dgu[:, :Fl], L["gate"], i, "gate", dh2, sv)
-                self._lora_bwd(dgu[:, Fl:], L["up"], i, "up", dh2, sv)
+            K.call("slx_swiglu_bwd", K.P(dax), dax.stride(0), K.P(Ls["gu"]), 2 * Fl, K.P(dgu), 2 * Fl, Ml, Fl,
+                   K.stream_ptr())
+            del dax
+            dh2x = self._e(Ml, d + Pg, dtype=F32)
+            K.mm(dgu, cat["gu"] if lora else self.W[p + "gate_up_w"], dh2x, tb=False)
+            if lora:
+                self._lora_bwd(dgu[:, :Fl], h2x[:, d:d + r], h2x[:, :d], dh2x[:, d:d + r], dh2x[:, :d], i, "gate", sv)
+                self._lora_bwd(dgu[:, Fl:], h2x[:, d + r:d + 2 * r], h2x[:, :d], dh2x[:, d + r:d + 2 * r], dh2x[:, :d], i,
+                               "up", sv)
             del dgu
-            K.norm_bwd(Ls["n2"], dh2, dX, dx_accumulate=True)
-            # o projection (+LoRA)
+            K.norm_bwd(Ls["n2"], dh2x, dX, dx_accumulate=True)
+            # o projection
             K.call("slx_cast_rows", K.P(dX), d, K.P(dxb), d, Ml, d, K.stream_ptr())
-            do = self._e(Ml, qn, dtype=F32)
-            K.mm(dxb, self.W[p + "o_w"], do, tb=False)
-            if cfg.lora:
-                self._lora_bwd(dxb, L["o"], i, "o", do, sv)
+            dox = self._e(Ml, qn + Po, dtype=F32)
+            K.mm(dxb, cat["o"] if lora else self.W[p + "o_w"], dox, tb=False)
+            if lora:
+                self._lora_bwd(dxb, ox[:, qn:qn + r], ox[:, :qn], dox[:, qn:qn + r], dox[:, :qn], i, "o", sv)
             dob = self._e(Ml, qn)
-            K.call("slx_cast_rows", K.P(do), qn, K.P(dob), qn, Ml, qn, K.stream_ptr())
-            del do
+            K.call("slx_cast_rows", K.P(dox), dox.stride(0), K.P(dob), qn, Ml, qn, K.stream_ptr())
+            del dox
             qkv = Ls["qkv"]
             dqkv = self._e(Ml, nqkv)
-            K.attn_bwd(qkv[:, :qn], qkv[:, qn:qn + kn], qkv[:, qn + kn:], Ls["o"], Ls["lse"], dob,
+            K.attn_bwd(qkv[:, :qn], qkv[:, qn:qn + kn], qkv[:, qn + kn:], ox[:, :qn], Ls["lse"], dob,
                        dqkv[:, :qn], dqkv[:, qn:qn + kn], dqkv[:, qn + kn:], ws, rope_cos=cos, rope_sin=sin,
                        B=B, S=S, Hq=Hq, Hkv=Hk, causal=True, seqlens=dplan["seqlens"])
-            dh = self._e(Ml, d, dtype=F32)
-            K.mm(dqkv, self.W[p + "qkv_w"], dh, tb=False)
-            if cfg.lora:
-                for site, c0, c1 in (("q", 0, qn), ("k", qn, qn + kn), ("v", qn + kn, nqkv)):
-                    self._lora_bwd(dqkv[:, c0:c1], L[site], i, site, dh, sv)
-            K.norm_bwd(Ls["n1"], dh, dX, dx_accumulate=True)
-            del dqkv, dh, dh2
-            if cfg.lora:
+            dhx = self._e(Ml, d + Pq, dtype=F32)
+            K.mm(dqkv, cat["qkv"] if lora else self.W[p + "qkv_w"], dhx, tb=False)
+            if lora:
+                for j, (site, c0, c1) in enumerate((("q", 0, qn), ("k", qn, qn + kn), ("v", qn + kn, nqkv))):
+                    self._lora_bwd(dqkv[:, c0:c1], hx[:, d + r * j:d + r * (j + 1)], hx[:, :d],
+                                   dhx[:, d + r * j:d + r * (j + 1)], dhx[:, :d], i, site, sv)
+            K.norm_bwd(Ls["n1"], dhx, dX, dx_accumulate=True)
+            del dqkv, dhx, dh2x
+            if lora:
                 self._group_done(f"llm{i}")
         # ---------------- token assembly backward ----------------
         qg = self.G["drv.query_route"]  # [20, d] followed by [10, d] (adjacent)
@@ -479,18 +542,19 @@ class VLAEngine:
         K.call("slx_gather_rows", K.P(dX), d, K.P(dplan["img_pos"]), Mi, d, K.P(dimg), d, 1, K.stream_ptr())
         del dX, dfeat
         # ---------------- mlp1 backward ----------------
-        K.mm(dimg, sv["a1"], self.G["proj.fc2.w"], ta=True, tb=False)
+        K.mm(dimg, sv["a1"], self.G["proj.fc2.w"], ta=True, tb=False, accumulate=True)
         self._colsum(dimg, self.G["proj.fc2.b"], 0)
         da1 = self._e(Mi, d)
         K.mm(dimg, self.W["proj.fc2.w"], da1, tb=False, epi=K.EPI_GELU_BWD, aux=sv["a1pre"], ldaux=d)
-        K.mm(da1, sv["z"], self.G["proj.fc1.w"], ta=True, tb=False)
+        K.mm(da1, sv["z"], self.G["proj.fc1.w"], ta=True, tb=False, accumulate=True)
         self._colsum(da1, self.G["proj.fc1.b"], 0)
         dz = self._e(Mi, 4 * D, dtype=F32)
         K.mm(da1, self.W["proj.fc1.w"], dz, tb=False)
         T = cfg.vit_tokens
         dxv = self._z(Mv, D)
         ws_n = self._ws(K.norm_ws_floats(4 * D))
-        K.norm_bwd(sv["nz"], dz, dxv, dgamma=self.G["proj.ln.w"], dbeta=self.G["proj.ln.b"], ws=ws_n, lddx=D)
+        K.norm_bwd(sv["nz"], dz, dxv, dgamma=self.G["proj.ln.w"], dbeta=self.G["proj.ln.b"], ws=ws_n, lddx=D,
+                   param_accumulate=True)
         del dz, da1, dimg
         self._group_done("proj")
         # ---------------- InternViT layers ----------------
@@ -503,21 +567,21 @@ class VLAEngine:
             Ls = sv["vit"][i]
             # x_out = x_mid + ls2 * (fc2(gelu(fc1(ln2(x_mid)))) )
             K.call("slx_ls_branch_bwd", K.P(dxv), D, K.P(self.P[p + "ls2"]), K.P(Ls["y2"]), D, K.P(g), D, Mv, D,
-                   K.P(self.G[p + "ls2"]), K.P(self.G[p + "fc2.b"]), 0, K.P(self._ws(2 * 256 * D)), K.stream_ptr())
-            K.mm(g, Ls["hact"], self.G[p + "fc2.w"], ta=True, tb=False)
+                   K.P(self.G[p + "ls2"]), K.P(self.G[p + "fc2.b"]), 1, K.P(self._ws(2 * 256 * D)), K.stream_ptr())
+            K.mm(g, Ls["hact"], self.G[p + "fc2.w"], ta=True, tb=False, accumulate=True)
             dh = self._e(Mv, F_)
             K.mm(g, self.W[p + "fc2.w"], dh, tb=False, epi=K.EPI_GELU_BWD, aux=Ls["hpre"], ldaux=F_)
-            K.mm(dh, Ls["h2"], self.G[p + "fc1.w"], ta=True, tb=False)
+            K.mm(dh, Ls["h2"], self.G[p + "fc1.w"], ta=True, tb=False, accumulate=True)
             self._colsum(dh, self.G[p + "fc1.b"], 0)
             dh2 = self._e(Mv, D, dtype=F32)
             K.mm(dh, self.W[p + "fc1.w"], dh2, tb=False)
             del dh
             K.norm_bwd(Ls["n2"], dh2, dxv, dx_accumulate=True, dgamma=self.G[p + "ln2.w"], dbeta=self.G[p + "ln2.b"],
-                       ws=self._ws(K.norm_ws_floats(D)))
+                       ws=self._ws(K.norm_ws_floats(D)), param_accumulate=True)
             # x_mid = x_in + ls1 * proj(attn(ln1(x_in)))
             K.call("slx_ls_branch_bwd", K.P(dxv), D, K.P(self.P[p + "ls1"]), K.P(Ls["y1"]), D, K.P(g), D, Mv, D,
-                   K.P(self.G[p + "ls1"]), K.P(self.G[p + "proj.b"]), 0, K.P(self._ws(2 * 256 * D)), K.stream_ptr())
-            K.mm(g, Ls["o"], self.G[p + "proj.w"], ta=True, tb=False)
+                   K.P(self.G[p + "ls1"]), K.P(self.G[p + "proj.b"]), 1, K.P(self._ws(2 * 256 * D)), K.stream_ptr())
+            K.mm(g, Ls["o"], self.G[p + "proj.w"], ta=True, tb=False, accumulate=True)
             do = self._e(Mv, D)
             K.mm(g, self.W[p + "proj.w"], do, tb=False)
             qkv = Ls["qkv"]
@@ -525,12 +589,12 @@ class VLAEngine:
             K.attn_bwd(qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], Ls["o"], Ls["lse"], do,
                        dqkv[:, :D], dqkv[:, D:2 * D], dqkv[:, 2 * D:], vws, B=N, S=T, Hq=H, Hkv=H, causal=False)
             del do
-            K.mm(dqkv, Ls["h1"], self.G[p + "qkv.w"], ta=True, tb=False)
+            K.mm(dqkv, Ls["h1"], self.G[p + "qkv.w"], ta=True, tb=False, accumulate=True)
             self._colsum(dqkv, self.G[p + "qkv.b"], 0)
             K.mm(dqkv, self.W[p + "qkv.w"], dh2, tb=False)
             del dqkv
             K.norm_bwd(Ls["n1"], dh2, dxv, dx_accumulate=True, dgamma=self.G[p + "ln1.w"], dbeta=self.G[p + "ln1.b"],
-                       ws=self._ws(K.norm_ws_floats(D)))
+                       ws=self._ws(K.norm_ws_floats(D)), param_accumulate=True)
             del dh2
             self._group_done(f"vit{i}")
         # ---------------- embeddings ----------------
@@ -545,23 +609,27 @@ class VLAEngine:
         self._group_done("vit_embed")
         self.saved = None
 
-    def _lora_bwd(self, dy, saved, i, site, dx, sv):
-        """dy: bf16 [M, out] (view); dx: f32 [M, in] accumulated."""
+    def _lora_bwd(self, dy, t, x, dt_f32, dx, i, site, sv):
+        """One LoRA site: dy bf16 [M, out] (view), t bf16 [M, r] (forward down-projection), x bf16 [M, in]
+        (undropped input), dt_f32 = s * dy B (already produced by the fused dgrad GEMM), dx f32 [M, in]
+        accumulated: dB = s dy^T t ; dA = dt^T drop(x) ; dx += drop'(dt A)."""
         cfg = self.cfg
-        t, xd, seed = saved
         p = f"llm.{i}.lora.{site}."
         s = cfg.lora_scale
         M = dy.shape[0]
-        K.mm(dy, t, self.G[p + "b"], ta=True, tb=False, alpha=s)            # dB = s dy^T t
+        kin = x.shape[1]
+        drop = sv["drop"]
+        seed = sv["llm"][i]["lora"][site]
+        K.mm(dy, t, self.G[p + "b"], ta=True, tb=False, alpha=s, accumulate=True)          # dB = s dy^T t
         dt = self._e(M, cfg.lora_r)
-        K.mm(dy, self.W[p + "b"], dt, tb=False, alpha=s)                    # dt = s dy B
-        K.mm(dt, xd, self.G[p + "a"], ta=True, tb=False)                    # dA = dt^T drop(x)
-        kin = xd.shape[1]
-        if sv["drop"] > 0:
-            K.mm(dt, self.W[p + "a"], dx, tb=False, epi=K.EPI_DROPMASK, accumulate=True, seed=seed, drop_p=sv["drop"],
+        K.call("slx_cast_rows", K.P(dt_f32), dt_f32.stride(0), K.P(dt), cfg.lora_r, M, cfg.lora_r, K.stream_ptr())
+        K.mm(dt, x, self.G[p + "a"], ta=True, tb=False, accumulate=True,                      # dA = dt^T drop(x)
+             drop_operand=2 if drop > 0 else 0, seed=seed, drop_p=drop, ldmask=kin)
+        if drop > 0:
+            K.mm(dt, self.W[p + "a"], dx, tb=False, epi=K.EPI_DROPMASK, accumulate=True, seed=seed, drop_p=drop,
                  ldmask=kin)
         else:
-            K.mm(dt, self.W[p + "a"], dx, tb=False, accumulate=True)      # dx += dt A
+            K.mm(dt, self.W[p + "a"], dx, tb=False, accumulate=True)                          # dx += dt A
 
     def _mlp_bwd(self, dout, saved, need_dx=True):
         """saved: [(out, pre, in, prefix, act)] from last layer to first; dout: grad of the last output."""

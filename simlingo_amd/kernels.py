@@ -19,6 +19,7 @@ c_int, c_i64, c_u64, c_float, c_vp = ctypes.c_int, ctypes.c_int64, ctypes.c_uint
 
 # ---- enums (mirror include/slx.h) --------------------------------------------------------------
 GEMM_NT, GEMM_NN, GEMM_TN, GEMM_TT = 0, 1, 2, 3
+GEMM_VARIANT = int(os.environ.get("SLX_GEMM_VARIANT", "0"))  # 0 = automatic (tuning hook)
 EPI_STORE, EPI_GELU, EPI_RESID_LS, EPI_GELU_BWD, EPI_SWIGLU_BWD, EPI_DROPMASK = 0, 1, 2, 3, 4, 5
 
 
@@ -36,7 +37,7 @@ class GemmDesc(ctypes.Structure):
         ("resid", c_vp), ("ldr", c_i64),
         ("accumulate", c_int),
         ("seed", c_u64), ("drop_p", c_float), ("ldmask", c_i64),
-        ("ksplit_max", c_int),
+        ("ksplit_max", c_int), ("variant", c_int), ("drop_operand", c_int),
     ]
 
 
@@ -111,7 +112,7 @@ def _require_cuda(*ts):
 # ------------------------------------------------------------------------------------------------
 def gemm(A, B, C, M, N, K, layout, lda, ldb, ldc, *, epi=EPI_STORE, alpha=1.0, bias=None, ls=None,
          aux=None, ldaux=0, aux_out=None, ldaux_out=0, resid=None, ldr=0, accumulate=False,
-         seed=0, drop_p=0.0, ldmask=0, batch=1, sA=0, sB=0, sC=0, ksplit_max=0):
+         seed=0, drop_p=0.0, ldmask=0, batch=1, sA=0, sB=0, sC=0, ksplit_max=0, variant=None, drop_operand=0):
     _require_cuda(A, B, C)
     d = GemmDesc()
     d.layout, d.epilogue = layout, epi
@@ -132,6 +133,8 @@ def gemm(A, B, C, M, N, K, layout, lda, ldb, ldc, *, epi=EPI_STORE, alpha=1.0, b
     d.accumulate = 1 if accumulate else 0
     d.seed, d.drop_p, d.ldmask = int(seed) & ((1 << 64) - 1), float(drop_p), int(ldmask)
     d.ksplit_max = int(ksplit_max)
+    d.variant = int(GEMM_VARIANT if variant is None else variant)
+    d.drop_operand = int(drop_operand)
     check(lib().slx_gemm_bf16(ctypes.byref(d), stream_ptr()), "slx_gemm_bf16")
 
 
@@ -232,6 +235,7 @@ for _n, _a in {
     "slx_gather_rows_b2f": [_vp, _I, _vp, _I, _i, _vp, _I, _vp],
     "slx_swiglu_bwd": [_vp, _I, _vp, _I, _vp, _I, _I, _i, _vp],
     "slx_cast_rows": [_vp, _I, _vp, _I, _I, _i, _vp],
+    "slx_pack_scaled": [_vp, _i, _vp],
     "slx_cast_f32_bf16": [_vp, _vp, _I, _vp],
 }.items():
     register(_n, _a)
@@ -278,8 +282,8 @@ def attn_bwd(q, k, v, o, lse, dout, dq, dk, dv, ws, *, rope_cos=None, rope_sin=N
 def attn_ws(B, S, Hq, Hkv, device):
     ws = {"delta": torch.empty(B * Hq * S, device=device), "dq_acc": torch.empty(B * S * Hq * 64, device=device)}
     if Hq != Hkv:
-        ws["dk_acc"] = torch.empty(B * S * Hkv * 64, device=device)
-        ws["dv_acc"] = torch.empty(B * S * Hkv * 64, device=device)
+        ws["dk_acc"] = torch.empty(B * S * Hq * 64, device=device)
+        ws["dv_acc"] = torch.empty(B * S * Hq * 64, device=device)
     return ws
 
 

@@ -88,3 +88,46 @@ def test_gemm_split_k(dev, M, N, Kd, layout, accumulate):
            accumulate=accumulate)
     ref = 0.5 * (a.float() @ b.float()) + bias + (C0 if accumulate else 0)
     assert (C - ref).abs().max().item() < 2e-3 * Kd ** 0.5
+
+
+@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("layout", [K.GEMM_NT, K.GEMM_NN, K.GEMM_TN, K.GEMM_TT])
+def test_gemm_variants(dev, variant, layout):
+    """Every main-loop variant (v1 register-staged, v2 LDS-DMA rings) on ragged M/N and K tails."""
+    M, N, Kd = 304, 392, 640 if layout != K.GEMM_TN else 600
+    g = torch.Generator(device=dev).manual_seed(variant * 10 + layout)
+    a = torch.randn(M, Kd, device=dev, generator=g).bfloat16()
+    b = torch.randn(Kd, N, device=dev, generator=g).bfloat16()
+    A = a if layout in (K.GEMM_NT, K.GEMM_NN) else a.t().contiguous()
+    B = b.t().contiguous() if layout in (K.GEMM_NT, K.GEMM_TT) else b
+    for out_dtype in (torch.float32, torch.bfloat16):
+        C = torch.empty(M, N, device=dev, dtype=out_dtype)
+        K.gemm(A, B, C, M, N, Kd, layout, A.stride(0), B.stride(0), C.stride(0), variant=variant, ksplit_max=-1)
+        ref = a.float() @ b.float()
+        tol = 2e-3 * Kd ** 0.5 + (0 if out_dtype == torch.float32 else 1e-2 * ref.abs().max().item())
+        assert (C.float() - ref).abs().max().item() < tol
+
+
+@pytest.mark.parametrize("variant", [1, 2])
+def test_gemm_unaligned_output_and_all_epilogues(dev, variant):
+    """Scalar epilogue fallback (C rows not 16-B aligned) and every epilogue through the DMA kernel."""
+    M, N, Kd = 200, 128, 256
+    g = torch.Generator(device=dev).manual_seed(7)
+    x = torch.randn(M, Kd, device=dev, generator=g).bfloat16()
+    w = (torch.randn(N, Kd, device=dev, generator=g) * 0.1).bfloat16()
+    bias = torch.randn(N, device=dev, generator=g)
+    ref = x.float() @ w.float().t() + bias
+    big = torch.zeros(M, N + 5, device=dev)
+    C = big[:, 3:3 + N]
+    K.linear(x, w, C, bias=bias, variant=variant)
+    torch.testing.assert_close(C, ref, atol=3e-3, rtol=3e-3)
+    # SwiGLU backward epilogue: aux = [g | u] (width 2N)
+    gu = torch.randn(M, 2 * N, device=dev, generator=g).bfloat16()
+    dy = torch.randn(M, Kd, device=dev, generator=g).bfloat16()
+    wd = (torch.randn(Kd, N, device=dev, generator=g) * 0.1).bfloat16()  # [Nout=Kd][Kin=N]
+    dgu = torch.empty(M, 2 * N, device=dev, dtype=torch.bfloat16)
+    K.gemm(dy, wd, dgu, M, N, Kd, K.GEMM_NN, Kd, N, 2 * N, epi=K.EPI_SWIGLU_BWD, aux=gu, ldaux=2 * N, variant=variant)
+    gg, uu = gu.float()[:, :N].requires_grad_(), gu.float()[:, N:].requires_grad_()
+    (torch.nn.functional.silu(gg) * uu).backward(dy.float() @ wd.float())
+    torch.testing.assert_close(dgu[:, :N].float(), gg.grad, atol=5e-2, rtol=2e-2)
+    torch.testing.assert_close(dgu[:, N:].float(), uu.grad, atol=5e-2, rtol=2e-2)

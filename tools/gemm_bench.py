@@ -1,37 +1,61 @@
-"""Microbenchmark of slx_gemm_bf16 on the hot-path shapes (HIP events, random operands)."""
+"""A/B microbenchmark of slx_gemm_bf16 main-loop variants on the hot-path shapes (HIP events,
+random operands, variants interleaved in one process)."""
+import os
 import sys
+
 import torch
-sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__))))
-from simlingo_amd import kernels as K
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from simlingo_amd import kernels as K  # noqa: E402
 
 SHAPES = {  # name: (M, N, K, layout)
     "vit_qkv": (16400, 3072, 1024, K.GEMM_NT),
     "vit_fc1": (16400, 4096, 1024, K.GEMM_NT),
     "vit_fc2": (16400, 1024, 4096, K.GEMM_NT),
+    "vit_proj": (16400, 1024, 1024, K.GEMM_NT),
+    "vit_fc2_dgrad": (16400, 4096, 1024, K.GEMM_NN),
     "vit_fc1_dgrad": (16400, 1024, 4096, K.GEMM_NN),
     "vit_fc1_wgrad": (4096, 1024, 16400, K.GEMM_TN),
+    "vit_qkv_wgrad": (3072, 1024, 16400, K.GEMM_TN),
+    "llm_qkv": (6384, 1152, 896, K.GEMM_NT),
     "llm_gateup": (6384, 9728, 896, K.GEMM_NT),
-    "llm_down_dgrad": (6384, 4864, 896, K.GEMM_NN),
+    "llm_down": (6384, 896, 4864, K.GEMM_NT),
+    "llm_gu_dgrad": (6384, 896, 9728, K.GEMM_NN),
     "sq8192": (8192, 8192, 8192, K.GEMM_NT),
 }
+VARIANTS = [int(v) for v in os.environ.get("VARIANTS", "1,2,3,4,5,6").split(",")]
 dev = torch.device("cuda")
-for name, (M, N, Kd, lay) in SHAPES.items():
+only = sys.argv[1:] or list(SHAPES)
+for name in only:
+    M, N, Kd, lay = SHAPES[name]
     A = (torch.randn(M, Kd, device=dev) if lay in (K.GEMM_NT, K.GEMM_NN) else torch.randn(Kd, M, device=dev)).bfloat16()
     B = (torch.randn(N, Kd, device=dev) if lay in (K.GEMM_NT, K.GEMM_TT) else torch.randn(Kd, N, device=dev)).bfloat16()
     C = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
-    f = lambda: K.gemm(A, B, C, M, N, Kd, lay, A.stride(0), B.stride(0), C.stride(0))
-    for _ in range(3): f()
-    torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    n = 20
-    e0.record()
-    for _ in range(n): f()
-    e1.record(); torch.cuda.synchronize()
-    ms = e0.elapsed_time(e1) / n
-    tf = 2.0 * M * N * Kd / ms / 1e9
-    print(f"{name:16s} M={M:6d} N={N:6d} K={Kd:6d}  {ms*1e3:9.1f} us  {tf:7.1f} TFLOP/s  ({tf/2500*100:5.1f}% of 2.5PF)", flush=True)
-    ref = A.float() if lay in (K.GEMM_NT, K.GEMM_NN) else A.float().t()
-    if M * N * Kd < 2e11:
-        bb = B.float().t() if lay in (K.GEMM_NT, K.GEMM_TT) else B.float()
-        err = (C.float() - ref @ bb).abs().max().item()
-        print(f"   max err {err:.3e}")
+    ref = None
+    if M * N * Kd < 3e11:
+        a = A.float() if lay in (K.GEMM_NT, K.GEMM_NN) else A.float().t()
+        b = B.float().t() if lay in (K.GEMM_NT, K.GEMM_TT) else B.float()
+        ref = a @ b
+    times = {v: [] for v in VARIANTS}
+    errs = {}
+    for v in VARIANTS:
+        K.gemm(A, B, C, M, N, Kd, lay, A.stride(0), B.stride(0), C.stride(0), variant=v)
+        torch.cuda.synchronize()
+        if ref is not None:
+            errs[v] = ((C.float() - ref).abs().max() / ref.abs().max()).item()
+    for rnd in range(5):
+        for v in VARIANTS:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            n = 10
+            e0.record()
+            for _ in range(n):
+                K.gemm(A, B, C, M, N, Kd, lay, A.stride(0), B.stride(0), C.stride(0), variant=v)
+            e1.record()
+            torch.cuda.synchronize()
+            times[v].append(e0.elapsed_time(e1) / n)
+    line = f"{name:14s} {M:6d}x{N:5d}x{Kd:5d} "
+    for v in VARIANTS:
+        ms = sorted(times[v])[len(times[v]) // 2]
+        tf = 2.0 * M * N * Kd / ms / 1e9
+        line += f"| v{v}: {tf:6.0f} TF" + (f" e{errs[v]:.0e}" if v in errs else "")
+    print(line, flush=True)
