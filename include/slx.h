@@ -142,6 +142,18 @@ int slx_gather_rows_bf16(const void* src, int64_t lds, const int* idx, int64_t n
 int slx_gather_sum(const float* src, int64_t lds, const int* pos, int B, int nq, int D, float* out, int accumulate, slx_stream_t s);
 /* peft LoRA dropout (lora_dropout, llm.py:113) with a counter-hash mask regenerated in backward */
 int slx_dropout(const void* src, int64_t lds, void* dst, int64_t ldd, int64_t M, int N, uint64_t seed, float p, int64_t ldmask, slx_stream_t s);
+/* LoRA down-projection of the sites sharing one input (peft LoraLayer.forward lora_A(dropout(x)),
+ * llm.py:106-119 / peft lora/layer.py): t[:, 32j:32j+32] = drop_j(x) A_j^T, bf16 out; r must be 32.
+ * Mask of site j: keep(seed[j], row*ldmask + col), the same hash as slx_dropout / drop_operand.   */
+typedef struct {
+  const void* x; int64_t ldx;         /* bf16 [M, Kin] */
+  int64_t M; int Kin; int r; int nsites;
+  const void* A[4];                   /* bf16 [r, Kin] per site */
+  uint64_t seed[4];
+  void* t; int64_t ldt;               /* bf16 [M, >= 32*nsites] */
+  float p; int64_t ldmask;
+} slx_lora_down_desc;
+int slx_lora_down(const slx_lora_down_desc* d, slx_stream_t stream);
 
 /* small strided f32 GEMM (driving heads adaptors.py:113-132, WaypointInputAdaptor :80)        */
 enum { SLX_ACT_NONE = 0, SLX_ACT_RELU = 1, SLX_ACT_SILU = 2 };

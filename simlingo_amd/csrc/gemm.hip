@@ -699,7 +699,7 @@ extern "C" int slx_gemm_bf16(const slx_gemm_desc* d, slx_stream_t stream) {
   {  // split-K for under-filled grids (weight gradients of skinny / LoRA GEMMs): >= 4 K-steps per split
     const int tiles = a.tilesM * a.tilesN * batch;
     const int ksteps = (d->K + BK - 1) / BK;
-    if (d->epilogue == SLX_EPI_STORE && d->out_f32 && tiles < 256 && ksteps >= 8) {
+    if (d->epilogue == SLX_EPI_STORE && d->out_f32 && tiles <= 256 && ksteps >= 8) {  // <= 1 block per CU
       int want = (512 + tiles - 1) / tiles;
       int maxs = ksteps / 4;
       int sp = want < maxs ? want : maxs;

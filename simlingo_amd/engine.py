@@ -176,6 +176,15 @@ class VLAEngine:
                                     int(np.float32(s).view(np.int32))])
                     row += out_s
                 cats[g] = w
+            # A_s zero-padded to 64 rows: the dropout-masked dgrad dx += drop'(dT_s A_s) then runs as a K=64 GEMM
+            # whose A operand is the 64-column window of the group's dT buffer starting at site s (the columns past
+            # the site multiply the zero rows), which keeps it on the LDS-DMA path.
+            for site in LORA_SITES:
+                a = self.P[p + f"lora.{site}.a"]  # [r, in] f32 master
+                ap = torch.zeros(64, a.shape[1], dtype=BF16, device=self.device)
+                entries.append([a.data_ptr(), a.stride(0), ap.data_ptr(), ap.stride(0), r, a.shape[1],
+                                int(np.float32(1.0).view(np.int32))])
+                cats["apad." + site] = ap
             self.cat.append(cats)
         self._pack_tab = torch.tensor(entries, dtype=torch.int64, device=self.device)
         self._pack_n = len(entries)
@@ -325,8 +334,7 @@ class VLAEngine:
             hx = (self._z if lora else self._e)(Ml, d + Pq, dtype=BF16)
             h, nrm1 = self._norm(X, self.P[p + "ln1"], None, Ml, d, cfg.rms_eps, rms=True, out=hx[:, :d])
             if lora:
-                for j, site in enumerate(("q", "k", "v")):
-                    L[site] = self._lora_down(hx[:, :d], i, site, hx[:, d + r * j: d + r * (j + 1)], sv)
+                L.update(self._lora_down(hx[:, :d], i, ("q", "k", "v"), hx[:, d:], sv))
             qkv = self._e(Ml, nqkv)
             K.mm(hx, cat["qkv"] if lora else self.W[p + "qkv_w"], qkv, bias=self.P[p + "qkv_b"])
             K.rope(qkv, Ml, S, Hq + Hk, cos, sin)  # q and k heads are the first Hq+Hk head slots
@@ -336,21 +344,20 @@ class VLAEngine:
             K.attn_fwd(qkv[:, :qn], qkv[:, qn:qn + kn], qkv[:, qn + kn:], o, lse, B=B, S=S, Hq=Hq, Hkv=Hk, causal=True,
                        seqlens=seql)
             if lora:
-                L["o"] = self._lora_down(o, i, "o", ox[:, qn:qn + r], sv)
+                L.update(self._lora_down(o, i, ("o",), ox[:, qn:], sv))
             Xm = self._e(Ml, d, dtype=F32)
             K.mm(ox, cat["o"] if lora else self.W[p + "o_w"], Xm, epi=K.EPI_RESID_LS, resid=X, ldr=d, ls=self.ones_d)
             h2x = (self._z if lora else self._e)(Ml, d + Pg, dtype=BF16)
             h2, nrm2 = self._norm(Xm, self.P[p + "ln2"], None, Ml, d, cfg.rms_eps, rms=True, out=h2x[:, :d])
             if lora:
-                L["gate"] = self._lora_down(h2, i, "gate", h2x[:, d:d + r], sv)
-                L["up"] = self._lora_down(h2, i, "up", h2x[:, d + r:d + 2 * r], sv)
+                L.update(self._lora_down(h2, i, ("gate", "up"), h2x[:, d:], sv))
             gu = self._e(Ml, 2 * Fl)
             K.mm(h2x, cat["gu"] if lora else self.W[p + "gate_up_w"], gu)
             ax = (self._z if lora else self._e)(Ml, Fl + Pd, dtype=BF16)
             act = ax[:, :Fl]
             K.call("slx_swiglu_fwd", K.P(gu), gu.stride(0), K.P(act), act.stride(0), Ml, Fl, K.stream_ptr())
             if lora:
-                L["down"] = self._lora_down(act, i, "down", ax[:, Fl:Fl + r], sv)
+                L.update(self._lora_down(act, i, ("down",), ax[:, Fl:], sv))
             Xo = self._e(Ml, d, dtype=F32)
             K.mm(ax, cat["down"] if lora else self.W[p + "down_w"], Xo, epi=K.EPI_RESID_LS, resid=Xm, ldr=d,
                  ls=self.ones_d)
@@ -402,16 +409,14 @@ class VLAEngine:
         self.saved = sv
         return out4, route_pred, speed_pred
 
-    def _lora_down(self, x, i, site, t_out, sv):
-        """t_out = drop(x) A^T (bf16, written into the extra columns of the activation buffer).
-        Dropout is applied while loading x (hash mask, regenerated in backward). Returns the seed."""
-        cfg = self.cfg
-        seed = sv["seed"] + 131 * i + 7 * LORA_SITES.index(site) + 1
-        kin = x.shape[1]
-        drop = sv["drop"]
-        K.mm(x, self.W[f"llm.{i}.lora.{site}.a"], t_out, drop_operand=1 if drop > 0 else 0, seed=seed, drop_p=drop,
-             ldmask=kin)
-        return seed
+    def _lora_down(self, x, i, sites, t_out, sv):
+        """t_out[:, 32j:32j+32] = drop_j(x) A_j^T for the sites sharing x (bf16, written into the extra columns of
+        the activation buffer), one launch. Dropout is applied while loading x (hash mask, regenerated in
+        backward). Returns {site: seed}."""
+        seeds = {site: sv["seed"] + 131 * i + 7 * LORA_SITES.index(site) + 1 for site in sites}
+        K.lora_down(x, [self.W[f"llm.{i}.lora.{site}.a"] for site in sites], t_out, [seeds[s_] for s_ in sites],
+                    p=sv["drop"])
+        return seeds
 
     def _mlp_fwd(self, x, layers):
         """driving head: list of (prefix, out_dim, act) -> saved [(out, pre, in)]"""
@@ -487,7 +492,7 @@ class VLAEngine:
             dax = self._e(Ml, Fl + Pd, dtype=F32)
             K.mm(dxb, cat["down"] if lora else self.W[p + "down_w"], dax, tb=False)
             if lora:
-                self._lora_bwd(dxb, ax[:, Fl:Fl + r], ax[:, :Fl], dax[:, Fl:Fl + r], dax[:, :Fl], i, "down", sv)
+                self._lora_bwd(i, ("down",), [dxb], ax[:, Fl:], ax[:, :Fl], dax[:, Fl:], dax[:, :Fl], sv)
             dgu = self._e(Ml, 2 * Fl)
             K.call("slx_swiglu_bwd", K.P(dax), dax.stride(0), K.P(Ls["gu"]), 2 * Fl, K.P(dgu), 2 * Fl, Ml, Fl,
                    K.stream_ptr())
@@ -495,9 +500,8 @@ class VLAEngine:
             dh2x = self._e(Ml, d + Pg, dtype=F32)
             K.mm(dgu, cat["gu"] if lora else self.W[p + "gate_up_w"], dh2x, tb=False)
             if lora:
-                self._lora_bwd(dgu[:, :Fl], h2x[:, d:d + r], h2x[:, :d], dh2x[:, d:d + r], dh2x[:, :d], i, "gate", sv)
-                self._lora_bwd(dgu[:, Fl:], h2x[:, d + r:d + 2 * r], h2x[:, :d], dh2x[:, d + r:d + 2 * r], dh2x[:, :d], i,
-                               "up", sv)
+                self._lora_bwd(i, ("gate", "up"), [dgu[:, :Fl], dgu[:, Fl:]], h2x[:, d:], h2x[:, :d], dh2x[:, d:],
+                               dh2x[:, :d], sv)
             del dgu
             K.norm_bwd(Ls["n2"], dh2x, dX, dx_accumulate=True)
             # o projection
@@ -505,7 +509,7 @@ class VLAEngine:
             dox = self._e(Ml, qn + Po, dtype=F32)
             K.mm(dxb, cat["o"] if lora else self.W[p + "o_w"], dox, tb=False)
             if lora:
-                self._lora_bwd(dxb, ox[:, qn:qn + r], ox[:, :qn], dox[:, qn:qn + r], dox[:, :qn], i, "o", sv)
+                self._lora_bwd(i, ("o",), [dxb], ox[:, qn:], ox[:, :qn], dox[:, qn:], dox[:, :qn], sv)
             dob = self._e(Ml, qn)
             K.call("slx_cast_rows", K.P(dox), dox.stride(0), K.P(dob), qn, Ml, qn, K.stream_ptr())
             del dox
@@ -517,9 +521,8 @@ class VLAEngine:
             dhx = self._e(Ml, d + Pq, dtype=F32)
             K.mm(dqkv, cat["qkv"] if lora else self.W[p + "qkv_w"], dhx, tb=False)
             if lora:
-                for j, (site, c0, c1) in enumerate((("q", 0, qn), ("k", qn, qn + kn), ("v", qn + kn, nqkv))):
-                    self._lora_bwd(dqkv[:, c0:c1], hx[:, d + r * j:d + r * (j + 1)], hx[:, :d],
-                                   dhx[:, d + r * j:d + r * (j + 1)], dhx[:, :d], i, site, sv)
+                self._lora_bwd(i, ("q", "k", "v"), [dqkv[:, :qn], dqkv[:, qn:qn + kn], dqkv[:, qn + kn:]], hx[:, d:],
+                               hx[:, :d], dhx[:, d:], dhx[:, :d], sv)
             K.norm_bwd(Ls["n1"], dhx, dX, dx_accumulate=True)
             del dqkv, dhx, dh2x
             if lora:
@@ -609,27 +612,32 @@ class VLAEngine:
         self._group_done("vit_embed")
         self.saved = None
 
-    def _lora_bwd(self, dy, t, x, dt_f32, dx, i, site, sv):
-        """One LoRA site: dy bf16 [M, out] (view), t bf16 [M, r] (forward down-projection), x bf16 [M, in]
-        (undropped input), dt_f32 = s * dy B (already produced by the fused dgrad GEMM), dx f32 [M, in]
-        accumulated: dB = s dy^T t ; dA = dt^T drop(x) ; dx += drop'(dt A)."""
+    def _lora_bwd(self, i, sites, dys, tx, x, dtx, dx, sv):
+        """LoRA sites of one group sharing the input x. dys[j] bf16 [M, out_j] (views of the output grad),
+        tx bf16 [M, P] (forward down-projections t_j in columns 32j..), x bf16 [M, in] (undropped input),
+        dtx f32 [M, P] (columns 32j.. hold dt_j = s dy_j B_j, produced by the fused dgrad GEMM; padding columns
+        are exactly 0 because W_cat's are), dx f32 [M, in] accumulated:
+        dB_j = s dy_j^T t_j ; dA_j = dt_j^T drop_j(x) ; dx += drop_j'(dt_j A_j)."""
         cfg = self.cfg
-        p = f"llm.{i}.lora.{site}."
         s = cfg.lora_scale
-        M = dy.shape[0]
-        kin = x.shape[1]
+        r = cfg.lora_r
+        M, kin = x.shape
+        n = len(sites)
         drop = sv["drop"]
-        seed = sv["llm"][i]["lora"][site]
-        K.mm(dy, t, self.G[p + "b"], ta=True, tb=False, alpha=s, accumulate=True)          # dB = s dy^T t
-        dt = self._e(M, cfg.lora_r)
-        K.call("slx_cast_rows", K.P(dt_f32), dt_f32.stride(0), K.P(dt), cfg.lora_r, M, cfg.lora_r, K.stream_ptr())
-        K.mm(dt, x, self.G[p + "a"], ta=True, tb=False, accumulate=True,                      # dA = dt^T drop(x)
-             drop_operand=2 if drop > 0 else 0, seed=seed, drop_p=drop, ldmask=kin)
-        if drop > 0:
-            K.mm(dt, self.W[p + "a"], dx, tb=False, epi=K.EPI_DROPMASK, accumulate=True, seed=seed, drop_p=drop,
-                 ldmask=kin)
-        else:
-            K.mm(dt, self.W[p + "a"], dx, tb=False, accumulate=True)                          # dx += dt A
+        P = dtx.shape[1]
+        W = r * n + r  # one spare 32-column block of zeros past the last site
+        dT = self._e(M, max(W, P))
+        K.call("slx_cast_rows", K.P(dtx), dtx.stride(0), K.P(dT), dT.stride(0), M, P, K.stream_ptr())
+        if P < W:
+            dT[:, P:].zero_()
+        for j, site in enumerate(sites):
+            p = f"llm.{i}.lora.{site}."
+            seed = sv["llm"][i]["lora"][site]
+            K.mm(dys[j], tx[:, r * j:r * (j + 1)], self.G[p + "b"], ta=True, tb=False, alpha=s, accumulate=True)
+            K.mm(dT[:, r * j:r * (j + 1)], x, self.G[p + "a"], ta=True, tb=False, accumulate=True,
+                 drop_operand=2 if drop > 0 else 0, seed=seed, drop_p=drop, ldmask=kin)
+            K.mm(dT[:, r * j:r * j + 64], self.cat[i]["apad." + site], dx, tb=False,
+                 epi=K.EPI_DROPMASK if drop > 0 else K.EPI_STORE, accumulate=True, seed=seed, drop_p=drop, ldmask=kin)
 
     def _mlp_bwd(self, dout, saved, need_dx=True):
         """saved: [(out, pre, in, prefix, act)] from last layer to first; dout: grad of the last output."""

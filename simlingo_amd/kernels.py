@@ -201,9 +201,17 @@ class SgemmDesc(ctypes.Structure):
     ]
 
 
+class LoraDownDesc(ctypes.Structure):
+    _fields_ = [
+        ("x", c_vp), ("ldx", c_i64), ("M", c_i64), ("Kin", c_int), ("r", c_int), ("nsites", c_int),
+        ("A", c_vp * 4), ("seed", ctypes.c_uint64 * 4), ("t", c_vp), ("ldt", c_i64), ("p", c_float), ("ldmask", c_i64),
+    ]
+
+
 _vp, _i, _I, _f = c_vp, c_int, c_i64, c_float
 for _n, _a in {
     "slx_attn_fwd": [ctypes.POINTER(AttnDesc), _vp],
+    "slx_lora_down": [ctypes.POINTER(LoraDownDesc), _vp],
     "slx_attn_bwd": [ctypes.POINTER(AttnDesc), ctypes.POINTER(AttnBwdDesc), _vp],
     "slx_rope": [_vp, _I, _I, _i, _i, _vp, _vp, _i, _vp],
     "slx_norm_fwd": [ctypes.POINTER(NormDesc), _vp],
@@ -346,6 +354,21 @@ def sgemm(A, sam, sak, B, sbk, sbn, C, scm, scn, M, N, Kd, *, bias=None, act=ACT
     d.ldpre = ldpre
     d.alpha = alpha
     check(lib().slx_sgemm(ctypes.byref(d), stream_ptr()), "slx_sgemm")
+
+
+def lora_down(x, As, t, seeds, p=0.0, ldmask=None):
+    """t[:, 32j:32j+32] = drop_j(x) As[j]^T for the sites sharing x (one launch)."""
+    assert x.dtype == torch.bfloat16 and t.dtype == torch.bfloat16 and 1 <= len(As) <= 4
+    M, kin = x.shape
+    assert t.shape[0] == M and t.shape[1] >= 32 * len(As)
+    d = LoraDownDesc()
+    d.x, d.ldx, d.M, d.Kin, d.r, d.nsites = P(x).value, x.stride(0), M, kin, As[0].shape[0], len(As)
+    for j, a in enumerate(As):
+        assert a.shape == (32, kin) and a.is_contiguous() and a.dtype == torch.bfloat16
+        d.A[j] = a.data_ptr()
+        d.seed[j] = int(seeds[j]) & ((1 << 64) - 1)
+    d.t, d.ldt, d.p, d.ldmask = P(t).value, t.stride(0), float(p), kin if ldmask is None else ldmask
+    check(lib().slx_lora_down(ctypes.byref(d), stream_ptr()), "slx_lora_down")
 
 
 def mm(A, B, C, *, ta=False, tb=True, **kw):

@@ -36,3 +36,39 @@ def test_dropout_mask_consistency(dev):
     y = torch.empty_like(x)
     K.call("slx_dropout", K.P(x), kin, K.P(y), kin, M, kin, seed, p, kin, K.stream_ptr())
     torch.testing.assert_close(y.float(), (x.float() * mask).bfloat16().float())
+
+
+@pytest.mark.parametrize("M,kin,nsites,p", [(300, 256, 3, 0.1), (6384 // 8 + 5, 896, 2, 0.1), (77, 4864 // 4, 1, 0.0),
+                                            (1, 64, 4, 0.1)])
+def test_lora_down_grouped(dev, M, kin, nsites, p):
+    """slx_lora_down: t[:, 32j:32j+32] = drop_j(x) A_j^T, one launch for the sites sharing x."""
+    g = torch.Generator(device=dev).manual_seed(11)
+    xfull = torch.randn(M, kin + 64, device=dev, generator=g).bfloat16()
+    x = xfull[:, :kin]  # strided view: ldx != kin, ldmask = kin
+    As = [(torch.randn(32, kin, device=dev, generator=g) * 0.1).bfloat16() for _ in range(nsites)]
+    seeds = [1234567 + 7919 * j for j in range(nsites)]
+    t = torch.full((M, 32 * nsites + 16), 7.0, device=dev).bfloat16()
+    K.lora_down(x, As, t, seeds, p=p)
+    for j in range(nsites):
+        mask = torch.from_numpy(keep_scale(seeds[j], M, kin, kin, p)).to(dev) if p > 0 else 1.0
+        xd = (x.float() * mask).bfloat16().float()
+        torch.testing.assert_close(t[:, 32 * j:32 * (j + 1)].float(), xd @ As[j].float().t(), atol=3e-2, rtol=2e-2)
+    assert (t[:, 32 * nsites:].float() == 7.0).all()  # columns past the sites untouched
+
+
+def test_dropmask_dgrad_padded_k64(dev):
+    """dx += mask * (dT_j A_j) as a K=64 GEMM: the A operand is a 64-column window of the group's dT buffer and
+    B is A_j zero-padded to 64 rows (engine._lora_bwd), so the columns past site j contribute exactly 0."""
+    M, kin, p, seed = 500, 896, 0.1, 424242
+    g = torch.Generator(device=dev).manual_seed(5)
+    dT = torch.randn(M, 96, device=dev, generator=g).bfloat16()
+    A = (torch.randn(32, kin, device=dev, generator=g) * 0.1).bfloat16()
+    Ap = torch.zeros(64, kin, device=dev, dtype=torch.bfloat16)
+    Ap[:32] = A
+    mask = torch.from_numpy(keep_scale(seed, M, kin, kin, p)).to(dev)
+    for j in (0, 1):
+        dx = torch.ones(M, kin, device=dev)
+        K.mm(dT[:, 32 * j:32 * j + 64], Ap, dx, tb=False, epi=K.EPI_DROPMASK, accumulate=True, seed=seed, drop_p=p,
+             ldmask=kin)
+        ref = 1 + mask * (dT[:, 32 * j:32 * (j + 1)].float() @ A.float())
+        torch.testing.assert_close(dx, ref, atol=2e-2, rtol=2e-2)
