@@ -19,6 +19,8 @@
 //    written to the other LDS buffer after them; one barrier per K-step.
 //  * Bijective XCD-aware block remap + GROUP_M=8 tile ordering so neighbouring tiles that share
 //    operand panels sit in one XCD's L2.
+#include <cmath>
+
 #include "common.h"
 #include "../../include/slx.h"
 
@@ -453,6 +455,44 @@ __device__ __forceinline__ void wait_vm() {
   else static_assert(N < 0, "unsupported vmcnt");
 }
 
+// LDS-staged epilogue of one 64x64 f32 sub-tile held in `ep` (row stride EP_LD), rows m_base.., cols n_base..
+template <int EPI, typename OutT>
+__device__ __forceinline__ void epilogue_tile64(const GemmArgs& p, OutT* __restrict__ C, const float* ep, int lane,
+                                                int m_base, int n_base) {
+  if constexpr (EPI == EPI_STORE) {
+    if (p.ksplit > 1) {  // split-K partials: one 64-float row (256 contiguous bytes) per atomic wave-instruction
+      const int n1 = n_base + lane;
+      const float bv = (p.bias && blockIdx.y == 0 && n1 < p.N) ? p.bias[n1] : 0.f;
+      float* Cf = reinterpret_cast<float*>(C);
+      for (int row = 0; row < 64; ++row) {
+        const int m = m_base + row;
+        if (m < p.M && n1 < p.N) atomicAdd(Cf + (long)m * p.ldc + n1, ep[row * EP_LD + lane] * p.alpha + bv);
+      }
+      return;
+    }
+  }
+  const int cc = (lane & 7) * 8;
+  const int n = n_base + cc;
+  const bool vec_ok = p.vec_ok && n + 8 <= p.N;
+#pragma unroll 2
+  for (int pass = 0; pass < 8; ++pass) {
+    const int row = pass * 8 + (lane >> 3);
+    const int m = m_base + row;
+    if (m >= p.M) continue;
+    float v[8];
+    const float4 a0 = *reinterpret_cast<const float4*>(ep + row * EP_LD + cc);
+    const float4 a1 = *reinterpret_cast<const float4*>(ep + row * EP_LD + cc + 4);
+    v[0] = a0.x; v[1] = a0.y; v[2] = a0.z; v[3] = a0.w; v[4] = a1.x; v[5] = a1.y; v[6] = a1.z; v[7] = a1.w;
+    if (vec_ok) {
+      epilogue_vec8<EPI, OutT>(p, C, m, n, v);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (n + e < p.N) epilogue_elem<EPI, OutT>(p, C, m, n + e, v[e]);
+    }
+  }
+}
+
 template <bool AK, bool BKc, int EPI, typename OutT, int BMv, int NS>
 __global__ __launch_bounds__(BMv * 2, 1) void gemm_bf16_dma_kernel(GemmArgs p) {
   constexpr int NW = BMv / 32;                 // waves: (BM/64) x 2
@@ -557,38 +597,214 @@ __global__ __launch_bounds__(BMv * 2, 1) void gemm_bf16_dma_kernel(GemmArgs p) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) ep[(i * 16 + (lane >> 4) * 4 + r) * EP_LD + j * 16 + (lane & 15)] = acc[i][j][r];
   __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS writes done (wave-private region)
-  if constexpr (EPI == EPI_STORE) {
-    if (p.ksplit > 1) {  // split-K partials: one 64-float row (256 contiguous bytes) per atomic wave-instruction
-      const int n1 = n0 + wn * 64 + lane;
-      const float bv = (p.bias && blockIdx.y == 0 && n1 < p.N) ? p.bias[n1] : 0.f;
-      float* Cf = reinterpret_cast<float*>(C);
-      for (int row = 0; row < 64; ++row) {
-        const int m = m0 + wm * 64 + row;
-        if (m < p.M && n1 < p.N) atomicAdd(Cf + (long)m * p.ldc + n1, ep[row * EP_LD + lane] * p.alpha + bv);
-      }
-      return;
-    }
-  }
-  const int cc = (lane & 7) * 8;
-  const int n = n0 + wn * 64 + cc;
-  const bool vec_ok = p.vec_ok && n + 8 <= p.N;
-#pragma unroll 2
-  for (int pass = 0; pass < 8; ++pass) {
-    const int row = pass * 8 + (lane >> 3);
-    const int m = m0 + wm * 64 + row;
-    if (m >= p.M) continue;
-    float v[8];
-    const float4 a0 = *reinterpret_cast<const float4*>(ep + row * EP_LD + cc);
-    const float4 a1 = *reinterpret_cast<const float4*>(ep + row * EP_LD + cc + 4);
-    v[0] = a0.x; v[1] = a0.y; v[2] = a0.z; v[3] = a0.w; v[4] = a1.x; v[5] = a1.y; v[6] = a1.z; v[7] = a1.w;
-    if (vec_ok) {
-      epilogue_vec8<EPI, OutT>(p, C, m, n, v);
-    } else {
+  epilogue_tile64<EPI, OutT>(p, C, ep, lane, m0 + wm * 64, n0 + wn * 64);
+}
+
+// ---------------------------------------------------------------------------------------------
+// v3 main loop: 256x256 tile, BK=64, 512 threads = 8 waves as 2 (M) x 4 (N), each wave 128x64
+// (8x4 tiles of v_mfma_f32_16x16x32_bf16). LDS = 2 stages x (A 32 KiB + B 32 KiB), filled by LDS-DMA.
+// The per-wave tile halves the LDS read bytes per MFMA of v2 (64x64 waves), which is what caps v2.
+//
+// Ping-pong: waves 0-3 (M half 0) and 4-7 (M half 1) are offset by one s_barrier, so one SIMD's two
+// waves alternate between a LOAD section (ds_reads of the next fragments + a slice of the DMA
+// prefetch) and an MFMA section (16 MFMAs = one 64x32 quadrant of the wave tile x K=64, at raised
+// priority). Every K-tile t is 4 phases:
+//   q0: read A[rows 0-63], B[cols 0-31] of tile t  | issue B pieces 0,1 of tile t+1 | MFMA (lo,lo)
+//   q1: read A[rows 64-127], B[cols 32-63]         | issue B pieces 2,3 of tile t+1 | MFMA (lo,hi)
+//   q2:                                            | issue A pieces 0,1 of tile t+2 | MFMA (hi,lo)
+//   q3:                           vmcnt(tile t+1)  | issue A pieces 2,3 of tile t+2 | MFMA (hi,hi)
+// Stage t&1 is last read in q1 (the load sections end with lgkmcnt(0) before their barrier, so the
+// reads are retired before the other group can pass that barrier and issue its q2 DMA into the same
+// stage). The wait for tile t+1 sits at the end of q3's load section, before the barrier that
+// precedes the leading group's first read of it; only tile t+2's 4 newest pieces stay in flight.
+constexpr int V3_BM = 256, V3_BN = 256;
+
+template <bool KC, int ROWS, int NW, int I0, int CNT>
+__device__ __forceinline__ void dma_issue_range(__amdgpu_buffer_rsrc_t rs, char* lds_tile, int wave, int k0, int K,
+                                                long ld, const long (&base)[ROWS * BK * 2 / 1024 / NW],
+                                                const int (&kr)[ROWS * BK * 2 / 1024 / NW],
+                                                const bool (&ok)[ROWS * BK * 2 / 1024 / NW]) {
+  constexpr int PER = ROWS * BK * 2 / 1024 / NW;
 #pragma unroll
-      for (int e = 0; e < 8; ++e)
-        if (n + e < p.N) epilogue_elem<EPI, OutT>(p, C, m, n + e, v[e]);
-    }
+  for (int i = I0; i < I0 + CNT; ++i) {
+    unsigned off;
+    if (KC) off = ok[i] ? (unsigned)((base[i] + k0) * 2) : kSent;
+    else off = (ok[i] && k0 + kr[i] < K) ? (unsigned)((base[i] + (long)k0 * ld) * 2) : kSent;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(lds_tile + (wave * PER + i) * 1024),
+                                             16, off, 0, 0, 0);
   }
+}
+
+__device__ __forceinline__ void v3_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <bool AK, bool BKc>
+__device__ __forceinline__ void v3_read(const char* As, const char* Bs, int arow, int bcol, int lane, bf16x8 (&af)[4][2],
+                                        bf16x8 (&bfr)[2][2]) {
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) bfr[j][s] = read_frag_p<BKc>(Bs, bcol + 16 * j, s, lane);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) af[i][s] = read_frag_p<AK>(As, arow + 16 * i, s, lane);
+  }
+}
+
+__device__ __forceinline__ void v3_mfma(f32x4 (&acc)[8][4], int mh, int nh, const bf16x8 (&af)[4][2],
+                                        const bf16x8 (&bfr)[2][2]) {
+  __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        acc[4 * mh + i][2 * nh + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][s], bfr[j][s], acc[4 * mh + i][2 * nh + j], 0, 0, 0);
+  __builtin_amdgcn_s_setprio(0);
+}
+
+template <bool AK, bool BKc, int EPI, typename OutT>
+__global__ __launch_bounds__(512, 1) void gemm_bf16_v3_kernel(GemmArgs p) {
+  constexpr int NW = 8;
+  constexpr int A_BYTES = V3_BM * BK * 2, B_BYTES = V3_BN * BK * 2;
+  constexpr int STAGE = A_BYTES + B_BYTES;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tilesM = p.tilesM, tilesN = p.tilesN;
+  const int nwg = tilesM * tilesN;
+  int bid = blockIdx.x;
+  {
+    const int q = nwg >> 3, r = nwg & 7, xcd = bid & 7;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  }
+  constexpr int GROUP = 4;
+  const int npg = GROUP * tilesN;
+  const int gid = bid / npg;
+  const int fm = gid * GROUP;
+  const int gs = min(tilesM - fm, GROUP);
+  const int tm = fm + (bid % npg) % gs;
+  const int tn = (bid % npg) / gs;
+  const int m0 = tm * V3_BM, n0 = tn * V3_BN;
+  const long z = blockIdx.z;
+  const bf16* A = p.A + z * p.sA;
+  const bf16* B = p.B + z * p.sB;
+  OutT* __restrict__ C = reinterpret_cast<OutT*>(p.C) + z * p.sC;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+
+  int kbeg = 0, kend = p.K;
+  if (p.ksplit > 1) {
+    kbeg = blockIdx.y * p.kchunk;
+    kend = min(p.K, kbeg + p.kchunk);
+  }
+  const int nk = (kend - kbeg + BK - 1) / BK;
+  const long extA = AK ? ((long)(p.M - 1) * p.lda + p.K) : ((long)(p.K - 1) * p.lda + p.M);
+  const long extB = BKc ? ((long)(p.N - 1) * p.ldb + p.K) : ((long)(p.K - 1) * p.ldb + p.N);
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)A, (short)0, (int)(extA * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)B, (short)0, (int)(extB * 2), 0x00020000);
+  constexpr int PA = A_BYTES / 1024 / NW, PB = B_BYTES / 1024 / NW;  // 4 + 4 pieces per wave per tile
+  static_assert(PA == 4 && PB == 4, "v3 piece schedule assumes 4+4 pieces per wave");
+  long baseA[PA], baseB[PB];
+  int krA[PA], krB[PB];
+  bool okA[PA], okB[PB];
+  dma_setup<AK, V3_BM, NW>(lane, wave, m0, p.M, p.lda, baseA, krA, okA);
+  dma_setup<BKc, V3_BN, NW>(lane, wave, n0, p.N, p.ldb, baseB, krB, okB);
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // prologue: tile 0 (A and B) and tile 1's A pieces
+  dma_issue_range<AK, V3_BM, NW, 0, 4>(ra, smem, wave, kbeg, kend, p.lda, baseA, krA, okA);
+  dma_issue_range<BKc, V3_BN, NW, 0, 4>(rb, smem + A_BYTES, wave, kbeg, kend, p.ldb, baseB, krB, okB);
+  if (nk > 1) {
+    dma_issue_range<AK, V3_BM, NW, 0, 4>(ra, smem + STAGE, wave, kbeg + BK, kend, p.lda, baseA, krA, okA);
+    wait_vm<4>();
+  } else {
+    wait_vm<0>();
+  }
+  v3_barrier();
+  if (wr == 1) v3_barrier();  // the M-half-1 waves run one barrier behind
+
+  const int arow = wr * 128, bcol = wc * 64;
+  bf16x8 alo[4][2], ahi[4][2], blo[2][2], bhi[2][2];
+  for (int t = 0; t < nk; ++t) {
+    const char* As = smem + (t & 1) * STAGE;
+    const char* Bs = As + A_BYTES;
+    char* st1 = smem + ((t + 1) & 1) * STAGE;  // tile t+1
+    char* st2 = smem + (t & 1) * STAGE;        // tile t+2 (this stage, free after q1)
+    const bool has1 = t + 1 < nk, has2 = t + 2 < nk;
+    const int k1 = kbeg + (t + 1) * BK, k2 = kbeg + (t + 2) * BK;
+    // ---- q0
+    v3_read<AK, BKc>(As, Bs, arow, bcol, lane, alo, blo);
+    if (has1) dma_issue_range<BKc, V3_BN, NW, 0, 2>(rb, st1 + A_BYTES, wave, k1, kend, p.ldb, baseB, krB, okB);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    v3_barrier();
+    v3_mfma(acc, 0, 0, alo, blo);
+    v3_barrier();
+    // ---- q1
+    v3_read<AK, BKc>(As, Bs, arow + 64, bcol + 32, lane, ahi, bhi);
+    if (has1) dma_issue_range<BKc, V3_BN, NW, 2, 2>(rb, st1 + A_BYTES, wave, k1, kend, p.ldb, baseB, krB, okB);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    v3_barrier();
+    v3_mfma(acc, 0, 1, alo, bhi);
+    v3_barrier();
+    // ---- q2
+    if (has2) dma_issue_range<AK, V3_BM, NW, 0, 2>(ra, st2, wave, k2, kend, p.lda, baseA, krA, okA);
+    v3_barrier();
+    v3_mfma(acc, 1, 0, ahi, blo);
+    v3_barrier();
+    // ---- q3
+    if (has2) {
+      dma_issue_range<AK, V3_BM, NW, 2, 2>(ra, st2, wave, k2, kend, p.lda, baseA, krA, okA);
+      wait_vm<4>();
+    } else {
+      wait_vm<0>();
+    }
+    v3_barrier();
+    v3_mfma(acc, 1, 1, ahi, bhi);
+    v3_barrier();
+  }
+  if (wr == 0) v3_barrier();  // re-align the barrier counts of the two wave groups
+
+  // ---- epilogue: two 64x64 passes per wave through a wave-private LDS region
+  __syncthreads();
+  float* ep = reinterpret_cast<float*>(smem) + wave * (64 * EP_LD);
+#pragma unroll
+  for (int mh = 0; mh < 2; ++mh) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) ep[(i * 16 + (lane >> 4) * 4 + r) * EP_LD + j * 16 + (lane & 15)] = acc[4 * mh + i][j][r];
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): wave-private region written
+    epilogue_tile64<EPI, OutT>(p, C, ep, lane, m0 + arow + 64 * mh, n0 + bcol);
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+  }
+}
+
+template <bool AK, bool BKc, int EPI, typename OutT>
+static int launch_v3(GemmArgs a, int batch, hipStream_t st) {
+  constexpr int LDS_RING = 2 * (V3_BM * BK * 2 + V3_BN * BK * 2);
+  constexpr int LDS_EP = 8 * 64 * EP_LD * 4;
+  constexpr int LDS = LDS_RING > LDS_EP ? LDS_RING : LDS_EP;
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)gemm_bf16_v3_kernel<AK, BKc, EPI, OutT>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    attr = true;
+  }
+  a.tilesM = (a.M + V3_BM - 1) / V3_BM;
+  a.tilesN = (a.N + V3_BN - 1) / V3_BN;
+  dim3 grid(a.tilesM * a.tilesN, a.ksplit > 1 ? a.ksplit : 1, batch);
+  hipLaunchKernelGGL((gemm_bf16_v3_kernel<AK, BKc, EPI, OutT>), grid, dim3(512), LDS, st, a);
+  SLX_LAUNCH_CHECK("slx_gemm_bf16(v3)");
+  return 0;
 }
 
 template <bool AK, bool BKc, int EPI, typename OutT>
@@ -618,7 +834,7 @@ static int launch_v2(GemmArgs a, int batch, hipStream_t st) {
 }
 
 // variant: 1 = v1 register-staged 128x128; 2 = DMA 128x128 NS2; 3 = DMA 128x128 NS3; 4 = DMA 128x128 NS4;
-//          5 = DMA 256x128 NS2; 6 = DMA 256x128 NS3; 0 = automatic
+//          5 = DMA 256x128 NS2; 6 = DMA 256x128 NS3; 7 = v3 256x256 ping-pong; 0 = automatic
 template <bool AK, bool BKc, int EPI, typename OutT>
 static int launch_any(GemmArgs& a, int batch, hipStream_t st, int variant) {
   const bool dma_ok = (!AK || a.K % BK == 0) && (!BKc || a.K % BK == 0) && (a.ksplit <= 1 || a.kchunk % BK == 0) &&
@@ -631,6 +847,7 @@ static int launch_any(GemmArgs& a, int batch, hipStream_t st, int variant) {
     case 4: return launch_v2<AK, BKc, EPI, OutT, 128, 4>(a, batch, st);
     case 5: return launch_v2<AK, BKc, EPI, OutT, 256, 2>(a, batch, st);
     case 6: return launch_v2<AK, BKc, EPI, OutT, 256, 3>(a, batch, st);
+    case 7: return launch_v3<AK, BKc, EPI, OutT>(a, batch, st);
     default: return launch<AK, BKc, EPI, OutT>(a, batch, st);
   }
 }
@@ -647,24 +864,40 @@ static int dispatch_layout(int layout, GemmArgs& a, int batch, hipStream_t st, i
   return -22;
 }
 
-}  // namespace slx
 
-using namespace slx;
+// ---- host side ------------------------------------------------------------------------------
+// Variant choice: per launch the chip holds 512 blocks of the 128x128 kernels (2 per CU) or 256 of v3
+// (one 512-thread block with 139 KB LDS per CU). The cost of a variant is its number of block rounds
+// x the work of one round at that kernel's rate (v3's per-CU rate ~1.26x v2's, measured at 8192^3), so
+// partially filled last rounds are priced in. For v3, a small M remainder (M % 256 <= 64, e.g. the 16
+// class tokens of 16 InternViT tiles: 16400 = 64*256 + 16) is peeled into a v2 launch so the main grid
+// is whole rounds.
+static int v_tile_m(int v) { return v == 7 ? 256 : (v == 5 || v == 6) ? 256 : 128; }
+static int v_tile_n(int v) { return v == 7 ? 256 : 128; }
+static int v_slots(int v) { return v == 7 ? 256 : 512; }
 
-extern "C" int slx_gemm_bf16(const slx_gemm_desc* d, slx_stream_t stream) {
-  SLX_CHECK_ARG(d != nullptr, "slx_gemm_bf16: null desc");
-  SLX_CHECK_ARG(d->M >= 0 && d->N >= 0 && d->K >= 0, "slx_gemm_bf16: negative dims");
-  if (d->M == 0 || d->N == 0 || d->batch == 0) return 0;
-  const bool ak = d->layout == SLX_GEMM_NT || d->layout == SLX_GEMM_NN;
-  const bool bk = d->layout == SLX_GEMM_NT || d->layout == SLX_GEMM_TT;
-  // contiguous dimension of every operand must allow 16-byte vector loads
-  SLX_CHECK_ARG((ak ? d->K : d->M) % 8 == 0, "slx_gemm_bf16: A contiguous dim (%d) must be a multiple of 8",
-                ak ? d->K : d->M);
-  SLX_CHECK_ARG((bk ? d->K : d->N) % 8 == 0, "slx_gemm_bf16: B contiguous dim (%d) must be a multiple of 8",
-                bk ? d->K : d->N);
-  SLX_CHECK_ARG(d->lda % 8 == 0 && d->ldb % 8 == 0, "slx_gemm_bf16: lda/ldb must be multiples of 8");
-  SLX_CHECK_ARG(((uintptr_t)d->A & 15) == 0 && ((uintptr_t)d->B & 15) == 0, "slx_gemm_bf16: A/B must be 16B aligned");
-  SLX_CHECK_ARG(d->batch == 1 || (d->sA % 8 == 0 && d->sB % 8 == 0), "slx_gemm_bf16: batch strides must be multiples of 8");
+static int split_for(const slx_gemm_desc* d, int v, int M, int batch) {
+  const int tiles = ((M + v_tile_m(v) - 1) / v_tile_m(v)) * ((d->N + v_tile_n(v) - 1) / v_tile_n(v)) * batch;
+  const int ksteps = (d->K + BK - 1) / BK;
+  const int slots = v_slots(v);
+  if (!(d->epilogue == SLX_EPI_STORE && d->out_f32 && batch == 1 && tiles <= slots / 2 && ksteps >= 8)) return 1;
+  if (d->ksplit_max < 0) return 1;
+  int sp = (slots + tiles - 1) / tiles;
+  sp = sp < ksteps / 4 ? sp : ksteps / 4;
+  if (d->ksplit_max > 0 && sp > d->ksplit_max) sp = d->ksplit_max;
+  return sp < 1 ? 1 : sp;
+}
+
+static double v_cost(const slx_gemm_desc* d, int v, int M, int batch) {
+  const double tiles = (double)((M + v_tile_m(v) - 1) / v_tile_m(v)) * ((d->N + v_tile_n(v) - 1) / v_tile_n(v)) * batch;
+  const int sp = split_for(d, v, M, batch);
+  const double rounds = std::ceil(tiles * sp / v_slots(v));
+  const double round_work = (double)v_slots(v) * v_tile_m(v) * v_tile_n(v) * ((double)d->K / sp);
+  const double rate = v == 7 ? 1.26 : 1.0;
+  return rounds * round_work / rate;
+}
+
+static int gemm_launch(const slx_gemm_desc* d, int v, hipStream_t st) {
   GemmArgs a;
   a.A = (const bf16*)d->A; a.B = (const bf16*)d->B; a.C = d->C;
   a.lda = d->lda; a.ldb = d->ldb; a.ldc = d->ldc;
@@ -678,14 +911,10 @@ extern "C" int slx_gemm_bf16(const slx_gemm_desc* d, slx_stream_t stream) {
   a.accumulate = d->accumulate;
   a.seed = d->seed; a.drop_p = d->drop_p; a.ldmask = d->ldmask;
   a.drop_operand = d->drop_operand;
-  SLX_CHECK_ARG(d->drop_operand == 0 || (d->epilogue == SLX_EPI_STORE && d->drop_p >= 0.f && d->drop_p < 1.f),
-                "slx_gemm_bf16: operand dropout needs EPI_STORE and 0 <= p < 1");
   a.tilesM = (d->M + BM - 1) / BM;
   a.tilesN = (d->N + BN - 1) / BN;
   {
-    const int esz = d->out_f32 ? 4 : 2;
     bool ok = d->ldc % 8 == 0 && ((uintptr_t)d->C % 16) == 0 && (d->batch <= 1 || d->sC % 8 == 0);
-    (void)esz;
     if (d->aux) ok = ok && d->ldaux % 8 == 0 && ((uintptr_t)d->aux % 16) == 0;
     if (d->aux_out) ok = ok && d->ldaux_out % 8 == 0 && ((uintptr_t)d->aux_out % 16) == 0;
     if (d->resid) ok = ok && d->ldr % 8 == 0 && ((uintptr_t)d->resid % 16) == 0;
@@ -693,32 +922,24 @@ extern "C" int slx_gemm_bf16(const slx_gemm_desc* d, slx_stream_t stream) {
     a.vec_ok = ok ? 1 : 0;
   }
   const int batch = d->batch < 1 ? 1 : d->batch;
-  hipStream_t st = (hipStream_t)stream;
   a.ksplit = 1;
   a.kchunk = d->K;
-  {  // split-K for under-filled grids (weight gradients of skinny / LoRA GEMMs): >= 4 K-steps per split
-    const int tiles = a.tilesM * a.tilesN * batch;
+  {  // split-K for under-filled grids (weight gradients): f32 atomics, >= 4 K-steps per split
+    int sp = split_for(d, v, d->M, batch);
     const int ksteps = (d->K + BK - 1) / BK;
-    if (d->epilogue == SLX_EPI_STORE && d->out_f32 && tiles <= 256 && ksteps >= 8) {  // <= 1 block per CU
-      int want = (512 + tiles - 1) / tiles;
-      int maxs = ksteps / 4;
-      int sp = want < maxs ? want : maxs;
-      if (d->ksplit_max > 0 && sp > d->ksplit_max) sp = d->ksplit_max;
-      if (d->ksplit_max < 0) sp = 1;
-      if (sp > 1) {
-        const int per = ((ksteps + sp - 1) / sp) * BK;
-        sp = (d->K + per - 1) / per;
-        a.ksplit = sp;
-        a.kchunk = per;
-        if (!d->accumulate) {
-          hipError_t e = hipMemset2DAsync(d->C, d->ldc * sizeof(float), 0, (size_t)d->N * sizeof(float), d->M, st);
-          if (e != hipSuccess) { set_error("slx_gemm_bf16: memset2D failed: %s", hipGetErrorString(e)); return -1000 - (int)e; }
-        }
-        SLX_CHECK_ARG(batch == 1, "slx_gemm_bf16: split-K with batch > 1 unsupported");
+    if (sp > 1) {
+      const int per = ((ksteps + sp - 1) / sp) * BK;
+      sp = (d->K + per - 1) / per;
+    }
+    if (sp > 1) {
+      a.ksplit = sp;
+      a.kchunk = ((ksteps + sp - 1) / sp) * BK;
+      if (!d->accumulate) {
+        hipError_t e = hipMemset2DAsync(d->C, d->ldc * sizeof(float), 0, (size_t)d->N * sizeof(float), d->M, st);
+        if (e != hipSuccess) { set_error("slx_gemm_bf16: memset2D failed: %s", hipGetErrorString(e)); return -1000 - (int)e; }
       }
     }
   }
-  const int v = d->variant;
   switch (d->epilogue) {
     case SLX_EPI_STORE:
       return d->out_f32 ? dispatch_layout<EPI_STORE, float>(d->layout, a, batch, st, v)
@@ -741,4 +962,58 @@ extern "C" int slx_gemm_bf16(const slx_gemm_desc* d, slx_stream_t stream) {
   }
   set_error("slx_gemm_bf16: bad epilogue %d", d->epilogue);
   return -22;
+}
+
+}  // namespace slx
+
+using namespace slx;
+
+extern "C" int slx_gemm_bf16(const slx_gemm_desc* d, slx_stream_t stream) {
+  SLX_CHECK_ARG(d != nullptr, "slx_gemm_bf16: null desc");
+  SLX_CHECK_ARG(d->M >= 0 && d->N >= 0 && d->K >= 0, "slx_gemm_bf16: negative dims");
+  if (d->M == 0 || d->N == 0 || d->batch == 0) return 0;
+  const bool ak = d->layout == SLX_GEMM_NT || d->layout == SLX_GEMM_NN;
+  const bool bk = d->layout == SLX_GEMM_NT || d->layout == SLX_GEMM_TT;
+  // contiguous dimension of every operand must allow 16-byte vector loads
+  SLX_CHECK_ARG((ak ? d->K : d->M) % 8 == 0, "slx_gemm_bf16: A contiguous dim (%d) must be a multiple of 8",
+                ak ? d->K : d->M);
+  SLX_CHECK_ARG((bk ? d->K : d->N) % 8 == 0, "slx_gemm_bf16: B contiguous dim (%d) must be a multiple of 8",
+                bk ? d->K : d->N);
+  SLX_CHECK_ARG(d->lda % 8 == 0 && d->ldb % 8 == 0, "slx_gemm_bf16: lda/ldb must be multiples of 8");
+  SLX_CHECK_ARG(((uintptr_t)d->A & 15) == 0 && ((uintptr_t)d->B & 15) == 0, "slx_gemm_bf16: A/B must be 16B aligned");
+  SLX_CHECK_ARG(d->batch == 1 || (d->sA % 8 == 0 && d->sB % 8 == 0), "slx_gemm_bf16: batch strides must be multiples of 8");
+  SLX_CHECK_ARG(d->drop_operand == 0 || (d->epilogue == SLX_EPI_STORE && d->drop_p >= 0.f && d->drop_p < 1.f),
+                "slx_gemm_bf16: operand dropout needs EPI_STORE and 0 <= p < 1");
+  hipStream_t st = (hipStream_t)stream;
+  const int batch = d->batch < 1 ? 1 : d->batch;
+  const bool dma_ok = (!ak || d->K % BK == 0) && (!bk || d->K % BK == 0) && d->drop_operand == 0;
+  int v = d->variant;
+  const int rem = d->M % V3_BM;
+  const bool peel_ok = batch == 1 && d->epilogue != SLX_EPI_DROPMASK && d->M > V3_BM && rem > 0 && rem <= 64;
+  if (v == 0) {
+    v = dma_ok ? 2 : 1;
+    if (dma_ok) {
+      const int Mmain = peel_ok ? d->M - rem : d->M;
+      double c3 = v_cost(d, 7, Mmain, batch);
+      if (peel_ok) c3 += v_cost(d, 2, rem, batch);
+      if (c3 < v_cost(d, 2, d->M, batch)) v = 7;
+    }
+  }
+  if (v == 7 && dma_ok && peel_ok) {
+    // main block rows on v3, the M remainder on v2 (same stream, same epilogue)
+    slx_gemm_desc m = *d, t = *d;
+    m.M = d->M - rem;
+    t.M = rem;
+    const long r0 = m.M;
+    const size_t csz = d->out_f32 ? 4 : 2;
+    t.A = ak ? (const void*)((const bf16*)d->A + r0 * d->lda) : (const void*)((const bf16*)d->A + r0);
+    t.C = (void*)((char*)d->C + (size_t)r0 * d->ldc * csz);
+    if (d->aux) t.aux = (const void*)((const bf16*)d->aux + r0 * d->ldaux);
+    if (d->aux_out) t.aux_out = (void*)((bf16*)d->aux_out + r0 * d->ldaux_out);
+    if (d->resid) t.resid = d->resid + r0 * d->ldr;
+    int rc = gemm_launch(&m, 7, st);
+    if (rc) return rc;
+    return gemm_launch(&t, 2, st);
+  }
+  return gemm_launch(d, v, st);
 }

@@ -90,7 +90,7 @@ def test_gemm_split_k(dev, M, N, Kd, layout, accumulate):
     assert (C - ref).abs().max().item() < 2e-3 * Kd ** 0.5
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7])
 @pytest.mark.parametrize("layout", [K.GEMM_NT, K.GEMM_NN, K.GEMM_TN, K.GEMM_TT])
 def test_gemm_variants(dev, variant, layout):
     """Every main-loop variant (v1 register-staged, v2 LDS-DMA rings) on ragged M/N and K tails."""
@@ -108,7 +108,7 @@ def test_gemm_variants(dev, variant, layout):
         assert (C.float() - ref).abs().max().item() < tol
 
 
-@pytest.mark.parametrize("variant", [1, 2])
+@pytest.mark.parametrize("variant", [1, 2, 7])
 def test_gemm_unaligned_output_and_all_epilogues(dev, variant):
     """Scalar epilogue fallback (C rows not 16-B aligned) and every epilogue through the DMA kernel."""
     M, N, Kd = 200, 128, 256
@@ -131,3 +131,55 @@ def test_gemm_unaligned_output_and_all_epilogues(dev, variant):
     (torch.nn.functional.silu(gg) * uu).backward(dy.float() @ wd.float())
     torch.testing.assert_close(dgu[:, :N].float(), gg.grad, atol=5e-2, rtol=2e-2)
     torch.testing.assert_close(dgu[:, N:].float(), uu.grad, atol=5e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("Kd", [64, 128, 192, 1024])
+@pytest.mark.parametrize("layout", [K.GEMM_NT, K.GEMM_NN, K.GEMM_TN])
+def test_gemm_v3_pipeline_depths(dev, Kd, layout):
+    """v3 (256x256 ping-pong) prologue/steady-state/drain paths: 1, 2, 3 and 16 K-tiles; multi-tile grid with
+    ragged edges; split-K (f32 atomics) on the same kernel."""
+    M, N = 600, 520
+    g = torch.Generator(device=dev).manual_seed(Kd + layout)
+    a = torch.randn(M, Kd, device=dev, generator=g).bfloat16()
+    b = torch.randn(Kd, N, device=dev, generator=g).bfloat16()
+    A = a if layout in (K.GEMM_NT, K.GEMM_NN) else a.t().contiguous()
+    B = b.t().contiguous() if layout in (K.GEMM_NT, K.GEMM_TT) else b
+    ref = a.float() @ b.float()
+    for ks in (-1, 0):
+        C = torch.full((M, N), 3.0, device=dev)
+        K.gemm(A, B, C, M, N, Kd, layout, A.stride(0), B.stride(0), C.stride(0), variant=7, ksplit_max=ks,
+               accumulate=True)
+        assert (C - 3.0 - ref).abs().max().item() < 2e-3 * Kd ** 0.5
+
+
+@pytest.mark.parametrize("variant", [0, 7])
+def test_gemm_v3_m_tail_peel_epilogues(dev, variant):
+    """M = 2*256 + 16: v3 runs the first 512 rows and the 16-row remainder is peeled into a v2 launch with offset
+    C/aux/aux_out/resid pointers (InternViT: 16400 = 64*256 + 16). Fused epilogues must agree across the seam."""
+    M, N, Kd = 528, 512, 256
+    g = torch.Generator(device=dev).manual_seed(21)
+    x = torch.randn(M, Kd, device=dev, generator=g).bfloat16()
+    w = (torch.randn(N, Kd, device=dev, generator=g) * 0.1).bfloat16()
+    bias = torch.randn(N, device=dev, generator=g)
+    pre = x.float() @ w.float().t() + bias
+    # GELU (bf16 out + pre-activation aux_out)
+    h = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    hpre = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    K.gemm(x, w, h, M, N, Kd, K.GEMM_NT, Kd, Kd, N, epi=K.EPI_GELU, bias=bias, aux_out=hpre, ldaux_out=N,
+           variant=variant)
+    torch.testing.assert_close(hpre.float(), pre, atol=3e-2, rtol=1e-2)
+    torch.testing.assert_close(h.float(), torch.nn.functional.gelu(hpre.float()), atol=3e-2, rtol=1e-2)
+    # RESID_LS (f32 out = resid + ls * y)
+    resid = torch.randn(M, N, device=dev, generator=g)
+    ls = torch.rand(N, device=dev, generator=g)
+    out = torch.empty(M, N, device=dev)
+    K.gemm(x, w, out, M, N, Kd, K.GEMM_NT, Kd, Kd, N, epi=K.EPI_RESID_LS, bias=bias, resid=resid, ldr=N, ls=ls,
+           variant=variant)
+    torch.testing.assert_close(out, resid + ls * pre, atol=3e-3, rtol=3e-3)
+    # GELU_BWD (NN, bf16 out, aux = pre-activation)
+    dy = torch.randn(M, N, device=dev, generator=g).bfloat16()
+    dx = torch.empty(M, Kd, device=dev, dtype=torch.bfloat16)
+    K.gemm(dy, w, dx, M, Kd, N, K.GEMM_NN, N, Kd, Kd, epi=K.EPI_GELU_BWD, aux=x, ldaux=Kd, variant=variant)
+    xx = x.float().requires_grad_()
+    torch.nn.functional.gelu(xx).backward(dy.float() @ w.float())
+    torch.testing.assert_close(dx.float(), xx.grad, atol=5e-2, rtol=2e-2)
