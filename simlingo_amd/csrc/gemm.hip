@@ -882,19 +882,27 @@ static int split_for(const slx_gemm_desc* d, int v, int M, int batch) {
   const int slots = v_slots(v);
   if (!(d->epilogue == SLX_EPI_STORE && d->out_f32 && batch == 1 && tiles <= slots / 2 && ksteps >= 8)) return 1;
   if (d->ksplit_max < 0) return 1;
-  int sp = (slots + tiles - 1) / tiles;
+  int sp = slots / tiles;  // floor: never more blocks than one round holds
   sp = sp < ksteps / 4 ? sp : ksteps / 4;
+  if (v == 7 && sp > 4) sp = 4;  // beyond 4 the f32 atomic traffic (sp x M x N x 4 B) dominates
   if (d->ksplit_max > 0 && sp > d->ksplit_max) sp = d->ksplit_max;
   return sp < 1 ? 1 : sp;
 }
 
+// Estimated seconds: block rounds x one block's time at its kernel's per-CU rate (v2 blocks share a CU two
+// at a time, so a lone v2 block is credited ~1.4x its shared rate), plus split-K atomic traffic.
 static double v_cost(const slx_gemm_desc* d, int v, int M, int batch) {
   const double tiles = (double)((M + v_tile_m(v) - 1) / v_tile_m(v)) * ((d->N + v_tile_n(v) - 1) / v_tile_n(v)) * batch;
   const int sp = split_for(d, v, M, batch);
-  const double rounds = std::ceil(tiles * sp / v_slots(v));
-  const double round_work = (double)v_slots(v) * v_tile_m(v) * v_tile_n(v) * ((double)d->K / sp);
-  const double rate = v == 7 ? 1.26 : 1.0;
-  return rounds * round_work / rate;
+  const double blocks = tiles * sp;
+  const double rounds = std::ceil(blocks / v_slots(v));
+  const double block_flop = 2.0 * v_tile_m(v) * v_tile_n(v) * ((double)d->K / sp);
+  double block_rate = v == 7 ? 1.35e15 / 256 : 1.1e15 / 512;
+  if (v != 7 && blocks <= 256) block_rate *= 1.4;
+  double t = rounds * block_flop / block_rate;
+  if (sp > 1) t += (double)sp * M * d->N * 4.0 / 2.0e12;
+  if (v == 7 && blocks < 192) t *= 1.5;  // an under-filled 256x256 grid leaves whole CUs idle
+  return t;
 }
 
 static int gemm_launch(const slx_gemm_desc* d, int v, hipStream_t st) {

@@ -17,6 +17,10 @@ SHAPES = {  # name: (M, N, K, layout)
     "vit_fc1_dgrad": (16400, 1024, 4096, K.GEMM_NN),
     "vit_fc1_wgrad": (4096, 1024, 16400, K.GEMM_TN),
     "vit_qkv_wgrad": (3072, 1024, 16400, K.GEMM_TN),
+    "vit_proj_wgrad": (1024, 1024, 16400, K.GEMM_TN),
+    "llm_gu_dgradx": (6384, 960, 9728, K.GEMM_NN),
+    "llm_qkv_dgrad": (6384, 1024, 1152, K.GEMM_NN),
+    "llm_down_dgrad": (6384, 4928, 896, K.GEMM_NN),
     "llm_qkv": (6384, 1152, 896, K.GEMM_NT),
     "llm_gateup": (6384, 9728, 896, K.GEMM_NT),
     "llm_down": (6384, 896, 4864, K.GEMM_NT),

@@ -14,9 +14,9 @@ top = int(sys.argv[3]) if len(sys.argv) > 3 and not sys.argv[3].startswith("--")
 by_grid = "--grid" in sys.argv
 c = sqlite3.connect(path)
 agg = defaultdict(lambda: [0, 0.0])
-for name, dur, gx, gy, gz in c.execute("select name, duration, grid_x, grid_y, grid_z from kernels"):
+for name, dur, gx, gy, gz, wx in c.execute("select name, duration, grid_x, grid_y, grid_z, workgroup_x from kernels"):
     short = name.replace("void ", "").replace("slx::", "")[:110]
-    key = (short, (gx // 256 if gx >= 256 else gx, gy, gz)) if by_grid else (short, None)
+    key = (short, (gx // max(wx, 1), gy, gz)) if by_grid else (short, None)  # blocks
     agg[key][0] += 1
     agg[key][1] += dur
 tot = sum(v[1] for v in agg.values())
