@@ -88,8 +88,8 @@ typedef struct slx_attn_bwd_desc {
   void* dk; int64_t lddk;
   void* dv; int64_t lddv;
   float* delta_ws;              /* [B, Hq, S]                                            */
-  float* dq_acc;                /* [B*S, Hq*64] f32 workspace                            */
-  float* dk_acc; float* dv_acc; /* [B*S, Hq*64] f32 per-q-head partial workspaces (GQA only) */
+  float* dq_acc;                /* [B*S, Hq*64] f32 workspace (fully overwritten)        */
+  float* dk_acc; float* dv_acc; /* [B*S, Hq*64] f32 workspaces, required for GQA or RoPE */
   const float* rope_cos; const float* rope_sin; /* [S, 32] tables: apply RoPE^T to dq/dk */
 } slx_attn_bwd_desc;
 int slx_attn_fwd(const slx_attn_desc* d, slx_stream_t stream);

@@ -14,12 +14,11 @@
 // double-buffered through LDS. Scores are computed transposed (S^T = K Q^T) so each lane owns one
 // query column: the row max needs one cross-half shuffle, the P^T accumulator feeds the P.V MFMA
 // directly as its B operand, and V is read with ds_read_b64_tr_b16 in the matching k order.
-// Backward: one workgroup = 4 waves = 128 keys of one (b, h); loops over 64-query chunks;
-// S and dP are recomputed with the key on the lane (their accumulators are the B operands of the
-// dV^T and dK^T products), dS^T goes through LDS once for dQ, which is accumulated with f32
-// atomics (2 x 128-B row segments per wave-instruction). For GQA each q-head's dK/dV partial is
-// stored with plain 16-B stores and a finalize kernel sums the group, applies the RoPE transpose
-// and converts to bf16 (row-scattered f32 atomics ran ~17x below the atomic rate here).
+// Backward: three launches, no atomics. delta = rowsum(dO*O); a dK/dV pass (one workgroup = 4 waves =
+// 128 keys of one (b, kv-head), sweeping the GQA group's q-heads x 64-query chunks, S and dP recomputed
+// with the key on the lane so their accumulators feed dV^T/dK^T directly); and a dQ pass shaped like the
+// forward (128 queries per workgroup, K/V tiles through LDS, dS^T in registers, dQ^T += K^T dS^T).
+// Summing dQ over key blocks with f32 atomics instead (one kernel) was bound by the ~1.3 TB/s atomic rate.
 #include "common.h"
 #include "../../include/slx.h"
 
@@ -72,10 +71,10 @@ struct AttnArgs {
   // backward
   const bf16* dout; long lddo;
   const float* delta;
-  float* dq_acc;               // [B*S, Hq*64] f32 (zeroed)
-  float* dk_acc; float* dv_acc;  // [B*S, Hq*64] f32 per-q-head partials when kv_atomic (GQA)
-  bf16* dk; bf16* dv; long lddk, lddv;  // direct bf16 outputs when !kv_atomic
-  int kv_atomic;
+  float* dq_acc;               // [B*S, Hq*64] f32, written by the dQ pass (finalized to bf16 + RoPE^T)
+  float* dk_acc; float* dv_acc;  // [nsplit][B*S, Hkv*64] f32 when GQA/RoPE (finalized), else null: direct bf16
+  bf16* dk; bf16* dv; long lddk, lddv;
+  int hsplit, nsplit;            // dK/dV pass: q-heads of a GQA group per workgroup, workgroups per group
 };
 
 // Stage 64 rows x 64 cols (bf16) of a token-major matrix into a swizzled LDS tile (8 KB).
@@ -101,9 +100,95 @@ __device__ __forceinline__ void store64(char* lds, const uint4 (&r)[2]) {
 constexpr float LOG2E = 1.4426950408889634f;
 constexpr float MASKED = -INFINITY;
 
+// XCD-aware block order: the hardware deals consecutive block ids round-robin over the 8 XCDs (each
+// with its own L2). Map the physical id to a logical one so every XCD gets a contiguous logical range,
+// and order logical ids (b, kv-head, q-head in group, 128-row block) fastest-last: all blocks that read
+// one (b, kv-head)'s K/V (or Q/dO in backward) then share one L2 instead of fetching it eight times.
+struct BlockCoord { int blk, h, b; };
+__device__ __forceinline__ BlockCoord attn_block(int nblk, int Hq, int Hkv, int B) {
+  const int nwg = nblk * Hq * B;
+  int bid = blockIdx.x;
+  const int q = nwg >> 3, r = nwg & 7, xcd = bid & 7;
+  bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  const int G = Hq / Hkv;
+  BlockCoord c;
+  c.blk = bid % nblk;
+  int t = bid / nblk;
+  const int hg = t % G;
+  t /= G;
+  const int hk = t % Hkv;
+  c.b = t / Hkv;
+  c.h = hk * G + hg;
+  return c;
+}
+
+// max over the two 32-lane halves (lane l and l^32) without an LDS round trip
+__device__ __forceinline__ float half_swap_max(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+
+// One 64-key tile of the forward for one wave (32 queries, query on the lane): S^T = K Q^T, online
+// softmax in the log2 domain with the scale folded into one FMA per score (max taken on raw scores,
+// c > 0), P^T from the accumulator straight into O^T += V^T P^T. MASK only for boundary tiles.
+template <bool MASK>
+__device__ __forceinline__ void fwd_tile(const char* Kl, const char* Vl, const bf16x8 (&qf)[4], f32x16& o0, f32x16& o1,
+                                         float& m, float& l, float c, int key0, int kvlen, int myq, bool causal,
+                                         int lane) {
+  const int hl = lane >> 5;
+  f32x16 s[2];
+#pragma unroll
+  for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s[kb][r] = 0.f;
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) s[kb] = mfma32(row_frag(Kl, kb * 32, kk, lane), qf[kk], s[kb]);
+  }
+  if constexpr (MASK) {
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = key0 + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
+        const bool ok = (key < kvlen) & (!causal | (key <= myq));
+        s[kb][r] = ok ? s[kb][r] : MASKED;
+      }
+  }
+  float mx = s[0][0];
+#pragma unroll
+  for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[kb][r]);
+  mx = half_swap_max(mx);
+  const float mnew = fmaxf(m, mx * c);
+  const float alpha = __builtin_amdgcn_exp2f(m - mnew);
+  m = mnew;
+  float ps = 0.f;
+#pragma unroll
+  for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[kb][r], c, -mnew));
+      s[kb][r] = p;
+      ps += p;
+    }
+  l = l * alpha + ps;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) { o0[r] *= alpha; o1[r] *= alpha; }
+#pragma unroll
+  for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      const bf16x8 pb = acc_frag(s[kb], st);
+      o0 = mfma32(tr_frag(Vl, kb * 32 + 16 * st, 0, lane), pb, o0);
+      o1 = mfma32(tr_frag(Vl, kb * 32 + 16 * st, 32, lane), pb, o1);
+    }
+}
+
 __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) char smem[2 * 2 * 8192];
-  const int qb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+  const BlockCoord bc = attn_block((a.S + 127) / 128, a.Hq, a.Hkv, a.B);
+  const int qb = bc.blk, h = bc.h, b = bc.b;
   const int hk = h / (a.Hq / a.Hkv);
   const int S = a.S;
   const int kvlen = a.seqlens ? min(a.seqlens[b], S) : S;
@@ -151,49 +236,10 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnArgs a) {
       load64(vbase, a.ldv, (t + 1) * 64, S, rv);
     }
     if (active) {
-      f32x16 s[2];
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) s[kb][r] = 0.f;
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk) s[kb] = mfma32(row_frag(Kl, kb * 32, kk, lane), qf[kk], s[kb]);
-      }
-      float mx = -1e30f;
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int key = t * 64 + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
-          float x = s[kb][r] * c;
-          if (key >= kvlen || (a.causal && key > myq)) x = MASKED;
-          s[kb][r] = x;
-          mx = fmaxf(mx, x);
-        }
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float mnew = fmaxf(m, mx);
-      const float alpha = exp2f(m - mnew);
-      m = mnew;
-      float ps = 0.f;
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float p = exp2f(s[kb][r] - m);
-          s[kb][r] = p;
-          ps += p;
-        }
-      l = l * alpha + ps;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) { o0[r] *= alpha; o1[r] *= alpha; }
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-        for (int st = 0; st < 2; ++st) {
-          const bf16x8 pb = acc_frag(s[kb], st);
-          o0 = mfma32(tr_frag(Vl, kb * 32 + 16 * st, 0, lane), pb, o0);
-          o1 = mfma32(tr_frag(Vl, kb * 32 + 16 * st, 32, lane), pb, o1);
-        }
+      // boundary tiles (past kvlen, or crossing this wave's causal diagonal) take the masked path
+      const int kfull = a.causal ? min(kvlen, q0 + 1) : kvlen;
+      if ((t + 1) * 64 <= kfull) fwd_tile<false>(Kl, Vl, qf, o0, o1, m, l, c, t * 64, kvlen, myq, false, lane);
+      else fwd_tile<true>(Kl, Vl, qf, o0, o1, m, l, c, t * 64, kvlen, myq, a.causal, lane);
     }
     if (t + 1 < nt) {
       char* nx = smem + ((t + 1) & 1) * 16384;
@@ -242,45 +288,81 @@ __global__ void attn_bwd_delta_kernel(AttnArgs a) {
   const_cast<float*>(a.delta)[((long)b * a.Hq + h) * a.S + s] = acc;
 }
 
-__global__ __launch_bounds__(256, 2) void attn_bwd_kernel(AttnArgs a) {
-  // LDS: K tile [128][64] 16 KB | Q chunk x2 (8 KB each) | dO chunk x2 | dS^T [128][64] 16 KB | lse,delta x2
-  __shared__ __attribute__((aligned(16))) char smem[16384 + 2 * 8192 + 2 * 8192 + 16384 + 2 * 2 * 64 * 4];
-  char* Kt = smem;
-  char* Qc = smem + 16384;
-  char* Dc = Qc + 2 * 8192;
-  char* dSt = Dc + 2 * 8192;
-  float* LD = reinterpret_cast<float*>(dSt + 16384);  // [buf][lse 64 | delta 64]
+// ---- backward, dK/dV pass: one workgroup = 4 waves = 128 keys of one (b, kv-head); sweeps every q-head of
+// the group x 64-query chunks (Q, dO, lse, delta staged through LDS). S and dP are computed with the key on
+// the lane, so their accumulators are the B operands of dV^T += dO^T P and dK^T += Q^T dS. dK/dV of the
+// whole GQA group accumulate in registers: no atomics, no cross-workgroup partials.
+template <bool MASK>
+__device__ __forceinline__ void bwd_kv_chunk(const char* Ql, const char* Dl, const float* lse_l, const float* del_l,
+                                             const bf16x8 (&kf)[4], const bf16x8 (&vf)[4], f32x16& dk0, f32x16& dk1,
+                                             f32x16& dv0, f32x16& dv1, float c, int qc, int S, int mykey, int kvlen,
+                                             bool causal, int lane) {
+  const int hl = lane >> 5;
+#pragma unroll
+  for (int qa = 0; qa < 2; ++qa) {
+    f32x16 sp, dp;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { sp[r] = 0.f; dp[r] = 0.f; }
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      sp = mfma32(row_frag(Ql, qa * 32, kk, lane), kf[kk], sp);
+      dp = mfma32(row_frag(Dl, qa * 32, kk, lane), vf[kk], dp);
+    }
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int ql = qa * 32 + 8 * g + 4 * hl;  // local query of register 4g
+      const f32x4 L4 = *reinterpret_cast<const f32x4*>(lse_l + ql);
+      const f32x4 D4 = *reinterpret_cast<const f32x4*>(del_l + ql);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int r = 4 * g + e;
+        float p = __builtin_amdgcn_exp2f(__builtin_fmaf(sp[r], c, -L4[e]));
+        if constexpr (MASK) {
+          const int q = qc + ql + e;
+          const bool ok = (q < S) & (mykey < kvlen) & (!causal | (mykey <= q));
+          p = ok ? p : 0.f;
+        }
+        sp[r] = p;
+        dp[r] = p * (dp[r] - D4[e]);
+      }
+    }
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      const bf16x8 pb = acc_frag(sp, st);
+      const bf16x8 sb = acc_frag(dp, st);
+      dv0 = mfma32(tr_frag(Dl, qa * 32 + 16 * st, 0, lane), pb, dv0);
+      dv1 = mfma32(tr_frag(Dl, qa * 32 + 16 * st, 32, lane), pb, dv1);
+      dk0 = mfma32(tr_frag(Ql, qa * 32 + 16 * st, 0, lane), sb, dk0);
+      dk1 = mfma32(tr_frag(Ql, qa * 32 + 16 * st, 32, lane), sb, dk1);
+    }
+  }
+}
 
-  const int kblk = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
-  const int hk = h / (a.Hq / a.Hkv);
+__global__ __launch_bounds__(256, 2) void attn_bwd_kv_kernel(AttnArgs a) {
+  // LDS: Q chunk x2 (8 KB each) | dO chunk x2 | lse,delta x2
+  __shared__ __attribute__((aligned(16))) char smem[2 * 8192 + 2 * 8192 + 2 * 2 * 64 * 4];
+  char* Qc = smem;
+  char* Dc = smem + 2 * 8192;
+  float* LD = reinterpret_cast<float*>(Dc + 2 * 8192);  // [buf][lse 64 | delta 64]
+
+  const BlockCoord bc = attn_block((a.S + 127) / 128, a.Hkv * a.nsplit, a.Hkv * a.nsplit, a.B);
+  const int kblk = bc.blk, hk = bc.h / a.nsplit, sp = bc.h % a.nsplit, b = bc.b;
+  const int G = a.Hq / a.Hkv;
+  const int hg0 = sp * a.hsplit;
+  const int ng = min(G, hg0 + a.hsplit) - hg0;  // q-heads of the group handled here
   const int S = a.S;
   const int kvlen = a.seqlens ? min(a.seqlens[b], S) : S;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hl = lane >> 5;
   const int k0 = kblk * 128;
-  const int mykey = k0 + 32 * w + (lane & 31);
+  const int kw0 = k0 + 32 * w;  // this wave's first key
+  const int mykey = kw0 + (lane & 31);
   const float c = a.scale * LOG2E;
 
-  const bf16* kbase = a.k + (long)b * S * a.ldk + hk * 64;
-  const bf16* vbase = a.v + (long)b * S * a.ldv + hk * 64;
-  const bf16* qbase = a.q + (long)b * S * a.ldq + h * 64;
-  const bf16* dobase = a.dout + (long)b * S * a.lddo + h * 64;
-  const float* lsebase = a.lse + ((long)b * a.Hq + h) * S;
-  const float* dlbase = a.delta + ((long)b * a.Hq + h) * S;
-
-  // K tile (128 keys) for the dQ product
-  {
-    uint4 r[2];
-    load64(kbase, a.ldk, k0, S, r);
-    store64(Kt, r);
-    load64(kbase, a.ldk, k0 + 64, S, r);
-    store64(Kt + 8192, r);
-  }
-  // K and V fragments of this wave's 32 keys (B operands of S = Q K^T and dP = dO V^T)
   bf16x8 kf[4], vf[4];
   {
     const int kr = min(mykey, S - 1);
-    const bf16* kp = kbase + (long)kr * a.ldk;
-    const bf16* vp = vbase + (long)kr * a.ldv;
+    const bf16* kp = a.k + ((long)b * S + kr) * a.ldk + hk * 64;
+    const bf16* vp = a.v + ((long)b * S + kr) * a.ldv + hk * 64;
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) {
       kf[kk] = *reinterpret_cast<const bf16x8*>(kp + 16 * kk + 8 * hl);
@@ -293,14 +375,16 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kernel(AttnArgs a) {
 
   const int qstart = a.causal ? (k0 / 64) * 64 : 0;
   const int nch = qstart < S ? (S - qstart + 63) / 64 : 0;
+  const int nit = nch * ng;  // (q-head, chunk) pairs, chunk fastest
 
-  auto stage = [&](int ci, int buf, uint4 (&rq)[2], uint4 (&rd)[2], float& ld) {
-    const int qc = qstart + ci * 64;
-    load64(qbase, a.ldq, qc, S, rq);
-    load64(dobase, a.lddo, qc, S, rd);
+  auto stage = [&](int it, uint4 (&rq)[2], uint4 (&rd)[2], float& ld) {
+    const int h = hk * G + hg0 + it / nch, qc = qstart + (it % nch) * 64;
+    load64(a.q + (long)b * S * a.ldq + h * 64, a.ldq, qc, S, rq);
+    load64(a.dout + (long)b * S * a.lddo + h * 64, a.lddo, qc, S, rd);
     if (tid < 128) {
       const int qi = qc + (tid & 63);
-      ld = qi < S ? (tid < 64 ? lsebase[qi] : dlbase[qi]) : 0.f;
+      const long base = ((long)b * a.Hq + h) * S;
+      ld = qi < S ? (tid < 64 ? a.lse[base + qi] : a.delta[base + qi]) : 0.f;
     }
   };
   auto commit = [&](int buf, const uint4 (&rq)[2], const uint4 (&rd)[2], float ld) {
@@ -311,95 +395,35 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kernel(AttnArgs a) {
 
   uint4 rq[2], rd[2];
   float ldv = 0.f;
-  if (nch > 0) {
-    stage(0, 0, rq, rd, ldv);
+  if (nit > 0) {
+    stage(0, rq, rd, ldv);
     commit(0, rq, rd, ldv);
   }
   __syncthreads();
-
-  for (int ci = 0; ci < nch; ++ci) {
-    const int buf = ci & 1;
-    const int qc = qstart + ci * 64;
+  for (int it = 0; it < nit; ++it) {
+    const int buf = it & 1;
+    const int qc = qstart + (it % nch) * 64;
+    if (it + 1 < nit) stage(it + 1, rq, rd, ldv);
     const char* Ql = Qc + buf * 8192;
     const char* Dl = Dc + buf * 8192;
     const float* lse_l = LD + buf * 128;
-    const float* del_l = lse_l + 64;
-    if (ci + 1 < nch) stage(ci + 1, buf ^ 1, rq, rd, ldv);
-
-#pragma unroll
-    for (int qa = 0; qa < 2; ++qa) {
-      f32x16 sp, dp;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) { sp[r] = 0.f; dp[r] = 0.f; }
-#pragma unroll
-      for (int kk = 0; kk < 4; ++kk) {
-        sp = mfma32(row_frag(Ql, qa * 32, kk, lane), kf[kk], sp);
-        dp = mfma32(row_frag(Dl, qa * 32, kk, lane), vf[kk], dp);
-      }
-      // P and dS with the query on the accumulator rows
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int ql = qa * 32 + 8 * g + 4 * hl;  // local query of register 4g
-        const f32x4 L4 = *reinterpret_cast<const f32x4*>(lse_l + ql);
-        const f32x4 D4 = *reinterpret_cast<const f32x4*>(del_l + ql);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int r = 4 * g + e;
-          const int q = qc + ql + e;
-          const bool ok = q < S && mykey < kvlen && !(a.causal && mykey > q);
-          const float p = ok ? exp2f(sp[r] * c - L4[e]) : 0.f;
-          sp[r] = p;
-          dp[r] = p * (dp[r] - D4[e]);
-        }
-      }
-      // dV^T += dO^T P ; dK^T += Q^T dS
-#pragma unroll
-      for (int st = 0; st < 2; ++st) {
-        const bf16x8 pb = acc_frag(sp, st);
-        const bf16x8 sb = acc_frag(dp, st);
-        dv0 = mfma32(tr_frag(Dl, qa * 32 + 16 * st, 0, lane), pb, dv0);
-        dv1 = mfma32(tr_frag(Dl, qa * 32 + 16 * st, 32, lane), pb, dv1);
-        dk0 = mfma32(tr_frag(Ql, qa * 32 + 16 * st, 0, lane), sb, dk0);
-        dk1 = mfma32(tr_frag(Ql, qa * 32 + 16 * st, 32, lane), sb, dk1);
-      }
-      // dS^T image row = local key, columns = local query
-      const int krow = 32 * w + (lane & 31);
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        bf16x4 v;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = (bf16)dp[4 * g + e];
-        *reinterpret_cast<bf16x4*>(dSt + sw_elem(krow, qa * 32 + 8 * g + 4 * hl)) = v;
-      }
-    }
-    __syncthreads();
-    {  // dQ[q][d] = sum over the block's 128 keys of dS[q][key] K[key][d]; wave -> (q half, d half)
-      const int qa = w >> 1, db = w & 1;
-      f32x16 acc;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-#pragma unroll
-      for (int kk = 0; kk < 8; ++kk) acc = mfma32(tr_frag(dSt, 16 * kk, 32 * qa, lane), tr_frag(Kt, 16 * kk, 32 * db, lane), acc);
-      const int d = 32 * db + (lane & 31);
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int q = qc + 32 * qa + (r & 3) + 8 * (r >> 2) + 4 * hl;
-        if (q < S) atomicAdd(a.dq_acc + ((long)b * S + q) * (a.Hq * 64) + h * 64 + d, acc[r] * a.scale);
-      }
-    }
-    if (ci + 1 < nch) commit(buf ^ 1, rq, rd, ldv);
+    // boundary chunks: past S (query tail), this wave's keys past kvlen, or crossing the causal diagonal
+    const bool full = (qc + 64 <= S) && (kw0 + 32 <= kvlen) && (!a.causal || kw0 + 31 <= qc);
+    if (full) bwd_kv_chunk<false>(Ql, Dl, lse_l, lse_l + 64, kf, vf, dk0, dk1, dv0, dv1, c, qc, S, mykey, kvlen, false, lane);
+    else bwd_kv_chunk<true>(Ql, Dl, lse_l, lse_l + 64, kf, vf, dk0, dk1, dv0, dv1, c, qc, S, mykey, kvlen, a.causal, lane);
+    if (it + 1 < nit) commit(buf ^ 1, rq, rd, ldv);
     __syncthreads();
   }
 
   if (mykey >= S) return;
-  // dK^T / dV^T accumulators: column = key (lane), rows = d
+  // accumulators: column = key (lane), rows = d
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
     const int d = 8 * g + 4 * hl;
-    if (a.kv_atomic) {
-      // GQA: per-q-head partials with plain 16-B stores; slx_attn_bwd's finalize sums the group
-      float* kp = a.dk_acc + ((long)b * S + mykey) * (a.Hq * 64) + h * 64;
-      float* vp = a.dv_acc + ((long)b * S + mykey) * (a.Hq * 64) + h * 64;
+    if (a.dk_acc) {  // f32 partial of this head split; the finalize sums splits, applies RoPE^T, casts
+      const long off = (long)sp * a.B * S * (a.Hkv * 64) + ((long)b * S + mykey) * (a.Hkv * 64) + hk * 64;
+      float* kp = a.dk_acc + off;
+      float* vp = a.dv_acc + off;
       *reinterpret_cast<float4*>(kp + d) = make_float4(dk0[4 * g] * a.scale, dk0[4 * g + 1] * a.scale, dk0[4 * g + 2] * a.scale, dk0[4 * g + 3] * a.scale);
       *reinterpret_cast<float4*>(kp + 32 + d) = make_float4(dk1[4 * g] * a.scale, dk1[4 * g + 1] * a.scale, dk1[4 * g + 2] * a.scale, dk1[4 * g + 3] * a.scale);
       *reinterpret_cast<float4*>(vp + d) = make_float4(dv0[4 * g], dv0[4 * g + 1], dv0[4 * g + 2], dv0[4 * g + 3]);
@@ -423,10 +447,121 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kernel(AttnArgs a) {
   }
 }
 
-// Rotary embedding (HF rotate_half convention, Qwen2): for i < 32
-//   y[i] = x[i] cos_i - x[i+32] sin_i ;  y[i+32] = x[i+32] cos_i + x[i] sin_i
-// with cos_i/sin_i of (pos * theta^(-2i/64)), pos = token index within its sequence.
-// inverse != 0 applies the transpose (backward).
+// ---- backward, dQ pass (the forward's structure): one workgroup = 4 waves = 128 queries of one (b, h);
+// K/V tiles of 64 keys double-buffered through LDS; per tile S^T = K Q^T and dP^T = V dO^T with the query on
+// the lane, dS^T = P^T (dP^T - delta) in registers, dQ^T += K^T dS^T (K read transposed). Plain stores, no
+// atomics: recomputing S and dP here costs less than summing dQ over key blocks with f32 atomics
+// (~1.3 TB/s chip-wide), which bounded the single-kernel backward.
+template <bool MASK>
+__device__ __forceinline__ void bwd_dq_tile(const char* Kl, const char* Vl, const bf16x8 (&qf)[4], const bf16x8 (&df)[4],
+                                            f32x16& dq0, f32x16& dq1, float c, float lse, float dlt, int key0,
+                                            int kvlen, int myq, bool causal, int lane) {
+  const int hl = lane >> 5;
+  f32x16 s[2], dp[2];
+#pragma unroll
+  for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { s[kb][r] = 0.f; dp[kb][r] = 0.f; }
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      s[kb] = mfma32(row_frag(Kl, kb * 32, kk, lane), qf[kk], s[kb]);
+      dp[kb] = mfma32(row_frag(Vl, kb * 32, kk, lane), df[kk], dp[kb]);
+    }
+  }
+#pragma unroll
+  for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[kb][r], c, -lse));
+      if constexpr (MASK) {
+        const int key = key0 + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
+        const bool ok = (key < kvlen) & (!causal | (key <= myq));
+        p = ok ? p : 0.f;
+      }
+      dp[kb][r] = p * (dp[kb][r] - dlt);
+    }
+#pragma unroll
+  for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      const bf16x8 sb = acc_frag(dp[kb], st);
+      dq0 = mfma32(tr_frag(Kl, kb * 32 + 16 * st, 0, lane), sb, dq0);
+      dq1 = mfma32(tr_frag(Kl, kb * 32 + 16 * st, 32, lane), sb, dq1);
+    }
+}
+
+__global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnArgs a) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * 8192];
+  const BlockCoord bc = attn_block((a.S + 127) / 128, a.Hq, a.Hkv, a.B);
+  const int qb = bc.blk, h = bc.h, b = bc.b;
+  const int hk = h / (a.Hq / a.Hkv);
+  const int S = a.S;
+  const int kvlen = a.seqlens ? min(a.seqlens[b], S) : S;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hl = lane >> 5;
+  const int q0 = qb * 128 + w * 32;
+  const int myq = q0 + (lane & 31);
+  const bool active = q0 < S;
+  const float c = a.scale * LOG2E;
+  const bf16* kbase = a.k + (long)b * S * a.ldk + hk * 64;
+  const bf16* vbase = a.v + (long)b * S * a.ldv + hk * 64;
+
+  bf16x8 qf[4], df[4];
+  float lse = 0.f, dlt = 0.f;
+  {
+    const int qr = min(myq, S - 1);
+    const bf16* qrow = a.q + ((long)b * S + qr) * a.ldq + h * 64;
+    const bf16* drow = a.dout + ((long)b * S + qr) * a.lddo + h * 64;
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      qf[kk] = *reinterpret_cast<const bf16x8*>(qrow + 16 * kk + 8 * hl);
+      df[kk] = *reinterpret_cast<const bf16x8*>(drow + 16 * kk + 8 * hl);
+    }
+    const long li = ((long)b * a.Hq + h) * S + qr;
+    lse = a.lse[li];
+    dlt = a.delta[li];
+  }
+  int kend = kvlen;
+  if (a.causal) kend = min(kend, qb * 128 + 128);
+  const int nt = (kend + 63) / 64;
+  f32x16 dq0, dq1;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) { dq0[r] = 0.f; dq1[r] = 0.f; }
+
+  uint4 rk[2], rv[2];
+  load64(kbase, a.ldk, 0, S, rk);
+  load64(vbase, a.ldv, 0, S, rv);
+  store64(smem, rk);
+  store64(smem + 8192, rv);
+  __syncthreads();
+  for (int t = 0; t < nt; ++t) {
+    const char* Kl = smem + (t & 1) * 16384;
+    const char* Vl = Kl + 8192;
+    if (t + 1 < nt) {
+      load64(kbase, a.ldk, (t + 1) * 64, S, rk);
+      load64(vbase, a.ldv, (t + 1) * 64, S, rv);
+    }
+    if (active) {
+      const int kfull = a.causal ? min(kvlen, q0 + 1) : kvlen;
+      if ((t + 1) * 64 <= kfull) bwd_dq_tile<false>(Kl, Vl, qf, df, dq0, dq1, c, lse, dlt, t * 64, kvlen, myq, false, lane);
+      else bwd_dq_tile<true>(Kl, Vl, qf, df, dq0, dq1, c, lse, dlt, t * 64, kvlen, myq, a.causal, lane);
+    }
+    if (t + 1 < nt) {
+      char* nx = smem + ((t + 1) & 1) * 16384;
+      store64(nx, rk);
+      store64(nx + 8192, rv);
+    }
+    __syncthreads();
+  }
+  if (!active || myq >= S) return;
+  float* qrow = a.dq_acc + ((long)b * S + myq) * (a.Hq * 64) + h * 64;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const int d = 8 * g + 4 * hl;
+    *reinterpret_cast<float4*>(qrow + d) = make_float4(dq0[4 * g] * a.scale, dq0[4 * g + 1] * a.scale, dq0[4 * g + 2] * a.scale, dq0[4 * g + 3] * a.scale);
+    *reinterpret_cast<float4*>(qrow + 32 + d) = make_float4(dq1[4 * g] * a.scale, dq1[4 * g + 1] * a.scale, dq1[4 * g + 2] * a.scale, dq1[4 * g + 3] * a.scale);
+  }
+}
+
 __device__ __forceinline__ void rope_pair(float& x0, float& x1, float cs, float sn, bool inverse) {
   const float a = x0, b = x1;
   if (!inverse) { x0 = a * cs - b * sn; x1 = b * cs + a * sn; }
@@ -436,6 +571,7 @@ __device__ __forceinline__ void rope_pair(float& x0, float& x1, float cs, float 
 struct RopeArgs {
   bf16* x; long ldx; int ntok, S, nheads; const float* cos; const float* sin; int inverse;
   const float* src_f32; long ldsrc;  // optional f32 source (finalize: dq/dk accumulators)
+  int nsplit; long split_stride;     // f32 source: sum of nsplit partials split_stride floats apart
 };
 
 // One thread per (token, head, i<32 pair-group of 4): 8 pairs per thread -> 256 threads per row
@@ -455,6 +591,11 @@ __global__ void rope_kernel(RopeArgs r) {
     const float* s = r.src_f32 + tok * r.ldsrc + hh * 64;
 #pragma unroll
     for (int j = 0; j < 8; ++j) { v0[j] = s[i0 + j]; v1[j] = s[32 + i0 + j]; }
+    for (int p = 1; p < r.nsplit; ++p) {
+      const float* t = s + p * r.split_stride;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { v0[j] += t[i0 + j]; v1[j] += t[32 + i0 + j]; }
+    }
   } else {
     const bf16x8 a = *reinterpret_cast<const bf16x8*>(x + i0);
     const bf16x8 b = *reinterpret_cast<const bf16x8*>(x + 32 + i0);
@@ -464,8 +605,7 @@ __global__ void rope_kernel(RopeArgs r) {
   bf16x8 oa, ob;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    const float cs = r.cos[(long)pos * 32 + i0 + j], sn = r.sin[(long)pos * 32 + i0 + j];
-    rope_pair(v0[j], v1[j], cs, sn, r.inverse != 0);
+    if (r.cos) rope_pair(v0[j], v1[j], r.cos[(long)pos * 32 + i0 + j], r.sin[(long)pos * 32 + i0 + j], r.inverse != 0);
     oa[j] = (bf16)v0[j];
     ob[j] = (bf16)v1[j];
   }
@@ -475,42 +615,6 @@ __global__ void rope_kernel(RopeArgs r) {
 
 // GQA finalize: dst[t, hk, :] = sum_{j<G} src[t, hk*G + j, :] (f32 per-q-head partials, row stride
 // Hq*64) -> optional RoPE^T -> bf16. One thread per (token, kv head, quarter of the pairs).
-__global__ void gqa_reduce_kernel(const float* src, int Hq, int Hkv, bf16* dst, long ldd, long ntok, int S, const float* cos,
-                                  const float* sin) {
-  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= ntok * Hkv * 4) return;
-  const int part = idx & 3;
-  const long th = idx >> 2;
-  const int hk = th % Hkv;
-  const long tok = th / Hkv;
-  const int G = Hq / Hkv, i0 = part * 8;
-  float v0[8], v1[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) { v0[j] = 0.f; v1[j] = 0.f; }
-  for (int g = 0; g < G; ++g) {
-    const float* sp = src + tok * (long)Hq * 64 + (hk * G + g) * 64;
-#pragma unroll
-    for (int j = 0; j < 8; j += 4) {
-      const float4 a = *reinterpret_cast<const float4*>(sp + i0 + j);
-      const float4 c = *reinterpret_cast<const float4*>(sp + 32 + i0 + j);
-      v0[j] += a.x; v0[j + 1] += a.y; v0[j + 2] += a.z; v0[j + 3] += a.w;
-      v1[j] += c.x; v1[j + 1] += c.y; v1[j + 2] += c.z; v1[j + 3] += c.w;
-    }
-  }
-  bf16x8 oa, ob;
-  const int pos = tok % S;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    if (cos) rope_pair(v0[j], v1[j], cos[(long)pos * 32 + i0 + j], sin[(long)pos * 32 + i0 + j], true);
-    oa[j] = (bf16)v0[j];
-    ob[j] = (bf16)v1[j];
-  }
-  bf16* dp = dst + tok * ldd + hk * 64;
-  *reinterpret_cast<bf16x8*>(dp + i0) = oa;
-  *reinterpret_cast<bf16x8*>(dp + 32 + i0) = ob;
-}
-
-// f32 [ntok, ncols] -> bf16 rows (ld) (no rope)
 __global__ void f32_to_bf16_rows_kernel(const float* src, long lds, bf16* dst, long ldd, long ntok, int ncols) {
   const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const int per = ncols / 8;
@@ -546,7 +650,7 @@ extern "C" int slx_attn_fwd(const slx_attn_desc* d, slx_stream_t stream) {
   int rc = fill_common(a, d);
   if (rc) return rc;
   if (a.B == 0 || a.S == 0) return 0;
-  dim3 grid((a.S + 127) / 128, a.Hq, a.B);
+  dim3 grid(((a.S + 127) / 128) * a.Hq * a.B);
   hipLaunchKernelGGL(attn_fwd_kernel, grid, dim3(256), 0, (hipStream_t)stream, a);
   SLX_LAUNCH_CHECK("slx_attn_fwd");
   return 0;
@@ -560,32 +664,43 @@ extern "C" int slx_attn_bwd(const slx_attn_desc* d, const slx_attn_bwd_desc* g, 
   hipStream_t st = (hipStream_t)stream;
   a.dout = (const bf16*)g->dout; a.lddo = g->lddo;
   a.delta = g->delta_ws;
-  a.dq_acc = g->dq_acc; a.dk_acc = g->dk_acc; a.dv_acc = g->dv_acc;
-  a.kv_atomic = d->Hq != d->Hkv ? 1 : 0;
+  a.dq_acc = g->dq_acc;
+  const bool gqa = d->Hq != d->Hkv;
+  const bool f32kv = gqa || g->rope_cos;  // dK needs RoPE^T or the layout differs: finalize from f32
   SLX_CHECK_ARG(a.lse && a.delta && a.dq_acc, "slx_attn_bwd: lse, delta_ws and dq_acc are required");
-  SLX_CHECK_ARG(!a.kv_atomic || (a.dk_acc && a.dv_acc), "slx_attn_bwd: GQA needs dk_acc/dv_acc workspaces");
+  SLX_CHECK_ARG(!f32kv || (g->dk_acc && g->dv_acc), "slx_attn_bwd: GQA/RoPE needs dk_acc/dv_acc workspaces");
+  a.dk_acc = f32kv ? g->dk_acc : nullptr;
+  a.dv_acc = f32kv ? g->dv_acc : nullptr;
+  a.dk = (bf16*)g->dk; a.dv = (bf16*)g->dv; a.lddk = g->lddk; a.lddv = g->lddv;
   const long ntok = (long)a.B * a.S;
-  hipMemsetAsync(a.dq_acc, 0, ntok * a.Hq * 64 * sizeof(float), st);
-  if (a.kv_atomic) {
-    // per-q-head partials, fully overwritten by the kernel (no memset)
-  } else {
-    a.dk = (bf16*)g->dk; a.dv = (bf16*)g->dv; a.lddk = g->lddk; a.lddv = g->lddv;
-  }
   {
     const long total = ntok * a.Hq;
     hipLaunchKernelGGL(attn_bwd_delta_kernel, dim3((total + 255) / 256), dim3(256), 0, st, a);
     SLX_LAUNCH_CHECK("slx_attn_bwd(delta)");
   }
-  dim3 grid((a.S + 127) / 128, a.Hq, a.B);
-  hipLaunchKernelGGL(attn_bwd_kernel, grid, dim3(256), 0, st, a);
-  SLX_LAUNCH_CHECK("slx_attn_bwd");
-  // finalize: dq (and dk/dv for GQA) -> bf16, with the RoPE transpose when tables are given
-  RopeArgs r;
-  memset(&r, 0, sizeof(r));
-  r.ntok = ntok; r.S = a.S; r.cos = g->rope_cos; r.sin = g->rope_sin; r.inverse = 1;
-  auto conv = [&](const float* src, int heads, bf16* dst, long ld, bool rope) -> int {
-    if (rope && r.cos) {
+  const int nblk = (a.S + 127) / 128;
+  {  // split a GQA group's q-heads over workgroups until the dK/dV grid fills the chip (~2 per CU)
+    const int G = a.Hq / a.Hkv, base = nblk * a.Hkv * a.B;
+    int ns = (512 + base - 1) / base;
+    ns = ns < 1 ? 1 : (ns > G ? G : ns);
+    if (!f32kv) ns = 1;
+    a.hsplit = (G + ns - 1) / ns;
+    a.nsplit = (G + a.hsplit - 1) / a.hsplit;
+  }
+  hipLaunchKernelGGL(attn_bwd_kv_kernel, dim3(nblk * a.Hkv * a.nsplit * a.B), dim3(256), 0, st, a);
+  SLX_LAUNCH_CHECK("slx_attn_bwd(dk/dv)");
+  hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3(nblk * a.Hq * a.B), dim3(256), 0, st, a);
+  SLX_LAUNCH_CHECK("slx_attn_bwd(dq)");
+  // finalize: f32 -> bf16, summing head-split partials and applying the RoPE transpose where asked
+  auto conv = [&](const float* src, int heads, bf16* dst, long ld, bool rope, int nsplit) -> int {
+    if ((rope && g->rope_cos) || nsplit > 1) {
+      RopeArgs r;
+      memset(&r, 0, sizeof(r));
+      r.ntok = ntok; r.S = a.S; r.inverse = 1;
+      r.cos = rope ? g->rope_cos : nullptr;
+      r.sin = rope ? g->rope_sin : nullptr;
       r.x = dst; r.ldx = ld; r.nheads = heads; r.src_f32 = src; r.ldsrc = (long)heads * 64;
+      r.nsplit = nsplit; r.split_stride = ntok * heads * 64;
       const long total = ntok * heads * 4;
       hipLaunchKernelGGL(rope_kernel, dim3((total + 255) / 256), dim3(256), 0, st, r);
     } else {
@@ -595,20 +710,10 @@ extern "C" int slx_attn_bwd(const slx_attn_desc* d, const slx_attn_bwd_desc* g, 
     SLX_LAUNCH_CHECK("slx_attn_bwd(finalize)");
     return 0;
   };
-  if ((rc = conv(a.dq_acc, a.Hq, (bf16*)g->dq, g->lddq, true))) return rc;
-  if (a.kv_atomic) {
-    const long total = ntok * a.Hkv * 4;
-    hipLaunchKernelGGL(gqa_reduce_kernel, dim3((total + 255) / 256), dim3(256), 0, st, a.dk_acc, a.Hq, a.Hkv, (bf16*)g->dk,
-                       (long)g->lddk, ntok, a.S, r.cos, r.sin);
-    hipLaunchKernelGGL(gqa_reduce_kernel, dim3((total + 255) / 256), dim3(256), 0, st, a.dv_acc, a.Hq, a.Hkv, (bf16*)g->dv,
-                       (long)g->lddv, ntok, a.S, (const float*)nullptr, (const float*)nullptr);
-    SLX_LAUNCH_CHECK("slx_attn_bwd(gqa reduce)");
-  } else if (r.cos) {
-    // direct bf16 dK still needs the RoPE transpose (in place)
-    r.x = (bf16*)g->dk; r.ldx = g->lddk; r.nheads = a.Hkv; r.src_f32 = nullptr;
-    const long total = ntok * a.Hkv * 4;
-    hipLaunchKernelGGL(rope_kernel, dim3((total + 255) / 256), dim3(256), 0, st, r);
-    SLX_LAUNCH_CHECK("slx_attn_bwd(rope dk)");
+  if ((rc = conv(a.dq_acc, a.Hq, (bf16*)g->dq, g->lddq, true, 1))) return rc;
+  if (f32kv) {
+    if ((rc = conv(a.dk_acc, a.Hkv, (bf16*)g->dk, g->lddk, true, a.nsplit))) return rc;
+    if ((rc = conv(a.dv_acc, a.Hkv, (bf16*)g->dv, g->lddv, false, a.nsplit))) return rc;
   }
   return 0;
 }

@@ -271,7 +271,7 @@ def attn_fwd(q, k, v, o, lse, **kw):
 
 
 def attn_bwd(q, k, v, o, lse, dout, dq, dk, dv, ws, *, rope_cos=None, rope_sin=None, **kw):
-    """ws: dict with 'delta' [B*Hq*S], 'dq_acc' [B*S*Hq*64], ('dk_acc','dv_acc' for GQA) f32 buffers."""
+    """ws: attn_ws(...) f32 buffers (delta, dq_acc, and dk_acc/dv_acc for GQA or RoPE)."""
     d = attn_desc(q, k, v, o, lse, **kw)
     g = AttnBwdDesc()
     g.dout, g.lddo = dout.data_ptr(), dout.stride(0)
@@ -287,9 +287,11 @@ def attn_bwd(q, k, v, o, lse, dout, dq, dk, dv, ws, *, rope_cos=None, rope_sin=N
     check(lib().slx_attn_bwd(ctypes.byref(d), ctypes.byref(g), stream_ptr()), "slx_attn_bwd")
 
 
-def attn_ws(B, S, Hq, Hkv, device):
+def attn_ws(B, S, Hq, Hkv, device, rope=False):
+    """f32 workspaces of slx_attn_bwd: delta, dq_acc; dk_acc/dv_acc [B*S, Hq*64] (head-split partials) for GQA
+    or RoPE."""
     ws = {"delta": torch.empty(B * Hq * S, device=device), "dq_acc": torch.empty(B * S * Hq * 64, device=device)}
-    if Hq != Hkv:
+    if Hq != Hkv or rope:
         ws["dk_acc"] = torch.empty(B * S * Hq * 64, device=device)
         ws["dv_acc"] = torch.empty(B * S * Hq * 64, device=device)
     return ws
