@@ -154,6 +154,17 @@ typedef struct {
   float p; int64_t ldmask;
 } slx_lora_down_desc;
 int slx_lora_down(const slx_lora_down_desc* d, slx_stream_t stream);
+/* LoRA A-gradient of the sites sharing one input (peft lora_A backward): dA_j[32, Kin] += dT_j^T drop_j(x),
+ * dT_j = columns 32j..32j+31 of dT (bf16 [M, >= 32*nsites]); f32 atomics into dA_j; masks as slx_lora_down. */
+typedef struct {
+  const void* x; int64_t ldx;         /* bf16 [M, Kin] (undropped forward input) */
+  int64_t M; int Kin; int r; int nsites;
+  const void* dT; int64_t ldt;        /* bf16 [M, >= 32*nsites] */
+  float* dA[4];                       /* f32 [r, Kin] per site, accumulated */
+  uint64_t seed[4];
+  float p; int64_t ldmask;
+} slx_lora_da_desc;
+int slx_lora_da(const slx_lora_da_desc* d, slx_stream_t stream);
 
 /* small strided f32 GEMM (driving heads adaptors.py:113-132, WaypointInputAdaptor :80)        */
 enum { SLX_ACT_NONE = 0, SLX_ACT_RELU = 1, SLX_ACT_SILU = 2 };

@@ -630,14 +630,14 @@ class VLAEngine:
         K.call("slx_cast_rows", K.P(dtx), dtx.stride(0), K.P(dT), dT.stride(0), M, P, K.stream_ptr())
         if P < W:
             dT[:, P:].zero_()
+        seeds = [sv["llm"][i]["lora"][site] for site in sites]
+        K.lora_da(x, dT, [self.G[f"llm.{i}.lora.{site}.a"] for site in sites], seeds, p=drop)   # dA_j += dT_j^T drop_j(x)
         for j, site in enumerate(sites):
             p = f"llm.{i}.lora.{site}."
-            seed = sv["llm"][i]["lora"][site]
             K.mm(dys[j], tx[:, r * j:r * (j + 1)], self.G[p + "b"], ta=True, tb=False, alpha=s, accumulate=True)
-            K.mm(dT[:, r * j:r * (j + 1)], x, self.G[p + "a"], ta=True, tb=False, accumulate=True,
-                 drop_operand=2 if drop > 0 else 0, seed=seed, drop_p=drop, ldmask=kin)
             K.mm(dT[:, r * j:r * j + 64], self.cat[i]["apad." + site], dx, tb=False,
-                 epi=K.EPI_DROPMASK if drop > 0 else K.EPI_STORE, accumulate=True, seed=seed, drop_p=drop, ldmask=kin)
+                 epi=K.EPI_DROPMASK if drop > 0 else K.EPI_STORE, accumulate=True, seed=seeds[j], drop_p=drop,
+                 ldmask=kin)
 
     def _mlp_bwd(self, dout, saved, need_dx=True):
         """saved: [(out, pre, in, prefix, act)] from last layer to first; dout: grad of the last output."""

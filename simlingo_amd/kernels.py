@@ -208,10 +208,19 @@ class LoraDownDesc(ctypes.Structure):
     ]
 
 
+class LoraDaDesc(ctypes.Structure):
+    _fields_ = [
+        ("x", c_vp), ("ldx", c_i64), ("M", c_i64), ("Kin", c_int), ("r", c_int), ("nsites", c_int),
+        ("dT", c_vp), ("ldt", c_i64), ("dA", c_vp * 4), ("seed", ctypes.c_uint64 * 4), ("p", c_float),
+        ("ldmask", c_i64),
+    ]
+
+
 _vp, _i, _I, _f = c_vp, c_int, c_i64, c_float
 for _n, _a in {
     "slx_attn_fwd": [ctypes.POINTER(AttnDesc), _vp],
     "slx_lora_down": [ctypes.POINTER(LoraDownDesc), _vp],
+    "slx_lora_da": [ctypes.POINTER(LoraDaDesc), _vp],
     "slx_attn_bwd": [ctypes.POINTER(AttnDesc), ctypes.POINTER(AttnBwdDesc), _vp],
     "slx_rope": [_vp, _I, _I, _i, _i, _vp, _vp, _i, _vp],
     "slx_norm_fwd": [ctypes.POINTER(NormDesc), _vp],
@@ -371,6 +380,22 @@ def lora_down(x, As, t, seeds, p=0.0, ldmask=None):
         d.seed[j] = int(seeds[j]) & ((1 << 64) - 1)
     d.t, d.ldt, d.p, d.ldmask = P(t).value, t.stride(0), float(p), kin if ldmask is None else ldmask
     check(lib().slx_lora_down(ctypes.byref(d), stream_ptr()), "slx_lora_down")
+
+
+def lora_da(x, dT, dAs, seeds, p=0.0, ldmask=None):
+    """dAs[j] (f32 [32, kin]) += dT[:, 32j:32j+32]^T drop_j(x) for the sites sharing x (one launch)."""
+    assert x.dtype == torch.bfloat16 and dT.dtype == torch.bfloat16 and 1 <= len(dAs) <= 4
+    M, kin = x.shape
+    assert dT.shape[0] == M and dT.shape[1] >= 32 * len(dAs) and dT.stride(1) == 1
+    d = LoraDaDesc()
+    d.x, d.ldx, d.M, d.Kin, d.r, d.nsites = P(x).value, x.stride(0), M, kin, 32, len(dAs)
+    d.dT, d.ldt = P(dT).value, dT.stride(0)
+    for j, g in enumerate(dAs):
+        assert g.shape == (32, kin) and g.is_contiguous() and g.dtype == torch.float32
+        d.dA[j] = g.data_ptr()
+        d.seed[j] = int(seeds[j]) & ((1 << 64) - 1)
+    d.p, d.ldmask = float(p), kin if ldmask is None else ldmask
+    check(lib().slx_lora_da(ctypes.byref(d), stream_ptr()), "slx_lora_da")
 
 
 def mm(A, B, C, *, ta=False, tb=True, **kw):

@@ -53,7 +53,8 @@ def test_struct_layouts_match_header(tmp_path):
         pytest.skip("gcc not available")
     structs = {"slx_gemm_desc": K.GemmDesc, "slx_attn_desc": K.AttnDesc, "slx_attn_bwd_desc": K.AttnBwdDesc,
                "slx_norm_desc": K.NormDesc, "slx_sgemm_desc": K.SgemmDesc,
-               "slx_lora_down_desc": K.LoraDownDesc}
+               "slx_lora_down_desc": K.LoraDownDesc,
+               "slx_lora_da_desc": K.LoraDaDesc}
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "slx.h"', "int main(void){"]
     for cname, cls in structs.items():
         lines.append(f'printf("{cname} size %zu\\n", sizeof({cname}));')

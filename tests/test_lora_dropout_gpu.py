@@ -72,3 +72,20 @@ def test_dropmask_dgrad_padded_k64(dev):
              ldmask=kin)
         ref = 1 + mask * (dT[:, 32 * j:32 * (j + 1)].float() @ A.float())
         torch.testing.assert_close(dx, ref, atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("M,kin,nsites,p", [(300, 256, 3, 0.1), (1000, 896, 2, 0.1), (130, 640, 1, 0.0),
+                                            (64, 128, 4, 0.1)])
+def test_lora_da_grouped(dev, M, kin, nsites, p):
+    """slx_lora_da: dA_j += dT_j^T drop_j(x) with per-site masks, one launch for the sites sharing x."""
+    g = torch.Generator(device=dev).manual_seed(13)
+    x = torch.randn(M, kin, device=dev, generator=g).bfloat16()
+    dT = torch.randn(M, 32 * nsites + 32, device=dev, generator=g).bfloat16()
+    seeds = [777 + 31 * j for j in range(nsites)]
+    dAs = [torch.full((32, kin), 0.5, device=dev) for _ in range(nsites)]
+    K.lora_da(x, dT, dAs, seeds, p=p)
+    for j in range(nsites):
+        mask = torch.from_numpy(keep_scale(seeds[j], M, kin, kin, p)).to(dev) if p > 0 else 1.0
+        xd = (x.float() * mask).bfloat16().float()
+        ref = 0.5 + dT[:, 32 * j:32 * (j + 1)].float().t() @ xd
+        torch.testing.assert_close(dAs[j], ref, atol=5e-2, rtol=1e-2)
