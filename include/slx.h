@@ -44,7 +44,9 @@ enum {
                              C(f32) = resid + ls[n]*y   (InternViT layer-scale residual)      */
   SLX_EPI_GELU_BWD = 3,   /* C = alpha*acc * gelu_erf'(aux[m,n])                              */
   SLX_EPI_SWIGLU_BWD = 4, /* aux=[g|u] (ld ldaux, width 2N): C[m,n]=d*u*silu'(g), C[m,N+n]=d*silu(g) */
-  SLX_EPI_DROPMASK = 5    /* C (+)= alpha*acc * keep(seed, m*ldmask+n)/(1-p)   (LoRA dropout bwd) */
+  SLX_EPI_DROPMASK = 5,   /* C (+)= alpha*acc * keep(seed, m*ldmask+n)/(1-p)   (LoRA dropout bwd) */
+  SLX_EPI_DROPMASK_SWIGLU = 6 /* d = resid + keep*alpha*acc; C[:, :N] = d*u*silu'(g), C[:, N:] = d*silu(g),
+                                 aux = [g | u] (Qwen2MLP down_proj LoRA dgrad fused into the SwiGLU backward) */
 };
 typedef struct slx_gemm_desc {
   int layout, epilogue, out_f32;

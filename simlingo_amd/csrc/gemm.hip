@@ -28,7 +28,8 @@ namespace slx {
 
 constexpr int BM = 128, BN = 128, BK = 64, NT = 256;
 
-enum { EPI_STORE = 0, EPI_GELU = 1, EPI_RESID_LS = 2, EPI_GELU_BWD = 3, EPI_SWIGLU_BWD = 4, EPI_DROPMASK = 5 };
+enum { EPI_STORE = 0, EPI_GELU = 1, EPI_RESID_LS = 2, EPI_GELU_BWD = 3, EPI_SWIGLU_BWD = 4, EPI_DROPMASK = 5,
+       EPI_DROPMASK_SWIGLU = 6 };
 
 struct GemmArgs {
   const bf16* A;
@@ -181,6 +182,13 @@ __device__ __forceinline__ void epilogue_elem(const GemmArgs& p, OutT* __restric
     v *= keep;
     if (p.accumulate) v += (float)C[ci];
     C[ci] = (OutT)v;
+  } else if constexpr (EPI == EPI_DROPMASK_SWIGLU) {
+    if (p.drop_p > 0.f) v *= uniform01(p.seed, (unsigned long long)m * p.ldmask + n) >= p.drop_p ? 1.0f / (1.0f - p.drop_p) : 0.0f;
+    const float d = v + p.resid[(long)m * p.ldr + n];
+    const long ai = (long)m * p.ldaux + n;
+    const float g = (float)p.aux[ai], u = (float)p.aux[ai + p.N];
+    C[ci] = (OutT)(d * u * silu_grad(g));
+    C[ci + p.N] = (OutT)(d * silu(g));
   }
 }
 
@@ -268,6 +276,24 @@ __device__ __forceinline__ void epilogue_vec8(const GemmArgs& p, OutT* __restric
 #pragma unroll
     for (int e = 0; e < 8; ++e) { o[e] = v[e] * u[e] * silu_grad(g[e]); u[e] = v[e] * silu(g[e]); }
     st8(C + ci, o);
+    st8(C + ci + p.N, u);
+  } else if constexpr (EPI == EPI_DROPMASK_SWIGLU) {
+    if (p.drop_p > 0.f) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        v[e] *= uniform01(p.seed, (unsigned long long)m * p.ldmask + n + e) >= p.drop_p ? 1.0f / (1.0f - p.drop_p) : 0.0f;
+    }
+    float r[8], g[8], u[8];
+    ld8(p.resid + (long)m * p.ldr + n, r);
+    ld8(p.aux + (long)m * p.ldaux + n, g);
+    ld8(p.aux + (long)m * p.ldaux + p.N + n, u);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float d = v[e] + r[e];
+      r[e] = d * u[e] * silu_grad(g[e]);
+      u[e] = d * silu(g[e]);
+    }
+    st8(C + ci, r);
     st8(C + ci + p.N, u);
   } else if constexpr (EPI == EPI_DROPMASK) {
 #pragma unroll
@@ -900,7 +926,7 @@ static double v_cost(const slx_gemm_desc* d, int v, int M, int batch) {
   double block_rate = v == 7 ? 1.35e15 / 256 : 1.1e15 / 512;
   if (v != 7 && blocks <= 256) block_rate *= 1.4;
   double t = rounds * block_flop / block_rate;
-  if (sp > 1) t += (double)sp * M * d->N * 4.0 / 2.0e12;
+  if (sp > 1) t += (double)sp * M * d->N * 4.0 / 1.3e12;  // f32 atomics: ~1.3 TB/s chip-wide
   if (v == 7 && blocks < 192) t *= 1.5;  // an under-filled 256x256 grid leaves whole CUs idle
   return t;
 }
@@ -926,7 +952,7 @@ static int gemm_launch(const slx_gemm_desc* d, int v, hipStream_t st) {
     if (d->aux) ok = ok && d->ldaux % 8 == 0 && ((uintptr_t)d->aux % 16) == 0;
     if (d->aux_out) ok = ok && d->ldaux_out % 8 == 0 && ((uintptr_t)d->aux_out % 16) == 0;
     if (d->resid) ok = ok && d->ldr % 8 == 0 && ((uintptr_t)d->resid % 16) == 0;
-    if (d->epilogue == SLX_EPI_SWIGLU_BWD) ok = ok && d->N % 8 == 0;
+    if (d->epilogue == SLX_EPI_SWIGLU_BWD || d->epilogue == SLX_EPI_DROPMASK_SWIGLU) ok = ok && d->N % 8 == 0;
     a.vec_ok = ok ? 1 : 0;
   }
   const int batch = d->batch < 1 ? 1 : d->batch;
@@ -967,6 +993,10 @@ static int gemm_launch(const slx_gemm_desc* d, int v, hipStream_t st) {
     case SLX_EPI_DROPMASK:
       SLX_CHECK_ARG(d->out_f32 && d->layout == SLX_GEMM_NN, "slx_gemm_bf16: DROPMASK needs NN, f32 out");
       return launch_any<true, false, EPI_DROPMASK, float>(a, batch, st, v);
+    case SLX_EPI_DROPMASK_SWIGLU:
+      SLX_CHECK_ARG(!d->out_f32 && d->layout == SLX_GEMM_NN && d->aux && d->resid,
+                    "slx_gemm_bf16: DROPMASK_SWIGLU needs NN, bf16 out, aux (gate|up), resid (f32 base grad)");
+      return launch_any<true, false, EPI_DROPMASK_SWIGLU, bf16>(a, batch, st, v);
   }
   set_error("slx_gemm_bf16: bad epilogue %d", d->epilogue);
   return -22;
@@ -997,7 +1027,8 @@ extern "C" int slx_gemm_bf16(const slx_gemm_desc* d, slx_stream_t stream) {
   const bool dma_ok = (!ak || d->K % BK == 0) && (!bk || d->K % BK == 0) && d->drop_operand == 0;
   int v = d->variant;
   const int rem = d->M % V3_BM;
-  const bool peel_ok = batch == 1 && d->epilogue != SLX_EPI_DROPMASK && d->M > V3_BM && rem > 0 && rem <= 64;
+  const bool peel_ok = batch == 1 && d->epilogue != SLX_EPI_DROPMASK && d->epilogue != SLX_EPI_DROPMASK_SWIGLU &&
+                       d->M > V3_BM && rem > 0 && rem <= 64;
   if (v == 0) {
     v = dma_ok ? 2 : 1;
     if (dma_ok) {

@@ -491,11 +491,13 @@ class VLAEngine:
             K.call("slx_cast_rows", K.P(dX), d, K.P(dxb), d, Ml, d, K.stream_ptr())
             dax = self._e(Ml, Fl + Pd, dtype=F32)
             K.mm(dxb, cat["down"] if lora else self.W[p + "down_w"], dax, tb=False)
-            if lora:
-                self._lora_bwd(i, ("down",), [dxb], ax[:, Fl:], ax[:, :Fl], dax[:, Fl:], dax[:, :Fl], sv)
             dgu = self._e(Ml, 2 * Fl)
-            K.call("slx_swiglu_bwd", K.P(dax), dax.stride(0), K.P(Ls["gu"]), 2 * Fl, K.P(dgu), 2 * Fl, Ml, Fl,
-                   K.stream_ptr())
+            if lora:  # the down-site dropout dgrad and the SwiGLU backward share one GEMM epilogue
+                self._lora_bwd(i, ("down",), [dxb], ax[:, Fl:], ax[:, :Fl], dax[:, Fl:], dax[:, :Fl], sv,
+                               swiglu=(Ls["gu"], dgu))
+            else:
+                K.call("slx_swiglu_bwd", K.P(dax), dax.stride(0), K.P(Ls["gu"]), 2 * Fl, K.P(dgu), 2 * Fl, Ml, Fl,
+                       K.stream_ptr())
             del dax
             dh2x = self._e(Ml, d + Pg, dtype=F32)
             K.mm(dgu, cat["gu"] if lora else self.W[p + "gate_up_w"], dh2x, tb=False)
@@ -612,12 +614,14 @@ class VLAEngine:
         self._group_done("vit_embed")
         self.saved = None
 
-    def _lora_bwd(self, i, sites, dys, tx, x, dtx, dx, sv):
+    def _lora_bwd(self, i, sites, dys, tx, x, dtx, dx, sv, swiglu=None):
         """LoRA sites of one group sharing the input x. dys[j] bf16 [M, out_j] (views of the output grad),
         tx bf16 [M, P] (forward down-projections t_j in columns 32j..), x bf16 [M, in] (undropped input),
         dtx f32 [M, P] (columns 32j.. hold dt_j = s dy_j B_j, produced by the fused dgrad GEMM; padding columns
         are exactly 0 because W_cat's are), dx f32 [M, in] accumulated:
-        dB_j = s dy_j^T t_j ; dA_j = dt_j^T drop_j(x) ; dx += drop_j'(dt_j A_j)."""
+        dB_j = s dy_j^T t_j ; dA_j = dt_j^T drop_j(x) ; dx += drop_j'(dt_j A_j).
+        swiglu=(gu, dgu) (down projection only): instead of accumulating into dx, run the SwiGLU backward in the
+        same GEMM's epilogue: dgu = swiglu'(gu) applied to dx + drop'(dt A)."""
         cfg = self.cfg
         s = cfg.lora_scale
         r = cfg.lora_r
@@ -635,6 +639,13 @@ class VLAEngine:
         for j, site in enumerate(sites):
             p = f"llm.{i}.lora.{site}."
             K.mm(dys[j], tx[:, r * j:r * (j + 1)], self.G[p + "b"], ta=True, tb=False, alpha=s, accumulate=True)
+            if swiglu is not None:
+                gu, dgu = swiglu
+                F = gu.shape[1] // 2
+                K.gemm(dT[:, r * j:r * j + 64], self.cat[i]["apad." + site], dgu, M, F, 64, K.GEMM_NN, dT.stride(0),
+                       kin, dgu.stride(0), epi=K.EPI_DROPMASK_SWIGLU, resid=dx, ldr=dx.stride(0), aux=gu,
+                       ldaux=gu.stride(0), seed=seeds[j], drop_p=drop, ldmask=kin)
+                continue
             K.mm(dT[:, r * j:r * j + 64], self.cat[i]["apad." + site], dx, tb=False,
                  epi=K.EPI_DROPMASK if drop > 0 else K.EPI_STORE, accumulate=True, seed=seeds[j], drop_p=drop,
                  ldmask=kin)

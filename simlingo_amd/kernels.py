@@ -20,7 +20,7 @@ c_int, c_i64, c_u64, c_float, c_vp = ctypes.c_int, ctypes.c_int64, ctypes.c_uint
 # ---- enums (mirror include/slx.h) --------------------------------------------------------------
 GEMM_NT, GEMM_NN, GEMM_TN, GEMM_TT = 0, 1, 2, 3
 GEMM_VARIANT = int(os.environ.get("SLX_GEMM_VARIANT", "0"))  # 0 = automatic (tuning hook)
-EPI_STORE, EPI_GELU, EPI_RESID_LS, EPI_GELU_BWD, EPI_SWIGLU_BWD, EPI_DROPMASK = 0, 1, 2, 3, 4, 5
+EPI_STORE, EPI_GELU, EPI_RESID_LS, EPI_GELU_BWD, EPI_SWIGLU_BWD, EPI_DROPMASK, EPI_DROPMASK_SWIGLU = 0, 1, 2, 3, 4, 5, 6
 
 
 class GemmDesc(ctypes.Structure):

@@ -183,3 +183,25 @@ def test_gemm_v3_m_tail_peel_epilogues(dev, variant):
     xx = x.float().requires_grad_()
     torch.nn.functional.gelu(xx).backward(dy.float() @ w.float())
     torch.testing.assert_close(dx.float(), xx.grad, atol=5e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_gemm_dropmask_swiglu_epilogue(dev, p):
+    """EPI_DROPMASK_SWIGLU: dgu = SwiGLU'(gu) applied to (resid + keep * dT.A): the Qwen2 down-projection LoRA
+    dropout dgrad fused into the SwiGLU backward (engine._lora_bwd, swiglu=...)."""
+    from simlingo_amd.dropmask import keep_scale
+    M, F, seed = 300, 256, 4242
+    g = torch.Generator(device=dev).manual_seed(3)
+    dT = torch.randn(M, 64, device=dev, generator=g).bfloat16()
+    A = (torch.randn(64, F, device=dev, generator=g) * 0.1).bfloat16()
+    base = torch.randn(M, F + 64, device=dev, generator=g)
+    gu = torch.randn(M, 2 * F, device=dev, generator=g).bfloat16()
+    dgu = torch.empty(M, 2 * F, device=dev, dtype=torch.bfloat16)
+    K.gemm(dT, A, dgu, M, F, 64, K.GEMM_NN, 64, F, 2 * F, epi=K.EPI_DROPMASK_SWIGLU, resid=base, ldr=F + 64, aux=gu,
+           ldaux=2 * F, seed=seed, drop_p=p, ldmask=F)
+    mask = torch.from_numpy(keep_scale(seed, M, F, F, p)).to(dev) if p > 0 else 1.0
+    d = base[:, :F] + mask * (dT.float() @ A.float())
+    gg, uu = gu.float()[:, :F].requires_grad_(), gu.float()[:, F:].requires_grad_()
+    (torch.nn.functional.silu(gg) * uu).backward(d)
+    torch.testing.assert_close(dgu[:, :F].float(), gg.grad, atol=3e-2, rtol=2e-2)
+    torch.testing.assert_close(dgu[:, F:].float(), uu.grad, atol=3e-2, rtol=2e-2)
