@@ -1,7 +1,7 @@
 // LayerNorm (InternViT blocks eps 1e-6, mlp1 eps 1e-5) and RMSNorm (Qwen2, eps 1e-6), fwd + bwd.
-// One workgroup per row in the forward (wave64 shuffle + LDS reduction); the backward walks a
-// strided set of rows per workgroup so the gamma/beta column partials stay in registers, then a
-// second pass reduces the partials. The mlp1 LayerNorm can gather its input through InternVL's
+// D <= 1024: one wave per row (shuffle reductions only). Wider rows (the mlp1 LayerNorm over 4096
+// channels): one workgroup per row. The backward walks a strided set of rows per wave/workgroup so the
+// gamma/beta column partials stay in registers and leave as one set of column atomics per workgroup. The mlp1 LayerNorm can gather its input through InternVL's
 // pixel_shuffle(0.5, ps_version v2) (remote `extract_feature`, called at
 // simlingo_training/models/encoder/internvl2_model.py:114), so the shuffled tensor never exists.
 #include "common.h"
@@ -86,6 +86,131 @@ __global__ __launch_bounds__(256) void norm_fwd_kernel(NormArgs a) {
       o[e] = (bf16)yv;
     }
     *reinterpret_cast<bf16x4*>(a.y + row * a.ldy + col) = o;
+  }
+}
+
+// Wave-per-row variants for D <= 1024 (InternViT 1024, Qwen2 896): one 64-lane wave owns a row, lane l
+// holds float4 chunks l, l+64, l+128, l+192; reductions are wave shuffles (no LDS, no barriers), so a
+// 4-wave block keeps four independent rows of loads in flight instead of serialising one row behind two
+// block-wide reductions.
+template <bool RMS>
+__global__ __launch_bounds__(256) void norm_fwd_wave_kernel(NormArgs a) {
+  const int lane = threadIdx.x & 63;
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= a.rows) return;
+  float v[16];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int col = (lane + 64 * i) * 4;
+    float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (col < a.D) {
+      const float* src = a.ps ? a.x + ps_src_row(row, col / a.C, a.G, a.tok_per_img) * a.ldx + (col % a.C)
+                              : a.x + row * a.ldx + col;
+      t = *reinterpret_cast<const float4*>(src);
+    }
+    v[4 * i] = t.x; v[4 * i + 1] = t.y; v[4 * i + 2] = t.z; v[4 * i + 3] = t.w;
+  }
+  float mu = 0.f;
+  if (!RMS) {
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) s += v[i];
+    mu = warp_sum(s) / a.D;
+  }
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const float d = ((lane + 64 * (i / 4)) * 4 < a.D) ? v[i] - mu : 0.f;
+    ss += d * d;
+  }
+  const float rs = rsqrtf(warp_sum(ss) / a.D + a.eps);
+  if (lane == 0) {
+    if (a.mean) a.mean[row] = mu;
+    a.rstd[row] = rs;
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int col = (lane + 64 * i) * 4;
+    if (col >= a.D) continue;
+    bf16x4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float xh = (v[4 * i + e] - mu) * rs;
+      o[e] = RMS ? (bf16)((float)(bf16)xh * a.gamma[col + e]) : (bf16)(xh * a.gamma[col + e] + a.beta[col + e]);
+    }
+    *reinterpret_cast<bf16x4*>(a.y + row * a.ldy + col) = o;
+  }
+}
+
+template <bool RMS>
+__global__ __launch_bounds__(256) void norm_bwd_wave_kernel(NormArgs a) {
+  __shared__ float cs[4][2][1024];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  float pg[16], pb[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) { pg[i] = 0.f; pb[i] = 0.f; }
+  for (long row = (long)blockIdx.x * 4 + w; row < a.rows; row += (long)gridDim.x * 4) {
+    const float mu = RMS ? 0.f : a.mean[row];
+    const float rs = a.rstd[row];
+    float xh[16], gd[16];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int col = (lane + 64 * i) * 4;
+      float4 t = make_float4(0.f, 0.f, 0.f, 0.f), d = make_float4(0.f, 0.f, 0.f, 0.f), g = t;
+      if (col < a.D) {
+        const float* src = a.ps ? a.x + ps_src_row(row, col / a.C, a.G, a.tok_per_img) * a.ldx + (col % a.C)
+                                : a.x + row * a.ldx + col;
+        t = *reinterpret_cast<const float4*>(src);
+        d = *reinterpret_cast<const float4*>(a.dy + row * a.lddy + col);
+        g = *reinterpret_cast<const float4*>(a.gamma + col);
+      }
+      const float tv[4] = {t.x, t.y, t.z, t.w}, dv[4] = {d.x, d.y, d.z, d.w}, gv[4] = {g.x, g.y, g.z, g.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int k = 4 * i + e;
+        xh[k] = col < a.D ? (tv[e] - mu) * rs : 0.f;
+        gd[k] = dv[e] * gv[e];
+        s1 += gd[k];
+        s2 += gd[k] * xh[k];
+        pg[k] += dv[e] * (RMS ? (float)(bf16)xh[k] : xh[k]);
+        pb[k] += dv[e];
+      }
+    }
+    const float m1 = RMS ? 0.f : warp_sum(s1) / a.D;
+    const float m2 = warp_sum(s2) / a.D;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int col = (lane + 64 * i) * 4;
+      if (col >= a.D) continue;
+      float* dst = a.ps ? a.dx + ps_src_row(row, col / a.C, a.G, a.tok_per_img) * a.lddx + (col % a.C)
+                        : a.dx + row * a.lddx + col;
+      float ov[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) ov[e] = rs * (gd[4 * i + e] - m1 - xh[4 * i + e] * m2);
+      if (a.dx_accumulate) {
+        const float4 q = *reinterpret_cast<const float4*>(dst);
+        ov[0] += q.x; ov[1] += q.y; ov[2] += q.z; ov[3] += q.w;
+      }
+      *reinterpret_cast<float4*>(dst) = make_float4(ov[0], ov[1], ov[2], ov[3]);
+    }
+  }
+  if (a.dgamma || a.dbeta) {  // 4 waves' column partials summed through LDS, then contiguous f32 atomics
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int col = (lane + 64 * i) * 4;
+      if (col >= a.D) continue;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        cs[w][0][col + e] = pg[4 * i + e];
+        cs[w][1][col + e] = pb[4 * i + e];
+      }
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < a.D; c += 256) {
+      if (a.dgamma) atomicAdd(a.dgamma + c, cs[0][0][c] + cs[1][0][c] + cs[2][0][c] + cs[3][0][c]);
+      if (a.dbeta) atomicAdd(a.dbeta + c, cs[0][1][c] + cs[1][1][c] + cs[2][1][c] + cs[3][1][c]);
+    }
   }
 }
 
@@ -185,7 +310,7 @@ static constexpr int kBwdBlocks = 512;
 template <bool RMS>
 static int norm_fwd(NormArgs& a, hipStream_t st) {
   SLX_CHECK_ARG(a.D % 4 == 0 && a.D <= 4096, "norm fwd: D=%d must be a multiple of 4 and <= 4096", a.D);
-  if (a.D <= 1024) hipLaunchKernelGGL((norm_fwd_kernel<4, RMS>), dim3(a.rows), dim3(256), 0, st, a);
+  if (a.D <= 1024) hipLaunchKernelGGL((norm_fwd_wave_kernel<RMS>), dim3((a.rows + 3) / 4), dim3(256), 0, st, a);
   else if (a.D <= 2048) hipLaunchKernelGGL((norm_fwd_kernel<8, RMS>), dim3(a.rows), dim3(256), 0, st, a);
   else hipLaunchKernelGGL((norm_fwd_kernel<16, RMS>), dim3(a.rows), dim3(256), 0, st, a);
   SLX_LAUNCH_CHECK("slx_norm_fwd");
@@ -202,7 +327,7 @@ static int norm_bwd(NormArgs& a, float* dgamma, float* dbeta, int accumulate, hi
     if (dgamma) hipMemsetAsync(dgamma, 0, a.D * sizeof(float), st);
     if (dbeta) hipMemsetAsync(dbeta, 0, a.D * sizeof(float), st);
   }
-  if (a.D <= 1024) hipLaunchKernelGGL((norm_bwd_kernel<4, RMS>), dim3(nblk), dim3(256), 0, st, a);
+  if (a.D <= 1024) hipLaunchKernelGGL((norm_bwd_wave_kernel<RMS>), dim3(nblk), dim3(256), 0, st, a);
   else if (a.D <= 2048) hipLaunchKernelGGL((norm_bwd_kernel<8, RMS>), dim3(nblk), dim3(256), 0, st, a);
   else hipLaunchKernelGGL((norm_bwd_kernel<16, RMS>), dim3(nblk), dim3(256), 0, st, a);
   SLX_LAUNCH_CHECK("slx_norm_bwd");
