@@ -110,8 +110,11 @@ def main():
         eng.adamw_step(lr, i + 1, betas=cfg.betas, eps=cfg.eps, weight_decay=cfg.weight_decay, max_norm=cfg.grad_clip)
         return out4
 
+    out4 = None
     for i in range(args.warmup):
         out4 = step(i)
+    if out4 is None:  # --warmup 0: the first timed step's loss is reported as loss_first
+        out4 = torch.full((4,), float("nan"), device=dev)
     torch.cuda.synchronize()
     loss0 = out4[0].item()
     if world > 1:
