@@ -211,6 +211,46 @@ int slx_cast_f32_bf16(const float* src, void* dst, int64_t n, slx_stream_t s);
  * dst = bf16(src * scale). Packs LoRA B (scaled by lora_alpha/r) into the fused [W | s*B] operands. */
 int slx_pack_scaled(const int64_t* table, int n, slx_stream_t s);
 
+/* ---- KV-cached greedy decode (agent call, BASELINE configs[4]) -------------------------------------
+ * Replaces the no-cache loop of LLM.greedy_sample (simlingo_training/models/language_model/llm.py:
+ * 178-250, called from DrivingModel.forward driving.py:131-176): the prefix runs once through the
+ * batched kernels above; every further token is slx_dec_begin + per layer {QKV GEMV (RMSNorm fused,
+ * row `pos` of the layer's q|k|v cache), slx_dec_attn (RoPE fused), O GEMV (+residual), gate/up GEMV
+ * (RMSNorm + SwiGLU fused), down GEMV (+residual)} + LM-head GEMV with the argmax folded in.
+ * Per-step scalars live in device memory (hipGraph-capturable); after EOS every kernel early-exits.*/
+typedef struct slx_dec_state {
+  int pos;      /* position of the token being processed (prefill leaves S0 - 1)               */
+  int n_gen;    /* tokens recorded so far                                                       */
+  int done;     /* 1 after EOS / max_new tokens were recorded                                   */
+  int max_new;  /* max_new_tokens (llm.py:181)                                                  */
+  int eos;      /* eos_token_id (driving.py:136-141)                                            */
+  int pad[3];
+} slx_dec_state;
+enum { SLX_DEC_STORE_ROW = 0, SLX_DEC_RESID = 1, SLX_DEC_SWIGLU = 2, SLX_DEC_ARGMAX = 3 };
+typedef struct slx_dec_gemv_desc {
+  int mode;
+  const void* W; int64_t ldw; int N; int K;   /* W bf16 [N][K] (SWIGLU: gate rows [0,N), up [N,2N)) */
+  const float* X; const float* gamma; float eps; /* input = RMSNorm(X f32 [K]) * gamma, or ...      */
+  const void* xb;                               /* ... a bf16 vector [K]                            */
+  const float* bias;
+  void* out; int64_t out_ld;                    /* STORE_ROW: bf16 row state->pos; SWIGLU: bf16 [N] */
+  float* resid;                                 /* RESID: resid[n] += y                            */
+  unsigned long long* keys;                     /* ARGMAX: slx_dec_key_shards() u64 keys (zeroed)  */
+  const slx_dec_state* state;                   /* NULL -> pos 0, never done                        */
+} slx_dec_gemv_desc;
+int slx_dec_key_shards(void);
+/* record the token of the previous step (argmax keys -> tokens[n_gen]), X = embed[token] f32     */
+int slx_dec_begin(slx_dec_state* st, unsigned long long* keys, const void* embed, int D, float* X, int* tokens,
+                  slx_stream_t s);
+int slx_dec_gemv(const slx_dec_gemv_desc* d, slx_stream_t s);
+/* one query row (cache row state->pos) over cache rows [0, pos]; q/k rotated with cos/sin row pos;
+ * split over keys (slx_dec_attn_nsplit(lmax) workgroups per kv head, partials in ws) + combine;
+ * out bf16 [Hq*64]; lmax = cache rows allocated (the split count is fixed by it: graph-safe)      */
+int slx_dec_attn_nsplit(int lmax);
+int slx_dec_attn_ws_floats(int Hq, int Hkv, int lmax);
+int slx_dec_attn(void* cache, int64_t ld, int Hq, int Hkv, const float* cos_tab, const float* sin_tab, int lmax,
+                 float* ws, void* out, const slx_dec_state* st, slx_stream_t s);
+
 #ifdef __cplusplus
 }
 #endif

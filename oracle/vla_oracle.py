@@ -225,6 +225,87 @@ def forward_loss(P, cfg, example):
             "inputs": inputs}
 
 
+# ---------------------------------------------------------------------------------------------
+# inference: DrivingModel.forward with predict_language=True (driving.py:104-187)
+
+
+def language_inputs(P, cfg, example, vit_embeds, inference=True):
+    """adaptor_dict['language_inputs'] / ['language_inputs_mask'] after replace_placeholder_tokens
+    (adaptors.py:256 embedding, internvl2_model.py:50-131 waypoint + image replacement) -> [B, L, d], [B, L]."""
+    di = example.driving_input
+    lab = di.prompt_inference if inference else di.prompt
+    ids = lab.phrase_ids.long()
+    valid = lab.phrase_valid.bool()
+    B, L = ids.shape
+    lang = P["llm.embed"][ids.clamp(min=0, max=cfg.vocab - 1)].clone()
+    special = sorted(set(ids[ids >= cfg.first_added_id].tolist()))
+    pv = lab.placeholder_values
+    if special and len(pv) > 0:
+        for b in range(B):
+            for key in special:
+                hit = (ids[b] == key).nonzero()
+                first = int(hit[0, 0]) if hit.numel() else 0
+                if first == 0:
+                    continue
+                coords = torch.as_tensor(pv[b][key], dtype=torch.float32).view(-1, 2)
+                lang[b, first:first + coords.shape[0]] = wp_encoder(P, coords)
+    flat = lang.reshape(B * L, -1)
+    sel = ids.reshape(-1) == cfg.img_context_id
+    flat[sel] = flat[sel] * 0.0 + vit_embeds.reshape(-1, flat.shape[-1])[: int(sel.sum())]
+    return flat.reshape(B, L, -1), valid
+
+
+def driving_heads(P, cfg, dfeat):
+    """DrivingAdaptor.get_predictions (adaptors.py:163-181): dfeat [B, 30, d] -> route [B,20,2], speed [B,10,2]."""
+    f_route, f_speed = dfeat[:, :cfg.n_route], dfeat[:, cfg.n_route:]
+    h = F.silu(f_route @ P["route.0.w"].t() + P["route.0.b"])
+    h = F.silu(h @ P["route.1.w"].t() + P["route.1.b"])
+    route = (h @ P["route.2.w"].t()).cumsum(1)
+    h = F.silu(f_speed @ P["speed.0.w"].t() + P["speed.0.b"])
+    return route, (h @ P["speed.1.w"].t()).cumsum(1)
+
+
+def greedy_sample(P, cfg, emb, max_new_tokens, eos):
+    """LLM.greedy_sample (llm.py:178-250) literally: the whole sequence is re-run for every token, argmax
+    of F.linear(features[:, -1], lm_head) (sample_categorical with temperature 0, llm.py:157-158), stop after
+    recording EOS. emb [S0, d] (one sample, valid rows) -> (tokens list, input_embeds [S0 + n, d])."""
+    x = emb[None]
+    toks = []
+    for _ in range(max_new_tokens):
+        feat, _ = llm_forward(P, cfg, x, torch.ones(1, x.shape[1], dtype=torch.bool))
+        tok = int((feat[0, -1] @ P["llm.lm_head"].t()).argmax())
+        toks.append(tok)
+        x = torch.cat([x, P["llm.embed"][tok][None, None]], 1)
+        if tok == eos:
+            break
+    return toks, x[0]
+
+
+def drive_after(P, cfg, input_embeds, queries):
+    """driving.py:156-165: forward(cat(input_embeds, driving inputs)) (no mask) -> heads on the last 30 rows."""
+    x = torch.cat([input_embeds, queries], 0)[None]
+    feat, _ = llm_forward(P, cfg, x, torch.ones(1, x.shape[1], dtype=torch.bool))
+    return driving_heads(P, cfg, feat[:, -queries.shape[0]:])
+
+
+def infer(P, cfg, example, max_new_tokens, eos):
+    """DrivingModel.forward (predict_language=True) per sample on its valid prompt rows
+    -> (speed [B,10,2], route [B,20,2], token lists)."""
+    pix = example.driving_input.camera_images
+    Bn, _, NP, C, H, W = pix.shape
+    vit = extract_feature(P, cfg, pix.reshape(Bn * NP, C, H, W))
+    lang, valid = language_inputs(P, cfg, example, vit, inference=True)
+    queries = torch.cat([P["drv.query_route"], P["drv.query_speed"]], 0)
+    speeds, routes, toks = [], [], []
+    for b in range(Bn):
+        t, xe = greedy_sample(P, cfg, lang[b][valid[b]], max_new_tokens, eos)
+        r, s = drive_after(P, cfg, xe, queries)
+        speeds.append(s[0])
+        routes.append(r[0])
+        toks.append(t)
+    return torch.stack(speeds), torch.stack(routes), toks
+
+
 def trainable_names(cfg, P):
     from simlingo_amd.params import param_specs
     return [s.name for s in param_specs(cfg) if s.trainable and s.name in P]

@@ -52,6 +52,7 @@ class VLAConfig:
     first_added_id: int = 151655        # '<WAYPOINTS>' = tokenizer.additional_special_tokens_ids[0]
     target_point_id: int = 151662       # '<TARGET_POINT>'
     pad_id: int = 151643                # <|endoftext|>
+    eos_id: int = 151645                # tokenizer.eos_token_id = <|im_end|> (driving.py:141) [third-party]
     # ---- optimisation (config.py:75-104, train.py:206) ----
     lr: float = 3e-5
     weight_decay: float = 0.1
@@ -107,6 +108,6 @@ def tiny_config(**kw) -> VLAConfig:
     base = dict(img_size=56, patch=14, vit_dim=128, vit_layers=2, vit_heads=2, vit_ffn=256,
                 llm_dim=128, llm_layers=2, llm_heads=2, llm_kv_heads=1, llm_ffn=256, vocab=256,
                 img_start_id=250, img_end_id=251, img_context_id=252, first_added_id=256,
-                target_point_id=263, pad_id=249, lora_dropout=0.0)
+                target_point_id=263, pad_id=249, eos_id=248, lora_dropout=0.0)
     base.update(kw)
     return VLAConfig(**base)

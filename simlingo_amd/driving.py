@@ -92,6 +92,10 @@ class DrivingModel(_Base):
         self.engine = None
         self.hidden_size = self.vla_cfg.llm_dim
         self._last_predictions = None
+        self.predict_language = bool(cfg.get("predict_language", True))   # driving.py:58
+        self.max_new_tokens = int(cfg.get("max_new_tokens", 100))   # driving.py:147
+        self._decoder = None
+        self.sampled_tokens = None
 
     # ---- device placement ----------------------------------------------------------------------
     def build_engine(self, device=None):
@@ -135,10 +139,32 @@ class DrivingModel(_Base):
             self.log("train/loss", output.loss.detach(), on_step=True, prog_bar=True, logger=True)
         return {"loss": output.loss, "outputs": output}
 
+    def decoder(self):
+        """The KV-cached greedy decoder (simlingo_amd.decode), built on first use."""
+        from .decode import GreedyDecoder
+        if self._decoder is None:
+            self._decoder = GreedyDecoder(self.build_engine(), max_new_tokens=self.max_new_tokens)
+        return self._decoder
+
     @torch.no_grad()
     def forward(self, example, return_language: Optional[bool] = None, prompt_ids=None):
-        """driving.py:104-187 with predict_language=False: one forward, driving predictions only.
-        Returns (speed_wps [B,10,2], route [B,20,2], language=[]). (Greedy text decode: next row.)"""
+        """driving.py:104-187 -> (speed_wps [B,10,2], route [B,20,2], language: List[str]).
+        predict_language=True (the reference's setting, :58): greedy decode of up to max_new_tokens tokens
+        per sample, then the driving forward over prompt + generated + queries (:131-176). The generated
+        ids are kept in self.sampled_tokens; language strings are decoded with the processor's tokenizer
+        when one was given (the InternVL2 tokenizer is not available offline), else the ids are joined.
+        predict_language=False: the single training-style forward (:177-185)."""
+        if self.predict_language:
+            from .decode import infer_example
+            eng = self.build_engine()
+            sp, rp, toks = infer_example(eng, self.decoder(), example)
+            self.sampled_tokens = toks
+            tok = getattr(self.processor, "tokenizer", self.processor)
+            if tok is not None and hasattr(tok, "batch_decode"):
+                language = [tok.batch_decode([t], skip_special_tokens=True)[0] for t in toks]
+            else:
+                language = [" ".join(str(t) for t in ts) for ts in toks]
+            return sp, rp, language
         eng = self.build_engine()
         plan = plan_from_example(self.vla_cfg, example, inference=True)
         dplan = plan.to_device(eng.device)

@@ -238,85 +238,12 @@ class VLAEngine:
         cfg = self.cfg
         sv = {}
         B = plan.B
-        pix = pix.reshape(-1, 3, cfg.img_size, cfg.img_size)
-        if pix.dtype != F32 or not pix.is_contiguous():
-            pix = pix.float().contiguous()
-        N = pix.shape[0]
         self.step_seed += 1
         sv["seed"] = self.step_seed * 1000003
         sv["drop"] = cfg.lora_dropout if (training and cfg.lora) else 0.0
-        sv["N"], sv["B"] = N, B
-        # ---------------- InternViT ----------------
-        D, T, F_, H = cfg.vit_dim, cfg.vit_tokens, cfg.vit_ffn, cfg.vit_heads
-        g = cfg.vit_grid
-        Mv = N * T
-        col = self._e(N * g * g, cfg.patch_kpad)
-        K.call("slx_im2col_patch", K.P(pix), N, cfg.img_size, cfg.img_size, cfg.patch, cfg.patch_kpad, K.P(col), K.stream_ptr())
-        pe = self._e(N * g * g, D, dtype=F32)
-        K.mm(col, self.wpatch, pe, bias=self.P["vit.patch.b"])
-        x = self._e(Mv, D, dtype=F32)
-        K.call("slx_vit_embed_fwd", K.P(pe), K.P(self.P["vit.cls"]), K.P(self.P["vit.pos"]), K.P(x), N, T, D, K.stream_ptr())
-        sv["col"] = col
-        vit_saved = []
-        for i in range(cfg.vit_layers):
-            p = f"vit.{i}."
-            h1, n1 = self._norm(x, self.P[p + "ln1.w"], self.P[p + "ln1.b"], Mv, D, cfg.vit_eps)
-            qkv = self._e(Mv, 3 * D)
-            K.mm(h1, self.W[p + "qkv.w"], qkv, bias=self.P[p + "qkv.b"])
-            o = self._e(Mv, D)
-            lse = self._e(N * H * T, dtype=F32)
-            with self._probe("vit.attn"):
-                K.attn_fwd(qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], o, lse, B=N, S=T, Hq=H, Hkv=H, causal=False)
-            xm = self._e(Mv, D, dtype=F32)
-            y1 = self._e(Mv, D)
-            K.mm(o, self.W[p + "proj.w"], xm, bias=self.P[p + "proj.b"], epi=K.EPI_RESID_LS, resid=x, ldr=D,
-                 ls=self.P[p + "ls1"], aux_out=y1, ldaux_out=D)
-            h2, n2 = self._norm(xm, self.P[p + "ln2.w"], self.P[p + "ln2.b"], Mv, D, cfg.vit_eps)
-            hpre = self._e(Mv, F_)
-            hact = self._e(Mv, F_)
-            with self._probe("vit.fc1"):
-                K.mm(h2, self.W[p + "fc1.w"], hact, bias=self.P[p + "fc1.b"], epi=K.EPI_GELU, aux_out=hpre, ldaux_out=F_)
-            xo = self._e(Mv, D, dtype=F32)
-            y2 = self._e(Mv, D)
-            K.mm(hact, self.W[p + "fc2.w"], xo, bias=self.P[p + "fc2.b"], epi=K.EPI_RESID_LS, resid=xm, ldr=D,
-                 ls=self.P[p + "ls2"], aux_out=y2, ldaux_out=D)
-            vit_saved.append(dict(x=x, h1=h1, n1=n1, qkv=qkv, o=o, lse=lse, y1=y1, xm=xm, h2=h2, n2=n2, hpre=hpre,
-                                  hact=hact, y2=y2))
-            x = xo
-        sv["vit"] = vit_saved
-        sv["vit_out"] = x
-        # ---------------- pixel_shuffle + mlp1 ----------------
-        d = cfg.llm_dim
-        Mi = N * cfg.img_tokens_per_tile
-        z, nz = self._norm(x, self.P["proj.ln.w"], self.P["proj.ln.b"], Mi, 4 * D, cfg.proj_eps, ps=g, tpi=T, ldx=D)
-        a1pre = self._e(Mi, d)
-        a1 = self._e(Mi, d)
-        K.mm(z, self.W["proj.fc1.w"], a1, bias=self.P["proj.fc1.b"], epi=K.EPI_GELU, aux_out=a1pre, ldaux_out=d)
-        img = self._e(Mi, d)
-        K.mm(a1, self.W["proj.fc2.w"], img, bias=self.P["proj.fc2.b"])
-        sv.update(z=z, nz=nz, a1pre=a1pre, a1=a1)
-        # ---------------- waypoint encoder (placeholder coords) ----------------
-        nwp = plan.wp_coords.shape[0]
-        wp_out = self._e(max(nwp, 1), d, dtype=F32)
-        if nwp:
-            c = dplan["wp_coords"]
-            w1pre = self._e(nwp, cfg.wp_hidden, dtype=F32)
-            w1 = self._e(nwp, cfg.wp_hidden, dtype=F32)
-            K.sgemm(c, 2, 1, self.P["wp.0.w"], 1, 2, w1, cfg.wp_hidden, 1, nwp, cfg.wp_hidden, 2, bias=self.P["wp.0.b"],
-                    act=K.ACT_RELU, pre=w1pre, ldpre=cfg.wp_hidden)
-            w2pre = self._e(nwp, cfg.wp_hidden2, dtype=F32)
-            w2 = self._e(nwp, cfg.wp_hidden2, dtype=F32)
-            K.sgemm(w1, cfg.wp_hidden, 1, self.P["wp.1.w"], 1, cfg.wp_hidden, w2, cfg.wp_hidden2, 1, nwp, cfg.wp_hidden2,
-                    cfg.wp_hidden, bias=self.P["wp.1.b"], act=K.ACT_RELU, pre=w2pre, ldpre=cfg.wp_hidden2)
-            K.sgemm(w2, cfg.wp_hidden2, 1, self.P["wp.2.w"], 1, cfg.wp_hidden2, wp_out, d, 1, nwp, d, cfg.wp_hidden2,
-                    bias=self.P["wp.2.b"])
-            sv.update(w1pre=w1pre, w1=w1, w2pre=w2pre, w2=w2)
-        # ---------------- token assembly ----------------
-        S = plan.S
+        X = self.encode_inputs(pix, plan, dplan, sv)
+        S, d = plan.S, cfg.llm_dim
         Ml = B * S
-        X = self._e(Ml, d, dtype=F32)
-        K.call("slx_assemble_tokens", K.P(dplan["code"]), Ml, d, K.P(self.W["llm.embed"]), cfg.vocab, K.P(img),
-               K.P(wp_out), K.P(self.P["drv.query_route"]), K.P(X), K.stream_ptr())
         # ---------------- Qwen2 + LoRA ----------------
         Hq, Hk, Fl = cfg.llm_heads, cfg.llm_kv_heads, cfg.llm_ffn
         qn, kn = Hq * 64, Hk * 64
@@ -404,10 +331,95 @@ class VLAEngine:
         K.call("slx_loss_finalize", K.P(ce_loss), R, K.P(route_loss), B * nr, K.P(speed_loss), B * ns, K.P(out4),
                K.stream_ptr())
         sv.update(plan=plan, dplan=dplan, rpos=rpos, spos=spos, fr=fr, fs=fs, hd=hd, sd=sd_, lab_r=lab_r, lab_s=lab_s,
-                  route_pred=route_pred, speed_pred=speed_pred, R=R, nwp=nwp, S=S, Ml=Ml, Mi=Mi, Mv=Mv,
+                  route_pred=route_pred, speed_pred=speed_pred, R=R, S=S, Ml=Ml,
                   ce_loss=ce_loss, route_loss=route_loss, speed_loss=speed_loss)
         self.saved = sv
         return out4, route_pred, speed_pred
+
+    def encode_inputs(self, pix: torch.Tensor, plan: Plan, dplan: dict, sv: dict) -> torch.Tensor:
+        """InternViT -> pixel_shuffle + mlp1 -> wp_encoder -> token assembly: the LLM input rows X [B*S, d] f32
+        (extract_feature internvl2_model.py:114, replace_placeholder_tokens :17-144, AdaptorList.forward
+        adaptors.py:301-331). Saves what the backward needs into `sv`."""
+        cfg = self.cfg
+        B = plan.B
+        pix = pix.reshape(-1, 3, cfg.img_size, cfg.img_size)
+        if pix.dtype != F32 or not pix.is_contiguous():
+            pix = pix.float().contiguous()
+        N = pix.shape[0]
+        sv["N"], sv["B"] = N, B
+        # ---------------- InternViT ----------------
+        D, T, F_, H = cfg.vit_dim, cfg.vit_tokens, cfg.vit_ffn, cfg.vit_heads
+        g = cfg.vit_grid
+        Mv = N * T
+        col = self._e(N * g * g, cfg.patch_kpad)
+        K.call("slx_im2col_patch", K.P(pix), N, cfg.img_size, cfg.img_size, cfg.patch, cfg.patch_kpad, K.P(col), K.stream_ptr())
+        pe = self._e(N * g * g, D, dtype=F32)
+        K.mm(col, self.wpatch, pe, bias=self.P["vit.patch.b"])
+        x = self._e(Mv, D, dtype=F32)
+        K.call("slx_vit_embed_fwd", K.P(pe), K.P(self.P["vit.cls"]), K.P(self.P["vit.pos"]), K.P(x), N, T, D, K.stream_ptr())
+        sv["col"] = col
+        vit_saved = []
+        for i in range(cfg.vit_layers):
+            p = f"vit.{i}."
+            h1, n1 = self._norm(x, self.P[p + "ln1.w"], self.P[p + "ln1.b"], Mv, D, cfg.vit_eps)
+            qkv = self._e(Mv, 3 * D)
+            K.mm(h1, self.W[p + "qkv.w"], qkv, bias=self.P[p + "qkv.b"])
+            o = self._e(Mv, D)
+            lse = self._e(N * H * T, dtype=F32)
+            with self._probe("vit.attn"):
+                K.attn_fwd(qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], o, lse, B=N, S=T, Hq=H, Hkv=H, causal=False)
+            xm = self._e(Mv, D, dtype=F32)
+            y1 = self._e(Mv, D)
+            K.mm(o, self.W[p + "proj.w"], xm, bias=self.P[p + "proj.b"], epi=K.EPI_RESID_LS, resid=x, ldr=D,
+                 ls=self.P[p + "ls1"], aux_out=y1, ldaux_out=D)
+            h2, n2 = self._norm(xm, self.P[p + "ln2.w"], self.P[p + "ln2.b"], Mv, D, cfg.vit_eps)
+            hpre = self._e(Mv, F_)
+            hact = self._e(Mv, F_)
+            with self._probe("vit.fc1"):
+                K.mm(h2, self.W[p + "fc1.w"], hact, bias=self.P[p + "fc1.b"], epi=K.EPI_GELU, aux_out=hpre, ldaux_out=F_)
+            xo = self._e(Mv, D, dtype=F32)
+            y2 = self._e(Mv, D)
+            K.mm(hact, self.W[p + "fc2.w"], xo, bias=self.P[p + "fc2.b"], epi=K.EPI_RESID_LS, resid=xm, ldr=D,
+                 ls=self.P[p + "ls2"], aux_out=y2, ldaux_out=D)
+            vit_saved.append(dict(x=x, h1=h1, n1=n1, qkv=qkv, o=o, lse=lse, y1=y1, xm=xm, h2=h2, n2=n2, hpre=hpre,
+                                  hact=hact, y2=y2))
+            x = xo
+        sv["vit"] = vit_saved
+        sv["vit_out"] = x
+        # ---------------- pixel_shuffle + mlp1 ----------------
+        d = cfg.llm_dim
+        Mi = N * cfg.img_tokens_per_tile
+        z, nz = self._norm(x, self.P["proj.ln.w"], self.P["proj.ln.b"], Mi, 4 * D, cfg.proj_eps, ps=g, tpi=T, ldx=D)
+        a1pre = self._e(Mi, d)
+        a1 = self._e(Mi, d)
+        K.mm(z, self.W["proj.fc1.w"], a1, bias=self.P["proj.fc1.b"], epi=K.EPI_GELU, aux_out=a1pre, ldaux_out=d)
+        img = self._e(Mi, d)
+        K.mm(a1, self.W["proj.fc2.w"], img, bias=self.P["proj.fc2.b"])
+        sv.update(z=z, nz=nz, a1pre=a1pre, a1=a1)
+        # ---------------- waypoint encoder (placeholder coords) ----------------
+        nwp = plan.wp_coords.shape[0]
+        wp_out = self._e(max(nwp, 1), d, dtype=F32)
+        if nwp:
+            c = dplan["wp_coords"]
+            w1pre = self._e(nwp, cfg.wp_hidden, dtype=F32)
+            w1 = self._e(nwp, cfg.wp_hidden, dtype=F32)
+            K.sgemm(c, 2, 1, self.P["wp.0.w"], 1, 2, w1, cfg.wp_hidden, 1, nwp, cfg.wp_hidden, 2, bias=self.P["wp.0.b"],
+                    act=K.ACT_RELU, pre=w1pre, ldpre=cfg.wp_hidden)
+            w2pre = self._e(nwp, cfg.wp_hidden2, dtype=F32)
+            w2 = self._e(nwp, cfg.wp_hidden2, dtype=F32)
+            K.sgemm(w1, cfg.wp_hidden, 1, self.P["wp.1.w"], 1, cfg.wp_hidden, w2, cfg.wp_hidden2, 1, nwp, cfg.wp_hidden2,
+                    cfg.wp_hidden, bias=self.P["wp.1.b"], act=K.ACT_RELU, pre=w2pre, ldpre=cfg.wp_hidden2)
+            K.sgemm(w2, cfg.wp_hidden2, 1, self.P["wp.2.w"], 1, cfg.wp_hidden2, wp_out, d, 1, nwp, d, cfg.wp_hidden2,
+                    bias=self.P["wp.2.b"])
+            sv.update(w1pre=w1pre, w1=w1, w2pre=w2pre, w2=w2)
+        # ---------------- token assembly ----------------
+        S = plan.S
+        Ml = B * S
+        X = self._e(Ml, d, dtype=F32)
+        K.call("slx_assemble_tokens", K.P(dplan["code"]), Ml, d, K.P(self.W["llm.embed"]), cfg.vocab, K.P(img),
+               K.P(wp_out), K.P(self.P["drv.query_route"]), K.P(X), K.stream_ptr())
+        sv.update(nwp=nwp, Mi=Mi, Mv=Mv)
+        return X
 
     def _lora_down(self, x, i, sites, t_out, sv):
         """t_out[:, 32j:32j+32] = drop_j(x) A_j^T for the sites sharing x (bf16, written into the extra columns of
