@@ -45,8 +45,10 @@ enum {
   SLX_EPI_GELU_BWD = 3,   /* C = alpha*acc * gelu_erf'(aux[m,n])                              */
   SLX_EPI_SWIGLU_BWD = 4, /* aux=[g|u] (ld ldaux, width 2N): C[m,n]=d*u*silu'(g), C[m,N+n]=d*silu(g) */
   SLX_EPI_DROPMASK = 5,   /* C (+)= alpha*acc * keep(seed, m*ldmask+n)/(1-p)   (LoRA dropout bwd) */
-  SLX_EPI_DROPMASK_SWIGLU = 6 /* d = resid + keep*alpha*acc; C[:, :N] = d*u*silu'(g), C[:, N:] = d*silu(g),
-                                 aux = [g | u] (Qwen2MLP down_proj LoRA dgrad fused into the SwiGLU backward) */
+  SLX_EPI_DROPMASK_SWIGLU = 6, /* d = resid + keep*alpha*acc; C[:, :N] = d*u*silu'(g), C[:, N:] = d*silu(g),
+                                  aux = [g | u] (Qwen2MLP down_proj LoRA dgrad fused into the SwiGLU backward) */
+  SLX_EPI_QGELU = 7,      /* aux_out = h = alpha*acc + bias; C = h*sigmoid(1.702h)  (CLIP quick_gelu, bf16) */
+  SLX_EPI_QGELU_BWD = 8   /* C = alpha*acc * quick_gelu'(aux[m,n])                                         */
 };
 typedef struct slx_gemm_desc {
   int layout, epilogue, out_f32;
@@ -113,6 +115,7 @@ typedef struct slx_norm_desc {
   float* mean; float* rstd;   /* [rows] saved statistics */
   int64_t rows; int D; float eps;
   int pixel_shuffle_grid; int tokens_per_image;
+  int y_f32;                  /* 1: y rows are f32 (ldy in floats) instead of bf16               */
 } slx_norm_desc;
 int slx_norm_fwd(const slx_norm_desc* d, slx_stream_t stream);
 int slx_norm_bwd(const slx_norm_desc* d, const float* dy, int64_t lddy, float* dx, int64_t lddx,
@@ -131,7 +134,8 @@ int slx_swiglu_fwd(const void* gu, int64_t ldgu, void* out, int64_t ldo, int64_t
 /* bias gradients: out[c] (+)= sum_r x[r,c]; mode 0 bf16 x, 1 f32 x                              */
 int slx_colsum(int mode, const void* x, int64_t ldx, int64_t M, int N, float* out, int accumulate, float* ws, slx_stream_t s);
 int slx_colsum_ws_floats(int N);
-/* InternViT layer-scale branch backward: g = dres*ls (bf16), dls = sum dres*y, dbias = sum g   */
+/* InternViT layer-scale branch backward: g = dres*ls (bf16), dls = sum dres*y, dbias = sum g.
+ * ls may be NULL (ls = 1: CLIP's plain residual), y and dls NULL together (no layer scale).     */
 int slx_ls_branch_bwd(const float* dres, int64_t ldr, const float* ls, const void* y, int64_t ldy, void* g, int64_t ldg,
                       int64_t M, int N, float* dls, float* dbias, int accumulate, float* ws, slx_stream_t s);
 /* LLM input assembly (AdaptorList.forward adaptors.py:301-331 + replace_placeholder_tokens
@@ -189,8 +193,12 @@ int slx_act_bwd(const float* dact, const float* pre, float* dpre, int64_t n, int
 int slx_ce_fwd(const float* logits, int64_t ld, const int* labels, int64_t R, int V, float* loss, float* lse, slx_stream_t s);
 int slx_ce_bwd(const float* logits, int64_t ld, const int* labels, const float* lse, int64_t R, int V, const float* gscale,
                void* dlogits, int64_t ldd, slx_stream_t s);
-int slx_wp_loss_fwd(const float* out, const float* label, int B, int n, int dims, float* pred, float* loss, slx_stream_t s);
-int slx_wp_loss_bwd(const float* pred, const float* label, int B, int n, int dims, const float* gscale, float* dout, slx_stream_t s);
+/* kind 0: smooth_l1(beta=1).sum(-1) per point (simlingo_training adaptors.py:205-213);
+ * kind 1: mse.sum(-1) per point (simlingo_base_training adaptors.py:226)                       */
+int slx_wp_loss_fwd(const float* out, const float* label, int B, int n, int dims, int kind, float* pred, float* loss,
+                    slx_stream_t s);
+int slx_wp_loss_bwd(const float* pred, const float* label, int B, int n, int dims, int kind, const float* gscale,
+                    float* dout, slx_stream_t s);
 int slx_loss_finalize(const float* lang, int nl, const float* route, int nr, const float* speed, int ns, float* out, slx_stream_t s);
 /* gs[0..2] = (dl[0] + dl[1+i]) / n_i : per-item gradient scales from the upstream grads of
  * [total, lang, route, speed] (dl may be NULL -> d total = 1).                                 */
@@ -207,6 +215,21 @@ int slx_sumsq(const float* g, int64_t n, float* out, int zero_first, slx_stream_
 int slx_adamw(float* p, const float* g, float* m, float* v, void* p_bf16, int64_t n, float lr, float beta1, float beta2,
               float eps, float weight_decay, int step, const float* sumsq, float max_norm, float grad_scale, slx_stream_t s);
 int slx_cast_f32_bf16(const float* src, void* dst, int64_t n, slx_stream_t s);
+
+/* ---- SimLingo-Base (LLaVA-NeXT CLIP encoder + tiny Llama, BASELINE configs[1]) ----------------- */
+/* NormZeroOne (simlingo_base_training/models/driving.py:89-103): out = x * scale + shift        */
+int slx_affine(const float* x, int64_t n, float scale, float shift, float* out, slx_stream_t s);
+/* out = a + b + c (projection bias + temporal_encoding + camera_encoding, llavanext.py:98-110)  */
+int slx_vec_sum3(const float* a, const float* b, const float* c, int64_t n, float* out, slx_stream_t s);
+/* LingoLlavaNextModel.forward_image spatial merge (llavanext_model.py:128-157): per image the
+ * npatch_h x npatch_w patches of g x g projector rows -> unpad_image rows [r0, r0+hu) x cols
+ * [c0, c0+wu) -> avg_pool2d(pool) -> + image_newline column: slx_llava_merge_tokens() rows of C.
+ * src/out bf16; bwd: dsrc (bf16, every source row; 0 where unpadded away) from dout (f32).      */
+int slx_llava_merge_tokens(int hu, int wu, int pool);
+int slx_llava_merge_fwd(const void* src, int C, int64_t n_img, int npatch_h, int npatch_w, int g, int r0, int hu, int c0,
+                        int wu, int pool, const float* newline, void* out, slx_stream_t s);
+int slx_llava_merge_bwd(const float* dout, int C, int64_t n_img, int npatch_h, int npatch_w, int g, int r0, int hu, int c0,
+                        int wu, int pool, void* dsrc, slx_stream_t s);
 /* table: n device-resident entries {src f32*, lds, dst bf16*, ldd, rows, cols, float-bits scale}:
  * dst = bf16(src * scale). Packs LoRA B (scaled by lora_alpha/r) into the fused [W | s*B] operands. */
 int slx_pack_scaled(const int64_t* table, int n, slx_stream_t s);

@@ -29,7 +29,14 @@ namespace slx {
 constexpr int BM = 128, BN = 128, BK = 64, NT = 256;
 
 enum { EPI_STORE = 0, EPI_GELU = 1, EPI_RESID_LS = 2, EPI_GELU_BWD = 3, EPI_SWIGLU_BWD = 4, EPI_DROPMASK = 5,
-       EPI_DROPMASK_SWIGLU = 6 };
+       EPI_DROPMASK_SWIGLU = 6, EPI_QGELU = 7, EPI_QGELU_BWD = 8 };
+
+// CLIP quick_gelu x*sigmoid(1.702x) (transformers ACT2FN["quick_gelu"], the LLaVA-NeXT vision tower)
+__device__ __forceinline__ float qgelu(float x) { return x / (1.0f + __expf(-1.702f * x)); }
+__device__ __forceinline__ float qgelu_grad(float x) {
+  const float s = 1.0f / (1.0f + __expf(-1.702f * x));
+  return s * (1.0f + 1.702f * x * (1.0f - s));
+}
 
 struct GemmArgs {
   const bf16* A;
@@ -169,6 +176,14 @@ __device__ __forceinline__ void epilogue_elem(const GemmArgs& p, OutT* __restric
     const bf16 yb = (bf16)v;
     if (p.aux_out) p.aux_out[(long)m * p.ldaux_out + n] = yb;
     C[ci] = (OutT)(p.resid[(long)m * p.ldr + n] + p.ls[n] * v);
+  } else if constexpr (EPI == EPI_QGELU) {
+    if (p.bias) v += p.bias[n];
+    const bf16 hb = (bf16)v;
+    p.aux_out[(long)m * p.ldaux_out + n] = hb;
+    C[ci] = (OutT)qgelu((float)hb);
+  } else if constexpr (EPI == EPI_QGELU_BWD) {
+    const float h = (float)p.aux[(long)m * p.ldaux + n];
+    C[ci] = (OutT)(v * qgelu_grad(h));
   } else if constexpr (EPI == EPI_GELU_BWD) {
     const float h = (float)p.aux[(long)m * p.ldaux + n];
     C[ci] = (OutT)(v * gelu_erf_grad(h));
@@ -263,6 +278,20 @@ __device__ __forceinline__ void epilogue_vec8(const GemmArgs& p, OutT* __restric
 #pragma unroll
     for (int e = 0; e < 8; ++e) r[e] += p.ls[n + e] * v[e];
     st8(C + ci, r);
+  } else if constexpr (EPI == EPI_QGELU) {
+    float h[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) h[e] = (float)(bf16)(v[e] + (p.bias ? p.bias[n + e] : 0.f));
+    st8(p.aux_out + (long)m * p.ldaux_out + n, h);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) h[e] = qgelu(h[e]);
+    st8(C + ci, h);
+  } else if constexpr (EPI == EPI_QGELU_BWD) {
+    float h[8];
+    ld8(p.aux + (long)m * p.ldaux + n, h);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] *= qgelu_grad(h[e]);
+    st8(C + ci, v);
   } else if constexpr (EPI == EPI_GELU_BWD) {
     float h[8];
     ld8(p.aux + (long)m * p.ldaux + n, h);
@@ -987,6 +1016,12 @@ static int gemm_launch(const slx_gemm_desc* d, int v, hipStream_t st) {
     case SLX_EPI_GELU_BWD:
       SLX_CHECK_ARG(!d->out_f32 && d->layout == SLX_GEMM_NN && d->aux, "slx_gemm_bf16: GELU_BWD needs NN, bf16 out, aux");
       return launch_any<true, false, EPI_GELU_BWD, bf16>(a, batch, st, v);
+    case SLX_EPI_QGELU:
+      SLX_CHECK_ARG(!d->out_f32 && d->layout == SLX_GEMM_NT && d->aux_out, "slx_gemm_bf16: QGELU needs NT, bf16 out, aux_out");
+      return launch_any<true, true, EPI_QGELU, bf16>(a, batch, st, v);
+    case SLX_EPI_QGELU_BWD:
+      SLX_CHECK_ARG(!d->out_f32 && d->layout == SLX_GEMM_NN && d->aux, "slx_gemm_bf16: QGELU_BWD needs NN, bf16 out, aux");
+      return launch_any<true, false, EPI_QGELU_BWD, bf16>(a, batch, st, v);
     case SLX_EPI_SWIGLU_BWD:
       SLX_CHECK_ARG(!d->out_f32 && d->layout == SLX_GEMM_NN && d->aux, "slx_gemm_bf16: SWIGLU_BWD needs NN, bf16 out, aux");
       return launch_any<true, false, EPI_SWIGLU_BWD, bf16>(a, batch, st, v);

@@ -90,7 +90,7 @@ __global__ __launch_bounds__(256) void colsum_kernel(const void* xv, long ldx, l
   const bool live = c0 < N;
   float s[4] = {0, 0, 0, 0}, s2[4] = {0, 0, 0, 0};
   float lsv[4] = {1, 1, 1, 1};
-  if (MODE == 2 && live) {
+  if (MODE == 2 && live && ls) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) lsv[e] = ls[c0 + e];
   }
@@ -105,11 +105,12 @@ __global__ __launch_bounds__(256) void colsum_kernel(const void* xv, long ldx, l
       v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
     }
     if (MODE == 2) {
-      const bf16x4 yy = *reinterpret_cast<const bf16x4*>(y + r * ldy + c0);
+      bf16x4 yy;
+      if (y) yy = *reinterpret_cast<const bf16x4*>(y + r * ldy + c0);
       bf16x4 go;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        s2[e] += v[e] * (float)yy[e];
+        if (y) s2[e] += v[e] * (float)yy[e];
         const float gv = v[e] * lsv[e];
         go[e] = (bf16)gv;
         s[e] += gv;
@@ -131,7 +132,7 @@ __global__ __launch_bounds__(256) void colsum_kernel(const void* xv, long ldx, l
   __syncthreads();
   const int cb = blockIdx.y * 1024;
   for (int c = threadIdx.x; c < 1024 && cb + c < N; c += 256) {
-    atomicAdd(out0 + cb + c, cs[0][c]);
+    if (out0) atomicAdd(out0 + cb + c, cs[0][c]);
     if (MODE == 2) atomicAdd(out1 + cb + c, cs[1][c]);
   }
 }
@@ -292,7 +293,10 @@ __global__ void ce_bwd_kernel(const float* logits, long ld, const int* labels, c
 // Driving heads (adaptors.py:183-221): pred[b, i] = sum_{j<=i} out[b, j]  (cumsum over points),
 // loss[b, i] = sum_xy smooth_l1(pred - label, beta=1). Backward: d_out = reverse-cumsum of
 // d_pred, d_pred = smooth_l1'(pred - label) * gscale.
-__global__ void wp_loss_fwd_kernel(const float* out, const float* label, int B, int n, int dims, float* pred, float* loss) {
+// kind 0: smooth_l1(beta 1).sum(-1) (simlingo_training adaptors.py:205-213);
+// kind 1: mse.sum(-1) (simlingo_base_training adaptors.py:226, .mean(-1) = the per-point average downstream)
+__global__ void wp_loss_fwd_kernel(const float* out, const float* label, int B, int n, int dims, int kind, float* pred,
+                                   float* loss) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
   float run[4] = {0, 0, 0, 0};
@@ -303,12 +307,13 @@ __global__ void wp_loss_fwd_kernel(const float* out, const float* label, int B, 
       pred[((long)b * n + i) * dims + c] = run[c];
       const float d = run[c] - label[((long)b * n + i) * dims + c];
       const float ad = fabsf(d);
-      l += ad < 1.f ? 0.5f * d * d : ad - 0.5f;
+      l += kind ? d * d : (ad < 1.f ? 0.5f * d * d : ad - 0.5f);
     }
     loss[(long)b * n + i] = l;
   }
 }
-__global__ void wp_loss_bwd_kernel(const float* pred, const float* label, int B, int n, int dims, const float* gscale, float* dout) {
+__global__ void wp_loss_bwd_kernel(const float* pred, const float* label, int B, int n, int dims, int kind,
+                                   const float* gscale, float* dout) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
   const float g = *gscale;
@@ -317,7 +322,7 @@ __global__ void wp_loss_bwd_kernel(const float* pred, const float* label, int B,
     for (int c = 0; c < dims; ++c) {
       const long k = ((long)b * n + i) * dims + c;
       const float d = pred[k] - label[k];
-      const float gd = (fabsf(d) < 1.f ? d : (d > 0.f ? 1.f : -1.f)) * g;
+      const float gd = (kind ? 2.f * d : (fabsf(d) < 1.f ? d : (d > 0.f ? 1.f : -1.f))) * g;
       run[c] += gd;
       dout[k] = run[c];
     }
@@ -467,6 +472,82 @@ __global__ void cast_kernel(const float* src, bf16* dst, long n) {
 
 using namespace slx;
 
+// out = a + b + c (the projection bias folded with temporal_encoding + camera_encoding, llavanext.py:98-110)
+__global__ void vec_sum3_kernel(const float* a, const float* b, const float* c, long n, float* out) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = a[i] + b[i] + c[i];
+}
+
+// out = x * scale + shift (NormZeroOne, simlingo_base_training/models/driving.py:89-103)
+__global__ void affine_kernel(const float* x, long n, float scale, float shift, float* out) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = x[i] * scale + shift;
+}
+
+// LLaVA-NeXT spatial merge (LingoLlavaNextModel.forward_image, llavanext_model.py:128-157, spatial_unpad):
+// per image the npatch_h x npatch_w patches of g x g features form an (npatch_h*g) x (npatch_w*g) grid;
+// unpad_image keeps rows [r0, r0+hu) and cols [c0, c0+wu); avg_pool2d(pool) (floor); then one
+// image_newline column -> tokens (i, j), j <= wo, row-major: T = ho * (wo + 1).
+struct MergeGeom { int npatch_h, npatch_w, g, r0, hu, c0, wu, pool; };
+__device__ __forceinline__ long merge_src_row(const MergeGeom& m, long img, int h, int w) {
+  const int ph = h / m.g, pw = w / m.g;
+  return (img * m.npatch_h * m.npatch_w + ph * m.npatch_w + pw) * (long)(m.g * m.g) + (h % m.g) * m.g + (w % m.g);
+}
+__global__ void llava_merge_fwd_kernel(const bf16* src, int C, MergeGeom m, long n_img, const float* newline, bf16* out) {
+  const int ho = m.hu / m.pool, wo = m.wu / m.pool, T = ho * (wo + 1);
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int c8 = C / 8;
+  if (idx >= n_img * T * c8) return;
+  const int c = (idx % c8) * 8;
+  const long tok = idx / c8;
+  const long img = tok / T;
+  const int t = tok % T, i = t / (wo + 1), j = t % (wo + 1);
+  bf16x8 o;
+  if (j == wo) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = (bf16)newline[c + e];
+  } else {
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int a = 0; a < m.pool; ++a)
+      for (int b = 0; b < m.pool; ++b) {
+        const long r = merge_src_row(m, img, m.r0 + i * m.pool + a, m.c0 + j * m.pool + b);
+        const bf16x8 v = *reinterpret_cast<const bf16x8*>(src + r * C + c);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] += (float)v[e];
+      }
+    const float inv = 1.0f / (m.pool * m.pool);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = (bf16)(acc[e] * inv);
+  }
+  *reinterpret_cast<bf16x8*>(out + tok * C + c) = o;
+}
+// backward: every source feature row gathers 1/pool^2 of its window's output gradient (0 outside)
+__global__ void llava_merge_bwd_kernel(const float* dout, int C, MergeGeom m, long n_img, bf16* dsrc) {
+  const int ho = m.hu / m.pool, wo = m.wu / m.pool, T = ho * (wo + 1);
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int c8 = C / 8;
+  const long rows_per_img = (long)m.npatch_h * m.npatch_w * m.g * m.g;
+  if (idx >= n_img * rows_per_img * c8) return;
+  const int c = (idx % c8) * 8;
+  const long r = idx / c8;
+  const long img = r / rows_per_img;
+  const int q = r % rows_per_img, p = q / (m.g * m.g), y = (q % (m.g * m.g)) / m.g, x = q % m.g;
+  const int h = (p / m.npatch_w) * m.g + y - m.r0, w = (p % m.npatch_w) * m.g + x - m.c0;
+  bf16x8 o;
+  if (h >= 0 && w >= 0 && h < ho * m.pool && w < wo * m.pool) {
+    const long tok = img * T + (h / m.pool) * (wo + 1) + w / m.pool;
+    const float inv = 1.0f / (m.pool * m.pool);
+    const float4 a = *reinterpret_cast<const float4*>(dout + tok * C + c);
+    const float4 b = *reinterpret_cast<const float4*>(dout + tok * C + c + 4);
+    o[0] = (bf16)(a.x * inv); o[1] = (bf16)(a.y * inv); o[2] = (bf16)(a.z * inv); o[3] = (bf16)(a.w * inv);
+    o[4] = (bf16)(b.x * inv); o[5] = (bf16)(b.y * inv); o[6] = (bf16)(b.z * inv); o[7] = (bf16)(b.w * inv);
+  } else {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = (bf16)0.f;
+  }
+  *reinterpret_cast<bf16x8*>(dsrc + r * C + c) = o;
+}
+
 static inline dim3 g1(long n, int bs = 256) { return dim3((unsigned)((n + bs - 1) / bs)); }
 
 extern "C" {
@@ -523,8 +604,9 @@ int slx_ls_branch_bwd(const float* dres, int64_t ldr, const float* ls, const voi
   SLX_CHECK_ARG(N % 4 == 0, "slx_ls_branch_bwd: N %% 4");
   (void)ws;
   hipStream_t st = (hipStream_t)s;
+  SLX_CHECK_ARG((dls == nullptr) == (y == nullptr) && dbias, "slx_ls_branch_bwd: dls iff y; dbias required");
   if (!accumulate) {
-    hipMemsetAsync(dls, 0, (size_t)N * sizeof(float), st);
+    if (dls) hipMemsetAsync(dls, 0, (size_t)N * sizeof(float), st);
     hipMemsetAsync(dbias, 0, (size_t)N * sizeof(float), st);
   }
   const int nblk = (int)(M < 512 ? (M > 0 ? M : 1) : 512);
@@ -603,15 +685,18 @@ int slx_ce_bwd(const float* logits, int64_t ld, const int* labels, const float* 
   return 0;
 }
 
-int slx_wp_loss_fwd(const float* out, const float* label, int B, int n, int dims, float* pred, float* loss, slx_stream_t s) {
-  SLX_CHECK_ARG(dims <= 4, "slx_wp_loss_fwd: dims <= 4");
-  hipLaunchKernelGGL(wp_loss_fwd_kernel, g1(B, 64), dim3(64), 0, (hipStream_t)s, out, label, B, n, dims, pred, loss);
+int slx_wp_loss_fwd(const float* out, const float* label, int B, int n, int dims, int kind, float* pred, float* loss,
+                    slx_stream_t s) {
+  SLX_CHECK_ARG(dims <= 4 && (kind == 0 || kind == 1), "slx_wp_loss_fwd: dims <= 4, kind 0/1");
+  hipLaunchKernelGGL(wp_loss_fwd_kernel, g1(B, 64), dim3(64), 0, (hipStream_t)s, out, label, B, n, dims, kind, pred, loss);
   SLX_LAUNCH_CHECK("slx_wp_loss_fwd");
   return 0;
 }
 
-int slx_wp_loss_bwd(const float* pred, const float* label, int B, int n, int dims, const float* gscale, float* dout, slx_stream_t s) {
-  hipLaunchKernelGGL(wp_loss_bwd_kernel, g1(B, 64), dim3(64), 0, (hipStream_t)s, pred, label, B, n, dims, gscale, dout);
+int slx_wp_loss_bwd(const float* pred, const float* label, int B, int n, int dims, int kind, const float* gscale,
+                    float* dout, slx_stream_t s) {
+  SLX_CHECK_ARG(dims <= 4 && (kind == 0 || kind == 1), "slx_wp_loss_bwd: dims <= 4, kind 0/1");
+  hipLaunchKernelGGL(wp_loss_bwd_kernel, g1(B, 64), dim3(64), 0, (hipStream_t)s, pred, label, B, n, dims, kind, gscale, dout);
   SLX_LAUNCH_CHECK("slx_wp_loss_bwd");
   return 0;
 }
@@ -689,6 +774,56 @@ int slx_pack_scaled(const int64_t* table, int n, slx_stream_t s) {
   if (n <= 0) return 0;
   hipLaunchKernelGGL(pack_scaled_kernel, dim3(n, 32), dim3(256), 0, (hipStream_t)s, (const long long*)table, n);
   SLX_LAUNCH_CHECK("slx_pack_scaled");
+  return 0;
+}
+
+int slx_affine(const float* x, int64_t n, float scale, float shift, float* out, slx_stream_t s) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(affine_kernel, g1(n), dim3(256), 0, (hipStream_t)s, x, n, scale, shift, out);
+  SLX_LAUNCH_CHECK("slx_affine");
+  return 0;
+}
+
+int slx_vec_sum3(const float* a, const float* b, const float* c, int64_t n, float* out, slx_stream_t s) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(vec_sum3_kernel, g1(n), dim3(256), 0, (hipStream_t)s, a, b, c, n, out);
+  SLX_LAUNCH_CHECK("slx_vec_sum3");
+  return 0;
+}
+
+static int merge_geom(MergeGeom& m, int npatch_h, int npatch_w, int g, int r0, int hu, int c0, int wu, int pool) {
+  m = MergeGeom{npatch_h, npatch_w, g, r0, hu, c0, wu, pool};
+  SLX_CHECK_ARG(pool >= 1 && r0 >= 0 && c0 >= 0 && hu >= pool && wu >= pool && r0 + hu <= npatch_h * g &&
+                c0 + wu <= npatch_w * g, "slx_llava_merge: bad geometry");
+  return 0;
+}
+
+int slx_llava_merge_tokens(int hu, int wu, int pool) { return (hu / pool) * (wu / pool + 1); }
+
+int slx_llava_merge_fwd(const void* src, int C, int64_t n_img, int npatch_h, int npatch_w, int g, int r0, int hu, int c0,
+                        int wu, int pool, const float* newline, void* out, slx_stream_t s) {
+  SLX_CHECK_ARG(C % 8 == 0, "slx_llava_merge_fwd: C %% 8");
+  MergeGeom m;
+  int rc = merge_geom(m, npatch_h, npatch_w, g, r0, hu, c0, wu, pool);
+  if (rc) return rc;
+  const long n = n_img * slx_llava_merge_tokens(hu, wu, pool) * (C / 8);
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(llava_merge_fwd_kernel, g1(n), dim3(256), 0, (hipStream_t)s, (const bf16*)src, C, m, (long)n_img,
+                     newline, (bf16*)out);
+  SLX_LAUNCH_CHECK("slx_llava_merge_fwd");
+  return 0;
+}
+
+int slx_llava_merge_bwd(const float* dout, int C, int64_t n_img, int npatch_h, int npatch_w, int g, int r0, int hu, int c0,
+                        int wu, int pool, void* dsrc, slx_stream_t s) {
+  SLX_CHECK_ARG(C % 8 == 0, "slx_llava_merge_bwd: C %% 8");
+  MergeGeom m;
+  int rc = merge_geom(m, npatch_h, npatch_w, g, r0, hu, c0, wu, pool);
+  if (rc) return rc;
+  const long n = n_img * (long)npatch_h * npatch_w * g * g * (C / 8);
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(llava_merge_bwd_kernel, g1(n), dim3(256), 0, (hipStream_t)s, dout, C, m, (long)n_img, (bf16*)dsrc);
+  SLX_LAUNCH_CHECK("slx_llava_merge_bwd");
   return 0;
 }
 

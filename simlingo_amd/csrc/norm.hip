@@ -26,6 +26,7 @@ struct NormArgs {
   float* mean; float* rstd;
   long rows; int D; float eps;
   int ps; int G; int C; int tok_per_img;  // pixel-shuffle gather
+  int y_f32;                              // y holds f32 rows (CLIP pre_layrnorm feeds the f32 residual)
   // bwd
   const float* dy; long lddy;
   float* dx; long lddx; int dx_accumulate;
@@ -76,16 +77,21 @@ __global__ __launch_bounds__(256) void norm_fwd_kernel(NormArgs a) {
   for (int i = 0; i < VPT / 4; ++i) {
     const int col = (tid + i * 256) * 4;
     if (col >= a.D) continue;
-    bf16x4 o;
+    float yv[4];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const float xh = (v[4 * i + e] - mu) * rs;
-      float yv;
-      if (RMS) yv = (float)(bf16)xh * a.gamma[col + e];  // Qwen2: weight * hs.to(input_dtype)
-      else yv = xh * a.gamma[col + e] + a.beta[col + e];
-      o[e] = (bf16)yv;
+      if (RMS) yv[e] = (float)(bf16)xh * a.gamma[col + e];  // Qwen2: weight * hs.to(input_dtype)
+      else yv[e] = xh * a.gamma[col + e] + a.beta[col + e];
     }
-    *reinterpret_cast<bf16x4*>(a.y + row * a.ldy + col) = o;
+    if (a.y_f32) {
+      *reinterpret_cast<float4*>(reinterpret_cast<float*>(a.y) + row * a.ldy + col) = make_float4(yv[0], yv[1], yv[2], yv[3]);
+    } else {
+      bf16x4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = (bf16)yv[e];
+      *reinterpret_cast<bf16x4*>(a.y + row * a.ldy + col) = o;
+    }
   }
 }
 
@@ -132,13 +138,20 @@ __global__ __launch_bounds__(256) void norm_fwd_wave_kernel(NormArgs a) {
   for (int i = 0; i < 4; ++i) {
     const int col = (lane + 64 * i) * 4;
     if (col >= a.D) continue;
-    bf16x4 o;
+    float yv[4];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const float xh = (v[4 * i + e] - mu) * rs;
-      o[e] = RMS ? (bf16)((float)(bf16)xh * a.gamma[col + e]) : (bf16)(xh * a.gamma[col + e] + a.beta[col + e]);
+      yv[e] = RMS ? (float)(bf16)xh * a.gamma[col + e] : xh * a.gamma[col + e] + a.beta[col + e];
     }
-    *reinterpret_cast<bf16x4*>(a.y + row * a.ldy + col) = o;
+    if (a.y_f32) {
+      *reinterpret_cast<float4*>(reinterpret_cast<float*>(a.y) + row * a.ldy + col) = make_float4(yv[0], yv[1], yv[2], yv[3]);
+    } else {
+      bf16x4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = (bf16)yv[e];
+      *reinterpret_cast<bf16x4*>(a.y + row * a.ldy + col) = o;
+    }
   }
 }
 
@@ -341,6 +354,7 @@ static void fill(NormArgs& a, const slx_norm_desc* d) {
   a.rows = d->rows; a.D = d->D; a.eps = d->eps;
   a.ps = d->pixel_shuffle_grid > 0; a.G = d->pixel_shuffle_grid; a.C = d->pixel_shuffle_grid > 0 ? d->D / 4 : d->D;
   a.tok_per_img = d->tokens_per_image;
+  a.y_f32 = d->y_f32;
 }
 
 extern "C" int slx_norm_fwd(const slx_norm_desc* d, slx_stream_t stream) {

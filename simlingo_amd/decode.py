@@ -276,8 +276,8 @@ class GreedyDecoder:
         route, speed = eng._e(1, nr, 2, dtype=F32), eng._e(1, ns, cfg.speed_dims, dtype=F32)
         dummy = eng._e(max(nr, ns), dtype=F32)
         lab_r, lab_s = torch.zeros(1, nr, 2, device=self.dev), torch.zeros(1, ns, cfg.speed_dims, device=self.dev)
-        K.call("slx_wp_loss_fwd", K.P(hd[0][0]), K.P(lab_r), 1, nr, 2, K.P(route), K.P(dummy), K.stream_ptr())
-        K.call("slx_wp_loss_fwd", K.P(sd_[0][0]), K.P(lab_s), 1, ns, cfg.speed_dims, K.P(speed), K.P(dummy),
+        K.call("slx_wp_loss_fwd", K.P(hd[0][0]), K.P(lab_r), 1, nr, 2, 0, K.P(route), K.P(dummy), K.stream_ptr())
+        K.call("slx_wp_loss_fwd", K.P(sd_[0][0]), K.P(lab_s), 1, ns, cfg.speed_dims, 0, K.P(speed), K.P(dummy),
                K.stream_ptr())
         return route[0], speed[0]
 

@@ -25,6 +25,7 @@ import torch
 from . import kernels as K
 from .config import VLAConfig
 from .ddp import GradBucketer
+from .engine_ops import EngineOps
 from .params import LORA_SITES, lora_io, param_specs
 from .plan import Plan
 
@@ -40,7 +41,7 @@ def _pad64(n):
     return (n + 63) // 64 * 64
 
 
-class VLAEngine:
+class VLAEngine(EngineOps):
     def __init__(self, cfg: VLAConfig, device, params: dict[str, torch.Tensor] | None = None, seed: int = 0,
                  bucket_bytes: int = 32 << 20):
         from .params import init_params
@@ -111,25 +112,6 @@ class VLAEngine:
         self.probe_site = None     # name of a call site to bracket with HIP events (bench roofline)
         self.probe_events = []
 
-    def _probe(self, site):
-        """Context manager: HIP events around one call site on the current stream (bench.py)."""
-        eng = self
-
-        class _P:
-            def __enter__(self):
-                if eng.probe_site == site:
-                    self.e0 = torch.cuda.Event(enable_timing=True)
-                    self.e0.record()
-                return self
-
-            def __exit__(self, *a):
-                if eng.probe_site == site:
-                    e1 = torch.cuda.Event(enable_timing=True)
-                    e1.record()
-                    eng.probe_events.append((self.e0, e1))
-                return False
-        return _P()
-
     # ------------------------------------------------------------------------------------------
     def _refresh_derived(self):
         """bf16 views that are not plain slices of the flat buffer (after every optimizer step)."""
@@ -190,16 +172,6 @@ class VLAEngine:
         self._pack_n = len(entries)
         K.call("slx_pack_scaled", K.P(self._pack_tab), self._pack_n, K.stream_ptr())
 
-    def set_distributed(self, pg=None, world: int = 1):
-        self.world = world
-        self.bucketer.set_distributed(pg, world)
-
-    def _group_done(self, g):
-        self.bucketer.group_done(g)
-
-    def wait_grads(self):
-        self.bucketer.wait()
-
     def rope_tables(self, S):
         if S not in self._cos_sin:
             self._cos_sin[S] = K.rope_tables(S, self.cfg.rope_theta, self.device)
@@ -207,29 +179,10 @@ class VLAEngine:
 
     # ------------------------------------------------------------------------------------------
     # helpers
-    def _e(self, *shape, dtype=BF16):
-        return torch.empty(*shape, dtype=dtype, device=self.device)
 
-    def _z(self, *shape, dtype=F32):
-        return torch.zeros(*shape, dtype=dtype, device=self.device)
 
-    def _norm(self, x, gamma, beta, rows, D, eps, rms=False, ps=0, tpi=0, ldx=None, out=None):
-        y = self._e(rows, D) if out is None else out
-        mean = None if rms else self._e(rows, dtype=F32)
-        rstd = self._e(rows, dtype=F32)
-        d = K.norm_desc(x, gamma, beta, y, mean, rstd, rows, D, eps, rms=rms, ps_grid=ps, tok_per_img=tpi, ldx=ldx)
-        K.norm_fwd(d)
-        return y, d
 
-    def _ws(self, nfloats):
-        if getattr(self, "_wsbuf", None) is None or self._wsbuf.numel() < nfloats:
-            self._wsbuf = self._e(max(nfloats, 1 << 20), dtype=F32)
-        return self._wsbuf
 
-    def _colsum(self, x, out, mode):
-        M, N = x.shape
-        ws = self._ws(K.lib().slx_colsum_ws_floats(N))
-        K.call("slx_colsum", mode, K.P(x), x.stride(0), M, N, K.P(out), 1, K.P(ws), K.stream_ptr())
 
     # ==========================================================================================
     # forward
@@ -322,10 +275,10 @@ class VLAEngine:
         route_loss = self._e(B * nr, dtype=F32)
         lab_r = path.float().contiguous()
         lab_s = waypoints[:, : nr + 1].float().contiguous()
-        K.call("slx_wp_loss_fwd", K.P(hd[0][0]), K.P(lab_r), B, nr, 2, K.P(route_pred), K.P(route_loss), K.stream_ptr())
+        K.call("slx_wp_loss_fwd", K.P(hd[0][0]), K.P(lab_r), B, nr, 2, 0, K.P(route_pred), K.P(route_loss), K.stream_ptr())
         speed_pred = self._e(B, ns, cfg.speed_dims, dtype=F32)
         speed_loss = self._e(B * ns, dtype=F32)
-        K.call("slx_wp_loss_fwd", K.P(sd_[0][0]), K.P(lab_s), B, ns, cfg.speed_dims, K.P(speed_pred), K.P(speed_loss),
+        K.call("slx_wp_loss_fwd", K.P(sd_[0][0]), K.P(lab_s), B, ns, cfg.speed_dims, 0, K.P(speed_pred), K.P(speed_loss),
                K.stream_ptr())
         out4 = self._e(4, dtype=F32)
         K.call("slx_loss_finalize", K.P(ce_loss), R, K.P(route_loss), B * nr, K.P(speed_loss), B * ns, K.P(out4),
@@ -430,22 +383,6 @@ class VLAEngine:
                     p=sv["drop"])
         return seeds
 
-    def _mlp_fwd(self, x, layers):
-        """driving head: list of (prefix, out_dim, act) -> saved [(out, pre, in)]"""
-        saved = []
-        h = x
-        M = x.shape[0]
-        for pre_name, n, act in layers:
-            kin = h.shape[1]
-            out = self._e(M, n, dtype=F32)
-            pre = self._e(M, n, dtype=F32) if act != K.ACT_NONE else None
-            bias = self.P.get(pre_name + ".b")
-            K.sgemm(h, kin, 1, self.P[pre_name + ".w"], 1, kin, out, n, 1, M, n, kin, bias=bias, act=act, pre=pre,
-                    ldpre=n)
-            saved.append((out, pre, h, pre_name, act))
-            h = out
-        saved.reverse()
-        return saved
 
     # ==========================================================================================
     # backward
@@ -468,7 +405,7 @@ class VLAEngine:
                                                  ("speed", ns, cfg.speed_dims, sv["sd"], sv["lab_s"], sv["spos"])):
             dout = self._e(B * npts, dims, dtype=F32)
             pred = sv["route_pred"] if tag == "route" else sv["speed_pred"]
-            K.call("slx_wp_loss_bwd", K.P(pred), K.P(lab), B, npts, dims, K.P(gs[1:2] if tag == "route" else gs[2:3]),
+            K.call("slx_wp_loss_bwd", K.P(pred), K.P(lab), B, npts, dims, 0, K.P(gs[1:2] if tag == "route" else gs[2:3]),
                    K.P(dout), K.stream_ptr())
             dx = self._mlp_bwd(dout, saved)
             K.call("slx_scatter_rows", K.P(dx), d, K.P(pos), B * npts, d, K.P(dfeat), d, 1, K.stream_ptr())
@@ -662,31 +599,7 @@ class VLAEngine:
                  epi=K.EPI_DROPMASK if drop > 0 else K.EPI_STORE, accumulate=True, seed=seeds[j], drop_p=drop,
                  ldmask=kin)
 
-    def _mlp_bwd(self, dout, saved, need_dx=True):
-        """saved: [(out, pre, in, prefix, act)] from last layer to first; dout: grad of the last output."""
-        g = dout
-        for (out, pre, inp, name, act) in saved:
-            M, n = g.shape
-            kin = inp.shape[1]
-            if act != K.ACT_NONE:
-                gp = self._e(M, n, dtype=F32)
-                K.call("slx_act_bwd", K.P(g), K.P(pre), K.P(gp), M * n, act, K.stream_ptr())
-                g = gp
-            # dW[n, kin] = g^T inp ; db = colsum(g) ; dinp = g W
-            K.sgemm(g, 1, n, inp, kin, 1, self.G[name + ".w"], kin, 1, n, kin, M)
-            if name + ".b" in self.G:
-                K.sgemm(g, 1, n, self.ones_col(M), 1, 1, self.G[name + ".b"], 1, 1, n, 1, M)
-            if inp is saved[-1][2] and not need_dx:
-                break
-            dinp = self._e(M, kin, dtype=F32)
-            K.sgemm(g, n, 1, self.P[name + ".w"], kin, 1, dinp, kin, 1, M, kin, n)
-            g = dinp
-        return g
 
-    def ones_col(self, M):
-        if getattr(self, "_ones", None) is None or self._ones.numel() < M:
-            self._ones = torch.ones(max(M, 1024), dtype=F32, device=self.device)
-        return self._ones
 
     # ==========================================================================================
     # optimizer
@@ -702,6 +615,3 @@ class VLAEngine:
                K.P(self.sumsq), float(max_norm if max_norm else 0.0), 1.0 / self.world, K.stream_ptr())
         self._refresh_derived()
 
-    def grad_norm(self):
-        """L2 norm of the (averaged) gradient — diagnostic (syncs)."""
-        return float(torch.linalg.vector_norm(self.grad).item()) / self.world

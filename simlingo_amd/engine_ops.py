@@ -1,0 +1,114 @@
+"""Shared host-side plumbing of the HIP engines (VLAEngine, BaseEngine): device allocation helpers, the
+norm / column-sum / small-MLP call patterns, gradient-bucket hooks and HIP-event probes. Every
+computation is a libslx_hip.so call; torch only allocates and supplies the stream."""
+from __future__ import annotations
+
+import torch
+
+from . import kernels as K
+
+BF16, F32 = torch.bfloat16, torch.float32
+
+
+class EngineOps:
+    """Mixin: expects self.device, self.bucketer (GradBucketer), self.world, self.P / self.G dicts."""
+
+    def _probe(self, site):
+        """Context manager: HIP events around one call site on the current stream (bench.py)."""
+        eng = self
+
+        class _P:
+            def __enter__(self):
+                if eng.probe_site == site:
+                    self.e0 = torch.cuda.Event(enable_timing=True)
+                    self.e0.record()
+                return self
+
+            def __exit__(self, *a):
+                if eng.probe_site == site:
+                    e1 = torch.cuda.Event(enable_timing=True)
+                    e1.record()
+                    eng.probe_events.append((self.e0, e1))
+                return False
+        return _P()
+
+    def set_distributed(self, pg=None, world: int = 1):
+        self.world = world
+        self.bucketer.set_distributed(pg, world)
+
+    def _group_done(self, g):
+        self.bucketer.group_done(g)
+
+    def wait_grads(self):
+        self.bucketer.wait()
+
+    def _e(self, *shape, dtype=BF16):
+        return torch.empty(*shape, dtype=dtype, device=self.device)
+
+    def _z(self, *shape, dtype=F32):
+        return torch.zeros(*shape, dtype=dtype, device=self.device)
+
+    def _norm(self, x, gamma, beta, rows, D, eps, rms=False, ps=0, tpi=0, ldx=None, out=None):
+        y = self._e(rows, D) if out is None else out
+        mean = None if rms else self._e(rows, dtype=F32)
+        rstd = self._e(rows, dtype=F32)
+        d = K.norm_desc(x, gamma, beta, y, mean, rstd, rows, D, eps, rms=rms, ps_grid=ps, tok_per_img=tpi, ldx=ldx)
+        K.norm_fwd(d)
+        return y, d
+
+    def _ws(self, nfloats):
+        if getattr(self, "_wsbuf", None) is None or self._wsbuf.numel() < nfloats:
+            self._wsbuf = self._e(max(nfloats, 1 << 20), dtype=F32)
+        return self._wsbuf
+
+    def _colsum(self, x, out, mode):
+        M, N = x.shape
+        ws = self._ws(K.lib().slx_colsum_ws_floats(N))
+        K.call("slx_colsum", mode, K.P(x), x.stride(0), M, N, K.P(out), 1, K.P(ws), K.stream_ptr())
+
+    def _mlp_fwd(self, x, layers):
+        """driving head: list of (prefix, out_dim, act) -> saved [(out, pre, in)]"""
+        saved = []
+        h = x
+        M = x.shape[0]
+        for pre_name, n, act in layers:
+            kin = h.shape[1]
+            out = self._e(M, n, dtype=F32)
+            pre = self._e(M, n, dtype=F32) if act != K.ACT_NONE else None
+            bias = self.P.get(pre_name + ".b")
+            K.sgemm(h, kin, 1, self.P[pre_name + ".w"], 1, kin, out, n, 1, M, n, kin, bias=bias, act=act, pre=pre,
+                    ldpre=n)
+            saved.append((out, pre, h, pre_name, act))
+            h = out
+        saved.reverse()
+        return saved
+
+    def _mlp_bwd(self, dout, saved, need_dx=True):
+        """saved: [(out, pre, in, prefix, act)] from last layer to first; dout: grad of the last output."""
+        g = dout
+        for (out, pre, inp, name, act) in saved:
+            M, n = g.shape
+            kin = inp.shape[1]
+            if act != K.ACT_NONE:
+                gp = self._e(M, n, dtype=F32)
+                K.call("slx_act_bwd", K.P(g), K.P(pre), K.P(gp), M * n, act, K.stream_ptr())
+                g = gp
+            # dW[n, kin] = g^T inp ; db = colsum(g) ; dinp = g W
+            K.sgemm(g, 1, n, inp, kin, 1, self.G[name + ".w"], kin, 1, n, kin, M)
+            if name + ".b" in self.G:
+                K.sgemm(g, 1, n, self.ones_col(M), 1, 1, self.G[name + ".b"], 1, 1, n, 1, M)
+            if inp is saved[-1][2] and not need_dx:
+                break
+            dinp = self._e(M, kin, dtype=F32)
+            K.sgemm(g, n, 1, self.P[name + ".w"], kin, 1, dinp, kin, 1, M, kin, n)
+            g = dinp
+        return g
+
+    def ones_col(self, M):
+        if getattr(self, "_ones", None) is None or self._ones.numel() < M:
+            self._ones = torch.ones(max(M, 1024), dtype=F32, device=self.device)
+        return self._ones
+
+    def grad_norm(self):
+        """L2 norm of the (averaged) gradient — diagnostic (syncs)."""
+        return float(torch.linalg.vector_norm(self.grad).item()) / self.world

@@ -21,6 +21,7 @@ c_int, c_i64, c_u64, c_float, c_vp = ctypes.c_int, ctypes.c_int64, ctypes.c_uint
 GEMM_NT, GEMM_NN, GEMM_TN, GEMM_TT = 0, 1, 2, 3
 GEMM_VARIANT = int(os.environ.get("SLX_GEMM_VARIANT", "0"))  # 0 = automatic (tuning hook)
 EPI_STORE, EPI_GELU, EPI_RESID_LS, EPI_GELU_BWD, EPI_SWIGLU_BWD, EPI_DROPMASK, EPI_DROPMASK_SWIGLU = 0, 1, 2, 3, 4, 5, 6
+EPI_QGELU, EPI_QGELU_BWD = 7, 8
 
 
 class GemmDesc(ctypes.Structure):
@@ -185,7 +186,7 @@ class NormDesc(ctypes.Structure):
     _fields_ = [
         ("rms", c_int), ("x", c_vp), ("ldx", c_i64), ("gamma", c_vp), ("beta", c_vp), ("y", c_vp), ("ldy", c_i64),
         ("mean", c_vp), ("rstd", c_vp), ("rows", c_i64), ("D", c_int), ("eps", c_float),
-        ("pixel_shuffle_grid", c_int), ("tokens_per_image", c_int),
+        ("pixel_shuffle_grid", c_int), ("tokens_per_image", c_int), ("y_f32", c_int),
     ]
 
 
@@ -242,8 +243,13 @@ for _n, _a in {
     "slx_act_bwd": [_vp, _vp, _vp, _I, _i, _vp],
     "slx_ce_fwd": [_vp, _I, _vp, _I, _i, _vp, _vp, _vp],
     "slx_ce_bwd": [_vp, _I, _vp, _vp, _I, _i, _vp, _vp, _I, _vp],
-    "slx_wp_loss_fwd": [_vp, _vp, _i, _i, _i, _vp, _vp, _vp],
-    "slx_wp_loss_bwd": [_vp, _vp, _i, _i, _i, _vp, _vp, _vp],
+    "slx_wp_loss_fwd": [_vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp],
+    "slx_wp_loss_bwd": [_vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp],
+    "slx_affine": [_vp, _I, _f, _f, _vp, _vp],
+    "slx_vec_sum3": [_vp, _vp, _vp, _I, _vp, _vp],
+    "slx_llava_merge_tokens": [_i, _i, _i],
+    "slx_llava_merge_fwd": [_vp, _i, _I, _i, _i, _i, _i, _i, _i, _i, _i, _vp, _vp, _vp],
+    "slx_llava_merge_bwd": [_vp, _i, _I, _i, _i, _i, _i, _i, _i, _i, _i, _vp, _vp],
     "slx_loss_finalize": [_vp, _i, _vp, _i, _vp, _i, _vp, _vp],
     "slx_loss_gscale": [_vp, _i, _i, _i, _vp, _vp],
     "slx_sumsq": [_vp, _I, _vp, _i, _vp],
@@ -322,6 +328,7 @@ def rope_tables(S, theta, device, head_dim=64):
 # Norms
 # ------------------------------------------------------------------------------------------------
 def norm_desc(x, gamma, beta, y, mean, rstd, rows, D, eps, rms=False, ps_grid=0, tok_per_img=0, ldx=None):
+    """y may be bf16 (GEMM operand) or f32 (a residual stream, e.g. CLIP's pre_layrnorm)."""
     """The descriptor keeps references to every tensor it points to (ctypes holds raw pointers only;
     without this the caching allocator could recycle the saved statistics before the backward)."""
     d = NormDesc()
@@ -335,6 +342,7 @@ def norm_desc(x, gamma, beta, y, mean, rstd, rows, D, eps, rms=False, ps_grid=0,
     d.rstd = rstd.data_ptr()
     d.rows, d.D, d.eps = int(rows), int(D), float(eps)
     d.pixel_shuffle_grid, d.tokens_per_image = int(ps_grid), int(tok_per_img)
+    d.y_f32 = int(y is not None and y.dtype == torch.float32)
     return d
 
 

@@ -1,0 +1,71 @@
+"""SimLingo-Base training step on the MI355X (BaseEngine, bf16 MFMA / f32 accumulation) vs the CPU fp32
+oracle (oracle/base_oracle.py, itself pinned to the reference fixture tests/golden/base_tiny.npz).
+
+Tolerances (bf16 operands, 2 CLIP + 2 Llama tiny layers): losses rel 3e-2; predictions: every per-point head
+output (the cumsum increment) within 0.02 m and the cumulated waypoints within 0.1 m; every trainable
+gradient cosine >= 0.98 and relative L2 error <= 0.2. Plus one optimizer step against torch.optim.AdamW with
+the reference's param groups (decay only on Linear/Conv weights, no decay on route_head) and clip 1.0."""
+import pytest
+import torch
+
+from base_golden_util import load_base_case
+from oracle import base_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def run(cfg, P, ex, dev):
+    from simlingo_amd.base_engine import BaseEngine
+    eng = BaseEngine(cfg, dev, P)
+    di, dl = ex.driving_input, ex.driving_label
+    out4, rp, sp = eng.forward(di.camera_images.to(dev), di.vehicle_speed.to(dev), di.map_route.to(dev),
+                               dl.route_adjusted.to(dev), dl.waypoints.to(dev), image_size=tuple(di.image_sizes[0].tolist()))
+    eng.backward(None)
+    torch.cuda.synchronize()
+    return eng, out4.cpu(), rp.cpu(), sp.cpu()
+
+
+def test_base_engine_vs_oracle(dev):
+    cfg, P, ex, _ = load_base_case()
+    ref, grads = O.loss_and_grads(P, cfg, ex)
+    eng, out4, rp, sp = run(cfg, P, ex, dev)
+    for got, k in ((out4[0], "loss"), (out4[2], "route_loss"), (out4[3], "speed_wps_loss")):
+        assert abs(got.item() - ref[k].item()) <= 3e-2 * abs(ref[k].item()) + 1e-3, (k, got.item(), ref[k].item())
+    for got, want in ((rp, ref["route_pred"]), (sp, ref["speed_pred"])):
+        inc = (torch.diff(got, dim=1, prepend=torch.zeros_like(got[:, :1]))
+               - torch.diff(want, dim=1, prepend=torch.zeros_like(want[:, :1]))).abs()
+        assert (got - want).abs().max().item() <= 0.1 and inc.max().item() <= 0.02, inc.max().item()
+    bad = []
+    for name, r in grads.items():
+        e = eng.G[name].detach().float().cpu().reshape(-1)
+        r = r.reshape(-1)
+        if r.norm() < 1e-12:
+            continue
+        cos = torch.nn.functional.cosine_similarity(e, r, dim=0).item()
+        rel = ((e - r).norm() / r.norm()).item()
+        if cos < 0.98 or rel > 0.2:
+            bad.append((name, round(cos, 4), round(rel, 4)))
+    assert not bad, bad
+
+
+def test_base_adamw_groups_match_torch(dev):
+    """One step of the 4-segment fused AdamW == torch.optim.AdamW over the same gradients and groups."""
+    from simlingo_amd.base_params import base_specs
+    cfg, P, ex, _ = load_base_case()
+    eng, _, _, _ = run(cfg, P, ex, dev)
+    lr, vlr, wd = 1e-3, 2e-3, 0.1
+    params = {s.name: eng.P[s.name].detach().clone().requires_grad_(True) for s in base_specs(cfg)}
+    for s in base_specs(cfg):
+        params[s.name].grad = eng.G[s.name].detach().clone()
+    groups = []
+    for vis in (False, True):
+        for dec in (True, False):
+            ps = [params[s.name] for s in base_specs(cfg) if s.vision == vis and s.decay == dec]
+            groups.append({"params": ps, "lr": vlr if vis else lr, "weight_decay": wd if dec else 0.0})
+    torch.nn.utils.clip_grad_norm_(list(params.values()), 1.0)
+    opt = torch.optim.AdamW(groups, betas=(0.9, 0.999), eps=1e-8)
+    opt.step()
+    eng.adamw_step(lr, vlr, 1, weight_decay=wd, max_norm=1.0)
+    torch.cuda.synchronize()
+    for n, p in params.items():
+        torch.testing.assert_close(eng.P[n], p.detach(), rtol=1e-5, atol=1e-6, msg=n)
