@@ -32,8 +32,8 @@ class BaseConfig:
     # ---- projector + spatial merge ----
     proj_dim: int = 4096            # text hidden size of the LLaVA-NeXT checkpoint (linear_1 / linear_2)
     pool: int = 2                   # downsample_feature_grid_factor (simlingo_base_1.yaml:27)
-    frame_h: int = 512              # original frame (image_sizes): 1024 x 512, cut_bottom_quarter False
-    frame_w: int = 1024
+    frame_h: int = 359              # image_sizes of the frame the processor sees: 1024 x 512 cropped to 359 rows
+    frame_w: int = 1024             # (dataset_base.py:464-467, img_shift_augmentation True) -> 200 image tokens
     embed_dim: int = 512            # LLaVAnextEncoderConfig.embed_dim (config.py)
     # ---- Llama 'tiny' (llama.py:46) ----
     llm_dim: int = 512
