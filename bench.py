@@ -1,27 +1,35 @@
-"""SimLingo VLA training throughput on MI355X (BASELINE.json metric).
+"""SimLingo training throughput on MI355X (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config vla|tiny] [--no-cpu-baseline]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config vla|base|tiny|base_tiny] [--no-cpu-baseline]
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
-Workload (BASELINE.json configs[2], the config the metric is quoted on at 1/2/4/8 GPUs): SimLingo full
-VLA = InternViT-300M (2 tiles of 448^2 per frame) + mlp1 + Qwen2-0.5B with LoRA r32 (dropout 0.1)
+Default workload `vla` (BASELINE.json configs[2], the config the metric is quoted on at 1/2/4/8 GPUs): SimLingo
+full VLA = InternViT-300M (2 tiles of 448^2 per frame) + mlp1 + Qwen2-0.5B with LoRA r32 (dropout 0.1)
 + driving heads, bf16 MFMA / f32 accumulation, B = 8 samples per GPU, 256 text tokens per prompt
 (S_llm = 798), 16 LM-loss tokens per sample. One step = forward + backward + bucketed RCCL
 gradient all-reduce + clip + AdamW on 327.5 M trainable parameters, synthetic seeded data of the
 reference's shape (no dataset / checkpoint offline), random-init weights of that architecture.
 Data parallel, one process per GPU, per-GPU batch fixed -> weak scaling.
 
-Roofline: the dominant kernel is the bf16 MFMA GEMM; `roofline` reports the InternViT FC1 GEMM
-(M = 16*1025 tokens, N = 4096, K = 1024, gelu epilogue, 24 launches per step) timed with HIP events
-on its launch stream during the timed steps, against the 2.5 PFLOP/s dense bf16 peak.
-`step_mfma_frac` = samples/s x 5670.1 GFLOP/sample (required FLOPs) / (n_gpu x peak).
-cpu_baseline: the oracle (CPU fp32 PyTorch restatement, oracle/vla_oracle.py) forward+backward of
-one full-size sample on the host cores, rank 0, N = 1 only.
+`base` (BASELINE.json configs[1]): SimLingo-Base = CLIP ViT-L/14-336 (2 tiles of 336^2, first 23 layers) +
+LLaVA-NeXT projector + unpad / avg-pool / image_newline (200 tokens for the 1024x359 frame) + Linear 4096->512
++ speed / target-point tokens + Llama 'tiny' + heads, every parameter trainable, B = 32, S = 233; one step =
+forward + backward + clip 1.0 + four-group AdamW.
+
+Roofline: the dominant kernel is the bf16 MFMA GEMM; `roofline` reports the ViT FC1 GEMM (vla: M = 16*1025,
+N = 4096, K = 1024, GELU epilogue, 24 launches per step; base: M = 64*577, quick_gelu, 23 launches) timed with
+HIP events on its launch stream during the timed steps, against the 2.5 PFLOP/s dense bf16 peak.
+`step_mfma_frac` = samples/s x required GFLOP/sample / (n_gpu x peak). `traffic` = HBM bytes
+per launch from the rocprofv3 FETCH_SIZE / WRITE_SIZE passes recorded in profiles/*_fc1_traffic.json
+(tools/pmc_traffic.py), when one matches the workload.
+cpu_baseline: the oracle (CPU fp32 PyTorch restatement, oracle/) forward+backward of one full-size sample on
+the host cores, rank 0, N = 1 only.
 """
 from __future__ import annotations
 
 import argparse
+import glob
 import json
 import os
 import sys
@@ -33,7 +41,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 PEAK_BF16_TFLOPS = 2500.0        # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
-GFLOP_PER_SAMPLE = {"vla": 5670.1, "tiny": None}  # SURVEY.md §8d config 3 (required FLOPs)
+VLA_GFLOP_PER_SAMPLE = 5670.1    # SURVEY.md §8d config 3 (required FLOPs)
 
 
 def parse():
@@ -41,8 +49,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="vla", choices=["vla", "tiny"])
-    ap.add_argument("--batch", type=int, default=8)
+    ap.add_argument("--config", default="vla", choices=["vla", "tiny", "base", "base_tiny"])
+    ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (vla 8, base 32)")
     ap.add_argument("--s-text", type=int, default=256)
     ap.add_argument("--n-loss", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -50,7 +58,25 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(cfg, s_text, n_loss, threads):
+def base_gflop(cfg) -> float:
+    """Required GFLOP per SimLingo-Base sample (2414.7 at S = 233): CLIP layers
+    0..vit_used-1 and the patch embedding on every tile, the projector on every patch feature, Linear(4096 -> E)
+    on the merged tokens, Llama with causal-half attention; backward = 2x forward minus the patch-embedding
+    dgrad (its input is the pixels). Heads and elementwise work ignored."""
+    T, D, F = cfg.vit_tokens, cfg.vit_dim, cfg.vit_ffn
+    g2 = cfg.vit_grid ** 2
+    n = cfg.npatch
+    clip = n * cfg.vit_used * (2 * T * (4 * D * D + 2 * D * F) + 4 * T * T * D)
+    patch = n * 2 * g2 * cfg.patch_k * D
+    proj = n * g2 * 2 * (D * cfg.proj_dim + cfg.proj_dim * cfg.proj_dim)
+    enc = 2 * cfg.img_tokens * cfg.proj_dim * cfg.embed_dim
+    S, d, Fl = cfg.seq, cfg.llm_dim, cfg.llm_ffn
+    llm = cfg.llm_layers * (2 * S * (4 * d * d + 3 * d * Fl) + 2 * S * S * d)
+    fwd = clip + patch + proj + enc + llm
+    return (fwd + 2 * fwd - patch) / 1e9
+
+
+def cpu_baseline_vla(cfg, s_text, n_loss, threads):
     """Oracle fwd+bwd of ONE full-size sample on the host (bounded ~10-30 s)."""
     from oracle import vla_oracle as O
     from simlingo_amd.params import init_params
@@ -65,6 +91,102 @@ def cpu_baseline(cfg, s_text, n_loss, threads):
             "sample": f"1 sample fwd+bwd (S_llm={s_text + cfg.img_tokens + cfg.n_queries}), fp32, {dt:.1f} s"}
 
 
+def cpu_baseline_base(cfg, threads):
+    from oracle import base_oracle as O
+    from simlingo_amd.base_params import init_base_params
+    from simlingo_amd.base_types import make_base_batch
+    torch.set_num_threads(threads)
+    P = init_base_params(cfg, seed=0)
+    ex = make_base_batch(cfg, B=1, seed=1234)
+    t0 = time.perf_counter()
+    O.loss_and_grads(P, cfg, ex)
+    dt = time.perf_counter() - t0
+    return {"value": 1.0 / dt, "unit": "samples/s", "cores": threads, "kind": "port",
+            "sample": f"1 sample fwd+bwd (S={cfg.seq}, 2 CLIP tiles), fp32, {dt:.1f} s"}
+
+
+def setup_vla(args, dev, world, rank):
+    from simlingo_amd.config import full_config, tiny_config
+    from simlingo_amd.engine import VLAEngine
+    from simlingo_amd.params import init_params
+    from simlingo_amd.plan import plan_from_example
+    from simlingo_amd.synthetic import make_batch
+    full = args.config == "vla"
+    cfg = full_config() if full else tiny_config(lora_dropout=0.1)
+    B = args.batch or (8 if full else 4)
+    s_text = args.s_text if full else 24
+    n_loss = args.n_loss if full else 6
+    eng = VLAEngine(cfg, dev, init_params(cfg, seed=0, device=dev))
+    ex = make_batch(cfg, B=B, s_text=s_text, n_loss=n_loss, seed=1000 + rank)
+    plan = plan_from_example(cfg, ex)
+    dplan = plan.to_device(dev)
+    pix = ex.driving_input.camera_images.to(dev)
+    path = ex.driving_label.path.to(dev)
+    wps = ex.driving_label.waypoints.to(dev)
+
+    def step(i):
+        out4, _, _ = eng.forward(pix, plan, dplan, path, wps, training=True)
+        eng.backward(None)
+        eng.adamw_step(cfg.lr, i + 1, betas=cfg.betas, eps=cfg.eps, weight_decay=cfg.weight_decay,
+                       max_norm=cfg.grad_clip)
+        return out4
+
+    return dict(
+        eng=eng, step=step, B=B, gflop=VLA_GFLOP_PER_SAMPLE if full else None,
+        metric_cfg={"workload": "simlingo full VLA train step (InternViT-300M x2 tiles + mlp1 + Qwen2-0.5B LoRA r32 + heads)"
+                    if full else "tiny parity geometry",
+                    "model": "InternVL2-1B geometry, random init" if full else "tiny", "seq_len": plan.S,
+                    "s_text": s_text, "loss_tokens_per_sample": n_loss},
+        probe=dict(M=2 * B * cfg.vit_tokens, N=cfg.vit_ffn, K=cfg.vit_dim, kernel="slx gemm_bf16 NT+gelu (InternViT fc1)",
+                   tag="vla_b8") if full else None,
+        cpu=(lambda: cpu_baseline_vla(cfg, s_text, n_loss, args.cpu_threads)) if full else None)
+
+
+def setup_base(args, dev, world, rank):
+    from simlingo_amd.base_config import base_config, base_tiny_config
+    from simlingo_amd.base_engine import BaseEngine
+    from simlingo_amd.base_params import init_base_params
+    from simlingo_amd.base_types import make_base_batch
+    full = args.config == "base"
+    cfg = base_config() if full else base_tiny_config()
+    B = args.batch or (32 if full else 4)
+    eng = BaseEngine(cfg, dev, init_base_params(cfg, seed=0))
+    ex = make_base_batch(cfg, B, seed=1000 + rank)
+    di, dl = ex.driving_input, ex.driving_label
+    pix, speed, tp = di.camera_images.to(dev), di.vehicle_speed.to(dev), di.map_route.to(dev)
+    route, wps = dl.route_adjusted.to(dev), dl.waypoints.to(dev)
+    size = (cfg.frame_h, cfg.frame_w)
+
+    def step(i):
+        out4, _, _ = eng.forward(pix, speed, tp, route, wps, image_size=size)
+        eng.backward(None)
+        eng.adamw_step(cfg.lr, cfg.vision_lr, i + 1, betas=cfg.betas, eps=cfg.eps, weight_decay=cfg.weight_decay,
+                       max_norm=cfg.grad_clip)
+        return out4
+
+    return dict(
+        eng=eng, step=step, B=B, gflop=base_gflop(cfg) if full else None,
+        metric_cfg={"workload": "SimLingo-Base train step (CLIP ViT-L/14-336 x2 tiles + LLaVA-NeXT projector/merge + "
+                                "Llama 'tiny' + heads, all trainable)" if full else "base tiny parity geometry",
+                    "model": "llava-v1.6 CLIP-L/14-336 + Llama CONFIGS['tiny'] geometry, random init" if full else "tiny",
+                    "seq_len": cfg.seq, "image_tokens": cfg.img_tokens, "frame": f"{cfg.frame_w}x{cfg.frame_h}"},
+        probe=dict(M=B * cfg.npatch * cfg.vit_tokens, N=cfg.vit_ffn, K=cfg.vit_dim,
+                   kernel="slx gemm_bf16 NT+quick_gelu (CLIP fc1)", tag="base_b32") if full else None,
+        cpu=(lambda: cpu_baseline_base(cfg, args.cpu_threads)) if full else None)
+
+
+def traffic_record(tag, flop_M):
+    """PMC-measured HBM bytes per FC1 launch (profiles/*_{tag}_fc1_traffic.json, newest first)."""
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", f"*{tag}_fc1_traffic.json")), reverse=True):
+        try:
+            rec = json.load(open(path))
+        except Exception:
+            continue
+        if rec.get("M") == flop_M:
+            return rec, os.path.relpath(path, ROOT)
+    return None, None
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -75,40 +197,15 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
-    from simlingo_amd.config import full_config, tiny_config
-    from simlingo_amd.engine import VLAEngine
-    from simlingo_amd.params import init_params
-    from simlingo_amd.plan import plan_from_example
-    from simlingo_amd.synthetic import make_batch
-
-    cfg = full_config() if args.config == "vla" else tiny_config(lora_dropout=0.1)
-    B = args.batch
-    s_text = args.s_text if args.config == "vla" else 24
-    n_loss = args.n_loss if args.config == "vla" else 6
-    params = init_params(cfg, seed=0, device=dev)
-    eng = VLAEngine(cfg, dev, params)
-    del params
+    w = (setup_base if args.config.startswith("base") else setup_vla)(args, dev, world, rank)
+    eng, step, B = w["eng"], w["step"], w["B"]
     if world > 1:
         import torch.distributed as dist
         dist.broadcast(eng.master, src=0)
         eng.wbf.copy_(eng.master.to(torch.bfloat16))
         eng._refresh_derived()
         eng.set_distributed(None, world)
-    # per-rank synthetic batch (rank-offset seed), resident in HBM before timing
-    ex = make_batch(cfg, B=B, s_text=s_text, n_loss=n_loss, seed=1000 + rank)
-    plan = plan_from_example(cfg, ex)
-    dplan = plan.to_device(dev)
-    pix = ex.driving_input.camera_images.to(dev)
-    path = ex.driving_label.path.to(dev)
-    wps = ex.driving_label.waypoints.to(dev)
     torch.cuda.synchronize()
-    lr = cfg.lr
-
-    def step(i):
-        out4, _, _ = eng.forward(pix, plan, dplan, path, wps, training=True)
-        eng.backward(None)
-        eng.adamw_step(lr, i + 1, betas=cfg.betas, eps=cfg.eps, weight_decay=cfg.weight_decay, max_norm=cfg.grad_clip)
-        return out4
 
     out4 = None
     for i in range(args.warmup):
@@ -120,7 +217,7 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    eng.probe_site = "vit.fc1" if args.config == "vla" else None
+    eng.probe_site = "vit.fc1" if w["probe"] else None
     eng.probe_events = []
     t0 = time.perf_counter()
     for i in range(args.steps):
@@ -137,35 +234,37 @@ def main():
     loss_last = out4[0].item()
     samples = B * world * args.steps
     value = samples / dt
+    cfg_out = dict(w["metric_cfg"])
+    cfg_out.update(global_batch=B * world, per_gpu_batch=B, parallelism=f"dp{world}")
     res = {
         "metric": "training samples/sec (frame+prompt->waypoints)",
         "value": round(value, 3), "unit": "samples/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
-        "config": {"workload": "simlingo full VLA train step (InternViT-300M x2 tiles + mlp1 + Qwen2-0.5B LoRA r32 + heads)"
-                   if args.config == "vla" else "tiny parity geometry",
-                   "model": "InternVL2-1B geometry, random init" if args.config == "vla" else "tiny",
-                   "global_batch": B * world, "per_gpu_batch": B, "seq_len": plan.S, "s_text": s_text,
-                   "loss_tokens_per_sample": n_loss, "parallelism": f"dp{world}"},
+        "vs_baseline": None, "dtype": "bf16", "data": "synthetic", "config": cfg_out,
         "loss_first": round(loss0, 5), "loss_last": round(loss_last, 5),
     }
-    gf = GFLOP_PER_SAMPLE[args.config]
+    gf = w["gflop"]
     if gf:
+        res["gflop_per_sample"] = round(gf, 1)
         res["step_mfma_frac"] = round(value * gf / 1e3 / (world * PEAK_BF16_TFLOPS), 4)
         res["step_tflops_per_gpu"] = round(value * gf / 1e3 / world, 1)
-    if eng.probe_events:
+    pr = w["probe"]
+    if pr and eng.probe_events:
         ms = [a.elapsed_time(b) for a, b in eng.probe_events]
         avg_ms = sum(ms) / len(ms)
-        M = 2 * B * cfg.vit_tokens
-        flop = 2.0 * M * cfg.vit_ffn * cfg.vit_dim
+        flop = 2.0 * pr["M"] * pr["N"] * pr["K"]
         ach = flop / (avg_ms * 1e-3) / 1e12
-        res["roofline"] = {"bound": "mfma", "kernel": "slx gemm_bf16 NT+gelu (InternViT fc1)",
-                           "achieved": round(ach, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                           "frac": round(ach / PEAK_BF16_TFLOPS, 4), "traffic": None,
+        rec, src = traffic_record(pr["tag"], pr["M"])
+        res["roofline"] = {"bound": "mfma", "kernel": pr["kernel"], "achieved": round(ach, 1), "peak": PEAK_BF16_TFLOPS,
+                           "unit": "TFLOP/s", "frac": round(ach / PEAK_BF16_TFLOPS, 4),
+                           "traffic": rec["traffic_bytes"] if rec else None,
                            "flop_per_launch": flop, "avg_launch_ms": round(avg_ms, 4), "launches": len(ms)}
-    if rank == 0 and world == 1 and args.config == "vla" and not args.no_cpu_baseline:
+        if rec:
+            res["roofline"]["traffic_source"] = src
+            res["roofline"]["algorithmic_bytes"] = rec.get("algorithmic_bytes")
+    if rank == 0 and world == 1 and w["cpu"] and not args.no_cpu_baseline:
         try:
-            res["cpu_baseline"] = cpu_baseline(cfg, s_text, n_loss, args.cpu_threads)
+            res["cpu_baseline"] = w["cpu"]()
         except Exception as e:  # the bench line must still be printed
             res["cpu_baseline"] = {"value": None, "error": repr(e)[:200]}
     if rank == 0:

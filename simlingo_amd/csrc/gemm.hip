@@ -1087,7 +1087,8 @@ extern "C" int slx_gemm_bf16(const slx_gemm_desc* d, slx_stream_t stream) {
     if (d->resid) t.resid = d->resid + r0 * d->ldr;
     int rc = gemm_launch(&m, 7, st);
     if (rc) return rc;
-    return gemm_launch(&t, 2, st);
+    // the peel is a handful of blocks walking the whole K: latency-bound, so give it the 4-stage ring
+    return gemm_launch(&t, 4, st);
   }
   return gemm_launch(d, v, st);
 }
