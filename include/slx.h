@@ -230,8 +230,9 @@ int slx_llava_merge_fwd(const void* src, int C, int64_t n_img, int npatch_h, int
                         int wu, int pool, const float* newline, void* out, slx_stream_t s);
 int slx_llava_merge_bwd(const float* dout, int C, int64_t n_img, int npatch_h, int npatch_w, int g, int r0, int hu, int c0,
                         int wu, int pool, void* dsrc, slx_stream_t s);
-/* table: n device-resident entries {src f32*, lds, dst bf16*, ldd, rows, cols, float-bits scale}:
- * dst = bf16(src * scale). Packs LoRA B (scaled by lora_alpha/r) into the fused [W | s*B] operands. */
+/* table: n device-resident entries {src f32*, lds, dst*, ldd, rows, cols, float-bits scale, dst_f32}:
+ * dst = src * scale (bf16, or f32 in the fp32 parity mode). Packs LoRA B (scaled by lora_alpha/r) into the
+ * fused [W | s*B] operands. */
 int slx_pack_scaled(const int64_t* table, int n, slx_stream_t s);
 
 /* ---- KV-cached greedy decode (agent call, BASELINE configs[4]) -------------------------------------
@@ -273,6 +274,23 @@ int slx_dec_attn_nsplit(int lmax);
 int slx_dec_attn_ws_floats(int Hq, int Hkv, int lmax);
 int slx_dec_attn(void* cache, int64_t ld, int Hq, int Hkv, const float* cos_tab, const float* sin_tab, int lmax,
                  float* ws, void* out, const slx_dec_state* st, slx_stream_t s);
+
+/* ---- fp32 parity mode (SURVEY.md §7 hard part 2; csrc/precise.hip) ---------------------------
+ * f32 twins of the bf16-only forward entry points, used by VLAEngine / BaseEngine(precise=True) to run the
+ * engines' own launch sequence with f32 activations and weights, so the forward can be held to the north-star
+ * tolerance (waypoint L2 <= 1e-4 m, LM CE <= 1e-4) against the reference fixtures. Same arguments and meaning
+ * as the bf16 entry point named; every void* operand is f32. Not tuned.                              */
+int slx_gemm_f32(const slx_gemm_desc* d, slx_stream_t stream);        /* slx_gemm_bf16, forward epilogues
+                                                                         STORE / GELU / QGELU / RESID_LS */
+int slx_attn_fwd_f32(const slx_attn_desc* d, slx_stream_t stream);    /* slx_attn_fwd                     */
+int slx_rope_f32(void* x, int64_t ldx, int64_t ntok, int S, int nheads, const float* cos_tab,
+                 const float* sin_tab, int inverse, slx_stream_t stream);                 /* slx_rope */
+int slx_swiglu_fwd_f32(const void* gu, int64_t ldgu, void* out, int64_t ldo, int64_t M, int F, slx_stream_t s);
+int slx_im2col_patch_f32(const float* pix, int N, int H, int W, int P, int kpad, void* out, slx_stream_t s);
+int slx_assemble_tokens_f32(const int* code, int64_t n, int D, const void* embed, int V, const void* img,
+                            const float* wp, const float* query, float* out, slx_stream_t s);
+int slx_llava_merge_fwd_f32(const void* src, int C, int64_t n_img, int npatch_h, int npatch_w, int g, int r0,
+                            int hu, int c0, int wu, int pool, const float* newline, void* out, slx_stream_t s);
 
 #ifdef __cplusplus
 }

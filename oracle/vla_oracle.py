@@ -161,7 +161,7 @@ def assemble(P, cfg, example, vit_embeds, inference=False):
                 first = int(hit[0, 0]) if hit.numel() else 0
                 if first == 0:
                     continue
-                coords = torch.as_tensor(pv[b][key], dtype=torch.float32).view(-1, 2)
+                coords = torch.as_tensor(pv[b][key], dtype=P["wp.0.w"].dtype).view(-1, 2)
                 lang[b, first:first + coords.shape[0]] = wp_encoder(P, coords)
     # image merge (internvl2_model.py:119-131)
     flat = lang.reshape(B * L, -1)
@@ -247,7 +247,7 @@ def language_inputs(P, cfg, example, vit_embeds, inference=True):
                 first = int(hit[0, 0]) if hit.numel() else 0
                 if first == 0:
                     continue
-                coords = torch.as_tensor(pv[b][key], dtype=torch.float32).view(-1, 2)
+                coords = torch.as_tensor(pv[b][key], dtype=P["wp.0.w"].dtype).view(-1, 2)
                 lang[b, first:first + coords.shape[0]] = wp_encoder(P, coords)
     flat = lang.reshape(B * L, -1)
     sel = ids.reshape(-1) == cfg.img_context_id

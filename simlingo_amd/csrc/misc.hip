@@ -446,20 +446,23 @@ __global__ void cast_rows_kernel(const float* src, long lds, bf16* dst, long ldd
   *reinterpret_cast<bf16x4*>(dst + m * ldd + c) = o;
 }
 
-// Batched 2-D scaled copy f32 -> bf16: entry e of `tab` = {src, lds, dst, ldd, rows, cols, scale(bits)}.
-// Packs every LoRA B (times alpha/r) into the fused [W | s*B] GEMM operands in one launch.
+// Batched 2-D scaled copy f32 -> bf16 (or f32, parity mode): entry e of `tab` =
+// {src, lds, dst, ldd, rows, cols, scale(bits), dst_f32}. Packs every LoRA B (times alpha/r) into the fused
+// [W | s*B] GEMM operands in one launch.
 __global__ void pack_scaled_kernel(const long long* tab, int n) {
   const int e = blockIdx.x;
-  const long long* t = tab + 7 * (long)e;
+  const long long* t = tab + 8 * (long)e;
   const float* src = reinterpret_cast<const float*>(t[0]);
   const long lds = t[1];
-  bf16* dst = reinterpret_cast<bf16*>(t[2]);
   const long ldd = t[3];
   const long rows = t[4], cols = t[5];
   const float sc = __int_as_float((int)t[6]);
+  const bool f32 = t[7] != 0;
   for (long i = (long)blockIdx.y * blockDim.x + threadIdx.x; i < rows * cols; i += (long)gridDim.y * blockDim.x) {
     const long r = i / cols, c = i % cols;
-    dst[r * ldd + c] = (bf16)(src[r * lds + c] * sc);
+    const float v = src[r * lds + c] * sc;
+    if (f32) reinterpret_cast<float*>(t[2])[r * ldd + c] = v;
+    else reinterpret_cast<bf16*>(t[2])[r * ldd + c] = (bf16)v;
   }
 }
 

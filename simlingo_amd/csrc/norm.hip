@@ -26,7 +26,8 @@ struct NormArgs {
   float* mean; float* rstd;
   long rows; int D; float eps;
   int ps; int G; int C; int tok_per_img;  // pixel-shuffle gather
-  int y_f32;                              // y holds f32 rows (CLIP pre_layrnorm feeds the f32 residual)
+  int y_f32;                              // y holds f32 rows (CLIP pre_layrnorm feeds the f32 residual; for
+                                          // RMS, the f32 parity mode: input dtype f32, no bf16 cast of x_hat)
   // bwd
   const float* dy; long lddy;
   float* dx; long lddx; int dx_accumulate;
@@ -81,7 +82,7 @@ __global__ __launch_bounds__(256) void norm_fwd_kernel(NormArgs a) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const float xh = (v[4 * i + e] - mu) * rs;
-      if (RMS) yv[e] = (float)(bf16)xh * a.gamma[col + e];  // Qwen2: weight * hs.to(input_dtype)
+      if (RMS) yv[e] = (a.y_f32 ? xh : (float)(bf16)xh) * a.gamma[col + e];  // Qwen2: weight * hs.to(input_dtype)
       else yv[e] = xh * a.gamma[col + e] + a.beta[col + e];
     }
     if (a.y_f32) {
@@ -142,7 +143,7 @@ __global__ __launch_bounds__(256) void norm_fwd_wave_kernel(NormArgs a) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const float xh = (v[4 * i + e] - mu) * rs;
-      yv[e] = RMS ? (float)(bf16)xh * a.gamma[col + e] : xh * a.gamma[col + e] + a.beta[col + e];
+      yv[e] = RMS ? (a.y_f32 ? xh : (float)(bf16)xh) * a.gamma[col + e] : xh * a.gamma[col + e] + a.beta[col + e];
     }
     if (a.y_f32) {
       *reinterpret_cast<float4*>(reinterpret_cast<float*>(a.y) + row * a.ldy + col) = make_float4(yv[0], yv[1], yv[2], yv[3]);

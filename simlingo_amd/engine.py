@@ -43,12 +43,16 @@ def _pad64(n):
 
 class VLAEngine(EngineOps):
     def __init__(self, cfg: VLAConfig, device, params: dict[str, torch.Tensor] | None = None, seed: int = 0,
-                 bucket_bytes: int = 32 << 20):
+                 bucket_bytes: int = 32 << 20, precise: bool = False):
+        """precise=True: fp32 parity mode — the same launch sequence with f32 activations and weights (the f32
+        twins of csrc/precise.hip), forward only; used to hold the forward to the north-star tolerance."""
         from .params import init_params
         self.cfg = cfg
         self.device = torch.device(device)
         if self.device.type != "cuda":
             raise RuntimeError("VLAEngine runs on the MI355X (HIP) only; there is no CPU path")
+        self.precise = bool(precise)
+        self.adt = F32 if self.precise else BF16   # activation / GEMM-operand dtype
         K.lib()  # fail loudly if the HIP library is missing
         params = params if params is not None else init_params(cfg, seed)
         self.specs = param_specs(cfg)
@@ -71,24 +75,24 @@ class VLAEngine(EngineOps):
                 o = offs[s.name]
                 self.P[s.name] = self.master[o:o + n].view(s.shape)
                 self.G[s.name] = self.grad[o:o + n].view(s.shape)
-                self.W[s.name] = self.wbf[o:o + n].view(s.shape)
+                self.W[s.name] = self.P[s.name] if self.precise else self.wbf[o:o + n].view(s.shape)
                 self.P[s.name].copy_(params[s.name].to(dev))
             else:
                 t = params[s.name].to(dev)
                 if len(s.shape) == 1:
                     self.P[s.name] = t.float().contiguous()
                 else:
-                    self.W[s.name] = t.to(BF16).contiguous()
+                    self.W[s.name] = t.to(self.adt).contiguous()
         self.wbf.copy_(self.master.to(BF16))
         # LM head padded to a multiple of 8 rows (its dgrad GEMM reads K = V rows as [K][N])
         V, d = cfg.vocab, cfg.llm_dim
         self.Vp = _pad64(V)
         if self.Vp != V:
-            lm = torch.zeros(self.Vp, d, dtype=BF16, device=dev)
+            lm = torch.zeros(self.Vp, d, dtype=self.adt, device=dev)
             lm[:V].copy_(self.W["llm.lm_head"])
             self.W["llm.lm_head"] = lm
         # patch-embedding weight padded to K = kpad columns for the im2col GEMM
-        self.wpatch = torch.zeros(cfg.vit_dim, cfg.patch_kpad, dtype=BF16, device=dev)
+        self.wpatch = torch.zeros(cfg.vit_dim, cfg.patch_kpad, dtype=self.adt, device=dev)
         self._refresh_derived()
         self.ones_d = torch.ones(d, dtype=F32, device=dev)
         # contiguity needed by the assembly kernel: the 30 query rows are one [30, d] block
@@ -147,7 +151,7 @@ class VLAEngine(EngineOps):
                 base = {"qkv": self.W[p + "qkv_w"], "o": self.W[p + "o_w"], "gu": self.W[p + "gate_up_w"],
                         "down": self.W[p + "down_w"]}[g]
                 N, Kin = base.shape
-                w = torch.zeros(N, Kin + pad, dtype=BF16, device=self.device)
+                w = torch.zeros(N, Kin + pad, dtype=self.adt, device=self.device)
                 w[:, :Kin].copy_(base)
                 row = 0
                 for j, site in enumerate(sites):
@@ -155,7 +159,7 @@ class VLAEngine(EngineOps):
                     b = self.P[p + f"lora.{site}.b"]  # [out_s, r] f32 master
                     dst = w[row:row + out_s, Kin + r * j: Kin + r * (j + 1)]
                     entries.append([b.data_ptr(), b.stride(0), dst.data_ptr(), dst.stride(0), out_s, r,
-                                    int(np.float32(s).view(np.int32))])
+                                    int(np.float32(s).view(np.int32)), int(self.precise)])
                     row += out_s
                 cats[g] = w
             # A_s zero-padded to 64 rows: the dropout-masked dgrad dx += drop'(dT_s A_s) then runs as a K=64 GEMM
@@ -163,9 +167,9 @@ class VLAEngine(EngineOps):
             # the site multiply the zero rows), which keeps it on the LDS-DMA path.
             for site in LORA_SITES:
                 a = self.P[p + f"lora.{site}.a"]  # [r, in] f32 master
-                ap = torch.zeros(64, a.shape[1], dtype=BF16, device=self.device)
+                ap = torch.zeros(64, a.shape[1], dtype=self.adt, device=self.device)
                 entries.append([a.data_ptr(), a.stride(0), ap.data_ptr(), ap.stride(0), r, a.shape[1],
-                                int(np.float32(1.0).view(np.int32))])
+                                int(np.float32(1.0).view(np.int32)), int(self.precise)])
                 cats["apad." + site] = ap
             self.cat.append(cats)
         self._pack_tab = torch.tensor(entries, dtype=torch.int64, device=self.device)
@@ -211,14 +215,14 @@ class VLAEngine(EngineOps):
             L = {}
             cat = self.cat[i] if lora else None
             Pq, Po, Pg, Pd = (128, 64, 64, 64) if lora else (0, 0, 0, 0)
-            hx = (self._z if lora else self._e)(Ml, d + Pq, dtype=BF16)
+            hx = (self._z if lora else self._e)(Ml, d + Pq, dtype=self.adt)
             h, nrm1 = self._norm(X, self.P[p + "ln1"], None, Ml, d, cfg.rms_eps, rms=True, out=hx[:, :d])
             if lora:
                 L.update(self._lora_down(hx[:, :d], i, ("q", "k", "v"), hx[:, d:], sv))
             qkv = self._e(Ml, nqkv)
             K.mm(hx, cat["qkv"] if lora else self.W[p + "qkv_w"], qkv, bias=self.P[p + "qkv_b"])
             K.rope(qkv, Ml, S, Hq + Hk, cos, sin)  # q and k heads are the first Hq+Hk head slots
-            ox = (self._z if lora else self._e)(Ml, qn + Po, dtype=BF16)
+            ox = (self._z if lora else self._e)(Ml, qn + Po, dtype=self.adt)
             o = ox[:, :qn]
             lse = self._e(B * Hq * S, dtype=F32)
             K.attn_fwd(qkv[:, :qn], qkv[:, qn:qn + kn], qkv[:, qn + kn:], o, lse, B=B, S=S, Hq=Hq, Hkv=Hk, causal=True,
@@ -227,15 +231,15 @@ class VLAEngine(EngineOps):
                 L.update(self._lora_down(o, i, ("o",), ox[:, qn:], sv))
             Xm = self._e(Ml, d, dtype=F32)
             K.mm(ox, cat["o"] if lora else self.W[p + "o_w"], Xm, epi=K.EPI_RESID_LS, resid=X, ldr=d, ls=self.ones_d)
-            h2x = (self._z if lora else self._e)(Ml, d + Pg, dtype=BF16)
+            h2x = (self._z if lora else self._e)(Ml, d + Pg, dtype=self.adt)
             h2, nrm2 = self._norm(Xm, self.P[p + "ln2"], None, Ml, d, cfg.rms_eps, rms=True, out=h2x[:, :d])
             if lora:
                 L.update(self._lora_down(h2, i, ("gate", "up"), h2x[:, d:], sv))
             gu = self._e(Ml, 2 * Fl)
             K.mm(h2x, cat["gu"] if lora else self.W[p + "gate_up_w"], gu)
-            ax = (self._z if lora else self._e)(Ml, Fl + Pd, dtype=BF16)
+            ax = (self._z if lora else self._e)(Ml, Fl + Pd, dtype=self.adt)
             act = ax[:, :Fl]
-            K.call("slx_swiglu_fwd", K.P(gu), gu.stride(0), K.P(act), act.stride(0), Ml, Fl, K.stream_ptr())
+            self._swiglu(gu, act, Ml, Fl)
             if lora:
                 L.update(self._lora_down(act, i, ("down",), ax[:, Fl:], sv))
             Xo = self._e(Ml, d, dtype=F32)
@@ -252,7 +256,7 @@ class VLAEngine(EngineOps):
         ce_loss = self._e(max(R, 1), dtype=F32)
         if R:
             fl = self._e(R, d)
-            K.call("slx_gather_rows_bf16", K.P(feat), d, K.P(dplan["loss_pos"]), R, d, K.P(fl), d, K.stream_ptr())
+            self._gather_feat(feat, d, dplan["loss_pos"], R, d, fl)
             logits = self._e(R, self.Vp, dtype=F32)
             K.mm(fl, self.W["llm.lm_head"][: cfg.vocab], logits)
             lse_ce = self._e(R, dtype=F32)
@@ -267,8 +271,8 @@ class VLAEngine(EngineOps):
         m = cfg.head_mlp
         fr = self._e(B * nr, d, dtype=F32)
         fs = self._e(B * ns, d, dtype=F32)
-        K.call("slx_gather_rows_b2f", K.P(feat), d, K.P(rpos), B * nr, d, K.P(fr), d, K.stream_ptr())
-        K.call("slx_gather_rows_b2f", K.P(feat), d, K.P(spos), B * ns, d, K.P(fs), d, K.stream_ptr())
+        self._gather_feat(feat, d, rpos, B * nr, d, fr)
+        self._gather_feat(feat, d, spos, B * ns, d, fs)
         hd = self._mlp_fwd(fr, [("route.0", 2 * m, K.ACT_SILU), ("route.1", m, K.ACT_SILU), ("route.2", 2, K.ACT_NONE)])
         sd_ = self._mlp_fwd(fs, [("speed.0", m, K.ACT_SILU), ("speed.1", cfg.speed_dims, K.ACT_NONE)])
         route_pred = self._e(B, nr, 2, dtype=F32)
@@ -305,7 +309,7 @@ class VLAEngine(EngineOps):
         g = cfg.vit_grid
         Mv = N * T
         col = self._e(N * g * g, cfg.patch_kpad)
-        K.call("slx_im2col_patch", K.P(pix), N, cfg.img_size, cfg.img_size, cfg.patch, cfg.patch_kpad, K.P(col), K.stream_ptr())
+        K.call("slx_im2col_patch_f32" if self.precise else "slx_im2col_patch", K.P(pix), N, cfg.img_size, cfg.img_size, cfg.patch, cfg.patch_kpad, K.P(col), K.stream_ptr())
         pe = self._e(N * g * g, D, dtype=F32)
         K.mm(col, self.wpatch, pe, bias=self.P["vit.patch.b"])
         x = self._e(Mv, D, dtype=F32)
@@ -369,7 +373,7 @@ class VLAEngine(EngineOps):
         S = plan.S
         Ml = B * S
         X = self._e(Ml, d, dtype=F32)
-        K.call("slx_assemble_tokens", K.P(dplan["code"]), Ml, d, K.P(self.W["llm.embed"]), cfg.vocab, K.P(img),
+        K.call("slx_assemble_tokens_f32" if self.precise else "slx_assemble_tokens", K.P(dplan["code"]), Ml, d, K.P(self.W["llm.embed"]), cfg.vocab, K.P(img),
                K.P(wp_out), K.P(self.P["drv.query_route"]), K.P(X), K.stream_ptr())
         sv.update(nwp=nwp, Mi=Mi, Mv=Mv)
         return X
@@ -379,6 +383,13 @@ class VLAEngine(EngineOps):
         the activation buffer), one launch. Dropout is applied while loading x (hash mask, regenerated in
         backward). Returns {site: seed}."""
         seeds = {site: sv["seed"] + 131 * i + 7 * LORA_SITES.index(site) + 1 for site in sites}
+        if self.precise:  # parity mode runs the eval forward: dropout off, t = x A^T as f32 GEMMs
+            if sv["drop"] > 0:
+                raise RuntimeError("fp32 parity mode runs the eval forward (LoRA dropout off): forward(training=False)")
+            r = self.cfg.lora_r
+            for j, site in enumerate(sites):
+                K.mm(x, self.W[f"llm.{i}.lora.{site}.a"], t_out[:, r * j:r * (j + 1)])
+            return seeds
         K.lora_down(x, [self.W[f"llm.{i}.lora.{site}.a"] for site in sites], t_out, [seeds[s_] for s_ in sites],
                     p=sv["drop"])
         return seeds
@@ -390,6 +401,8 @@ class VLAEngine(EngineOps):
         cfg = self.cfg
         sv = self.saved
         assert sv is not None, "backward() without forward()"
+        if self.precise:
+            raise RuntimeError("the fp32 parity mode is forward-only (it pins the forward outputs)")
         B, S, Ml, Mv, Mi, R = sv["B"], sv["S"], sv["Ml"], sv["Mv"], sv["Mi"], sv["R"]
         d, D = cfg.llm_dim, cfg.vit_dim
         nr, ns = cfg.n_route, cfg.n_speed

@@ -42,8 +42,23 @@ class EngineOps:
     def wait_grads(self):
         self.bucketer.wait()
 
-    def _e(self, *shape, dtype=BF16):
-        return torch.empty(*shape, dtype=dtype, device=self.device)
+    def _e(self, *shape, dtype=None):
+        """Uninitialised device buffer; default dtype = the engine's activation dtype (bf16, f32 in parity mode)."""
+        return torch.empty(*shape, dtype=dtype or getattr(self, "adt", BF16), device=self.device)
+
+    def _swiglu(self, gu, act, M, F):
+        name = "slx_swiglu_fwd_f32" if gu.dtype == F32 else "slx_swiglu_fwd"
+        K.call(name, K.P(gu), gu.stride(0), K.P(act), act.stride(0), M, F, K.stream_ptr())
+
+    def _gather_feat(self, src, ld, idx, n, D, dst):
+        """rows of a norm output (bf16, or f32 in parity mode) -> dst rows (f32 or bf16)."""
+        if src.dtype == F32:
+            K.call("slx_gather_rows", K.P(src), ld, K.P(idx), n, D, K.P(dst), dst.stride(0), int(dst.dtype == BF16),
+                   K.stream_ptr())
+        elif dst.dtype == F32:
+            K.call("slx_gather_rows_b2f", K.P(src), ld, K.P(idx), n, D, K.P(dst), dst.stride(0), K.stream_ptr())
+        else:
+            K.call("slx_gather_rows_bf16", K.P(src), ld, K.P(idx), n, D, K.P(dst), dst.stride(0), K.stream_ptr())
 
     def _z(self, *shape, dtype=F32):
         return torch.zeros(*shape, dtype=dtype, device=self.device)

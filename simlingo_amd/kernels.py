@@ -136,6 +136,11 @@ def gemm(A, B, C, M, N, K, layout, lda, ldb, ldc, *, epi=EPI_STORE, alpha=1.0, b
     d.ksplit_max = int(ksplit_max)
     d.variant = int(GEMM_VARIANT if variant is None else variant)
     d.drop_operand = int(drop_operand)
+    if A.dtype == torch.float32:  # fp32 parity mode (csrc/precise.hip)
+        if B.dtype != torch.float32 or C.dtype != torch.float32:
+            raise RuntimeError("fp32 parity-mode GEMM needs f32 A, B and C")
+        check(lib().slx_gemm_f32(ctypes.byref(d), stream_ptr()), "slx_gemm_f32")
+        return
     check(lib().slx_gemm_bf16(ctypes.byref(d), stream_ptr()), "slx_gemm_bf16")
 
 
@@ -260,6 +265,14 @@ for _n, _a in {
     "slx_cast_rows": [_vp, _I, _vp, _I, _I, _i, _vp],
     "slx_pack_scaled": [_vp, _i, _vp],
     "slx_cast_f32_bf16": [_vp, _vp, _I, _vp],
+    # fp32 parity mode (csrc/precise.hip)
+    "slx_gemm_f32": [ctypes.POINTER(GemmDesc), _vp],
+    "slx_attn_fwd_f32": [ctypes.POINTER(AttnDesc), _vp],
+    "slx_rope_f32": [_vp, _I, _I, _i, _i, _vp, _vp, _i, _vp],
+    "slx_swiglu_fwd_f32": [_vp, _I, _vp, _I, _I, _i, _vp],
+    "slx_im2col_patch_f32": [_vp, _i, _i, _i, _i, _i, _vp, _vp],
+    "slx_assemble_tokens_f32": [_vp, _I, _i, _vp, _i, _vp, _vp, _vp, _vp, _vp],
+    "slx_llava_merge_fwd_f32": [_vp, _i, _I, _i, _i, _i, _i, _i, _i, _i, _i, _vp, _vp, _vp],
 }.items():
     register(_n, _a)
 
@@ -282,7 +295,8 @@ def attn_fwd(q, k, v, o, lse, **kw):
     """q/k/v/o: 2-D token-major views [B*S, >= H*64] (column slices allowed)."""
     _require_cuda(q, k, v, o)
     d = attn_desc(q, k, v, o, lse, **kw)
-    check(lib().slx_attn_fwd(ctypes.byref(d), stream_ptr()), "slx_attn_fwd")
+    name = "slx_attn_fwd_f32" if q.dtype == torch.float32 else "slx_attn_fwd"  # f32: parity mode
+    check(getattr(lib(), name)(ctypes.byref(d), stream_ptr()), name)
 
 
 def attn_bwd(q, k, v, o, lse, dout, dq, dk, dv, ws, *, rope_cos=None, rope_sin=None, **kw):
@@ -313,7 +327,8 @@ def attn_ws(B, S, Hq, Hkv, device, rope=False):
 
 
 def rope(x, ntok, S, nheads, cos, sin, inverse=False):
-    call("slx_rope", P(x), x.stride(0), ntok, S, nheads, P(cos), P(sin), int(inverse), stream_ptr())
+    call("slx_rope_f32" if x.dtype == torch.float32 else "slx_rope", P(x), x.stride(0), ntok, S, nheads, P(cos), P(sin),
+         int(inverse), stream_ptr())
 
 
 def rope_tables(S, theta, device, head_dim=64):

@@ -50,3 +50,32 @@ def test_engine_vs_oracle(dev, case):
         if cos < 0.98 or rel > 0.2:
             bad.append((name, round(cos, 4), round(rel, 4)))
     assert not bad, bad
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_precise_forward_north_star(dev, case):
+    """fp32 parity mode (csrc/precise.hip): the engine's own launch sequence with f32 operands, held to the
+    north-star tolerance against the fp32 oracle — waypoint / route points max |diff| <= 1e-4 m, LM
+    cross-entropy |diff| <= 1e-4 (BASELINE.json north_star)."""
+    from simlingo_amd.engine import VLAEngine
+    from simlingo_amd.plan import plan_from_example
+    cfg, P, ex, z = load_case(case)
+    ref, _ = O.loss_and_grads(P, cfg, ex)
+    eng = VLAEngine(cfg, dev, P, precise=True)
+    plan = plan_from_example(cfg, ex)
+    lab = ex.driving_label
+    out4, rp, sp = eng.forward(ex.driving_input.camera_images.to(dev), plan, plan.to_device(dev), lab.path.to(dev),
+                               lab.waypoints.to(dev), training=False)
+    torch.cuda.synchronize()
+    out4, rp, sp = out4.cpu(), rp.cpu(), sp.cpu()
+    want = torch.tensor([ref["loss"].item(), ref["language_loss"].item(), ref["route_loss"].item(),
+                         ref["speed_wps_loss"].item()])
+    d_loss = (out4 - want).abs()
+    d_route = (rp - ref["route_pred"]).abs().max().item()
+    d_speed = (sp - ref["speed_pred"]).abs().max().item()
+    msg = f"loss diffs {d_loss.tolist()} route {d_route:.3g} speed {d_speed:.3g}"
+    print(msg)
+    assert d_loss[1].item() <= 1e-4 and d_route <= 1e-4 and d_speed <= 1e-4, msg
+    assert torch.allclose(out4, want, rtol=1e-4, atol=1e-5), msg
+    with pytest.raises(RuntimeError):
+        eng.backward(None)
