@@ -33,8 +33,12 @@ ALIGN = 64
 
 class BaseEngine(EngineOps):
     def __init__(self, cfg: BaseConfig, device, params: dict[str, torch.Tensor] | None = None, seed: int = 0,
-                 bucket_bytes: int = 32 << 20):
+                 bucket_bytes: int = 32 << 20, precise: bool = False):
+        """precise=True: fp32 parity mode — the same launch sequence with f32 activations and weights (the f32
+        twins of csrc/precise.hip), forward only; used to hold the forward to the north-star tolerance."""
         self.cfg = cfg
+        self.precise = bool(precise)
+        self.adt = F32 if self.precise else BF16   # activation / GEMM-operand dtype
         self.device = torch.device(device)
         if self.device.type != "cuda":
             raise RuntimeError("BaseEngine runs on the MI355X (HIP) only; there is no CPU path")
@@ -52,7 +56,7 @@ class BaseEngine(EngineOps):
             o, sz = offs[s.name], math.prod(s.shape)
             self.P[s.name] = self.master[o:o + sz].view(s.shape)
             self.G[s.name] = self.grad[o:o + sz].view(s.shape)
-            self.W[s.name] = self.wbf[o:o + sz].view(s.shape)
+            self.W[s.name] = self.P[s.name] if self.precise else self.wbf[o:o + sz].view(s.shape)
             self.P[s.name].copy_(params[s.name].to(dev))
             e = o + (sz + ALIGN - 1) // ALIGN * ALIGN
             a, b = group_ranges.get(groups[s.name], (o, e))
@@ -60,7 +64,7 @@ class BaseEngine(EngineOps):
         self.wbf.copy_(self.master.to(BF16))
         qr, qs = offs["drv.query_route"], offs["drv.query_speed"]
         assert qs == qr + cfg.n_route * cfg.llm_dim, "query parameters must be adjacent"
-        self.wpatch = torch.zeros(cfg.vit_dim, cfg.patch_kpad, dtype=BF16, device=dev)
+        self.wpatch = torch.zeros(cfg.vit_dim, cfg.patch_kpad, dtype=self.adt, device=dev)
         self.ones_D = torch.ones(cfg.vit_dim, dtype=F32, device=dev)
         self.ones_d = torch.ones(cfg.llm_dim, dtype=F32, device=dev)
         self.bias_eff = torch.zeros(cfg.embed_dim, dtype=F32, device=dev)
@@ -127,7 +131,7 @@ class BaseEngine(EngineOps):
             pix = pix.float().contiguous()
         # ---- CLIP embeddings + pre_layrnorm ----
         col = self._e(N * g * g, cfg.patch_kpad)
-        K.call("slx_im2col_patch", K.P(pix), N, cfg.img_size, cfg.img_size, cfg.patch, cfg.patch_kpad, K.P(col),
+        K.call("slx_im2col_patch_f32" if self.precise else "slx_im2col_patch", K.P(pix), N, cfg.img_size, cfg.img_size, cfg.patch, cfg.patch_kpad, K.P(col),
                K.stream_ptr())
         pe = self._e(N * g * g, D, dtype=F32)
         K.mm(col, self.wpatch, pe)
@@ -164,7 +168,7 @@ class BaseEngine(EngineOps):
         Pd, E, d = cfg.proj_dim, cfg.embed_dim, cfg.llm_dim
         Mf = N * g * g
         feat = self._e(Mf, D)
-        K.call("slx_gather_rows", K.P(x), D, K.P(pl["nocls"]), Mf, D, K.P(feat), D, 1, K.stream_ptr())
+        self._gather_feat(x, D, pl["nocls"], Mf, D, feat)
         p1pre, p1 = self._e(Mf, Pd), self._e(Mf, Pd)
         K.mm(feat, self.W["mm.fc1.w"], p1, bias=self.P["mm.fc1.b"], epi=K.EPI_GELU, aux_out=p1pre, ldaux_out=Pd)
         p2 = self._e(Mf, Pd)
@@ -172,7 +176,7 @@ class BaseEngine(EngineOps):
         r0, hu, c0, wu = cfg.unpad()
         Ti = cfg.img_tokens
         merged = self._e(B * Ti, Pd)
-        K.call("slx_llava_merge_fwd", K.P(p2), Pd, B, cfg.npatch_h, cfg.npatch_w, g, r0, hu, c0, wu, cfg.pool,
+        K.call("slx_llava_merge_fwd_f32" if self.precise else "slx_llava_merge_fwd", K.P(p2), Pd, B, cfg.npatch_h, cfg.npatch_w, g, r0, hu, c0, wu, cfg.pool,
                K.P(self.P["mm.newline"]), K.P(merged), K.stream_ptr())
         S, NQ = cfg.seq, cfg.n_queries
         Sf = S - NQ
@@ -199,7 +203,7 @@ class BaseEngine(EngineOps):
         # ---- [fixed | queries] -> Llama ----
         Ml = B * S
         X = self._e(Ml, d, dtype=F32)
-        K.call("slx_assemble_tokens", K.P(pl["code"]), Ml, d, K.P(None), 1, K.P(None), K.P(pre),
+        K.call("slx_assemble_tokens_f32" if self.precise else "slx_assemble_tokens", K.P(pl["code"]), Ml, d, K.P(None), 1, K.P(None), K.P(pre),
                K.P(self.P["drv.query_route"]), K.P(X), K.stream_ptr())
         Hh, Fl = cfg.llm_heads, cfg.llm_ffn
         cos, sin = self.rope_tables(S)
@@ -219,7 +223,7 @@ class BaseEngine(EngineOps):
             gu = self._e(Ml, 2 * Fl)
             K.mm(h2, self.W[p + "gate_up_w"], gu)
             act = self._e(Ml, Fl)
-            K.call("slx_swiglu_fwd", K.P(gu), gu.stride(0), K.P(act), act.stride(0), Ml, Fl, K.stream_ptr())
+            self._swiglu(gu, act, Ml, Fl)
             Xo = self._e(Ml, d, dtype=F32)
             K.mm(act, self.W[p + "down_w"], Xo, epi=K.EPI_RESID_LS, resid=Xm, ldr=d, ls=self.ones_d)
             llm_saved.append(dict(h=h, n1=n1, qkv=qkv, o=o, lse=lse, h2=h2, n2=n2, gu=gu, act=act))
@@ -229,8 +233,8 @@ class BaseEngine(EngineOps):
         # ---- driving heads + MSE (adaptors.py:163-232) ----
         nr, ns = cfg.n_route, cfg.n_speed
         fr, fs = self._e(B * nr, d, dtype=F32), self._e(B * ns, d, dtype=F32)
-        K.call("slx_gather_rows_b2f", K.P(featL), d, K.P(pl["rpos"]), B * nr, d, K.P(fr), d, K.stream_ptr())
-        K.call("slx_gather_rows_b2f", K.P(featL), d, K.P(pl["spos"]), B * ns, d, K.P(fs), d, K.stream_ptr())
+        self._gather_feat(featL, d, pl["rpos"], B * nr, d, fr)
+        self._gather_feat(featL, d, pl["spos"], B * ns, d, fs)
         m = cfg.head_mlp
         hd = self._mlp_fwd(fr, [("route.0", m, K.ACT_SILU), ("route.1", 2, K.ACT_NONE)])
         sd_ = self._mlp_fwd(fs, [("speed.0", m, K.ACT_SILU), ("speed.1", cfg.speed_dims, K.ACT_NONE)])
@@ -255,6 +259,8 @@ class BaseEngine(EngineOps):
         cfg = self.cfg
         sv = self.saved
         assert sv is not None, "backward() without forward()"
+        if self.precise:
+            raise RuntimeError("the fp32 parity mode is forward-only (it pins the forward outputs)")
         B, Mv, N, Mf, Ml, pl = sv["B"], sv["Mv"], sv["N"], sv["Mf"], sv["Ml"], sv["pl"]
         D, d, Pd, E = cfg.vit_dim, cfg.llm_dim, cfg.proj_dim, cfg.embed_dim
         nr, ns = cfg.n_route, cfg.n_speed

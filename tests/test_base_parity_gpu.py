@@ -69,3 +69,28 @@ def test_base_adamw_groups_match_torch(dev):
     torch.cuda.synchronize()
     for n, p in params.items():
         torch.testing.assert_close(eng.P[n], p.detach(), rtol=1e-5, atol=1e-6, msg=n)
+
+
+def test_base_precise_forward_north_star(dev):
+    """fp32 parity mode (csrc/precise.hip): BaseEngine's own launch sequence with f32 operands vs the fp32 oracle,
+    held to the north-star tolerance — route / speed waypoints max |diff| <= 1e-4 m, losses rel 1e-4."""
+    from simlingo_amd.base_engine import BaseEngine
+    cfg, P, ex, _ = load_base_case()
+    ref = O.forward_loss(P, cfg, ex)
+    eng = BaseEngine(cfg, dev, P, precise=True)
+    di, dl = ex.driving_input, ex.driving_label
+    out4, rp, sp = eng.forward(di.camera_images.to(dev), di.vehicle_speed.to(dev), di.map_route.to(dev),
+                               dl.route_adjusted.to(dev), dl.waypoints.to(dev),
+                               image_size=tuple(di.image_sizes[0].tolist()))
+    torch.cuda.synchronize()
+    out4, rp, sp = out4.cpu(), rp.cpu(), sp.cpu()
+    d_route = (rp - ref["route_pred"]).abs().max().item()
+    d_speed = (sp - ref["speed_pred"]).abs().max().item()
+    d_loss = [abs(out4[i].item() - ref[k].item()) for i, k in ((0, "loss"), (2, "route_loss"), (3, "speed_wps_loss"))]
+    msg = f"loss diffs {d_loss} route {d_route:.3g} speed {d_speed:.3g}"
+    print(msg)
+    assert d_route <= 1e-4 and d_speed <= 1e-4, msg
+    for i, k in ((0, "loss"), (2, "route_loss"), (3, "speed_wps_loss")):
+        assert abs(out4[i].item() - ref[k].item()) <= 1e-4 * abs(ref[k].item()) + 1e-6, msg
+    with pytest.raises(RuntimeError):
+        eng.backward(None)
