@@ -275,6 +275,34 @@ int slx_dec_attn_ws_floats(int Hq, int Hkv, int lmax);
 int slx_dec_attn(void* cache, int64_t ld, int Hq, int Hkv, const float* cos_tab, const float* sin_tab, int lmax,
                  float* ws, void* out, const slx_dec_state* st, slx_stream_t s);
 
+/* ---- collate image path: uint8 frames -> InternVL2 pixel tiles (csrc/frames.hip) --------
+ * Replaces preprocess_image_batch (simlingo_training/utils/internvl2_utils.py:179-203) per batch: the bottom crop
+ * (dataloader/dataset_base.py:464-467) is a row count, dynamic_preprocess (internvl2_utils.py:231-266) picks the
+ * grid on the host, and one kernel does Pillow's BICUBIC Image.resize (Resample.c ImagingResample, bit-exact
+ * uint8), the 448-tile crop, ToTensor and Normalize (build_transform, internvl2_utils.py:206-214).
+ * slx_resample_ksize / slx_resample_coeffs are host functions (no GPU): Pillow's precompute_coeffs +
+ * normalize_coeffs_8bpc for one axis, in_size -> out_size, box = whole axis; bounds[2*o] = first source
+ * index, bounds[2*o+1] = tap count, kk[o*kmax + j] = 22-bit fixed-point weight. Returns ksize (or < 0). */
+int slx_resample_ksize(int in_size, int out_size);
+int slx_resample_coeffs(int in_size, int out_size, int kmax, int32_t* bounds, int32_t* kk);
+typedef struct {
+  const uint8_t* src;               /* frames, element strides: frame sb, row sy, pixel sx, channel sc (RGB)  */
+  int64_t sb, sy, sx, sc;
+  int B, H, W;                      /* H = rows kept by the bottom crop (rows 0..H-1 are read)                */
+  int tw, th, tile;                 /* resized size (multiples of tile) and tile edge (448)                    */
+  const int32_t* hbounds;           /* device: slx_resample_coeffs(W, tw) tables (unused when need_h == 0)      */
+  const int32_t* hcoeffs;
+  int hksize;
+  const int32_t* vbounds;           /* device: slx_resample_coeffs(H, th) tables (unused when need_v == 0)      */
+  const int32_t* vcoeffs;
+  int vksize;
+  int need_h, need_v;               /* Pillow skips a pass (and its rounding) when that axis keeps its size     */
+  int rows_per_block, lds_rows;     /* output rows per block; max source rows any strip needs (LDS <= 64 KiB)  */
+  float mean[3], std[3];            /* Normalize constants as f32 (IMAGENET_MEAN / IMAGENET_STD)               */
+  float* out;                       /* [B][tiles][3][tile][tile] f32, tile t = row-major over the tile grid     */
+} slx_frame_desc;
+int slx_frames_to_tiles(const slx_frame_desc* d, slx_stream_t stream);
+
 /* ---- fp32 parity mode (SURVEY.md §7 hard part 2; csrc/precise.hip) ---------------------------
  * f32 twins of the bf16-only forward entry points, used by VLAEngine / BaseEngine(precise=True) to run the
  * engines' own launch sequence with f32 activations and weights, so the forward can be held to the north-star

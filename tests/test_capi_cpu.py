@@ -8,6 +8,7 @@ import pytest
 
 from simlingo_amd import kernels as K
 from simlingo_amd.decode import DecGemvDesc
+from simlingo_amd.frames import FrameDesc
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -55,7 +56,8 @@ def test_struct_layouts_match_header(tmp_path):
     structs = {"slx_gemm_desc": K.GemmDesc, "slx_attn_desc": K.AttnDesc, "slx_attn_bwd_desc": K.AttnBwdDesc,
                "slx_norm_desc": K.NormDesc, "slx_sgemm_desc": K.SgemmDesc,
                "slx_lora_down_desc": K.LoraDownDesc,
-               "slx_lora_da_desc": K.LoraDaDesc, "slx_dec_gemv_desc": DecGemvDesc}
+               "slx_lora_da_desc": K.LoraDaDesc, "slx_dec_gemv_desc": DecGemvDesc,
+               "slx_frame_desc": FrameDesc}
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "slx.h"', "int main(void){"]
     for cname, cls in structs.items():
         lines.append(f'printf("{cname} size %zu\\n", sizeof({cname}));')
