@@ -297,7 +297,8 @@ typedef struct {
   const int32_t* vcoeffs;
   int vksize;
   int need_h, need_v;               /* Pillow skips a pass (and its rounding) when that axis keeps its size     */
-  int rows_per_block, lds_rows;     /* output rows per block; max source rows any strip needs (LDS <= 64 KiB)  */
+  int rows_per_block, cols_per_block; /* output rows x columns per block                                     */
+  int lds_rows, lds_cols;           /* max source rows / columns any block reads (LDS window <= 64 KiB)        */
   float mean[3], std[3];            /* Normalize constants as f32 (IMAGENET_MEAN / IMAGENET_STD)               */
   float* out;                       /* [B][tiles][3][tile][tile] f32, tile t = row-major over the tile grid     */
 } slx_frame_desc;

@@ -12,9 +12,9 @@
 // normalisation), once per geometry. ToTensor / Normalize are the same f32 operations torchvision performs
 // (u / 255, then (x - mean) / std, IEEE division), so the tiles are bit-identical to the reference's.
 //
-// Work split: one 256-thread block per (strip of RY output rows, frame). The block first runs the horizontal
-// pass for the source rows its strip needs into LDS (uint8, [rows][tw*3]), then the vertical pass, the
-// normalisation and the scatter into the tile layout [B][blocks][3][448][448] with x fastest (coalesced f32
+// Work split: one 256-thread block per (RY output rows x CW output columns, frame): the source window it needs is
+// staged into LDS (4-byte loads for packed HWC frames), the horizontal pass writes uint8 rows to LDS, the vertical
+// pass + normalisation scatter f32 into the tile layout [B][tiles][3][448][448] with x fastest (coalesced
 // stores). Byte work, HBM-bound: 1 read of the cropped frame + 1 f32 write of the tiles.
 #include <cmath>
 
@@ -24,6 +24,7 @@
 namespace slx {
 
 static constexpr int kPrecisionBits = 32 - 8 - 2;  // Resample.c PRECISION_BITS
+static constexpr int kCW = 128;                      // output columns per block (one per thread of a row group)
 
 __device__ __forceinline__ int clip8(int in) {
   if (in >= (1 << kPrecisionBits << 8)) return 255;
@@ -34,90 +35,171 @@ __device__ __forceinline__ int clip8(int in) {
 struct FrameArgs {
   const uint8_t* src;
   long sb, sy, sx, sc;
-  int H, W, tw, th, tile, tiles_x, blocks, RY, lds_rows;
+  int H, W, tw, th, tile, tiles_x, blocks, RY, CW, lds_rows, lds_cols;
   const int* hb;
   const int* hk;
   int hks;
   const int* vb;
   const int* vk;
   int vks;
-  int need_h, need_v;
+  int need_h, need_v, packed;
   float mean[3], stdv[3];
   float* out;
 };
 
+// One 256-thread block per (RY output rows) x (CW output columns) x frame. LDS holds the source window the block
+// needs ([lds_rows][lds_cols*3] bytes, staged with 4-byte loads when the frame is packed HWC) and the horizontal
+// pass result ([lds_rows][CW*3] bytes); the vertical pass reads the latter and writes f32 tiles, x fastest.
+template <int KH, int KV>  // tap-loop bounds (>= hks / vks): unrolled with a guard so the LDS reads batch
 __global__ __launch_bounds__(256) void frames_to_tiles_kernel(FrameArgs a) {
-  extern __shared__ uint8_t rowbuf[];  // [lds_rows][tw*3]
-  const int b = blockIdx.y;
-  const int y0 = blockIdx.x * a.RY;
-  const int y1 = min(y0 + a.RY, a.th);
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const int b = blockIdx.z;
+  const int y0 = blockIdx.y * a.RY, y1 = min(y0 + a.RY, a.th);
+  const int x0 = blockIdx.x * a.CW, x1 = min(x0 + a.CW, a.tw);
+  const int ncol = x1 - x0;
   const int tid = threadIdx.x;
-  // source rows this strip reads (vertical bounds are monotone in y)
-  int ylo, yhi;
+  // source rows / columns this block reads: Pillow's first index and first+count are both non-decreasing in the
+  // output index, so the window is [first of the first output, end of the last output)
+  int ylo, yhi, xlo, xhi;
   if (a.need_v) {
     ylo = a.vb[2 * y0];
-    yhi = 0;
-    for (int y = y0; y < y1; ++y) yhi = max(yhi, a.vb[2 * y] + a.vb[2 * y + 1]);
+    yhi = a.vb[2 * (y1 - 1)] + a.vb[2 * (y1 - 1) + 1];  // window end = the last output's end (monotone)
   } else {
     ylo = y0;
     yhi = y1;
   }
-  const int nrows = yhi - ylo;  // <= lds_rows (host-checked for every strip)
-  const int row3 = a.tw * 3;
+  if (a.need_h) {
+    xlo = a.hb[2 * x0];
+    xhi = a.hb[2 * (x1 - 1)] + a.hb[2 * (x1 - 1) + 1];
+  } else {
+    xlo = x0;
+    xhi = x1;
+  }
+  const int nrows = yhi - ylo, nsc = xhi - xlo;  // <= lds_rows, lds_cols (host-checked)
+  // LDS: coefficient rows of this block's outputs (int32), then the source window, then the horizontal result
+  int* lhk = reinterpret_cast<int*>(smem);                  // [CW][hks]
+  int* lhb = lhk + a.CW * a.hks;                            // [CW][2] (first index relative to xlo, count)
+  int* lvk = lhb + 2 * a.CW;                                // [RY][vks]
+  int* lvb = lvk + a.RY * a.vks;                            // [RY][2] (first index relative to ylo, count)
+  uint8_t* sbuf = reinterpret_cast<uint8_t*>(lvb + 2 * a.RY);  // [lds_rows][lds_cols*3 + 4] source window
+  const int sld = a.lds_cols * 3 + 4;
+  uint8_t* hbuf = sbuf + a.lds_rows * sld;            // [lds_rows][CW*3] horizontal-pass result
+  const int hld = a.CW * 3;
   const uint8_t* fb = a.src + (long)b * a.sb;
-  // ---- horizontal pass (or plain copy when the width is unchanged) -> LDS ----
-  for (int i = tid; i < nrows * a.tw; i += 256) {
-    const int r = i / a.tw, xx = i - r * a.tw;
-    const uint8_t* srow = fb + (long)(ylo + r) * a.sy;
-    int s0, s1, s2;
-    if (a.need_h) {
-      const int xmin = a.hb[2 * xx], xl = a.hb[2 * xx + 1];
-      const int* k = a.hk + (long)xx * a.hks;
-      s0 = s1 = s2 = 1 << (kPrecisionBits - 1);
-      for (int x = 0; x < xl; ++x) {
-        const uint8_t* p = srow + (long)(xmin + x) * a.sx;
-        const int kx = k[x];
-        s0 += (int)p[0] * kx;
-        s1 += (int)p[a.sc] * kx;
-        s2 += (int)p[2 * a.sc] * kx;
-      }
-      s0 = clip8(s0);
-      s1 = clip8(s1);
-      s2 = clip8(s2);
-    } else {
-      const uint8_t* p = srow + (long)xx * a.sx;
-      s0 = p[0];
-      s1 = p[a.sc];
-      s2 = p[2 * a.sc];
+  if (a.need_h) {
+    for (int i = tid; i < ncol * a.hks; i += 256) lhk[i] = a.hk[(long)x0 * a.hks + i];
+    for (int i = tid; i < ncol; i += 256) {
+      lhb[2 * i] = a.hb[2 * (x0 + i)] - xlo;
+      lhb[2 * i + 1] = a.hb[2 * (x0 + i) + 1];
     }
-    uint8_t* d = rowbuf + r * row3 + xx * 3;
-    d[0] = (uint8_t)s0;
-    d[1] = (uint8_t)s1;
-    d[2] = (uint8_t)s2;
+  }
+  if (a.need_v) {
+    for (int i = tid; i < (y1 - y0) * a.vks; i += 256) lvk[i] = a.vk[(long)y0 * a.vks + i];
+    for (int i = tid; i < y1 - y0; i += 256) {
+      lvb[2 * i] = a.vb[2 * (y0 + i)] - ylo;
+      lvb[2 * i + 1] = a.vb[2 * (y0 + i) + 1];
+    }
+  }
+  // ---- stage the source window ----
+  if (a.packed) {  // HWC bytes contiguous along x: dword loads from the 4-aligned start of each row segment
+    const long bx0 = (long)xlo * 3;
+    const int lead = (int)(bx0 & 3);  // rows and frames start 4-aligned (checked on the host)
+    const int nw = (nsc * 3 + lead + 3) >> 2;
+    const long rowend = (long)a.W * 3 - bx0 + lead;  // bytes of a row from the aligned start
+    for (int i = tid; i < nrows * nw; i += 256) {
+      const int r = i / nw, wi = i - r * nw;
+      const uint8_t* rowp = fb + (long)(ylo + r) * a.sy + bx0 - lead;
+      uint32_t w;
+      if ((long)(wi + 1) * 4 <= rowend) {
+        w = *reinterpret_cast<const uint32_t*>(rowp + wi * 4);
+      } else {
+        w = 0;
+        for (int q = 0; q < 4; ++q)
+          if ((long)wi * 4 + q < rowend) w |= (uint32_t)rowp[wi * 4 + q] << (8 * q);
+      }
+      uint8_t* d = sbuf + r * sld;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int o = wi * 4 + q - lead;
+        if (o >= 0 && o < nsc * 3) d[o] = (uint8_t)(w >> (8 * q));
+      }
+    }
+  } else {
+    for (int i = tid; i < nrows * nsc * 3; i += 256) {
+      const int r = i / (nsc * 3), j = i - r * (nsc * 3);
+      const int x = j / 3, c = j - x * 3;
+      sbuf[r * sld + j] = fb[(long)(ylo + r) * a.sy + (long)(xlo + x) * a.sx + (long)c * a.sc];
+    }
   }
   __syncthreads();
+  // Each thread owns one output column xl = tid % CW for both passes (CW = 128: two row groups of 128 threads, one
+  // wave never straddles them), so its horizontal taps, tile column and store offset are computed once.
+  const int xl = tid & (kCW - 1), rg = tid / kCW;
+  const bool live = xl < ncol;
+  const int xx = x0 + xl;
+  // ---- horizontal pass (or copy when the width is unchanged) ----
+  int hx0 = xx - xlo, hn = 0, hk[KH];
+  if (a.need_h && live) {
+    hx0 = lhb[2 * xl];
+    hn = lhb[2 * xl + 1];
+#pragma unroll
+    for (int x = 0; x < KH; ++x) hk[x] = x < hn ? lhk[xl * a.hks + x] : 0;
+  }
+  if (live) {
+    for (int r = rg; r < nrows; r += 256 / kCW) {
+      const uint8_t* p = sbuf + r * sld + hx0 * 3;
+      int s0, s1, s2;
+      if (a.need_h) {
+        s0 = s1 = s2 = 1 << (kPrecisionBits - 1);
+#pragma unroll
+        for (int x = 0; x < KH; ++x) {
+          if (x < hn) {
+            s0 += (int)p[3 * x] * hk[x];
+            s1 += (int)p[3 * x + 1] * hk[x];
+            s2 += (int)p[3 * x + 2] * hk[x];
+          }
+        }
+        s0 = clip8(s0);
+        s1 = clip8(s1);
+        s2 = clip8(s2);
+      } else {
+        s0 = p[0];
+        s1 = p[1];
+        s2 = p[2];
+      }
+      uint8_t* d = hbuf + r * hld + xl * 3;
+      d[0] = (uint8_t)s0;
+      d[1] = (uint8_t)s1;
+      d[2] = (uint8_t)s2;
+    }
+  }
+  __syncthreads();
+  if (!live) return;
   // ---- vertical pass + ToTensor + Normalize + tile scatter ----
-  const int n = (y1 - y0) * 3 * a.tw;
   const long plane = (long)a.tile * a.tile;
-  for (int i = tid; i < n; i += 256) {
-    const int xx = i % a.tw;
-    const int t = i / a.tw;
-    const int c = t % 3, y = y0 + t / 3;
+  const int tx = xx / a.tile;
+  const int xin = xx - tx * a.tile;
+  float* ob = a.out + ((long)b * a.blocks + tx) * 3 * plane + xin;
+  for (int t = rg; t < (y1 - y0) * 3; t += 256 / kCW) {  // t = (row, channel), uniform across the wave
+    const int yl = t / 3, c = t - yl * 3, y = y0 + yl;
     int u;
     if (a.need_v) {
-      const int ymin = a.vb[2 * y], yl = a.vb[2 * y + 1];
-      const int* k = a.vk + (long)y * a.vks;
-      int s = 1 << (kPrecisionBits - 1);
-      const uint8_t* col = rowbuf + (ymin - ylo) * row3 + xx * 3 + c;
-      for (int j = 0; j < yl; ++j) s += (int)col[j * row3] * k[j];
-      u = clip8(s);
+      const int ymin = lvb[2 * yl], n = lvb[2 * yl + 1];
+      const int* k = lvk + yl * a.vks;
+      int sacc = 1 << (kPrecisionBits - 1);
+      const uint8_t* col = hbuf + ymin * hld + xl * 3 + c;
+#pragma unroll
+      for (int j = 0; j < KV; ++j)
+        if (j < n) sacc += (int)col[j * hld] * k[j];
+      u = clip8(sacc);
     } else {
-      u = rowbuf[(y - ylo) * row3 + xx * 3 + c];
+      u = hbuf[(y - ylo) * hld + xl * 3 + c];
     }
-    const float v = ((float)u / 255.0f - a.mean[c]) / a.stdv[c];
-    const int tx = xx / a.tile, ty = y / a.tile;
-    const long tileix = (long)b * a.blocks + ty * a.tiles_x + tx;
-    a.out[(tileix * 3 + c) * plane + (long)(y - ty * a.tile) * a.tile + (xx - tx * a.tile)] = v;
+    const float mean = c == 0 ? a.mean[0] : (c == 1 ? a.mean[1] : a.mean[2]);
+    const float sd = c == 0 ? a.stdv[0] : (c == 1 ? a.stdv[1] : a.stdv[2]);
+    const float v = ((float)u / 255.0f - mean) / sd;
+    const int ty = y / a.tile;
+    ob[((long)ty * a.tiles_x * 3 + c) * plane + (long)(y - ty * a.tile) * a.tile] = v;
   }
 }
 
@@ -198,10 +280,12 @@ int slx_frames_to_tiles(const slx_frame_desc* d, slx_stream_t stream) {
   SLX_CHECK_ARG(d->need_v || d->th == d->H, "slx_frames_to_tiles: height changes but need_v = 0");
   SLX_CHECK_ARG(!d->need_h || (d->hbounds && d->hcoeffs && d->hksize > 0), "slx_frames_to_tiles: missing horizontal coeffs");
   SLX_CHECK_ARG(!d->need_v || (d->vbounds && d->vcoeffs && d->vksize > 0), "slx_frames_to_tiles: missing vertical coeffs");
-  SLX_CHECK_ARG(d->rows_per_block > 0 && d->lds_rows > 0, "slx_frames_to_tiles: rows_per_block / lds_rows unset");
-  const size_t lds = (size_t)d->lds_rows * d->tw * 3;
-  SLX_CHECK_ARG(lds <= 64 * 1024, "slx_frames_to_tiles: strip needs %zu B of LDS (> 64 KiB): fewer rows_per_block",
-                lds);
+  SLX_CHECK_ARG(d->rows_per_block > 0 && d->cols_per_block == kCW && d->lds_rows > 0 && d->lds_cols > 0,
+                "slx_frames_to_tiles: rows_per_block, lds_rows/lds_cols must be set and cols_per_block == %d", kCW);
+  const int hks = d->need_h ? d->hksize : 0, vks = d->need_v ? d->vksize : 0;
+  const size_t lds = (size_t)4 * (d->cols_per_block * (hks + 2) + d->rows_per_block * (vks + 2)) +
+                     (size_t)d->lds_rows * (d->lds_cols * 3 + 4) + (size_t)d->lds_rows * d->cols_per_block * 3;
+  SLX_CHECK_ARG(lds <= 64 * 1024, "slx_frames_to_tiles: block window needs %zu B of LDS (> 64 KiB)", lds);
   if (d->B == 0) return 0;
   FrameArgs a;
   a.src = d->src;
@@ -209,17 +293,22 @@ int slx_frames_to_tiles(const slx_frame_desc* d, slx_stream_t stream) {
   a.H = d->H; a.W = d->W; a.tw = d->tw; a.th = d->th; a.tile = d->tile;
   a.tiles_x = d->tw / d->tile;
   a.blocks = a.tiles_x * (d->th / d->tile);
-  a.RY = d->rows_per_block; a.lds_rows = d->lds_rows;
-  a.hb = d->hbounds; a.hk = d->hcoeffs; a.hks = d->hksize;
-  a.vb = d->vbounds; a.vk = d->vcoeffs; a.vks = d->vksize;
+  a.RY = d->rows_per_block; a.CW = d->cols_per_block; a.lds_rows = d->lds_rows; a.lds_cols = d->lds_cols;
+  a.hb = d->hbounds; a.hk = d->hcoeffs; a.hks = hks;
+  a.vb = d->vbounds; a.vk = d->vcoeffs; a.vks = vks;
   a.need_h = d->need_h; a.need_v = d->need_v;
+  a.packed = d->sx == 3 && d->sc == 1 && d->sy % 4 == 0 && d->sb % 4 == 0 && ((uintptr_t)d->src & 3) == 0;
   for (int c = 0; c < 3; ++c) {
     a.mean[c] = d->mean[c];
     a.stdv[c] = d->std[c];
   }
   a.out = d->out;
-  const dim3 grid((unsigned)((d->th + a.RY - 1) / a.RY), (unsigned)d->B);
-  hipLaunchKernelGGL(frames_to_tiles_kernel, grid, dim3(256), lds, (hipStream_t)stream, a);
+  const dim3 grid((unsigned)((d->tw + a.CW - 1) / a.CW), (unsigned)((d->th + a.RY - 1) / a.RY), (unsigned)d->B);
+  SLX_CHECK_ARG(hks <= 64 && vks <= 64, "slx_frames_to_tiles: ksize > 64");
+  hipStream_t st = (hipStream_t)stream;
+  if (hks <= 8 && vks <= 8) hipLaunchKernelGGL((frames_to_tiles_kernel<8, 8>), grid, dim3(256), lds, st, a);
+  else if (hks <= 16 && vks <= 16) hipLaunchKernelGGL((frames_to_tiles_kernel<16, 16>), grid, dim3(256), lds, st, a);
+  else hipLaunchKernelGGL((frames_to_tiles_kernel<64, 64>), grid, dim3(256), lds, st, a);
   SLX_LAUNCH_CHECK("slx_frames_to_tiles");
   return 0;
 }

@@ -31,7 +31,7 @@ class FrameDesc(ctypes.Structure):  # include/slx.h slx_frame_desc
                 ("hbounds", ctypes.c_void_p), ("hcoeffs", ctypes.c_void_p), ("hksize", ctypes.c_int),
                 ("vbounds", ctypes.c_void_p), ("vcoeffs", ctypes.c_void_p), ("vksize", ctypes.c_int),
                 ("need_h", ctypes.c_int), ("need_v", ctypes.c_int), ("rows_per_block", ctypes.c_int),
-                ("lds_rows", ctypes.c_int), ("mean", ctypes.c_float * 3), ("std", ctypes.c_float * 3),
+                ("cols_per_block", ctypes.c_int), ("lds_rows", ctypes.c_int), ("lds_cols", ctypes.c_int), ("mean", ctypes.c_float * 3), ("std", ctypes.c_float * 3),
                 ("out", ctypes.c_void_p)]
 
 
@@ -75,6 +75,9 @@ def resample_coeffs(in_size: int, out_size: int):
     rc = K.lib().slx_resample_coeffs(in_size, out_size, k, bounds.ctypes.data_as(_i32p), kk.ctypes.data_as(_i32p))
     if rc != k:
         K.check(rc if rc < 0 else -1, "slx_resample_coeffs")
+    # the kernel derives each block's source window from its first and last output: both ends must be monotone
+    if not (np.all(np.diff(bounds[:, 0]) >= 0) and np.all(np.diff(bounds[:, 0] + bounds[:, 1]) >= 0)):
+        raise RuntimeError(f"resample bounds {in_size}->{out_size} are not monotone")
     return bounds, kk
 
 
@@ -86,7 +89,8 @@ class FramePreprocessor:
     bottom_crop_rows(H0) when `cut_bottom` (the dataset's `cut_bottom_quarter`)."""
 
     def __init__(self, H0: int, W0: int, device, input_size: int = 448, max_num_grid: int = 2,
-                 use_global_img: bool = False, cut_bottom: bool = True, rows_per_block: int = 8):
+                 use_global_img: bool = False, cut_bottom: bool = True, rows_per_block: int = 16,
+                 cols_per_block: int = 128):
         if use_global_img:
             raise NotImplementedError("use_global_img (thumbnail tile) is off in every simlingo config "
                                       "(datamodule.py:349 use_global_img=False)")
@@ -107,31 +111,34 @@ class FramePreprocessor:
             hb, hk = resample_coeffs(self.W, self.tw)
             self.hb, self.hk = torch.from_numpy(hb).to(dev), torch.from_numpy(hk).to(dev)
         else:
-            hb = None
+            hb = hk = None
             self.hb, self.hk = z, z
         if self.need_v:
             vb, vk = resample_coeffs(self.H, self.th)
             self.vb, self.vk = torch.from_numpy(vb).to(dev), torch.from_numpy(vk).to(dev)
         else:
-            vb = None
+            vb = vk = None
             self.vb, self.vk = z, z
-        # largest source-row span any strip of `rows_per_block` output rows reads; shrink the strip until the
-        # span fits 64 KiB of LDS
-        ry = rows_per_block
+        # block = rows_per_block x cols_per_block outputs; its source window = the largest row / column span any
+        # block reads; halve the block until window + horizontal-pass buffer fit 64 KiB of LDS
+        def span(bounds, n_out, step):
+            if bounds is None:
+                return min(step, n_out)
+            return max(int((bounds[o:o + step, 0] + bounds[o:o + step, 1]).max() - bounds[o, 0])
+                       for o in range(0, n_out, step))
+
+        ry, cw = rows_per_block, cols_per_block
         while True:
-            span = 0
-            for y0 in range(0, self.th, ry):
-                y1 = min(y0 + ry, self.th)
-                if vb is not None:
-                    span = max(span, int((vb[y0:y1, 0] + vb[y0:y1, 1]).max() - vb[y0, 0]))
-                else:
-                    span = max(span, y1 - y0)
-            if span * self.tw * 3 <= 64 * 1024 or ry == 1:
+            lr, lc = span(vb, self.th, ry), span(hb, self.tw, cw)
+            lds = lr * (lc * 3 + 4) + lr * cw * 3 + 4 * (cw * (hk.shape[1] + 2 if hb is not None else 2)
+                                                          + ry * (vk.shape[1] + 2 if vb is not None else 2))
+            if lds <= 64 * 1024 or ry == 1:
                 break
-            ry //= 2
-        if span * self.tw * 3 > 64 * 1024:
-            raise ValueError(f"frame geometry {W0}x{H0} -> {self.tw}x{self.th} needs {span} source rows per strip")
-        self.rows_per_block, self.lds_rows = ry, span
+            ry //= 2  # the kernel fixes 128 output columns per block; only the row count shrinks
+        if lds > 64 * 1024:
+            raise ValueError(f"frame geometry {W0}x{H0} -> {self.tw}x{self.th} needs {lds} B of LDS per block")
+        self.rows_per_block, self.cols_per_block, self.lds_rows, self.lds_cols = ry, cw, lr, lc
+        self._desc_cache = {}
         self.mean = [float(np.float32(m)) for m in IMAGENET_MEAN]
         self.std = [float(np.float32(s)) for s in IMAGENET_STD]
 
@@ -155,17 +162,26 @@ class FramePreprocessor:
             out = torch.empty(B, self.tiles, 3, self.tile, self.tile, dtype=torch.float32, device=self.device)
         elif out.dtype != torch.float32 or not out.is_contiguous() or out.numel() != B * self.tiles * 3 * self.tile ** 2:
             raise ValueError("out must be a contiguous f32 [B, tiles, 3, tile, tile] buffer")
-        d = FrameDesc()
-        d.src, d.sb, d.sy, d.sx, d.sc = frames.data_ptr(), sb, sy, sx, sc
-        d.B, d.H, d.W = B, self.H, self.W
-        d.tw, d.th, d.tile = self.tw, self.th, self.tile
-        d.hbounds, d.hcoeffs, d.hksize = self.hb.data_ptr(), self.hk.data_ptr(), self.hk.shape[-1] if self.need_h else 0
-        d.vbounds, d.vcoeffs, d.vksize = self.vb.data_ptr(), self.vk.data_ptr(), self.vk.shape[-1] if self.need_v else 0
-        d.need_h, d.need_v = self.need_h, self.need_v
-        d.rows_per_block, d.lds_rows = self.rows_per_block, self.lds_rows
-        d.mean[:] = self.mean
-        d.std[:] = self.std
-        d.out = out.data_ptr()
+        key = (frames.data_ptr(), sb, sy, sx, sc, B, out.data_ptr())
+        d = self._desc_cache.get(key)
+        if d is None:  # the descriptor is rebuilt only when the buffers change (steady state: ctypes call only)
+            d = FrameDesc()
+            d.src, d.sb, d.sy, d.sx, d.sc = frames.data_ptr(), sb, sy, sx, sc
+            d.B, d.H, d.W = B, self.H, self.W
+            d.tw, d.th, d.tile = self.tw, self.th, self.tile
+            d.hbounds, d.hcoeffs = self.hb.data_ptr(), self.hk.data_ptr()
+            d.hksize = self.hk.shape[-1] if self.need_h else 0
+            d.vbounds, d.vcoeffs = self.vb.data_ptr(), self.vk.data_ptr()
+            d.vksize = self.vk.shape[-1] if self.need_v else 0
+            d.need_h, d.need_v = self.need_h, self.need_v
+            d.rows_per_block, d.cols_per_block = self.rows_per_block, self.cols_per_block
+            d.lds_rows, d.lds_cols = self.lds_rows, self.lds_cols
+            d.mean[:] = self.mean
+            d.std[:] = self.std
+            d.out = out.data_ptr()
+            if len(self._desc_cache) > 16:
+                self._desc_cache.clear()
+            self._desc_cache[key] = d
         K.check(K.lib().slx_frames_to_tiles(ctypes.byref(d), K.stream_ptr()), "slx_frames_to_tiles")
         return out
 
