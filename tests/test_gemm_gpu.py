@@ -185,6 +185,26 @@ def test_gemm_v3_m_tail_peel_epilogues(dev, variant):
     torch.testing.assert_close(dx.float(), xx.grad, atol=5e-2, rtol=2e-2)
 
 
+def test_gemm_v3_overlapped_last_tile(dev):
+    """Write-once epilogues run the partial last M tile of v3 shifted to end at M (rows shared with the previous
+    tile are recomputed): the shared rows must be bit-identical to a launch without a remainder, the tail rows
+    correct; an accumulating launch (C += ...) still takes the peel path and must not double-add."""
+    M, N, Kd = 528, 512, 256
+    g = torch.Generator(device=dev).manual_seed(33)
+    x = torch.randn(M, Kd, device=dev, generator=g).bfloat16()
+    w = (torch.randn(N, Kd, device=dev, generator=g) * 0.1).bfloat16()
+    full = torch.empty(M, N, device=dev)
+    K.gemm(x, w, full, M, N, Kd, K.GEMM_NT, Kd, Kd, N, variant=7, ksplit_max=-1)
+    head = torch.empty(512, N, device=dev)
+    K.gemm(x, w, head, 512, N, Kd, K.GEMM_NT, Kd, Kd, N, variant=7, ksplit_max=-1)
+    torch.cuda.synchronize()
+    assert torch.equal(full[:512], head)
+    torch.testing.assert_close(full, x.float() @ w.float().t(), atol=2e-3, rtol=2e-3)
+    acc = torch.ones(M, N, device=dev)
+    K.gemm(x, w, acc, M, N, Kd, K.GEMM_NT, Kd, Kd, N, variant=7, ksplit_max=-1, accumulate=True)
+    torch.testing.assert_close(acc, 1.0 + x.float() @ w.float().t(), atol=2e-3, rtol=2e-3)
+
+
 @pytest.mark.parametrize("p", [0.0, 0.1])
 def test_gemm_dropmask_swiglu_epilogue(dev, p):
     """EPI_DROPMASK_SWIGLU: dgu = SwiGLU'(gu) applied to (resid + keep * dT.A): the Qwen2 down-projection LoRA
