@@ -82,7 +82,7 @@ def cpu_baseline_vla(cfg, s_text, n_loss, threads):
     from simlingo_amd.params import init_params
     from simlingo_amd.synthetic import make_batch
     torch.set_num_threads(threads)
-    P = init_params(cfg, seed=0)
+    P = init_params(cfg, seed=0, lora_b_std=0.02)
     ex = make_batch(cfg, B=1, s_text=s_text, n_loss=n_loss, seed=1234)
     t0 = time.perf_counter()
     O.loss_and_grads(P, cfg, ex)
@@ -116,7 +116,7 @@ def setup_vla(args, dev, world, rank):
     B = args.batch or (8 if full else 4)
     s_text = args.s_text if full else 24
     n_loss = args.n_loss if full else 6
-    eng = VLAEngine(cfg, dev, init_params(cfg, seed=0, device=dev))
+    eng = VLAEngine(cfg, dev, init_params(cfg, seed=0, lora_b_std=0.02, device=dev))
     ex = make_batch(cfg, B=B, s_text=s_text, n_loss=n_loss, seed=1000 + rank)
     plan = plan_from_example(cfg, ex)
     dplan = plan.to_device(dev)

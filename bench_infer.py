@@ -41,7 +41,7 @@ def main():
 
     dev = torch.device("cuda", 0)
     cfg = full_config()
-    eng = VLAEngine(cfg, dev, init_params(cfg, seed=0, device=dev))
+    eng = VLAEngine(cfg, dev, init_params(cfg, seed=0, lora_b_std=0.02, device=dev))
     dec = GreedyDecoder(eng, max_len=1024, max_new_tokens=args.new_tokens, eos_id=cfg.eos_id)
     ex = make_batch(cfg, B=1, s_text=args.s_text, n_loss=1, seed=7)
     pix = ex.driving_input.camera_images.to(dev)

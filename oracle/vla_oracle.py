@@ -90,13 +90,17 @@ def apply_rope(x, cos, sin):  # x [B, H, S, 64]
     return x * cos + rot * sin
 
 
-def lora(P, cfg, i, site, x):
+def lora(P, cfg, i, site, x, masks=None):
+    """peft LoRA: scale * B(A(dropout(x))). masks: optional {(layer, site): keep-scale [B*S, in]} — the
+    dropout masks the engine applied (simlingo_amd.dropmask.lora_masks), so a dropout-on step can be checked."""
     if not cfg.lora:
         return 0.0
+    if masks is not None:
+        x = x * torch.as_tensor(masks[(i, site)]).view(x.shape)
     return (x @ P[f"llm.{i}.lora.{site}.a"].t()) @ P[f"llm.{i}.lora.{site}.b"].t() * cfg.lora_scale
 
 
-def llm_forward(P, cfg, x, mask):
+def llm_forward(P, cfg, x, mask, masks=None):
     """x [B, S, d] inputs_embeds, mask [B, S] bool (valid) -> (post-norm features, logits)."""
     B, S, d = x.shape
     H, Hk, Fd = cfg.llm_heads, cfg.llm_kv_heads, cfg.llm_ffn
@@ -108,23 +112,23 @@ def llm_forward(P, cfg, x, mask):
         h = rms(x, g("ln1"), cfg.rms_eps)
         qkv = h @ g("qkv_w").t() + g("qkv_b")
         q, k, v = qkv.split([H * 64, Hk * 64, Hk * 64], -1)
-        q = q + lora(P, cfg, i, "q", h)
-        k = k + lora(P, cfg, i, "k", h)
-        v = v + lora(P, cfg, i, "v", h)
+        q = q + lora(P, cfg, i, "q", h, masks)
+        k = k + lora(P, cfg, i, "k", h, masks)
+        v = v + lora(P, cfg, i, "v", h, masks)
         q = apply_rope(q.view(B, S, H, 64).transpose(1, 2), cos, sin)
         k = apply_rope(k.view(B, S, Hk, 64).transpose(1, 2), cos, sin).repeat_interleave(H // Hk, 1)
         v = v.view(B, S, Hk, 64).transpose(1, 2).repeat_interleave(H // Hk, 1)
         s = (q @ k.transpose(-1, -2)) / 8.0
         s = s.masked_fill(~allowed[:, None], float("-inf"))
         a = (torch.softmax(s, -1) @ v).transpose(1, 2).reshape(B, S, H * 64)
-        x = x + a @ g("o_w").t() + lora(P, cfg, i, "o", a)
+        x = x + a @ g("o_w").t() + lora(P, cfg, i, "o", a, masks)
         h = rms(x, g("ln2"), cfg.rms_eps)
         gu = h @ g("gate_up_w").t()
         gate, up = gu.split([Fd, Fd], -1)
-        gate = gate + lora(P, cfg, i, "gate", h)
-        up = up + lora(P, cfg, i, "up", h)
+        gate = gate + lora(P, cfg, i, "gate", h, masks)
+        up = up + lora(P, cfg, i, "up", h, masks)
         act = F.silu(gate) * up
-        x = x + act @ g("down_w").t() + lora(P, cfg, i, "down", act)
+        x = x + act @ g("down_w").t() + lora(P, cfg, i, "down", act, masks)
     feat = rms(x, P["llm.norm"], cfg.rms_eps)
     return feat, feat @ P["llm.lm_head"].t()
 
@@ -187,14 +191,14 @@ def smooth_l1_sum(pred, label):
     return F.smooth_l1_loss(pred, label, reduction="none").sum(-1)
 
 
-def forward_loss(P, cfg, example):
+def forward_loss(P, cfg, example, dropout_masks=None):
     """DrivingModel.forward_loss (driving.py:236-261) -> dict of scalar losses and predictions."""
     di = example.driving_input
     pix = di.camera_images
     Bn, T_, NP, C, H, W = pix.shape
     vit = extract_feature(P, cfg, pix.reshape(Bn * NP, C, H, W))
     inputs, mask, perm = assemble(P, cfg, example, vit)
-    feat, logits = llm_forward(P, cfg, inputs, mask)
+    feat, logits = llm_forward(P, cfg, inputs, mask, dropout_masks)
     # split_outputs_by_adaptor (adaptors.py:357-370)
     inv = perm.argsort(-1)
     ar = torch.arange(feat.shape[0])[:, None]
@@ -311,14 +315,14 @@ def trainable_names(cfg, P):
     return [s.name for s in param_specs(cfg) if s.trainable and s.name in P]
 
 
-def loss_and_grads(P, cfg, example):
+def loss_and_grads(P, cfg, example, dropout_masks=None):
     """fp32 forward + autograd backward; returns (outputs, {name: grad})."""
     Pg = {k: (v.detach().clone().requires_grad_(True)) for k, v in P.items()}
     names = trainable_names(cfg, Pg)
     for k in Pg:
         if k not in names:
             Pg[k].requires_grad_(False)
-    out = forward_loss(Pg, cfg, example)
+    out = forward_loss(Pg, cfg, example, dropout_masks)
     out["loss"].backward()
     grads = {k: Pg[k].grad.detach().clone() if Pg[k].grad is not None else torch.zeros_like(Pg[k]) for k in names}
     return {k: (v.detach() if torch.is_tensor(v) else v) for k, v in out.items()}, grads

@@ -18,6 +18,8 @@
 // stores). Byte work, HBM-bound: 1 read of the cropped frame + 1 f32 write of the tiles.
 #include <cmath>
 
+#include <vector>
+
 #include "common.h"
 #include "../../include/slx.h"
 
@@ -75,7 +77,21 @@ __global__ __launch_bounds__(256) void frames_to_tiles_kernel(FrameArgs a) {
     xlo = x0;
     xhi = x1;
   }
-  const int nrows = yhi - ylo, nsc = xhi - xlo;  // <= lds_rows, lds_cols (host-checked)
+  const int nrows = yhi - ylo, nsc = xhi - xlo;  // <= lds_rows, lds_cols: host-checked against Pillow's bounds
+  if (nrows > a.lds_rows || nsc > a.lds_cols) {
+    // caller-supplied bounds need a wider window than the LDS was sized for: never stage past the buffers; the
+    // block's outputs become NaN so the failure is loud (slx_frames_to_tiles already rejects Pillow geometries
+    // whose window exceeds lds_rows / lds_cols, so only inconsistent custom tables reach this)
+    const int yl0 = y0, xl0 = x0;
+    const long plane = (long)a.tile * a.tile;
+    for (int i = tid; i < (y1 - y0) * ncol * 3; i += 256) {
+      const int yy = yl0 + i / (ncol * 3), rem = i % (ncol * 3), xx = xl0 + rem / 3, c = rem % 3;
+      const int tx = xx / a.tile, ty = yy / a.tile;
+      a.out[((long)b * a.blocks + (long)ty * a.tiles_x + tx) * 3 * plane + (long)c * plane +
+            (long)(yy - ty * a.tile) * a.tile + (xx - tx * a.tile)] = __builtin_nanf("");
+    }
+    return;
+  }
   // LDS: coefficient rows of this block's outputs (int32), then the source window, then the horizontal result
   int* lhk = reinterpret_cast<int*>(smem);                  // [CW][hks]
   int* lhb = lhk + a.CW * a.hks;                            // [CW][2] (first index relative to xlo, count)
@@ -270,6 +286,22 @@ int slx_resample_coeffs(int in_size, int out_size, int kmax, int32_t* bounds, in
   return ksize;
 }
 
+// Largest source span any block of `per_block` consecutive outputs reads, from Pillow's bounds recomputed on the
+// host (the same precompute_coeffs the caller's tables come from); per_block outputs if the size is unchanged.
+static int max_block_window(int in_size, int out_size, int per_block, int need) {
+  if (!need) return per_block < out_size ? per_block : out_size;
+  const int ks = slx_resample_ksize(in_size, out_size);
+  std::vector<int32_t> bnd(2 * (size_t)out_size), kk((size_t)out_size * ks);
+  if (slx_resample_coeffs(in_size, out_size, ks, bnd.data(), kk.data()) < 0) return -1;
+  int mx = 0;
+  for (int o0 = 0; o0 < out_size; o0 += per_block) {
+    const int o1 = (o0 + per_block < out_size ? o0 + per_block : out_size) - 1;
+    const int span = bnd[2 * o1] + bnd[2 * o1 + 1] - bnd[2 * o0];
+    mx = span > mx ? span : mx;
+  }
+  return mx;
+}
+
 int slx_frames_to_tiles(const slx_frame_desc* d, slx_stream_t stream) {
   SLX_CHECK_ARG(d != nullptr && d->src != nullptr && d->out != nullptr, "slx_frames_to_tiles: null pointer");
   SLX_CHECK_ARG(d->B >= 0 && d->H > 0 && d->W > 0 && d->tw > 0 && d->th > 0 && d->tile > 0,
@@ -286,6 +318,13 @@ int slx_frames_to_tiles(const slx_frame_desc* d, slx_stream_t stream) {
   const size_t lds = (size_t)4 * (d->cols_per_block * (hks + 2) + d->rows_per_block * (vks + 2)) +
                      (size_t)d->lds_rows * (d->lds_cols * 3 + 4) + (size_t)d->lds_rows * d->cols_per_block * 3;
   SLX_CHECK_ARG(lds <= 64 * 1024, "slx_frames_to_tiles: block window needs %zu B of LDS (> 64 KiB)", lds);
+  {
+    const int wr = max_block_window(d->H, d->th, d->rows_per_block, d->need_v);
+    const int wc = max_block_window(d->W, d->tw, d->cols_per_block, d->need_h);
+    SLX_CHECK_ARG(wr > 0 && wc > 0 && wr <= d->lds_rows && wc <= d->lds_cols,
+                  "slx_frames_to_tiles: blocks of %dx%d outputs read %dx%d source pixels but the LDS window is %dx%d",
+                  d->rows_per_block, d->cols_per_block, wr, wc, d->lds_rows, d->lds_cols);
+  }
   if (d->B == 0) return 0;
   FrameArgs a;
   a.src = d->src;

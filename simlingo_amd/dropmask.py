@@ -29,3 +29,21 @@ def keep_scale(seed: int, rows: int, cols: int, ldmask: int, p: float) -> np.nda
     """[rows, cols] float32: 1/(1-p) where kept, 0 where dropped (index = row*ldmask + col)."""
     idx = np.arange(rows, dtype=np.uint64)[:, None] * np.uint64(ldmask) + np.arange(cols, dtype=np.uint64)[None, :]
     return np.where(uniform01(seed, idx) >= p, 1.0 / (1.0 - p), 0.0).astype(np.float32)
+
+
+def lora_site_seed(step_seed: int, layer: int, site_index: int) -> int:
+    """Seed of the LoRA dropout mask of one (layer, site) in one training step (engine._lora_down)."""
+    return step_seed * 1000003 + 131 * layer + 7 * site_index + 1
+
+
+def lora_masks(cfg, rows: int, step_seed: int) -> dict:
+    """{(layer, site): [rows, in_features] float32 keep-scale} — exactly the masks the engine's forward with
+    this step_seed applies (rows = flat B*S LLM rows in the permuted order). Test helper for the oracle."""
+    from .params import LORA_SITES, lora_io
+    p = cfg.lora_dropout
+    out = {}
+    for i in range(cfg.llm_layers):
+        for j, site in enumerate(LORA_SITES):
+            kin = lora_io(cfg, site)[0]
+            out[(i, site)] = keep_scale(lora_site_seed(step_seed, i, j), rows, kin, kin, p)
+    return out

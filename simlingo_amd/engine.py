@@ -25,6 +25,7 @@ import torch
 from . import kernels as K
 from .config import VLAConfig
 from .ddp import GradBucketer
+from .dropmask import lora_site_seed
 from .engine_ops import EngineOps
 from .params import LORA_SITES, lora_io, param_specs
 from .plan import Plan
@@ -196,7 +197,7 @@ class VLAEngine(EngineOps):
         sv = {}
         B = plan.B
         self.step_seed += 1
-        sv["seed"] = self.step_seed * 1000003
+        sv["step_seed"] = self.step_seed
         sv["drop"] = cfg.lora_dropout if (training and cfg.lora) else 0.0
         X = self.encode_inputs(pix, plan, dplan, sv)
         S, d = plan.S, cfg.llm_dim
@@ -249,7 +250,8 @@ class VLAEngine(EngineOps):
                                   lora=L))
             X = Xo
         sv["llm"] = llm_saved
-        feat, nf = self._norm(X, self.P["llm.norm"], None, Ml, d, cfg.rms_eps, rms=True)
+        # final RMSNorm kept in f32: the driving heads read it unrounded (only the LM-head rows are cast to bf16)
+        feat, nf = self._norm(X, self.P["llm.norm"], None, Ml, d, cfg.rms_eps, rms=True, out=self._e(Ml, d, dtype=F32))
         sv.update(X_last=X, feat=feat, nf=nf)
         # ---------------- language loss rows ----------------
         R = plan.loss_pos.shape[0]
@@ -382,7 +384,7 @@ class VLAEngine(EngineOps):
         """t_out[:, 32j:32j+32] = drop_j(x) A_j^T for the sites sharing x (bf16, written into the extra columns of
         the activation buffer), one launch. Dropout is applied while loading x (hash mask, regenerated in
         backward). Returns {site: seed}."""
-        seeds = {site: sv["seed"] + 131 * i + 7 * LORA_SITES.index(site) + 1 for site in sites}
+        seeds = {site: lora_site_seed(sv["step_seed"], i, LORA_SITES.index(site)) for site in sites}
         if self.precise:  # parity mode runs the eval forward: dropout off, t = x A^T as f32 GEMMs
             if sv["drop"] > 0:
                 raise RuntimeError("fp32 parity mode runs the eval forward (LoRA dropout off): forward(training=False)")

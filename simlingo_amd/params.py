@@ -100,7 +100,7 @@ def param_specs(cfg: VLAConfig) -> list[PSpec]:
     return out
 
 
-def init_params(cfg: VLAConfig, seed: int = 0, lora_b_std: float = 0.02, std: float = 0.02,
+def init_params(cfg: VLAConfig, seed: int = 0, lora_b_std: float = 0.0, std: float = 0.02,
                 device="cpu") -> dict[str, torch.Tensor]:
     """Seeded fp32 CPU initialisation. Weights N(0, std) (HF default initializer_range 0.02), biases 0,
     norms 1, layer scale ls_init (InternViT), queries 0.02*randn (adaptors.py:112,129),

@@ -63,3 +63,21 @@ def test_grid_and_crop_host_logic():
         for mx in (1, 2, 4, 6, 12):
             assert F.closest_grid(W, H, 1, mx) == O.closest_grid(W, H, 1, mx), (W, H, mx)
     assert F.closest_grid(1024, 359, 1, 2) == (2, 1)
+
+
+def test_capi_frames_rejects_undersized_lds_window():
+    """a C-ABI caller that passes an LDS window smaller than the blocks' Pillow source span is rejected
+    before any launch (no GPU needed: the argument check runs on the host)."""
+    import ctypes
+    from simlingo_amd import kernels as K
+    d = F.FrameDesc()
+    d.src, d.out, d.hbounds, d.hcoeffs, d.vbounds, d.vcoeffs = 16, 16, 16, 16, 16, 16  # never dereferenced
+    d.B, d.H, d.W, d.tw, d.th, d.tile = 1, 359, 1024, 896, 448, 448
+    d.sb, d.sy, d.sx, d.sc = 359 * 1024 * 3, 1024 * 3, 3, 1
+    d.hksize, d.vksize = 5, 7
+    d.need_h, d.need_v = 1, 1
+    d.rows_per_block, d.cols_per_block = 16, 128
+    d.lds_rows, d.lds_cols = 4, 40   # far below the real span (about 15 rows x 147 columns)
+    rc = K.lib().slx_frames_to_tiles(ctypes.byref(d), None)
+    assert rc != 0
+    assert b"LDS window" in K.lib().slx_last_error()

@@ -1,9 +1,10 @@
 """Full VLA training step on the MI355X (HIP engine, bf16 MFMA) vs the CPU fp32 oracle.
 
-Tolerances (bf16 operands, f32 accumulation, 2+2 tiny layers): losses rel 3e-2; waypoint predictions
-(cumsum of 20 / 10 head outputs, so per-point bf16 error accumulates) max |diff| <= 0.1 m and mean
-|diff| <= 0.02 m; every trainable gradient cosine >= 0.98 and relative L2 error <= 0.2.
-(The north-star 1e-4 m waypoint bound needs an fp32 mode of the kernels: SURVEY.md §7 hard part 2.)
+Tolerances (bf16 operands, f32 accumulation, 2+2 tiny layers, weights N(0, 0.05)) = SURVEY.md §8d's bf16
+gate: losses rel <= 1e-2; waypoint predictions (cumsum of 20 / 10 head outputs) max |diff| <= 5e-2 m; every
+trainable gradient cosine >= 0.98 and relative L2 error <= 0.2 (tiny widths: a 128-wide bf16 dot product
+carries relatively more rounding than the real 896/1024 widths, which tests/test_fullgeom_parity_gpu.py holds to
+cosine >= 0.99 / rel <= 0.1). The north-star 1e-4 m bound is held by the fp32 parity mode below.
 """
 import numpy as np
 import pytest
@@ -35,10 +36,10 @@ def test_engine_vs_oracle(dev, case):
     ref, grads = O.loss_and_grads(P, cfg, ex)
     eng, out4, rp, sp = run_engine(cfg, P, ex, dev)
     want = [ref["loss"].item(), ref["language_loss"].item(), ref["route_loss"].item(), ref["speed_wps_loss"].item()]
-    np.testing.assert_allclose(out4.numpy(), want, rtol=3e-2, atol=1e-3)
-    for got, w in ((rp, ref["route_pred"]), (sp, ref["speed_pred"])):
-        diff = (got - w).abs()
-        assert diff.max().item() <= 0.1 and diff.mean().item() <= 0.02, (diff.max().item(), diff.mean().item())
+    dr, ds = (rp - ref["route_pred"]).abs().max().item(), (sp - ref["speed_pred"]).abs().max().item()
+    print(f"[{case}] loss {out4.tolist()} vs {want}; route max {dr:.4g} speed max {ds:.4g}")
+    np.testing.assert_allclose(out4.numpy(), want, rtol=1e-2, atol=1e-4)
+    assert dr <= 5e-2 and ds <= 5e-2, (dr, ds)
     bad = []
     for name, g in grads.items():
         e = eng.G[name].detach().float().cpu().reshape(-1)

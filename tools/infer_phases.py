@@ -13,7 +13,7 @@ from simlingo_amd.params import init_params  # noqa: E402
 
 dev = torch.device("cuda", 0)
 cfg = full_config()
-eng = VLAEngine(cfg, dev, init_params(cfg, seed=0, device=dev))
+eng = VLAEngine(cfg, dev, init_params(cfg, seed=0, lora_b_std=0.02, device=dev))
 dec = GreedyDecoder(eng, max_len=1024, max_new_tokens=int(os.environ.get("NEW", "100")), eos_id=-7)
 prefix = torch.randn(576, cfg.llm_dim, device=dev) * 0.02
 for it in range(3):
