@@ -68,6 +68,14 @@ typedef struct slx_gemm_desc {
   int variant;      /* 0 = automatic main-loop choice (tuning/testing hook; see gemm.hip)         */
   int drop_operand; /* 0 none; 1/2: LoRA dropout applied to A/B while loading, mask index =
                        storage_row*ldmask + storage_col, hash of slx_dropout (seed, drop_p)      */
+  float* colsum;    /* optional [N] f32: += column sums of the epilogue's f32 output (the bias gradient
+                       of the layer whose output gradient this GEMM produces, e.g. fc1.b from the
+                       GELU_BWD dgrad); STORE (no split-K) / GELU_BWD / QGELU_BWD, N % 8 == 0        */
+  float* colsum_ws; /* required with colsum: [ceil(M/64), N] f32 partials (one row per 64-row subtile,
+                       plain stores, then one small reduce launch: no same-address atomics)          */
+  float* rem_ws; int64_t rem_ws_floats; /* optional scratch for the M % 256 remainder rows (<= 64 of them):
+                       split-K f32 partials [splits][rem][N], then one epilogue pass; without it (or if
+                       it is too small) the remainder runs as a latency-bound 16..64-row tile           */
 } slx_gemm_desc;
 int slx_gemm_bf16(const slx_gemm_desc* d, slx_stream_t stream);
 
@@ -116,6 +124,8 @@ typedef struct slx_norm_desc {
   int64_t rows; int D; float eps;
   int pixel_shuffle_grid; int tokens_per_image;
   int y_f32;                  /* 1: y rows are f32 (ldy in floats) instead of bf16               */
+  void* dx_bf16; int64_t lddx_bf16; /* bwd, optional: bf16 copy of the (accumulated) dx rows, written
+                                       in the same pass (the next dgrad GEMM's operand; no cast kernel) */
 } slx_norm_desc;
 int slx_norm_fwd(const slx_norm_desc* d, slx_stream_t stream);
 int slx_norm_bwd(const slx_norm_desc* d, const float* dy, int64_t lddy, float* dx, int64_t lddx,

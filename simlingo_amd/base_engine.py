@@ -283,17 +283,16 @@ class BaseEngine(EngineOps):
             K.call("slx_scatter_rows", K.P(dx), d, K.P(pos), B * npts, d, K.P(dfeat), d, 1, K.stream_ptr())
         self._group_done("heads")
         dX = self._z(Ml + 1, d)
+        dxb = self._e(Ml, d)  # bf16 copy of dX written by every norm backward that updates dX
         K.norm_bwd(sv["nf"], dfeat, dX, dgamma=self.G["llm.norm"], param_accumulate=True,
-                   ws=self._ws(K.norm_ws_floats(d)))
+                   ws=self._ws(K.norm_ws_floats(d)), dx_bf16=dxb)
         # ---- Llama (all weights trainable) ----
         Hh, Fl = cfg.llm_heads, cfg.llm_ffn
         cos, sin = self.rope_tables(S)
         ws = K.attn_ws(B, S, Hh, Hh, self.device, rope=True)
-        dxb = self._e(Ml, d)
         for i in reversed(range(cfg.llm_layers)):
             p = f"llm.{i}."
             L = sv["llm"][i]
-            K.call("slx_cast_rows", K.P(dX), d, K.P(dxb), d, Ml, d, K.stream_ptr())
             K.mm(dxb, L["act"], self.G[p + "down_w"], ta=True, tb=False, accumulate=True)
             dgu = self._e(Ml, 2 * Fl)
             K.gemm(dxb, self.W[p + "down_w"], dgu, Ml, Fl, d, K.GEMM_NN, d, Fl, 2 * Fl, epi=K.EPI_SWIGLU_BWD,
@@ -303,8 +302,7 @@ class BaseEngine(EngineOps):
             K.mm(dgu, self.W[p + "gate_up_w"], dh2, tb=False)
             del dgu
             K.norm_bwd(L["n2"], dh2, dX, dx_accumulate=True, dgamma=self.G[p + "ln2"], param_accumulate=True,
-                       ws=self._ws(K.norm_ws_floats(d)))
-            K.call("slx_cast_rows", K.P(dX), d, K.P(dxb), d, Ml, d, K.stream_ptr())
+                       ws=self._ws(K.norm_ws_floats(d)), dx_bf16=dxb)
             K.mm(dxb, L["o"], self.G[p + "o_w"], ta=True, tb=False, accumulate=True)
             do = self._e(Ml, d)
             K.mm(dxb, self.W[p + "o_w"], do, tb=False)
@@ -316,7 +314,7 @@ class BaseEngine(EngineOps):
             dh = self._e(Ml, d, dtype=F32)
             K.mm(dqkv, self.W[p + "qkv_w"], dh, tb=False)
             K.norm_bwd(L["n1"], dh, dX, dx_accumulate=True, dgamma=self.G[p + "ln1"], param_accumulate=True,
-                       ws=self._ws(K.norm_ws_floats(d)))
+                       ws=self._ws(K.norm_ws_floats(d)), dx_bf16=dxb)
             del dqkv, dh, dh2, do
             self._group_done(f"llm{i}")
         # ---- assembly backward: queries, speed / target-point encoders ----
@@ -355,10 +353,10 @@ class BaseEngine(EngineOps):
         K.mm(dp2, sv["p1"], self.G["mm.fc2.w"], ta=True, tb=False, accumulate=True)
         self._colsum(dp2, self.G["mm.fc2.b"], 0)
         dp1 = self._e(Mf, Pd)
-        K.mm(dp2, self.W["mm.fc2.w"], dp1, tb=False, epi=K.EPI_GELU_BWD, aux=sv["p1pre"], ldaux=Pd)
+        K.mm(dp2, self.W["mm.fc2.w"], dp1, tb=False, epi=K.EPI_GELU_BWD, aux=sv["p1pre"], ldaux=Pd,
+             colsum=self.G["mm.fc1.b"])
         del dp2
         K.mm(dp1, sv["feat"], self.G["mm.fc1.w"], ta=True, tb=False, accumulate=True)
-        self._colsum(dp1, self.G["mm.fc1.b"], 0)
         dfeatv = self._e(Mf, D, dtype=F32)
         K.mm(dp1, self.W["mm.fc1.w"], dfeatv, tb=False)
         del dp1
@@ -379,9 +377,9 @@ class BaseEngine(EngineOps):
                    K.P(self.G[p + "fc2.b"]), 1, K.P(None), K.stream_ptr())
             K.mm(gb, L["hact"], self.G[p + "fc2.w"], ta=True, tb=False, accumulate=True)
             dh = self._e(Mv, F_)
-            K.mm(gb, self.W[p + "fc2.w"], dh, tb=False, epi=K.EPI_QGELU_BWD, aux=L["hpre"], ldaux=F_)
+            K.mm(gb, self.W[p + "fc2.w"], dh, tb=False, epi=K.EPI_QGELU_BWD, aux=L["hpre"], ldaux=F_,
+                 colsum=self.G[p + "fc1.b"])
             K.mm(dh, L["h2"], self.G[p + "fc1.w"], ta=True, tb=False, accumulate=True)
-            self._colsum(dh, self.G[p + "fc1.b"], 0)
             dh2 = self._e(Mv, D, dtype=F32)
             K.mm(dh, self.W[p + "fc1.w"], dh2, tb=False)
             del dh

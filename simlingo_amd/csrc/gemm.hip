@@ -64,6 +64,10 @@ struct GemmArgs {
   int vec_ok;        // 16-B aligned rows for C / aux / resid -> vectorised epilogue
   int drop_operand;  // 0 none, 1 = dropout on A while loading, 2 = on B (v1 main loop only)
   int mshift_last;   // v3: the last M tile starts at M - 256 (overlaps its neighbour; idempotent epilogues only)
+  float* colsum;     // optional [N]: += column sums of the f32 epilogue output (vector epilogue path only)
+  float* colsum_ws;  // [ceil(M/64) + colsum_row0][N] partials, one row per 64-row output subtile
+  int colsum_row0;   // subtile-row offset of this launch (the M-remainder launch continues the main grid's rows)
+  long split_stride; // split-K: 0 = f32 atomics into C; > 0 = split y stores its partial to C + y * split_stride
 };
 
 // Dropout applied while loading an operand (LoRA dropout, regenerated bit-exactly in backward):
@@ -520,6 +524,14 @@ __device__ __forceinline__ void epilogue_tile64(const GemmArgs& p, OutT* __restr
       const int n1 = n_base + lane;
       const float bv = (p.bias && blockIdx.y == 0 && n1 < p.N) ? p.bias[n1] : 0.f;
       float* Cf = reinterpret_cast<float*>(C);
+      if (p.split_stride) {  // partials mode: plain stores, summed by the caller's next kernel
+        float* Cy = Cf + (long)blockIdx.y * p.split_stride;
+        for (int row = 0; row < 64; ++row) {
+          const int m = m_base + row;
+          if (m < p.M && n1 < p.N) Cy[(long)m * p.ldc + n1] = ep[row * EP_LD + lane] * p.alpha + bv;
+        }
+        return;
+      }
       for (int row = 0; row < 64; ++row) {
         const int m = m_base + row;
         if (m < p.M && n1 < p.N) atomicAdd(Cf + (long)m * p.ldc + n1, ep[row * EP_LD + lane] * p.alpha + bv);
@@ -530,6 +542,7 @@ __device__ __forceinline__ void epilogue_tile64(const GemmArgs& p, OutT* __restr
   const int cc = (lane & 7) * 8;
   const int n = n_base + cc;
   const bool vec_ok = p.vec_ok && n + 8 <= p.N;
+  float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll 2
   for (int pass = 0; pass < 8; ++pass) {
     const int row = pass * 8 + (lane >> 3);
@@ -541,10 +554,30 @@ __device__ __forceinline__ void epilogue_tile64(const GemmArgs& p, OutT* __restr
     v[0] = a0.x; v[1] = a0.y; v[2] = a0.z; v[3] = a0.w; v[4] = a1.x; v[5] = a1.y; v[6] = a1.z; v[7] = a1.w;
     if (vec_ok) {
       epilogue_vec8<EPI, OutT>(p, C, m, n, v);
+      if constexpr (EPI == EPI_STORE || EPI == EPI_GELU_BWD || EPI == EPI_QGELU_BWD) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) cs[e] += v[e];
+      }
     } else {
 #pragma unroll
       for (int e = 0; e < 8; ++e)
         if (n + e < p.N) epilogue_elem<EPI, OutT>(p, C, m, n + e, v[e]);
+    }
+  }
+  if constexpr (EPI == EPI_STORE || EPI == EPI_GELU_BWD || EPI == EPI_QGELU_BWD) {
+    // bias gradient: the 8 lanes sharing columns (lane & 7) hold partials of 8 rows each -> 3 xor-shuffles
+    if (p.colsum) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        cs[e] += __shfl_xor(cs[e], 8, 64);
+        cs[e] += __shfl_xor(cs[e], 16, 64);
+        cs[e] += __shfl_xor(cs[e], 32, 64);
+      }
+      if (lane < 8 && vec_ok && m_base < p.M) {  // partial row of this 64-row subtile (reduced after the GEMM)
+        float* w = p.colsum_ws + (long)(p.colsum_row0 + m_base / 64) * p.N + n;
+        *reinterpret_cast<float4*>(w) = make_float4(cs[0], cs[1], cs[2], cs[3]);
+        *reinterpret_cast<float4*>(w + 4) = make_float4(cs[4], cs[5], cs[6], cs[7]);
+      }
     }
   }
 }
@@ -939,7 +972,7 @@ static int split_for(const slx_gemm_desc* d, int v, int M, int batch) {
   const int ksteps = (d->K + BK - 1) / BK;
   const int slots = v_slots(v);
   if (!(d->epilogue == SLX_EPI_STORE && d->out_f32 && batch == 1 && tiles <= slots / 2 && ksteps >= 8)) return 1;
-  if (d->ksplit_max < 0) return 1;
+  if (d->ksplit_max < 0 || d->colsum) return 1;
   int sp = slots / tiles;  // floor: never more blocks than one round holds
   sp = sp < ksteps / 4 ? sp : ksteps / 4;
   if (v == 7 && sp > 4) sp = 4;  // beyond 4 the f32 atomic traffic (sp x M x N x 4 B) dominates
@@ -963,8 +996,70 @@ static double v_cost(const slx_gemm_desc* d, int v, int M, int batch) {
   return t;
 }
 
-static int gemm_launch(const slx_gemm_desc* d, int v, hipStream_t st, int mshift_last = 0) {
+// ---- M remainder (rows past the last whole 256-row tile, e.g. InternViT's 16 class-token rows of 16400) ----
+// Instead of a 16-row tile walking the whole K on a few CUs (latency-bound, 15-85 us), the remainder is a split-K
+// GEMM over ~all CUs writing f32 partials (plain stores, split-major), then one kernel that sums the splits and runs
+// the real epilogue on the rem x N accumulators. One thread per output column walks the rem rows, so the colsum
+// partial row of these rows comes out of the same pass.
+template <int EPI, typename OutT>
+__global__ __launch_bounds__(256) void rows_epilogue_kernel(GemmArgs p, const float* __restrict__ part, int nsplit,
+                                                            long split_stride, int colsum_row) {
+  // block = 64 columns x 4 row lanes; each thread walks rows ty, ty+4, ... summing the split partials
+  __shared__ float red[4][64];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int n = blockIdx.x * 64 + tx;
+  float cs = 0.f;
+  if (n < p.N) {
+    OutT* C = reinterpret_cast<OutT*>(p.C);
+    for (int m = ty; m < p.M; m += 4) {
+      const float* q = part + (long)m * p.N + n;
+      float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+      int y = 0;
+      for (; y + 4 <= nsplit; y += 4) {
+        a0 += q[(long)y * split_stride];
+        a1 += q[(long)(y + 1) * split_stride];
+        a2 += q[(long)(y + 2) * split_stride];
+        a3 += q[(long)(y + 3) * split_stride];
+      }
+      for (; y < nsplit; ++y) a0 += q[(long)y * split_stride];
+      const float acc = (a0 + a1) + (a2 + a3);
+      epilogue_elem<EPI, OutT>(p, C, m, n, acc);
+      if constexpr (EPI == EPI_STORE) cs += acc * p.alpha + (p.bias ? p.bias[n] : 0.f);
+      else if constexpr (EPI == EPI_GELU_BWD) cs += acc * p.alpha * gelu_erf_grad((float)p.aux[(long)m * p.ldaux + n]);
+      else if constexpr (EPI == EPI_QGELU_BWD) cs += acc * p.alpha * qgelu_grad((float)p.aux[(long)m * p.ldaux + n]);
+    }
+  }
+  if (p.colsum) {
+    red[ty][tx] = cs;
+    __syncthreads();
+    if (ty == 0 && n < p.N) p.colsum_ws[(long)colsum_row * p.N + n] = red[0][tx] + red[1][tx] + red[2][tx] + red[3][tx];
+  }
+}
+
+// colsum partials: out[n] += sum over rows r < nrows of ws[r][n]; 32 rows per thread, one atomic per (column, 32 rows)
+__global__ __launch_bounds__(256) void colsum_reduce_kernel(const float* __restrict__ ws, int nrows, int N,
+                                                            float* __restrict__ out) {
+  const int n = blockIdx.x * 256 + threadIdx.x;
+  if (n >= N) return;
+  const int r0 = blockIdx.y * 32, r1 = min(nrows, r0 + 32);
+  float s = 0.f;
+#pragma unroll 8
+  for (int r = r0; r < r1; ++r) s += ws[(long)r * N + n];
+  atomicAdd(out + n, s);
+}
+
+static int colsum_reduce(const slx_gemm_desc* d, hipStream_t st) {
+  const int nrows = (d->M + 63) / 64;
+  hipLaunchKernelGGL(colsum_reduce_kernel, dim3((d->N + 255) / 256, (nrows + 31) / 32), dim3(256), 0, st,
+                     (const float*)d->colsum_ws, nrows, d->N, d->colsum);
+  SLX_LAUNCH_CHECK("slx_gemm_bf16(colsum reduce)");
+  return 0;
+}
+
+static int gemm_launch(const slx_gemm_desc* d, int v, hipStream_t st, int mshift_last = 0, int colsum_row0 = 0,
+                       int force_split = 0, long split_stride = 0) {
   GemmArgs a;
+  a.split_stride = split_stride;
   a.A = (const bf16*)d->A; a.B = (const bf16*)d->B; a.C = d->C;
   a.lda = d->lda; a.ldb = d->ldb; a.ldc = d->ldc;
   a.sA = d->sA; a.sB = d->sB; a.sC = d->sC;
@@ -977,6 +1072,9 @@ static int gemm_launch(const slx_gemm_desc* d, int v, hipStream_t st, int mshift
   a.accumulate = d->accumulate;
   a.seed = d->seed; a.drop_p = d->drop_p; a.ldmask = d->ldmask;
   a.drop_operand = d->drop_operand;
+  a.colsum = d->colsum;
+  a.colsum_ws = d->colsum_ws;
+  a.colsum_row0 = colsum_row0;
   a.mshift_last = 0;
   a.tilesM = (d->M + BM - 1) / BM;
   a.tilesN = (d->N + BN - 1) / BN;
@@ -993,7 +1091,7 @@ static int gemm_launch(const slx_gemm_desc* d, int v, hipStream_t st, int mshift
   a.ksplit = 1;
   a.kchunk = d->K;
   {  // split-K for under-filled grids (weight gradients): f32 atomics, >= 4 K-steps per split
-    int sp = split_for(d, v, d->M, batch);
+    int sp = force_split > 0 ? force_split : split_for(d, v, d->M, batch);
     const int ksteps = (d->K + BK - 1) / BK;
     if (sp > 1) {
       const int per = ((ksteps + sp - 1) / sp) * BK;
@@ -1002,12 +1100,17 @@ static int gemm_launch(const slx_gemm_desc* d, int v, hipStream_t st, int mshift
     if (sp > 1) {
       a.ksplit = sp;
       a.kchunk = ((ksteps + sp - 1) / sp) * BK;
-      if (!d->accumulate) {
+      if (!d->accumulate && !split_stride) {
         hipError_t e = hipMemset2DAsync(d->C, d->ldc * sizeof(float), 0, (size_t)d->N * sizeof(float), d->M, st);
         if (e != hipSuccess) { set_error("slx_gemm_bf16: memset2D failed: %s", hipGetErrorString(e)); return -1000 - (int)e; }
       }
     }
   }
+  SLX_CHECK_ARG(!d->colsum || (d->colsum_ws && a.vec_ok && a.ksplit == 1 && v != 1 && d->N % 8 == 0 &&
+                                (d->epilogue == SLX_EPI_STORE || d->epilogue == SLX_EPI_GELU_BWD ||
+                                 d->epilogue == SLX_EPI_QGELU_BWD)),
+                "slx_gemm_bf16: colsum needs the vector epilogue (16-B aligned rows, N %% 8 == 0), no split-K, a "
+                "DMA/v3 main loop and a STORE / GELU_BWD / QGELU_BWD epilogue");
   switch (d->epilogue) {
     case SLX_EPI_STORE:
       return d->out_f32 ? dispatch_layout<EPI_STORE, float>(d->layout, a, batch, st, v)
@@ -1040,6 +1143,66 @@ static int gemm_launch(const slx_gemm_desc* d, int v, hipStream_t st, int mshift
   }
   set_error("slx_gemm_bf16: bad epilogue %d", d->epilogue);
   return -22;
+}
+
+template <int EPI, typename OutT>
+static int launch_rows(GemmArgs& a, const float* part, int nsplit, long split_stride, int colsum_row, hipStream_t st) {
+  hipLaunchKernelGGL((rows_epilogue_kernel<EPI, OutT>), dim3((a.N + 63) / 64), dim3(256), 0, st, a, part, nsplit,
+                     split_stride, colsum_row);
+  SLX_LAUNCH_CHECK("slx_gemm_bf16(remainder epilogue)");
+  return 0;
+}
+
+// Rows [r0, M) of d (fewer than 256): split-K partials over the whole chip, then the epilogue kernel. Returns 1 (and
+// launches nothing) when the caller's remainder workspace is missing or too small.
+static int gemm_remainder(const slx_gemm_desc* d, int r0, hipStream_t st) {
+  const int rem = d->M - r0;
+  const bool ak = d->layout == SLX_GEMM_NT || d->layout == SLX_GEMM_NN;
+  const int ksteps = (d->K + BK - 1) / BK;
+  const int tilesN = (d->N + BN - 1) / BN;
+  int sp = 512 / tilesN;                 // ~2 blocks per CU
+  sp = sp < ksteps / 2 ? sp : ksteps / 2;  // >= 2 K-steps per split
+  sp = sp < 1 ? 1 : (sp > 32 ? 32 : sp);
+  const int kchunk = ((ksteps + sp - 1) / sp);
+  sp = (ksteps + kchunk - 1) / kchunk;
+  const long stride = (long)rem * d->N;
+  if (!d->rem_ws || d->rem_ws_floats < stride * sp) return 1;
+  slx_gemm_desc t = *d;
+  t.M = rem;
+  t.A = ak ? (const void*)((const bf16*)d->A + (long)r0 * d->lda) : (const void*)((const bf16*)d->A + r0);
+  t.C = d->rem_ws; t.ldc = d->N; t.out_f32 = 1;
+  t.epilogue = SLX_EPI_STORE; t.alpha = 1.f; t.bias = nullptr; t.ls = nullptr; t.accumulate = 0;
+  t.aux = nullptr; t.aux_out = nullptr; t.resid = nullptr; t.colsum = nullptr; t.batch = 1;
+  int rc = gemm_launch(&t, 2, st, 0, 0, sp, stride);
+  if (rc) return rc;
+  GemmArgs a;
+  memset(&a, 0, sizeof(a));
+  const size_t csz = d->out_f32 ? 4 : 2;
+  a.C = (void*)((char*)d->C + (size_t)r0 * d->ldc * csz);
+  a.ldc = d->ldc;
+  a.M = rem; a.N = d->N; a.K = d->K;
+  a.alpha = d->alpha;
+  a.bias = d->bias; a.ls = d->ls;
+  a.aux = d->aux ? (const bf16*)d->aux + (long)r0 * d->ldaux : nullptr; a.ldaux = d->ldaux;
+  a.aux_out = d->aux_out ? (bf16*)d->aux_out + (long)r0 * d->ldaux_out : nullptr; a.ldaux_out = d->ldaux_out;
+  a.resid = d->resid ? d->resid + (long)r0 * d->ldr : nullptr; a.ldr = d->ldr;
+  a.accumulate = d->accumulate;
+  a.ksplit = 1;
+  a.colsum = d->colsum; a.colsum_ws = d->colsum_ws;
+  const float* part = d->rem_ws;
+  const int crow = r0 / 64;
+  switch (d->epilogue) {
+    case SLX_EPI_STORE:
+      return d->out_f32 ? launch_rows<EPI_STORE, float>(a, part, sp, stride, crow, st)
+                        : launch_rows<EPI_STORE, bf16>(a, part, sp, stride, crow, st);
+    case SLX_EPI_GELU: return launch_rows<EPI_GELU, bf16>(a, part, sp, stride, crow, st);
+    case SLX_EPI_RESID_LS: return launch_rows<EPI_RESID_LS, float>(a, part, sp, stride, crow, st);
+    case SLX_EPI_GELU_BWD: return launch_rows<EPI_GELU_BWD, bf16>(a, part, sp, stride, crow, st);
+    case SLX_EPI_QGELU: return launch_rows<EPI_QGELU, bf16>(a, part, sp, stride, crow, st);
+    case SLX_EPI_QGELU_BWD: return launch_rows<EPI_QGELU_BWD, bf16>(a, part, sp, stride, crow, st);
+    case SLX_EPI_SWIGLU_BWD: return launch_rows<EPI_SWIGLU_BWD, bf16>(a, part, sp, stride, crow, st);
+  }
+  return 1;  // DROPMASK epilogues index the mask by absolute row: not handled here
 }
 
 }  // namespace slx
@@ -1081,13 +1244,13 @@ extern "C" int slx_gemm_bf16(const slx_gemm_desc* d, slx_stream_t stream) {
   // A write-once epilogue (no accumulation into C, no split-K atomics) tolerates two blocks storing the same
   // rows: the last M tile is shifted to end at M instead of peeling the remainder into a second, latency-bound
   // launch (16 extra rows cost 1/65 of the grid; the peel cost ~8% of an InternViT FC1).
-  const bool overlap_ok = peel_ok && !d->accumulate && split_for(d, 7, d->M, batch) == 1 &&
+  const bool overlap_ok = peel_ok && !d->accumulate && !d->colsum && split_for(d, 7, d->M, batch) == 1 &&
                           !(d->resid && d->resid == (const float*)d->C) && d->aux != (const void*)d->C;
   // ... but only when the extra tile row does not cost a whole extra block round (measured: InternViT FC1's
   // 64x16 main grid is exactly 4 rounds of 256, the overlap makes it 5 and the step 5% slower than the peel)
   if (v == 7 && dma_ok && overlap_ok &&
       v_cost(d, 7, d->M, batch) < v_cost(d, 7, d->M - rem, batch) + v_cost(d, 2, rem, batch))
-    return gemm_launch(d, 7, st, 1);
+    return gemm_launch(d, 7, st, 1);  // (overlap_ok excludes colsum: shifted rows would be summed twice)
   if (v == 7 && dma_ok && peel_ok) {
     // main block rows on v3, the M remainder on v2 (same stream, same epilogue)
     slx_gemm_desc m = *d, t = *d;
@@ -1100,10 +1263,20 @@ extern "C" int slx_gemm_bf16(const slx_gemm_desc* d, slx_stream_t stream) {
     if (d->aux) t.aux = (const void*)((const bf16*)d->aux + r0 * d->ldaux);
     if (d->aux_out) t.aux_out = (void*)((bf16*)d->aux_out + r0 * d->ldaux_out);
     if (d->resid) t.resid = d->resid + r0 * d->ldr;
+    // The peel is a handful of blocks walking the whole K: latency-bound, so give it the 4-stage ring and run it on
+    // a side stream next to the main grid (it writes disjoint rows of C); the caller's stream joins it after.
+    const int row0 = m.M / 64;  // the remainder's colsum partial rows follow the main grid's
+    // Remainder rows: split-K over the whole chip + epilogue kernel (workspace permitting), else the classic peel
+    // (a few latency-bound blocks walking all of K on the 4-stage ring). Serial on the caller's stream: running
+    // them next to the main grid (side stream) measured slower - v3 holds one 139 KB block per CU and whole rounds
+    // of 256 blocks, so any CU taken by a side kernel delays a main block.
     int rc = gemm_launch(&m, 7, st);
+    if (!rc) rc = gemm_remainder(d, m.M, st);
+    if (rc == 1) rc = gemm_launch(&t, 4, st, 0, row0);
     if (rc) return rc;
-    // the peel is a handful of blocks walking the whole K: latency-bound, so give it the 4-stage ring
-    return gemm_launch(&t, 4, st);
+    return d->colsum ? colsum_reduce(d, st) : 0;
   }
-  return gemm_launch(d, v, st);
+  const int rc = gemm_launch(d, v, st);
+  if (rc) return rc;
+  return d->colsum ? colsum_reduce(d, st) : 0;
 }

@@ -31,6 +31,7 @@ struct NormArgs {
   // bwd
   const float* dy; long lddy;
   float* dx; long lddx; int dx_accumulate;
+  bf16* dxb; long lddxb;  // optional bf16 copy of dx (non-pixel-shuffle rows only)
   float* partial;   // unused (kept for ABI workspace sizing)
   float* dgamma; float* dbeta;
 };
@@ -207,6 +208,12 @@ __global__ __launch_bounds__(256) void norm_bwd_wave_kernel(NormArgs a) {
         ov[0] += q.x; ov[1] += q.y; ov[2] += q.z; ov[3] += q.w;
       }
       *reinterpret_cast<float4*>(dst) = make_float4(ov[0], ov[1], ov[2], ov[3]);
+      if (a.dxb) {
+        bf16x4 ob;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) ob[e] = (bf16)ov[e];
+        *reinterpret_cast<bf16x4*>(a.dxb + row * a.lddxb + col) = ob;
+      }
     }
   }
   if (a.dgamma || a.dbeta) {  // 4 waves' column partials summed through LDS, then contiguous f32 atomics
@@ -290,6 +297,12 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(NormArgs a) {
       }
       o.x = ov[0]; o.y = ov[1]; o.z = ov[2]; o.w = ov[3];
       *reinterpret_cast<float4*>(dst) = o;
+      if (a.dxb) {
+        bf16x4 ob;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) ob[e] = (bf16)ov[e];
+        *reinterpret_cast<bf16x4*>(a.dxb + row * a.lddxb + col) = ob;
+      }
     }
   }
   // column partials -> dgamma / dbeta (pre-zeroed or accumulating) with f32 atomics, transposed
@@ -374,6 +387,8 @@ extern "C" int slx_norm_bwd(const slx_norm_desc* d, const float* dy, int64_t ldd
   fill(a, d);
   a.dy = dy; a.lddy = lddy; a.dx = dx; a.lddx = lddx; a.dx_accumulate = dx_accumulate;
   a.partial = (dgamma || dbeta) ? partial_ws : nullptr;
+  a.dxb = (bf16*)d->dx_bf16; a.lddxb = d->lddx_bf16;
+  SLX_CHECK_ARG(!a.dxb || (!a.ps && a.lddxb % 4 == 0), "slx_norm_bwd: dx_bf16 needs plain rows and lddx_bf16 %% 4 == 0");
 
   return d->rms ? norm_bwd<true>(a, dgamma, dbeta, param_accumulate, (hipStream_t)stream)
                 : norm_bwd<false>(a, dgamma, dbeta, param_accumulate, (hipStream_t)stream);

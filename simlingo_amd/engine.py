@@ -216,14 +216,14 @@ class VLAEngine(EngineOps):
             L = {}
             cat = self.cat[i] if lora else None
             Pq, Po, Pg, Pd = (128, 64, 64, 64) if lora else (0, 0, 0, 0)
-            hx = (self._z if lora else self._e)(Ml, d + Pq, dtype=self.adt)
+            hx = self._buf(("hx", i), Ml, d + Pq, zero=lora)
             h, nrm1 = self._norm(X, self.P[p + "ln1"], None, Ml, d, cfg.rms_eps, rms=True, out=hx[:, :d])
             if lora:
                 L.update(self._lora_down(hx[:, :d], i, ("q", "k", "v"), hx[:, d:], sv))
             qkv = self._e(Ml, nqkv)
             K.mm(hx, cat["qkv"] if lora else self.W[p + "qkv_w"], qkv, bias=self.P[p + "qkv_b"])
             K.rope(qkv, Ml, S, Hq + Hk, cos, sin)  # q and k heads are the first Hq+Hk head slots
-            ox = (self._z if lora else self._e)(Ml, qn + Po, dtype=self.adt)
+            ox = self._buf(("ox", i), Ml, qn + Po, zero=lora)
             o = ox[:, :qn]
             lse = self._e(B * Hq * S, dtype=F32)
             K.attn_fwd(qkv[:, :qn], qkv[:, qn:qn + kn], qkv[:, qn + kn:], o, lse, B=B, S=S, Hq=Hq, Hkv=Hk, causal=True,
@@ -232,13 +232,13 @@ class VLAEngine(EngineOps):
                 L.update(self._lora_down(o, i, ("o",), ox[:, qn:], sv))
             Xm = self._e(Ml, d, dtype=F32)
             K.mm(ox, cat["o"] if lora else self.W[p + "o_w"], Xm, epi=K.EPI_RESID_LS, resid=X, ldr=d, ls=self.ones_d)
-            h2x = (self._z if lora else self._e)(Ml, d + Pg, dtype=self.adt)
+            h2x = self._buf(("h2x", i), Ml, d + Pg, zero=lora)
             h2, nrm2 = self._norm(Xm, self.P[p + "ln2"], None, Ml, d, cfg.rms_eps, rms=True, out=h2x[:, :d])
             if lora:
                 L.update(self._lora_down(h2, i, ("gate", "up"), h2x[:, d:], sv))
             gu = self._e(Ml, 2 * Fl)
             K.mm(h2x, cat["gu"] if lora else self.W[p + "gate_up_w"], gu)
-            ax = (self._z if lora else self._e)(Ml, Fl + Pd, dtype=self.adt)
+            ax = self._buf(("ax", i), Ml, Fl + Pd, zero=lora)
             act = ax[:, :Fl]
             self._swiglu(gu, act, Ml, Fl)
             if lora:
@@ -435,14 +435,14 @@ class VLAEngine(EngineOps):
             K.call("slx_scatter_rows", K.P(dfl), d, K.P(dplan["loss_pos"]), R, d, K.P(dfeat), d, 1, K.stream_ptr())
         # ---------------- final RMSNorm ----------------
         dX = self._z(Ml + 1, d)
-        K.norm_bwd(sv["nf"], dfeat, dX)
+        dxb = self._e(Ml, d)  # bf16 copy of dX, written by every norm backward that updates dX (dgrad operand)
+        K.norm_bwd(sv["nf"], dfeat, dX, dx_bf16=dxb)
         # ---------------- Qwen2 layers ----------------
         Hq, Hk, Fl = cfg.llm_heads, cfg.llm_kv_heads, cfg.llm_ffn
         qn, kn = Hq * 64, Hk * 64
         nqkv = qn + 2 * kn
         cos, sin = self.rope_tables(S)
         ws = K.attn_ws(B, S, Hq, Hk, self.device)
-        dxb = self._e(Ml, d)
         lora = cfg.lora
         r = cfg.lora_r
         for i in reversed(range(cfg.llm_layers)):
@@ -451,8 +451,7 @@ class VLAEngine(EngineOps):
             cat = self.cat[i] if lora else None
             Pq, Po, Pg, Pd = (128, 64, 64, 64) if lora else (0, 0, 0, 0)
             hx, ox, h2x, ax = Ls["hx"], Ls["ox"], Ls["h2x"], Ls["ax"]
-            # down projection: Xo = Xm + [act | t_d] . [Wd | s B_d]^T
-            K.call("slx_cast_rows", K.P(dX), d, K.P(dxb), d, Ml, d, K.stream_ptr())
+            # down projection: Xo = Xm + [act | t_d] . [Wd | s B_d]^T   (dxb = bf16(dX), from the last norm backward)
             dax = self._e(Ml, Fl + Pd, dtype=F32)
             K.mm(dxb, cat["down"] if lora else self.W[p + "down_w"], dax, tb=False)
             dgu = self._e(Ml, 2 * Fl)
@@ -469,9 +468,8 @@ class VLAEngine(EngineOps):
                 self._lora_bwd(i, ("gate", "up"), [dgu[:, :Fl], dgu[:, Fl:]], h2x[:, d:], h2x[:, :d], dh2x[:, d:],
                                dh2x[:, :d], sv)
             del dgu
-            K.norm_bwd(Ls["n2"], dh2x, dX, dx_accumulate=True)
+            K.norm_bwd(Ls["n2"], dh2x, dX, dx_accumulate=True, dx_bf16=dxb)
             # o projection
-            K.call("slx_cast_rows", K.P(dX), d, K.P(dxb), d, Ml, d, K.stream_ptr())
             dox = self._e(Ml, qn + Po, dtype=F32)
             K.mm(dxb, cat["o"] if lora else self.W[p + "o_w"], dox, tb=False)
             if lora:
@@ -489,7 +487,7 @@ class VLAEngine(EngineOps):
             if lora:
                 self._lora_bwd(i, ("q", "k", "v"), [dqkv[:, :qn], dqkv[:, qn:qn + kn], dqkv[:, qn + kn:]], hx[:, d:],
                                hx[:, :d], dhx[:, d:], dhx[:, :d], sv)
-            K.norm_bwd(Ls["n1"], dhx, dX, dx_accumulate=True)
+            K.norm_bwd(Ls["n1"], dhx, dX, dx_accumulate=True, dx_bf16=dxb)
             del dqkv, dhx, dh2x
             if lora:
                 self._group_done(f"llm{i}")
@@ -514,9 +512,9 @@ class VLAEngine(EngineOps):
         K.mm(dimg, sv["a1"], self.G["proj.fc2.w"], ta=True, tb=False, accumulate=True)
         self._colsum(dimg, self.G["proj.fc2.b"], 0)
         da1 = self._e(Mi, d)
-        K.mm(dimg, self.W["proj.fc2.w"], da1, tb=False, epi=K.EPI_GELU_BWD, aux=sv["a1pre"], ldaux=d)
+        K.mm(dimg, self.W["proj.fc2.w"], da1, tb=False, epi=K.EPI_GELU_BWD, aux=sv["a1pre"], ldaux=d,
+             colsum=self.G["proj.fc1.b"])
         K.mm(da1, sv["z"], self.G["proj.fc1.w"], ta=True, tb=False, accumulate=True)
-        self._colsum(da1, self.G["proj.fc1.b"], 0)
         dz = self._e(Mi, 4 * D, dtype=F32)
         K.mm(da1, self.W["proj.fc1.w"], dz, tb=False)
         T = cfg.vit_tokens
@@ -539,9 +537,9 @@ class VLAEngine(EngineOps):
                    K.P(self.G[p + "ls2"]), K.P(self.G[p + "fc2.b"]), 1, K.P(self._ws(2 * 256 * D)), K.stream_ptr())
             K.mm(g, Ls["hact"], self.G[p + "fc2.w"], ta=True, tb=False, accumulate=True)
             dh = self._e(Mv, F_)
-            K.mm(g, self.W[p + "fc2.w"], dh, tb=False, epi=K.EPI_GELU_BWD, aux=Ls["hpre"], ldaux=F_)
+            K.mm(g, self.W[p + "fc2.w"], dh, tb=False, epi=K.EPI_GELU_BWD, aux=Ls["hpre"], ldaux=F_,
+                 colsum=self.G[p + "fc1.b"])  # fc1.b grad = column sums of dh, in the same epilogue
             K.mm(dh, Ls["h2"], self.G[p + "fc1.w"], ta=True, tb=False, accumulate=True)
-            self._colsum(dh, self.G[p + "fc1.b"], 0)
             dh2 = self._e(Mv, D, dtype=F32)
             K.mm(dh, self.W[p + "fc1.w"], dh2, tb=False)
             del dh
@@ -594,10 +592,8 @@ class VLAEngine(EngineOps):
         drop = sv["drop"]
         P = dtx.shape[1]
         W = r * n + r  # one spare 32-column block of zeros past the last site
-        dT = self._e(M, max(W, P))
+        dT = self._buf(("dT", n), M, max(W, P), zero=True)  # columns past P stay zero (never written)
         K.call("slx_cast_rows", K.P(dtx), dtx.stride(0), K.P(dT), dT.stride(0), M, P, K.stream_ptr())
-        if P < W:
-            dT[:, P:].zero_()
         seeds = [sv["llm"][i]["lora"][site] for site in sites]
         K.lora_da(x, dT, [self.G[f"llm.{i}.lora.{site}.a"] for site in sites], seeds, p=drop)   # dA_j += dT_j^T drop_j(x)
         for j, site in enumerate(sites):

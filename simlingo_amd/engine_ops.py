@@ -63,6 +63,17 @@ class EngineOps:
     def _z(self, *shape, dtype=F32):
         return torch.zeros(*shape, dtype=dtype, device=self.device)
 
+    def _buf(self, key, *shape, dtype=None, zero=False):
+        """Persistent activation buffer (the step's arena): allocated (and zeroed, if asked) once per key and shape,
+        then reused every step - buffers whose padding columns must stay zero are not re-filled per step."""
+        dtype = dtype or getattr(self, "adt", BF16)
+        arena = self.__dict__.setdefault("_arena", {})
+        t = arena.get(key)
+        if t is None or tuple(t.shape) != tuple(shape) or t.dtype != dtype:
+            t = (torch.zeros if zero else torch.empty)(*shape, dtype=dtype, device=self.device)
+            arena[key] = t
+        return t
+
     def _norm(self, x, gamma, beta, rows, D, eps, rms=False, ps=0, tpi=0, ldx=None, out=None):
         y = self._e(rows, D) if out is None else out
         mean = None if rms else self._e(rows, dtype=F32)

@@ -39,6 +39,7 @@ class GemmDesc(ctypes.Structure):
         ("accumulate", c_int),
         ("seed", c_u64), ("drop_p", c_float), ("ldmask", c_i64),
         ("ksplit_max", c_int), ("variant", c_int), ("drop_operand", c_int),
+        ("colsum", c_vp), ("colsum_ws", c_vp), ("rem_ws", c_vp), ("rem_ws_floats", c_i64),
     ]
 
 
@@ -111,9 +112,15 @@ def _require_cuda(*ts):
 # ------------------------------------------------------------------------------------------------
 # GEMM
 # ------------------------------------------------------------------------------------------------
+_colsum_ws: dict = {}  # per-device partials workspace of the colsum epilogue (stream-ordered reuse)
+_rem_ws: dict = {}     # per-device split-K scratch of the M-remainder rows (stream-ordered reuse)
+REM_WS_FLOATS = 16 << 20  # 64 MB: 32 splits x 64 rows x 8192 columns
+
+
 def gemm(A, B, C, M, N, K, layout, lda, ldb, ldc, *, epi=EPI_STORE, alpha=1.0, bias=None, ls=None,
          aux=None, ldaux=0, aux_out=None, ldaux_out=0, resid=None, ldr=0, accumulate=False,
-         seed=0, drop_p=0.0, ldmask=0, batch=1, sA=0, sB=0, sC=0, ksplit_max=0, variant=None, drop_operand=0):
+         seed=0, drop_p=0.0, ldmask=0, batch=1, sA=0, sB=0, sC=0, ksplit_max=0, variant=None, drop_operand=0,
+         colsum=None):
     _require_cuda(A, B, C)
     d = GemmDesc()
     d.layout, d.epilogue = layout, epi
@@ -136,6 +143,18 @@ def gemm(A, B, C, M, N, K, layout, lda, ldb, ldc, *, epi=EPI_STORE, alpha=1.0, b
     d.ksplit_max = int(ksplit_max)
     d.variant = int(GEMM_VARIANT if variant is None else variant)
     d.drop_operand = int(drop_operand)
+    d.colsum = colsum.data_ptr() if colsum is not None else 0
+    rw = _rem_ws.get(C.device)
+    if rw is None:
+        rw = _rem_ws[C.device] = torch.empty(REM_WS_FLOATS, dtype=torch.float32, device=C.device)
+    d.rem_ws, d.rem_ws_floats = rw.data_ptr(), rw.numel()
+    if colsum is not None:
+        need = (int(M) + 63) // 64 * int(N)
+        ws = _colsum_ws.get(C.device)
+        if ws is None or ws.numel() < need:
+            ws = torch.empty(max(need, 1 << 20), dtype=torch.float32, device=C.device)
+            _colsum_ws[C.device] = ws
+        d.colsum_ws = ws.data_ptr()
     if A.dtype == torch.float32:  # fp32 parity mode (csrc/precise.hip)
         if B.dtype != torch.float32 or C.dtype != torch.float32:
             raise RuntimeError("fp32 parity-mode GEMM needs f32 A, B and C")
@@ -192,6 +211,7 @@ class NormDesc(ctypes.Structure):
         ("rms", c_int), ("x", c_vp), ("ldx", c_i64), ("gamma", c_vp), ("beta", c_vp), ("y", c_vp), ("ldy", c_i64),
         ("mean", c_vp), ("rstd", c_vp), ("rows", c_i64), ("D", c_int), ("eps", c_float),
         ("pixel_shuffle_grid", c_int), ("tokens_per_image", c_int), ("y_f32", c_int),
+        ("dx_bf16", c_vp), ("lddx_bf16", c_i64),
     ]
 
 
@@ -366,7 +386,9 @@ def norm_fwd(d: NormDesc):
 
 
 def norm_bwd(d: NormDesc, dy, dx, *, dx_accumulate=False, dgamma=None, dbeta=None, param_accumulate=False, ws=None,
-             lddx=None):
+             lddx=None, dx_bf16=None):
+    """dx_bf16: optional bf16 [rows, >= D] view that receives a bf16 copy of the (accumulated) dx in the same pass."""
+    d.dx_bf16, d.lddx_bf16 = (dx_bf16.data_ptr(), dx_bf16.stride(0)) if dx_bf16 is not None else (0, 0)
     check(lib().slx_norm_bwd(ctypes.byref(d), P(dy), dy.stride(0), P(dx), lddx if lddx is not None else dx.stride(0),
                              int(dx_accumulate), P(dgamma), P(dbeta), int(param_accumulate), P(ws), stream_ptr()),
           "slx_norm_bwd")

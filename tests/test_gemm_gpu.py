@@ -225,3 +225,31 @@ def test_gemm_dropmask_swiglu_epilogue(dev, p):
     (torch.nn.functional.silu(gg) * uu).backward(d)
     torch.testing.assert_close(dgu[:, :F].float(), gg.grad, atol=3e-2, rtol=2e-2)
     torch.testing.assert_close(dgu[:, F:].float(), uu.grad, atol=3e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("epi,M", [(K.EPI_GELU_BWD, 16400), (K.EPI_GELU_BWD, 1000), (K.EPI_QGELU_BWD, 2308),
+                                   (K.EPI_STORE, 1000)])
+def test_gemm_colsum_bias_grad(dev, epi, M):
+    """colsum: the epilogue adds the column sums of its f32 output into a [N] vector (fc1.b's gradient from the
+    GELU_BWD dgrad), including the M % 256 remainder that runs on the side stream."""
+    N, Kd = 512, 256
+    g = torch.Generator(device=dev).manual_seed(M + epi)
+    dy = torch.randn(M, Kd, device=dev, generator=g).bfloat16()
+    w = torch.randn(Kd, N, device=dev, generator=g).bfloat16() * 0.1
+    h = torch.randn(M, N, device=dev, generator=g).bfloat16()
+    out = torch.empty(M, N, device=dev, dtype=torch.float32 if epi == K.EPI_STORE else torch.bfloat16)
+    cs = torch.full((N,), 0.5, device=dev)
+    K.mm(dy, w, out, tb=False, epi=epi, aux=h if epi != K.EPI_STORE else None, ldaux=N, colsum=cs)
+    pre = dy.float() @ w.float()
+    if epi == K.EPI_GELU_BWD:
+        x = h.float()
+        grad = 0.5 * (1 + torch.erf(x / 2 ** 0.5)) + x * torch.exp(-0.5 * x * x) / (2 * torch.pi) ** 0.5
+        ref = pre * grad
+    elif epi == K.EPI_QGELU_BWD:
+        x = h.float()
+        s = torch.sigmoid(1.702 * x)
+        ref = pre * s * (1 + 1.702 * x * (1 - s))
+    else:
+        ref = pre
+    torch.testing.assert_close(out.float(), ref, atol=3e-2 * Kd ** 0.5 / 16, rtol=2e-2)
+    torch.testing.assert_close(cs, 0.5 + ref.sum(0), atol=2e-3 * M ** 0.5, rtol=1e-3)

@@ -74,3 +74,24 @@ def test_layernorm_pixel_shuffle_gather(dev):
     dx = torch.zeros(n * T, C, device=dev)
     K.norm_bwd(d, dy, dx, lddx=C)
     torch.testing.assert_close(dx, xr.grad, atol=2e-3, rtol=2e-3)
+
+
+@pytest.mark.parametrize("rms", [False, True])
+def test_norm_bwd_bf16_copy(dev, rms):
+    """dx_bf16: the norm backward writes a bf16 copy of the accumulated f32 dx in the same pass."""
+    M, D = 777, 896
+    g = torch.Generator(device=dev).manual_seed(17)
+    x = torch.randn(M, D, device=dev, generator=g)
+    gamma = torch.rand(D, device=dev, generator=g) + 0.5
+    beta = None if rms else torch.randn(D, device=dev, generator=g)
+    y = torch.empty(M, D, device=dev, dtype=torch.bfloat16)
+    mean = None if rms else torch.empty(M, device=dev)
+    rstd = torch.empty(M, device=dev)
+    d = K.norm_desc(x, gamma, beta, y, mean, rstd, M, D, 1e-6, rms=rms)
+    K.norm_fwd(d)
+    dy = torch.randn(M, D, device=dev, generator=g)
+    dx = torch.randn(M, D, device=dev, generator=g)
+    dxb = torch.empty(M, D + 64, device=dev, dtype=torch.bfloat16)[:, :D]
+    K.norm_bwd(d, dy, dx, dx_accumulate=True, dx_bf16=dxb)
+    torch.cuda.synchronize()
+    assert torch.equal(dxb, dx.bfloat16())

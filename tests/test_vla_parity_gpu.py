@@ -30,11 +30,26 @@ def run_engine(cfg, P, ex, dev):
     return eng, out4.cpu(), rp.cpu(), sp.cpu()
 
 
+def engine_precision_params(eng, P):
+    """The parameters as the bf16 engine computes with them: every tensor it reads as a GEMM operand (eng.W: the
+    2-D weights, frozen LLM, embeddings, LoRA A/B) is held in bf16, the rest (biases, norms, layer scales,
+    position / query embeddings, the f32 heads and wp_encoder) in f32."""
+    return {k: (v.bfloat16().float() if k in eng.W else v) for k, v in P.items()}
+
+
 @pytest.mark.parametrize("case", CASES)
 def test_engine_vs_oracle(dev, case):
+    """At the tiny widths (128) with N(0, 0.05) weights, rounding the weights to bf16 alone moves the oracle's route
+    points by up to 0.065 m (a systematic shift shared by the 20 query rows, which the cumsum adds up), so the
+    arithmetic is judged against the oracle evaluated on the engine's own parameter precision; the losses are
+    also held to 1e-2 against the f32-parameter oracle."""
     cfg, P, ex, z = load_case(case)
-    ref, grads = O.loss_and_grads(P, cfg, ex)
     eng, out4, rp, sp = run_engine(cfg, P, ex, dev)
+    ref32, _ = O.loss_and_grads(P, cfg, ex)
+    want32 = [ref32["loss"].item(), ref32["language_loss"].item(), ref32["route_loss"].item(),
+              ref32["speed_wps_loss"].item()]
+    np.testing.assert_allclose(out4.numpy(), want32, rtol=1e-2, atol=1e-4)
+    ref, grads = O.loss_and_grads(engine_precision_params(eng, P), cfg, ex)
     want = [ref["loss"].item(), ref["language_loss"].item(), ref["route_loss"].item(), ref["speed_wps_loss"].item()]
     dr, ds = (rp - ref["route_pred"]).abs().max().item(), (sp - ref["speed_pred"]).abs().max().item()
     print(f"[{case}] loss {out4.tolist()} vs {want}; route max {dr:.4g} speed max {ds:.4g}")
