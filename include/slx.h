@@ -73,6 +73,8 @@ typedef struct slx_gemm_desc {
                        GELU_BWD dgrad); STORE (no split-K) / GELU_BWD / QGELU_BWD, N % 8 == 0        */
   float* colsum_ws; /* required with colsum: [ceil(M/64), N] f32 partials (one row per 64-row subtile,
                        plain stores, then one small reduce launch: no same-address atomics)          */
+  const uint32_t* maskbits; int64_t ldbits; /* DROPMASK epilogues: keep bits [M][ldbits] written by
+                       slx_lora_down (bit n&31 of word n>>5); NULL = regenerate from (seed, drop_p, ldmask)  */
   float* rem_ws; int64_t rem_ws_floats; /* optional scratch for the M % 256 remainder rows (<= 64 of them):
                        split-K f32 partials [splits][rem][N], then one epilogue pass; without it (or if
                        it is too small) the remainder runs as a latency-bound 16..64-row tile           */
@@ -158,9 +160,19 @@ int slx_gather_rows_bf16(const void* src, int64_t lds, const int* idx, int64_t n
 int slx_gather_sum(const float* src, int64_t lds, const int* pos, int B, int nq, int D, float* out, int accumulate, slx_stream_t s);
 /* peft LoRA dropout (lora_dropout, llm.py:113) with a counter-hash mask regenerated in backward */
 int slx_dropout(const void* src, int64_t lds, void* dst, int64_t ldd, int64_t M, int N, uint64_t seed, float p, int64_t ldmask, slx_stream_t s);
+/* LoRA dropout keep masks (peft lora_dropout, llm.py:113) as bits: for each job, bits[row][w] bit c =
+ * keep(seed, row*ldmask + 32w + c) (common.h drop_keep: one hash per index pair, 16-bit uniforms, p -> round(p*65536)),
+ * rows x cols (cols % 32 == 0, ldmask even). One launch for up to 8 jobs (a layer's 7 sites); every LoRA consumer
+ * (slx_lora_down, slx_lora_bwd, the GEMM DROPMASK epilogues) reads these bits.                   */
+typedef struct { uint64_t seed; uint32_t* bits; int64_t ldbits; int64_t ldmask; int cols; } slx_dropout_bits_job;
+typedef struct {
+  int njobs; float p; int64_t rows;
+  slx_dropout_bits_job job[8];
+} slx_dropout_bits_desc;
+int slx_dropout_bits(const slx_dropout_bits_desc* d, slx_stream_t stream);
 /* LoRA down-projection of the sites sharing one input (peft LoraLayer.forward lora_A(dropout(x)),
- * llm.py:106-119 / peft lora/layer.py): t[:, 32j:32j+32] = drop_j(x) A_j^T, bf16 out; r must be 32.
- * Mask of site j: keep(seed[j], row*ldmask + col), the same hash as slx_dropout / drop_operand.   */
+ * llm.py:106-119 / peft lora/layer.py): t[:, 32j:32j+32] = drop_j(x) A_j^T, bf16 out; r must be 32, Kin % 32 == 0.
+ * p > 0: the keep mask of site j is read from bits[j] ([M][ldbits] uint32, slx_dropout_bits); seed is unused. */
 typedef struct {
   const void* x; int64_t ldx;         /* bf16 [M, Kin] */
   int64_t M; int Kin; int r; int nsites;
@@ -168,19 +180,26 @@ typedef struct {
   uint64_t seed[4];
   void* t; int64_t ldt;               /* bf16 [M, >= 32*nsites] */
   float p; int64_t ldmask;
+  const uint32_t* bits[4]; int64_t ldbits;  /* keep bits per site (p > 0), ldbits >= Kin/32 words per row */
 } slx_lora_down_desc;
 int slx_lora_down(const slx_lora_down_desc* d, slx_stream_t stream);
-/* LoRA A-gradient of the sites sharing one input (peft lora_A backward): dA_j[32, Kin] += dT_j^T drop_j(x),
- * dT_j = columns 32j..32j+31 of dT (bf16 [M, >= 32*nsites]); f32 atomics into dA_j; masks as slx_lora_down. */
+/* LoRA backward of the sites sharing one input (peft lora_A backward + the dropout's input gradient):
+ *   dA_j[32, Kin] += dT_j^T drop_j(x)                     (f32 atomics)
+ *   dx[M, Kin]    += sum_j keep_j/(1-p) * (dT_j A_j)      (if dx; or bf16(dx + ...) written to dx_bf16 instead)
+ * dT_j = columns 32j..32j+31 of dt (f32 [M, >= 32*nsites]: the extra columns of the fused [dy | s dy B] dgrad GEMM).
+ * keep_j from bits[j] (slx_dropout_bits); p == 0: no mask. Kin % 128 == 0.                        */
 typedef struct {
   const void* x; int64_t ldx;         /* bf16 [M, Kin] (undropped forward input) */
   int64_t M; int Kin; int r; int nsites;
-  const void* dT; int64_t ldt;        /* bf16 [M, >= 32*nsites] */
-  float* dA[4];                       /* f32 [r, Kin] per site, accumulated */
-  uint64_t seed[4];
-  float p; int64_t ldmask;
-} slx_lora_da_desc;
-int slx_lora_da(const slx_lora_da_desc* d, slx_stream_t stream);
+  const float* dt; int64_t lddt;      /* f32 [M, >= 32*nsites] */
+  const void* A[4];                   /* bf16 [32, Kin] per site */
+  const uint32_t* bits[4]; int64_t ldbits;
+  float* dA[4];                       /* f32 [32, Kin] per site, accumulated */
+  float* dx; int64_t lddx;            /* f32 [M, Kin] or NULL (no input gradient) */
+  void* dx_bf16; int64_t lddx_bf16;   /* optional bf16 [M, Kin] output instead of updating dx in place */
+  float p;
+} slx_lora_bwd_desc;
+int slx_lora_bwd(const slx_lora_bwd_desc* d, slx_stream_t stream);
 
 /* small strided f32 GEMM (driving heads adaptors.py:113-132, WaypointInputAdaptor :80)        */
 enum { SLX_ACT_NONE = 0, SLX_ACT_RELU = 1, SLX_ACT_SILU = 2 };

@@ -103,16 +103,33 @@ __device__ __forceinline__ float silu_grad(float x) {
   return s * (1.0f + x * (1.0f - s));
 }
 
-// Counter-based hash RNG (for LoRA dropout masks): deterministic in (seed, index)
-// so forward and backward regenerate the identical mask without storing it.
-__device__ __forceinline__ uint32_t hash_u32(uint32_t x) {
+// Counter-based hash RNG for the LoRA dropout masks: deterministic in (seed, index). One 32-bit hash per PAIR of
+// consecutive mask indices (idx >> 1); its low / high 16 bits are the uniforms of the even / odd element, and an
+// element is kept iff its uniform >= thr = round(p * 65536) (p = 0.1 -> 6554 / 65536 = 0.100006). The forward
+// (slx_lora_down) evaluates it once per element and stores the keep bits; the backward reads the bits.
+__host__ __device__ __forceinline__ uint32_t hash_u32(uint32_t x) {
   x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16;
   return x;
 }
-__device__ __forceinline__ float uniform01(uint64_t seed, uint64_t idx) {
-  uint32_t h = hash_u32((uint32_t)idx ^ hash_u32((uint32_t)seed ^ (uint32_t)(idx >> 32) * 0x9e3779b9U) ^
-                        (uint32_t)(seed >> 32));
-  return (h >> 8) * (1.0f / 16777216.0f);
+__host__ __device__ __forceinline__ uint32_t drop_seed_mix(uint64_t seed) {
+  return hash_u32((uint32_t)seed ^ hash_u32((uint32_t)(seed >> 32) ^ 0x9e3779b9U));
+}
+__device__ __forceinline__ uint32_t drop_thr(float p) { return (uint32_t)(p * 65536.0f + 0.5f); }
+__device__ __forceinline__ uint32_t drop_pair_hash(uint32_t s1, uint64_t idx) { return hash_u32((uint32_t)(idx >> 1) ^ s1); }
+__device__ __forceinline__ bool drop_keep(uint32_t s1, uint64_t idx, uint32_t thr) {
+  const uint32_t h = drop_pair_hash(s1, idx);
+  return ((idx & 1) ? (h >> 16) : (h & 0xFFFFu)) >= thr;
+}
+// keep bits of 8 consecutive indices idx0..idx0+7 (idx0 even): bit j = keep(idx0 + j); 4 hashes
+__device__ __forceinline__ uint32_t drop_keep8(uint32_t s1, uint64_t idx0, uint32_t thr) {
+  uint32_t b = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const uint32_t h = drop_pair_hash(s1, idx0 + 2 * j);
+    b |= (uint32_t)((h & 0xFFFFu) >= thr) << (2 * j);
+    b |= (uint32_t)((h >> 16) >= thr) << (2 * j + 1);
+  }
+  return b;
 }
 
 }  // namespace slx

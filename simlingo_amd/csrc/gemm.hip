@@ -68,6 +68,8 @@ struct GemmArgs {
   float* colsum_ws;  // [ceil(M/64) + colsum_row0][N] partials, one row per 64-row output subtile
   int colsum_row0;   // subtile-row offset of this launch (the M-remainder launch continues the main grid's rows)
   long split_stride; // split-K: 0 = f32 atomics into C; > 0 = split y stores its partial to C + y * split_stride
+  const uint32_t* maskbits;  // DROPMASK epilogues: keep bits [M][ldbits] (slx_lora_down), else the hash
+  long ldbits;
 };
 
 // Dropout applied while loading an operand (LoRA dropout, regenerated bit-exactly in backward):
@@ -82,9 +84,28 @@ struct LoadMask {
 __device__ __forceinline__ uint4 mask8(uint4 v, const LoadMask& mk, long base) {
   bf16x8 x = __builtin_bit_cast(bf16x8, v);
   const float sc = 1.0f / (1.0f - mk.p);
+  const uint32_t s1 = drop_seed_mix(mk.seed), thr = drop_thr(mk.p);
 #pragma unroll
-  for (int j = 0; j < 8; ++j) x[j] = (bf16)((float)x[j] * (uniform01(mk.seed, (unsigned long long)(base + j)) >= mk.p ? sc : 0.f));
+  for (int j = 0; j < 8; ++j) x[j] = (bf16)((float)x[j] * (drop_keep(s1, (unsigned long long)(base + j), thr) ? sc : 0.f));
   return __builtin_bit_cast(uint4, x);
+}
+
+// keep factor of element (m, n) of a DROPMASK epilogue: the stored keep bits when given, else the hash
+__device__ __forceinline__ float epi_keep(const GemmArgs& p, int m, int n) {
+  const float sc = 1.0f / (1.0f - p.drop_p);
+  if (p.maskbits) return (p.maskbits[(long)m * p.ldbits + (n >> 5)] >> (n & 31)) & 1u ? sc : 0.f;
+  return drop_keep(drop_seed_mix(p.seed), (unsigned long long)m * p.ldmask + n, drop_thr(p.drop_p)) ? sc : 0.f;
+}
+// keep bits of columns n..n+7 (n % 8 == 0) of row m
+__device__ __forceinline__ uint32_t epi_keep8(const GemmArgs& p, int m, int n) {
+  if (p.maskbits) return (p.maskbits[(long)m * p.ldbits + (n >> 5)] >> (n & 31)) & 0xFFu;
+  const unsigned long long i0 = (unsigned long long)m * p.ldmask + n;
+  const uint32_t s1 = drop_seed_mix(p.seed), thr = drop_thr(p.drop_p);
+  if ((i0 & 1) == 0) return drop_keep8(s1, i0, thr);
+  uint32_t b = 0;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) b |= (uint32_t)drop_keep(s1, i0 + e, thr) << e;
+  return b;
 }
 
 template <bool KC>
@@ -198,12 +219,11 @@ __device__ __forceinline__ void epilogue_elem(const GemmArgs& p, OutT* __restric
     C[ci] = (OutT)(v * u * silu_grad(g));
     C[ci + p.N] = (OutT)(v * silu(g));
   } else if constexpr (EPI == EPI_DROPMASK) {
-    const float keep = uniform01(p.seed, (unsigned long long)m * p.ldmask + n) >= p.drop_p ? 1.0f / (1.0f - p.drop_p) : 0.0f;
-    v *= keep;
+    v *= epi_keep(p, m, n);
     if (p.accumulate) v += (float)C[ci];
     C[ci] = (OutT)v;
   } else if constexpr (EPI == EPI_DROPMASK_SWIGLU) {
-    if (p.drop_p > 0.f) v *= uniform01(p.seed, (unsigned long long)m * p.ldmask + n) >= p.drop_p ? 1.0f / (1.0f - p.drop_p) : 0.0f;
+    if (p.drop_p > 0.f) v *= epi_keep(p, m, n);
     const float d = v + p.resid[(long)m * p.ldr + n];
     const long ai = (long)m * p.ldaux + n;
     const float g = (float)p.aux[ai], u = (float)p.aux[ai + p.N];
@@ -313,9 +333,10 @@ __device__ __forceinline__ void epilogue_vec8(const GemmArgs& p, OutT* __restric
     st8(C + ci + p.N, u);
   } else if constexpr (EPI == EPI_DROPMASK_SWIGLU) {
     if (p.drop_p > 0.f) {
+      const uint32_t kb = epi_keep8(p, m, n);
+      const float sc = 1.0f / (1.0f - p.drop_p);
 #pragma unroll
-      for (int e = 0; e < 8; ++e)
-        v[e] *= uniform01(p.seed, (unsigned long long)m * p.ldmask + n + e) >= p.drop_p ? 1.0f / (1.0f - p.drop_p) : 0.0f;
+      for (int e = 0; e < 8; ++e) v[e] *= (kb >> e) & 1u ? sc : 0.f;
     }
     float r[8], g[8], u[8];
     ld8(p.resid + (long)m * p.ldr + n, r);
@@ -330,9 +351,12 @@ __device__ __forceinline__ void epilogue_vec8(const GemmArgs& p, OutT* __restric
     st8(C + ci, r);
     st8(C + ci + p.N, u);
   } else if constexpr (EPI == EPI_DROPMASK) {
+    {
+      const uint32_t kb = epi_keep8(p, m, n);
+      const float sc = 1.0f / (1.0f - p.drop_p);
 #pragma unroll
-    for (int e = 0; e < 8; ++e)
-      v[e] *= uniform01(p.seed, (unsigned long long)m * p.ldmask + n + e) >= p.drop_p ? 1.0f / (1.0f - p.drop_p) : 0.0f;
+      for (int e = 0; e < 8; ++e) v[e] *= (kb >> e) & 1u ? sc : 0.f;
+    }
     if (p.accumulate) {
       float c[8];
       ld8(C + ci, c);
@@ -1074,6 +1098,7 @@ static int gemm_launch(const slx_gemm_desc* d, int v, hipStream_t st, int mshift
   a.drop_operand = d->drop_operand;
   a.colsum = d->colsum;
   a.colsum_ws = d->colsum_ws;
+  a.maskbits = d->maskbits; a.ldbits = d->ldbits;
   a.colsum_row0 = colsum_row0;
   a.mshift_last = 0;
   a.tilesM = (d->M + BM - 1) / BM;

@@ -205,9 +205,10 @@ __global__ void dropout_kernel(const bf16* src, long lds, bf16* dst, long ldd, l
   const bf16x8 x = *reinterpret_cast<const bf16x8*>(src + m * lds + n0);
   bf16x8 o;
   const float sc = 1.0f / (1.0f - p);
+  const uint32_t s1 = drop_seed_mix(seed), thr = drop_thr(p);
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    const float keep = uniform01(seed, (unsigned long long)m * ldmask + n0 + j) >= p ? sc : 0.f;
+    const float keep = drop_keep(s1, (unsigned long long)m * ldmask + n0 + j, thr) ? sc : 0.f;
     o[j] = (bf16)((float)x[j] * keep);
   }
   *reinterpret_cast<bf16x8*>(dst + m * ldd + n0) = o;

@@ -122,15 +122,35 @@ class DrivingModel(_Base):
         plan = plan_from_example(self.vla_cfg, example)
         dplan = plan.to_device(eng.device)
         out4 = _VLAStep.apply(self.anchor, self, example, plan, dplan)
-        sv_counts = {"language_loss": torch.full((1,), plan.loss_pos.shape[0]),
-                     "route_loss": torch.full((1,), plan.B * self.vla_cfg.n_route),
-                     "speed_wps_loss": torch.full((1,), plan.B * self.vla_cfg.n_speed)}
+        values, counts = self._per_sample_losses(eng, plan)
         averages = {"language_loss": out4[1], "route_loss": out4[2], "speed_wps_loss": out4[3]}
         preds = self._last_predictions
-        if per_sample:
-            return averages, {"route_prediction": preds["route"], "speed_wps_prediction": preds["speed_wps"]}
-        out = TrainingOutput(loss=out4[0], loss_averages=averages, loss_values=averages, loss_counts=sv_counts)
+        if per_sample:  # driving.py:256-259: ({key: (values, counts)}, prediction labels)
+            return ({k: (values[k], counts[k]) for k in values},
+                    {"route_prediction": preds["route"], "speed_wps_prediction": preds["speed_wps"]})
+        out = TrainingOutput(loss=out4[0], loss_averages=averages, loss_values=values, loss_counts=counts)
         return out, {}
+
+    def _per_sample_losses(self, eng, plan):
+        """summarise_losses inputs (models/utils.py:7-41, AdaptorList.compute_loss adaptors.py:333-355): language_loss
+        CE per shifted label position [B, L-1] with its mask, route_loss [B, 20] and speed_wps_loss [B, 10] with ones
+        counts - read from the engine's per-row loss buffers of this step (no host sync)."""
+        sv = eng.saved
+        cfg = self.vla_cfg
+        B, L = plan.B, plan.L
+        dev = eng.device
+        lang = torch.zeros(B, max(L - 1, 0), dtype=torch.float32, device=dev)
+        cnt = torch.zeros(B, max(L - 1, 0), dtype=torch.bool, device=dev)
+        R = plan.loss_pos.shape[0]
+        if R:
+            bt = torch.from_numpy(plan.loss_bt).to(dev)
+            lang[bt[:, 0], bt[:, 1]] = sv["ce_loss"][:R]
+            cnt[bt[:, 0], bt[:, 1]] = True
+        route = sv["route_loss"].view(B, cfg.n_route)
+        speed = sv["speed_loss"].view(B, cfg.n_speed)
+        values = {"language_loss": lang, "route_loss": route, "speed_wps_loss": speed}
+        counts = {"language_loss": cnt, "route_loss": torch.ones_like(route), "speed_wps_loss": torch.ones_like(speed)}
+        return values, counts
 
     def training_step(self, batch, _batch_idx: int = 0):
         """driving.py:263-271 (logging through Lightning when present; sync_dist scalars dropped)."""
@@ -193,15 +213,50 @@ class DrivingModel(_Base):
                                                     pct_start=self.vla_cfg.pct_start)
         return {"optimizer": opt, "lr_scheduler": {"scheduler": sched, "frequency": 1, "interval": "step"}}
 
-    # ---- parameters (reference key names) ------------------------------------------------------
-    def vla_state_dict(self):
-        """{internal name: fp32/bf16 tensor} of the engine's parameters."""
-        eng = self.build_engine()
-        out = {k: v for k, v in eng.P.items()}
-        for k, v in eng.W.items():
-            if k not in out:
-                out[k] = v
-        return out
+    # ---- parameters in the reference's state-dict layout ------------------
+    def vla_params(self) -> dict:
+        """{internal name: f32 CPU tensor}: the engine's parameters, or the ones it will be built with."""
+        if self.engine is not None:
+            return self.engine.params_cpu()
+        if self._init_params is None:
+            from .params import init_params
+            self._init_params = init_params(self.vla_cfg, self.seed)
+        return {k: v.detach().float().cpu() for k, v in self._init_params.items()}
+
+    def state_dict(self, *args, **kwargs):
+        """The reference DrivingModel.state_dict() layout (vision_model.image_encoder.model..., language_model.model.
+        base_model.model... with peft base_layer / lora_A.default / lora_B.default names, adaptors..., wp_encoder...,
+        shared-module aliases included), so checkpoints round-trip with the reference trainer and agent
+        (train.py:104-111, agent_simlingo.py:223). Frozen LLM weights come from the engine's bf16 copies."""
+        from .checkpoint import to_reference
+        prefix = kwargs.get("prefix", args[1] if len(args) > 1 else "") or ""
+        return type(torch.nn.Module.state_dict(self))(
+            (prefix + k, v) for k, v in to_reference(self.vla_params(), self.vla_cfg).items())
+
+    def load_state_dict(self, state_dict, strict: bool = True, assign: bool = False):
+        """Load a reference-layout state dict (flat, Lightning {'state_dict'}, DeepSpeed {'module'}, 'module.' /
+        '_forward_module.' prefixes, or a ZeRO directory path / checkpoint file path). q/k/v and gate/up are fused,
+        the engine (if built) is overwritten in place and its optimizer moments reset."""
+        from torch.nn.modules.module import _IncompatibleKeys
+        from .checkpoint import from_reference, load_checkpoint, to_reference
+        from .checkpoint import _unwrap
+        if isinstance(state_dict, str):
+            state_dict = load_checkpoint(state_dict)
+        missing, unexpected = [], []
+        if strict:
+            P = from_reference(state_dict, self.vla_cfg, strict=True)
+        else:  # keys the dict does not carry keep their current values (torch's strict=False semantics)
+            sd = _unwrap(state_dict)
+            full = to_reference(self.vla_params(), self.vla_cfg, aliases=False)
+            missing = [k for k in full if k not in sd]
+            unexpected = [k for k in sd if k not in full and k not in to_reference(self.vla_params(), self.vla_cfg)]
+            full.update({k: v for k, v in sd.items() if k in full})
+            P = from_reference(full, self.vla_cfg, strict=True)
+        if self.engine is not None:
+            self.engine.load_params(P)
+        else:
+            self._init_params = P
+        return _IncompatibleKeys(missing, unexpected)
 
 
 class FusedAdamW(torch.optim.Optimizer):

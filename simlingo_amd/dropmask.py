@@ -1,5 +1,5 @@
-"""Host mirror of the counter-based dropout mask used by the HIP kernels (common.h: hash_u32 /
-uniform01). Test helper: lets a PyTorch reference apply exactly the mask the kernels apply."""
+"""Host mirror of the counter-based dropout mask used by the HIP kernels (common.h: hash_u32 / drop_keep).
+Test helper: lets a PyTorch reference apply exactly the mask the kernels apply."""
 import numpy as np
 
 M32 = np.uint64(0xFFFFFFFF)
@@ -15,20 +15,32 @@ def _hash_u32(x):
     return x
 
 
-def uniform01(seed: int, idx: np.ndarray) -> np.ndarray:
+def seed_mix(seed: int) -> np.uint64:
+    s = np.uint64(seed & 0xFFFFFFFFFFFFFFFF)
+    inner = _hash_u32(np.asarray([(s >> np.uint64(32)) ^ np.uint64(0x9E3779B9)]))
+    return _hash_u32(np.asarray([(s & M32) ^ inner[0]]))[0]
+
+
+def keep_mask(seed: int, idx: np.ndarray, p: float) -> np.ndarray:
+    """common.h drop_keep: one hash per index pair (idx >> 1), low / high 16 bits for even / odd idx."""
     idx = idx.astype(np.uint64)
-    seed = np.uint64(seed & 0xFFFFFFFFFFFFFFFF)
-    lo = idx & M32
-    hi = idx >> np.uint64(32)
-    inner = _hash_u32((seed & M32) ^ ((hi * np.uint64(0x9E3779B9)) & M32))
-    h = _hash_u32(lo ^ inner ^ (seed >> np.uint64(32)))
-    return (h >> np.uint64(8)).astype(np.float64) * (1.0 / 16777216.0)
+    h = _hash_u32((idx >> np.uint64(1)) ^ seed_mix(seed))
+    u = np.where((idx & np.uint64(1)) == 1, h >> np.uint64(16), h & np.uint64(0xFFFF))
+    thr = np.uint64(int(p * 65536.0 + 0.5))
+    return u >= thr
 
 
 def keep_scale(seed: int, rows: int, cols: int, ldmask: int, p: float) -> np.ndarray:
     """[rows, cols] float32: 1/(1-p) where kept, 0 where dropped (index = row*ldmask + col)."""
     idx = np.arange(rows, dtype=np.uint64)[:, None] * np.uint64(ldmask) + np.arange(cols, dtype=np.uint64)[None, :]
-    return np.where(uniform01(seed, idx) >= p, 1.0 / (1.0 - p), 0.0).astype(np.float32)
+    return np.where(keep_mask(seed, idx, p), 1.0 / (1.0 - p), 0.0).astype(np.float32)
+
+
+def keep_bits(seed: int, rows: int, cols: int, ldmask: int, p: float) -> np.ndarray:
+    """[rows, cols // 32] uint32 keep bitmask as slx_lora_down writes it (bit c & 31 of word c >> 5)."""
+    k = keep_scale(seed, rows, cols, ldmask, p) > 0
+    w = k.reshape(rows, cols // 32, 32).astype(np.uint64) << np.arange(32, dtype=np.uint64)
+    return w.sum(-1).astype(np.uint32)
 
 
 def lora_site_seed(step_seed: int, layer: int, site_index: int) -> int:

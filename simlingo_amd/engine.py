@@ -117,6 +117,43 @@ class VLAEngine(EngineOps):
         self.probe_site = None     # name of a call site to bracket with HIP events (bench roofline)
         self.probe_events = []
 
+    def load_params(self, params: dict):
+        """Overwrite every parameter from {internal name: tensor} (checkpoint load): trainable -> f32 master + bf16
+        working copy, frozen -> bf16 (1-D f32); derived operands (padded LM head, patch weight, LoRA-concatenated
+        weights) are rebuilt and the optimizer moments reset."""
+        with torch.no_grad():
+            for s in self.specs:
+                t = params[s.name]
+                if tuple(t.shape) != tuple(s.shape):
+                    raise ValueError(f"{s.name}: shape {tuple(t.shape)} != {tuple(s.shape)}")
+                if s.trainable:
+                    self.P[s.name].copy_(t.to(self.device, torch.float32))
+                elif len(s.shape) == 1:
+                    self.P[s.name].copy_(t.to(self.device, torch.float32))
+                elif s.name == "llm.lm_head":
+                    self.W[s.name][: self.cfg.vocab].copy_(t.to(self.device, self.adt))
+                else:
+                    self.W[s.name].copy_(t.to(self.device, self.adt))
+            self.wbf.copy_(self.master.to(BF16))
+            self._refresh_derived()
+            self._build_lora_cat()
+        for name in ("m_state", "v_state"):
+            if hasattr(self, name):
+                delattr(self, name)
+
+    def params_cpu(self) -> dict:
+        """{internal name: f32 CPU tensor} of the current parameters (trainable from the f32 master, frozen from the
+        engine's bf16 copies) - the inverse of load_params."""
+        out = {}
+        for s in self.specs:
+            if s.trainable or len(s.shape) == 1:
+                out[s.name] = self.P[s.name].detach().float().cpu().clone()
+            elif s.name == "llm.lm_head":
+                out[s.name] = self.W[s.name][: self.cfg.vocab].detach().float().cpu()
+            else:
+                out[s.name] = self.W[s.name].detach().float().cpu()
+        return out
+
     # ------------------------------------------------------------------------------------------
     def _refresh_derived(self):
         """bf16 views that are not plain slices of the flat buffer (after every optimizer step)."""
@@ -382,19 +419,35 @@ class VLAEngine(EngineOps):
 
     def _lora_down(self, x, i, sites, t_out, sv):
         """t_out[:, 32j:32j+32] = drop_j(x) A_j^T for the sites sharing x (bf16, written into the extra columns of
-        the activation buffer), one launch. Dropout is applied while loading x (hash mask, regenerated in
-        backward). Returns {site: seed}."""
-        seeds = {site: lora_site_seed(sv["step_seed"], i, LORA_SITES.index(site)) for site in sites}
+        the activation buffer), one launch. Dropout is applied while loading x (hash mask); the keep masks are also
+        stored as bits (persistent per layer and site) for the backward. Returns {site: keep bits or None}."""
+        seeds = [lora_site_seed(sv["step_seed"], i, LORA_SITES.index(site)) for site in sites]
         if self.precise:  # parity mode runs the eval forward: dropout off, t = x A^T as f32 GEMMs
             if sv["drop"] > 0:
                 raise RuntimeError("fp32 parity mode runs the eval forward (LoRA dropout off): forward(training=False)")
             r = self.cfg.lora_r
             for j, site in enumerate(sites):
                 K.mm(x, self.W[f"llm.{i}.lora.{site}.a"], t_out[:, r * j:r * (j + 1)])
-            return seeds
-        K.lora_down(x, [self.W[f"llm.{i}.lora.{site}.a"] for site in sites], t_out, [seeds[s_] for s_ in sites],
-                    p=sv["drop"])
-        return seeds
+            return {site: None for site in sites}
+        bits = [self._lora_bits(i, site, x.shape[0], sv) for site in sites]
+        K.lora_down(x, [self.W[f"llm.{i}.lora.{site}.a"] for site in sites], t_out, seeds, p=sv["drop"], bits=bits)
+        return dict(zip(sites, bits))
+
+    def _lora_bits(self, i, site, M, sv):
+        """Keep-bit mask of one (layer, site) for this step (persistent buffer; None without dropout). The 7 sites of
+        a layer are generated by one slx_dropout_bits launch, the first time any of them is asked for in a step."""
+        if sv["drop"] <= 0:
+            return None
+        key = sv.setdefault("bits_done", set())
+        if i not in key:
+            jobs = []
+            for j, s in enumerate(LORA_SITES):
+                kin = lora_io(self.cfg, s)[0]
+                b = self._buf(("bits", i, s), M, kin // 32, dtype=torch.int32)
+                jobs.append((lora_site_seed(sv["step_seed"], i, j), b, kin, kin))
+            K.dropout_bits(jobs, M, sv["drop"])
+            key.add(i)
+        return self._buf(("bits", i, site), M, lora_io(self.cfg, site)[0] // 32, dtype=torch.int32)
 
 
     # ==========================================================================================
@@ -472,10 +525,11 @@ class VLAEngine(EngineOps):
             # o projection
             dox = self._e(Ml, qn + Po, dtype=F32)
             K.mm(dxb, cat["o"] if lora else self.W[p + "o_w"], dox, tb=False)
-            if lora:
-                self._lora_bwd(i, ("o",), [dxb], ox[:, qn:], ox[:, :qn], dox[:, qn:], dox[:, :qn], sv)
             dob = self._e(Ml, qn)
-            K.call("slx_cast_rows", K.P(dox), dox.stride(0), K.P(dob), qn, Ml, qn, K.stream_ptr())
+            if lora:  # the LoRA dx term and the bf16 cast of dO in one pass
+                self._lora_bwd(i, ("o",), [dxb], ox[:, qn:], ox[:, :qn], dox[:, qn:], dox[:, :qn], sv, dx_bf16=dob)
+            else:
+                K.call("slx_cast_rows", K.P(dox), dox.stride(0), K.P(dob), qn, Ml, qn, K.stream_ptr())
             del dox
             qkv = Ls["qkv"]
             dqkv = self._e(Ml, nqkv)
@@ -576,40 +630,37 @@ class VLAEngine(EngineOps):
         self._group_done("vit_embed")
         self.saved = None
 
-    def _lora_bwd(self, i, sites, dys, tx, x, dtx, dx, sv, swiglu=None):
+    def _lora_bwd(self, i, sites, dys, tx, x, dtx, dx, sv, swiglu=None, dx_bf16=None):
         """LoRA sites of one group sharing the input x. dys[j] bf16 [M, out_j] (views of the output grad),
         tx bf16 [M, P] (forward down-projections t_j in columns 32j..), x bf16 [M, in] (undropped input),
         dtx f32 [M, P] (columns 32j.. hold dt_j = s dy_j B_j, produced by the fused dgrad GEMM; padding columns
-        are exactly 0 because W_cat's are), dx f32 [M, in] accumulated:
-        dB_j = s dy_j^T t_j ; dA_j = dt_j^T drop_j(x) ; dx += drop_j'(dt_j A_j).
-        swiglu=(gu, dgu) (down projection only): instead of accumulating into dx, run the SwiGLU backward in the
-        same GEMM's epilogue: dgu = swiglu'(gu) applied to dx + drop'(dt A)."""
+        are exactly 0 because W_cat's are), dx f32 [M, in] (the base input gradient):
+        dB_j = s dy_j^T t_j (GEMMs) ; dA_j = dt_j^T drop_j(x) and dx += drop_j'(dt_j A_j) in one slx_lora_bwd launch
+        (dx_bf16: write bf16(dx + ...) there instead of updating dx).
+        swiglu=(gu, dgu) (down projection only): the dx term and the SwiGLU backward run in one GEMM epilogue instead:
+        dgu = swiglu'(gu) applied to dx + drop'(dt A)."""
         cfg = self.cfg
         s = cfg.lora_scale
         r = cfg.lora_r
-        M, kin = x.shape
-        n = len(sites)
         drop = sv["drop"]
-        P = dtx.shape[1]
-        W = r * n + r  # one spare 32-column block of zeros past the last site
-        dT = self._buf(("dT", n), M, max(W, P), zero=True)  # columns past P stay zero (never written)
-        K.call("slx_cast_rows", K.P(dtx), dtx.stride(0), K.P(dT), dT.stride(0), M, P, K.stream_ptr())
-        seeds = [sv["llm"][i]["lora"][site] for site in sites]
-        K.lora_da(x, dT, [self.G[f"llm.{i}.lora.{site}.a"] for site in sites], seeds, p=drop)   # dA_j += dT_j^T drop_j(x)
+        keep = sv["llm"][i]["lora"]
+        bits = [keep[site] for site in sites]
         for j, site in enumerate(sites):
-            p = f"llm.{i}.lora.{site}."
-            K.mm(dys[j], tx[:, r * j:r * (j + 1)], self.G[p + "b"], ta=True, tb=False, alpha=s, accumulate=True)
-            if swiglu is not None:
-                gu, dgu = swiglu
-                F = gu.shape[1] // 2
-                K.gemm(dT[:, r * j:r * j + 64], self.cat[i]["apad." + site], dgu, M, F, 64, K.GEMM_NN, dT.stride(0),
-                       kin, dgu.stride(0), epi=K.EPI_DROPMASK_SWIGLU, resid=dx, ldr=dx.stride(0), aux=gu,
-                       ldaux=gu.stride(0), seed=seeds[j], drop_p=drop, ldmask=kin)
-                continue
-            K.mm(dT[:, r * j:r * j + 64], self.cat[i]["apad." + site], dx, tb=False,
-                 epi=K.EPI_DROPMASK if drop > 0 else K.EPI_STORE, accumulate=True, seed=seeds[j], drop_p=drop,
-                 ldmask=kin)
-
+            K.mm(dys[j], tx[:, r * j:r * (j + 1)], self.G[f"llm.{i}.lora.{site}.b"], ta=True, tb=False, alpha=s,
+                 accumulate=True)
+        K.lora_bwd(x, dtx, [self.W[f"llm.{i}.lora.{site}.a"] for site in sites], bits,
+                   [self.G[f"llm.{i}.lora.{site}.a"] for site in sites], dx=None if swiglu is not None else dx,
+                   dx_bf16=dx_bf16, p=drop)
+        if swiglu is not None:
+            gu, dgu = swiglu
+            M = x.shape[0]
+            F = gu.shape[1] // 2
+            dT = self._buf(("dT_down",), M, 64)  # bf16 K=64 operand: dt_down | 32 zero columns (W_cat padding)
+            K.call("slx_cast_rows", K.P(dtx), dtx.stride(0), K.P(dT), dT.stride(0), M, 64, K.stream_ptr())
+            K.gemm(dT, self.cat[i]["apad.down"], dgu, M, F, 64, K.GEMM_NN, dT.stride(0), x.shape[1], dgu.stride(0),
+                   epi=K.EPI_DROPMASK_SWIGLU, resid=dx, ldr=dx.stride(0), aux=gu, ldaux=gu.stride(0),
+                   seed=lora_site_seed(sv["step_seed"], i, LORA_SITES.index("down")), drop_p=drop,
+                   ldmask=x.shape[1], maskbits=bits[0])
 
 
     # ==========================================================================================

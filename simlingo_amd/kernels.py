@@ -39,7 +39,8 @@ class GemmDesc(ctypes.Structure):
         ("accumulate", c_int),
         ("seed", c_u64), ("drop_p", c_float), ("ldmask", c_i64),
         ("ksplit_max", c_int), ("variant", c_int), ("drop_operand", c_int),
-        ("colsum", c_vp), ("colsum_ws", c_vp), ("rem_ws", c_vp), ("rem_ws_floats", c_i64),
+        ("colsum", c_vp), ("colsum_ws", c_vp), ("maskbits", c_vp), ("ldbits", c_i64), ("rem_ws", c_vp),
+        ("rem_ws_floats", c_i64),
     ]
 
 
@@ -120,7 +121,7 @@ REM_WS_FLOATS = 16 << 20  # 64 MB: 32 splits x 64 rows x 8192 columns
 def gemm(A, B, C, M, N, K, layout, lda, ldb, ldc, *, epi=EPI_STORE, alpha=1.0, bias=None, ls=None,
          aux=None, ldaux=0, aux_out=None, ldaux_out=0, resid=None, ldr=0, accumulate=False,
          seed=0, drop_p=0.0, ldmask=0, batch=1, sA=0, sB=0, sC=0, ksplit_max=0, variant=None, drop_operand=0,
-         colsum=None):
+         colsum=None, maskbits=None):
     _require_cuda(A, B, C)
     d = GemmDesc()
     d.layout, d.epilogue = layout, epi
@@ -144,6 +145,8 @@ def gemm(A, B, C, M, N, K, layout, lda, ldb, ldc, *, epi=EPI_STORE, alpha=1.0, b
     d.variant = int(GEMM_VARIANT if variant is None else variant)
     d.drop_operand = int(drop_operand)
     d.colsum = colsum.data_ptr() if colsum is not None else 0
+    if maskbits is not None:
+        d.maskbits, d.ldbits = maskbits.data_ptr(), maskbits.stride(0)
     rw = _rem_ws.get(C.device)
     if rw is None:
         rw = _rem_ws[C.device] = torch.empty(REM_WS_FLOATS, dtype=torch.float32, device=C.device)
@@ -231,14 +234,23 @@ class LoraDownDesc(ctypes.Structure):
     _fields_ = [
         ("x", c_vp), ("ldx", c_i64), ("M", c_i64), ("Kin", c_int), ("r", c_int), ("nsites", c_int),
         ("A", c_vp * 4), ("seed", ctypes.c_uint64 * 4), ("t", c_vp), ("ldt", c_i64), ("p", c_float), ("ldmask", c_i64),
+        ("bits", c_vp * 4), ("ldbits", c_i64),
     ]
 
 
-class LoraDaDesc(ctypes.Structure):
+class DropoutBitsJob(ctypes.Structure):
+    _fields_ = [("seed", ctypes.c_uint64), ("bits", c_vp), ("ldbits", c_i64), ("ldmask", c_i64), ("cols", c_int)]
+
+
+class DropoutBitsDesc(ctypes.Structure):
+    _fields_ = [("njobs", c_int), ("p", c_float), ("rows", c_i64), ("job", DropoutBitsJob * 8)]
+
+
+class LoraBwdDesc(ctypes.Structure):
     _fields_ = [
         ("x", c_vp), ("ldx", c_i64), ("M", c_i64), ("Kin", c_int), ("r", c_int), ("nsites", c_int),
-        ("dT", c_vp), ("ldt", c_i64), ("dA", c_vp * 4), ("seed", ctypes.c_uint64 * 4), ("p", c_float),
-        ("ldmask", c_i64),
+        ("dt", c_vp), ("lddt", c_i64), ("A", c_vp * 4), ("bits", c_vp * 4), ("ldbits", c_i64), ("dA", c_vp * 4),
+        ("dx", c_vp), ("lddx", c_i64), ("dx_bf16", c_vp), ("lddx_bf16", c_i64), ("p", c_float),
     ]
 
 
@@ -246,7 +258,8 @@ _vp, _i, _I, _f = c_vp, c_int, c_i64, c_float
 for _n, _a in {
     "slx_attn_fwd": [ctypes.POINTER(AttnDesc), _vp],
     "slx_lora_down": [ctypes.POINTER(LoraDownDesc), _vp],
-    "slx_lora_da": [ctypes.POINTER(LoraDaDesc), _vp],
+    "slx_lora_bwd": [ctypes.POINTER(LoraBwdDesc), _vp],
+    "slx_dropout_bits": [ctypes.POINTER(DropoutBitsDesc), _vp],
     "slx_attn_bwd": [ctypes.POINTER(AttnDesc), ctypes.POINTER(AttnBwdDesc), _vp],
     "slx_rope": [_vp, _I, _I, _i, _i, _vp, _vp, _i, _vp],
     "slx_norm_fwd": [ctypes.POINTER(NormDesc), _vp],
@@ -412,8 +425,22 @@ def sgemm(A, sam, sak, B, sbk, sbn, C, scm, scn, M, N, Kd, *, bias=None, act=ACT
     check(lib().slx_sgemm(ctypes.byref(d), stream_ptr()), "slx_sgemm")
 
 
-def lora_down(x, As, t, seeds, p=0.0, ldmask=None):
-    """t[:, 32j:32j+32] = drop_j(x) As[j]^T for the sites sharing x (one launch)."""
+def dropout_bits(jobs, rows, p):
+    """Keep masks as bits, one launch for up to 8 (seed, bits int32 [rows, >= cols/32], cols, ldmask) jobs:
+    bits[r][w] bit c = keep(seed, r*ldmask + 32w + c) (common.h drop_keep; host mirror simlingo_amd.dropmask)."""
+    assert 1 <= len(jobs) <= 8 and p > 0
+    d = DropoutBitsDesc()
+    d.njobs, d.p, d.rows = len(jobs), float(p), int(rows)
+    for j, (seed, bits, cols, ldmask) in enumerate(jobs):
+        assert bits.dtype == torch.int32 and bits.shape[0] >= rows and bits.shape[1] * 32 >= cols and bits.is_cuda
+        d.job[j].seed = int(seed) & ((1 << 64) - 1)
+        d.job[j].bits, d.job[j].ldbits, d.job[j].ldmask, d.job[j].cols = bits.data_ptr(), bits.stride(0), int(ldmask), int(cols)
+    check(lib().slx_dropout_bits(ctypes.byref(d), stream_ptr()), "slx_dropout_bits")
+
+
+def lora_down(x, As, t, seeds, p=0.0, ldmask=None, bits=None):
+    """t[:, 32j:32j+32] = drop_j(x) As[j]^T for the sites sharing x (one launch); p > 0: bits[j] (int32
+    [M, >= kin/32]) holds site j's keep mask (dropout_bits); seeds are not used by the kernel."""
     assert x.dtype == torch.bfloat16 and t.dtype == torch.bfloat16 and 1 <= len(As) <= 4
     M, kin = x.shape
     assert t.shape[0] == M and t.shape[1] >= 32 * len(As)
@@ -423,24 +450,40 @@ def lora_down(x, As, t, seeds, p=0.0, ldmask=None):
         assert a.shape == (32, kin) and a.is_contiguous() and a.dtype == torch.bfloat16
         d.A[j] = a.data_ptr()
         d.seed[j] = int(seeds[j]) & ((1 << 64) - 1)
+        if bits is not None and bits[j] is not None:
+            assert bits[j].dtype == torch.int32 and bits[j].shape[0] == M and bits[j].shape[1] * 32 >= kin
+            d.bits[j] = bits[j].data_ptr()
+            d.ldbits = bits[j].stride(0)
     d.t, d.ldt, d.p, d.ldmask = P(t).value, t.stride(0), float(p), kin if ldmask is None else ldmask
     check(lib().slx_lora_down(ctypes.byref(d), stream_ptr()), "slx_lora_down")
 
 
-def lora_da(x, dT, dAs, seeds, p=0.0, ldmask=None):
-    """dAs[j] (f32 [32, kin]) += dT[:, 32j:32j+32]^T drop_j(x) for the sites sharing x (one launch)."""
-    assert x.dtype == torch.bfloat16 and dT.dtype == torch.bfloat16 and 1 <= len(dAs) <= 4
+def lora_bwd(x, dt, As, bits, dAs, dx=None, dx_bf16=None, p=0.0):
+    """peft LoRA backward of the sites sharing x (one launch): dAs[j] (f32 [32, kin]) += dT_j^T drop_j(x) and, if dx
+    (f32 [M, kin]) is given, dx += sum_j drop_j'(dT_j As[j]) in place - or written as bf16(dx + ...) to dx_bf16.
+    dt: f32 [M, >= 32 n] (dT_j = columns 32j..); bits[j]: keep bits from lora_down (None when p == 0)."""
+    assert x.dtype == torch.bfloat16 and dt.dtype == torch.float32 and 1 <= len(As) <= 4
     M, kin = x.shape
-    assert dT.shape[0] == M and dT.shape[1] >= 32 * len(dAs) and dT.stride(1) == 1
-    d = LoraDaDesc()
-    d.x, d.ldx, d.M, d.Kin, d.r, d.nsites = P(x).value, x.stride(0), M, kin, 32, len(dAs)
-    d.dT, d.ldt = P(dT).value, dT.stride(0)
-    for j, g in enumerate(dAs):
+    assert dt.shape[0] == M and dt.shape[1] >= 32 * len(As) and dt.stride(1) == 1
+    d = LoraBwdDesc()
+    d.x, d.ldx, d.M, d.Kin, d.r, d.nsites = P(x).value, x.stride(0), M, kin, 32, len(As)
+    d.dt, d.lddt = P(dt).value, dt.stride(0)
+    for j, (a, g) in enumerate(zip(As, dAs)):
+        assert a.shape == (32, kin) and a.is_contiguous() and a.dtype == torch.bfloat16
         assert g.shape == (32, kin) and g.is_contiguous() and g.dtype == torch.float32
-        d.dA[j] = g.data_ptr()
-        d.seed[j] = int(seeds[j]) & ((1 << 64) - 1)
-    d.p, d.ldmask = float(p), kin if ldmask is None else ldmask
-    check(lib().slx_lora_da(ctypes.byref(d), stream_ptr()), "slx_lora_da")
+        d.A[j], d.dA[j] = a.data_ptr(), g.data_ptr()
+        if p > 0:
+            assert bits[j] is not None and bits[j].shape[0] == M
+            d.bits[j] = bits[j].data_ptr()
+            d.ldbits = bits[j].stride(0)
+    if dx is not None:
+        assert dx.dtype == torch.float32 and dx.shape[0] == M and dx.shape[1] >= kin
+        d.dx, d.lddx = dx.data_ptr(), dx.stride(0)
+    if dx_bf16 is not None:
+        assert dx_bf16.dtype == torch.bfloat16 and dx_bf16.shape[0] == M
+        d.dx_bf16, d.lddx_bf16 = dx_bf16.data_ptr(), dx_bf16.stride(0)
+    d.p = float(p)
+    check(lib().slx_lora_bwd(ctypes.byref(d), stream_ptr()), "slx_lora_bwd")
 
 
 def mm(A, B, C, *, ta=False, tb=True, **kw):

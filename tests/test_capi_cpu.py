@@ -56,7 +56,8 @@ def test_struct_layouts_match_header(tmp_path):
     structs = {"slx_gemm_desc": K.GemmDesc, "slx_attn_desc": K.AttnDesc, "slx_attn_bwd_desc": K.AttnBwdDesc,
                "slx_norm_desc": K.NormDesc, "slx_sgemm_desc": K.SgemmDesc,
                "slx_lora_down_desc": K.LoraDownDesc,
-               "slx_lora_da_desc": K.LoraDaDesc, "slx_dec_gemv_desc": DecGemvDesc,
+               "slx_lora_bwd_desc": K.LoraBwdDesc, "slx_dropout_bits_desc": K.DropoutBitsDesc,
+               "slx_dropout_bits_job": K.DropoutBitsJob, "slx_dec_gemv_desc": DecGemvDesc,
                "slx_frame_desc": FrameDesc}
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "slx.h"', "int main(void){"]
     for cname, cls in structs.items():

@@ -1,0 +1,148 @@
+"""Checkpoint compatibility on the CPU: the reference state-dict layout, both directions.
+
+Pins: tests/golden/ckpt_keys.json and vla_tiny_refsd.safetensors were produced by oracle/gen_golden_ckpt.py from the
+reference's own adaptor modules + transformers' Qwen2ForCausalLM with the llm.py alias and peft naming (the InternViT
+remote code is restated there). The ZeRO-2 directory reader follows deepspeed 0.16.2's zero_to_fp32 file format
+(deepspeed is absent: parity unpinned beyond the synthetic directory built here the way DeepSpeed lays it out).
+"""
+import json
+import os
+
+import pytest
+import torch
+
+from golden_util import GOLDEN, load_case
+from simlingo_amd.checkpoint import ALIASES, consolidate_zero, from_reference, load_checkpoint, to_reference
+from simlingo_amd.config import full_config
+from simlingo_amd.params import param_specs
+
+KEYS = json.load(open(os.path.join(GOLDEN, "ckpt_keys.json")))
+
+
+def _empty(cfg):
+    return {s.name: torch.zeros(s.shape) for s in param_specs(cfg)}
+
+
+def test_key_layout_matches_reference_tree():
+    cfg, P, _, _ = load_case("nopad")
+    sd = to_reference(P, cfg)
+    assert {k: list(v.shape) for k, v in sd.items()} == KEYS["tiny"]
+    full = full_config()
+    sdf = to_reference(_empty(full), full)
+    assert {k: list(v.shape) for k, v in sdf.items()} == KEYS["full"]
+    assert len(KEYS["full"]) == 992  # 24 ViT layers x 14 + 4 + 6 mlp1 + 24 x 26 LLM + 3 + 3 aliases + 16 heads/wp
+
+
+def test_reference_fixture_loads_to_the_golden_parameters():
+    from safetensors.torch import load_file
+    cfg, P, _, _ = load_case("nopad")
+    sd = load_file(os.path.join(GOLDEN, "vla_tiny_refsd.safetensors"))  # aliases stripped by safetensors
+    back = from_reference(sd, cfg)
+    assert set(back) == set(P)
+    for k in P:
+        assert torch.equal(back[k], P[k]), k
+
+
+def test_round_trip_and_wrappers():
+    cfg, P, _, _ = load_case("leftpad")
+    sd = to_reference(P, cfg)
+    for wrapped in ({"state_dict": sd}, {"module": {"module." + k: v for k, v in sd.items()}},
+                    {"_forward_module." + k: v for k, v in sd.items()}):
+        back = from_reference(wrapped, cfg)
+        assert all(torch.equal(back[k], P[k]) for k in P)
+
+
+def test_strict_errors():
+    cfg, P, _, _ = load_case("nopad")
+    sd = dict(to_reference(P, cfg))
+    bad = dict(sd)
+    del bad["adaptors.driving.query_embeds_wps"]
+    with pytest.raises(KeyError, match="missing"):
+        from_reference(bad, cfg)
+    bad = dict(sd, **{"vision_model.extra.weight": torch.zeros(1)})
+    with pytest.raises(KeyError, match="unexpected"):
+        from_reference(bad, cfg)
+    bad = dict(sd)
+    k = "language_model.model.base_model.model.model.layers.0.self_attn.q_proj.base_layer.weight"
+    bad[k] = torch.zeros(3, 3)
+    with pytest.raises(ValueError, match="shape"):
+        from_reference(bad, cfg)
+    bad = dict(sd)
+    a = next(iter(ALIASES))
+    bad[a] = bad[a] + 1
+    with pytest.raises(ValueError, match="alias"):
+        from_reference(bad, cfg)
+
+
+def test_fusion_layout():
+    """q/k/v and gate/up are concatenated along the output rows in that order (the engine's fused operands)."""
+    cfg, P, _, _ = load_case("nopad")
+    sd = to_reference(P, cfg)
+    base = "language_model.model.base_model.model.model.layers.1."
+    qkv = torch.cat([sd[base + f"self_attn.{s}_proj.base_layer.weight"] for s in "qkv"])
+    assert torch.equal(qkv, P["llm.1.qkv_w"])
+    gu = torch.cat([sd[base + "mlp.gate_proj.base_layer.weight"], sd[base + "mlp.up_proj.base_layer.weight"]])
+    assert torch.equal(gu, P["llm.1.gate_up_w"])
+    pw = sd["vision_model.image_encoder.model.vision_model.embeddings.patch_embedding.weight"]
+    assert torch.equal(pw.reshape(pw.shape[0], -1), P["vit.patch.w"])
+
+
+def _write_zero2_dir(root, sd, world, group_split):
+    """A ZeRO stage-2 checkpoint as DeepSpeed 0.16 lays it out: <root>/latest -> tag; the tag dir holds
+    mp_rank_00_model_states.pt (module = non-trainable state, param_shapes = [OrderedDict] per group) and one
+    zero_pp_rank_{r}_mp_rank_00_optim_states.pt per rank with that rank's slice of every flat fp32 group."""
+    from collections import OrderedDict
+    tag = os.path.join(root, "global_step7")
+    os.makedirs(tag)
+    open(os.path.join(root, "latest"), "w").write("global_step7")
+    names = [k for k in sd if k not in ALIASES]
+    trainable = [k for k in names if not k.startswith("language_model.model.base_model.model.model.embed_tokens")
+                 and "base_layer" not in k and "lm_head" not in k and "norm.weight" not in k
+                 and "layernorm" not in k]
+    frozen = [k for k in names if k not in trainable]
+    groups = [trainable[:group_split], trainable[group_split:]]
+    shapes = [OrderedDict((k, torch.Size(sd[k].shape)) for k in g) for g in groups]
+    torch.save({"module": {k: sd[k].clone() for k in frozen}, "param_shapes": shapes},
+               os.path.join(tag, "mp_rank_00_model_states.pt"))
+    flats = []
+    for g in groups:
+        flat = torch.cat([sd[k].reshape(-1).float() for k in g])
+        pad = (-flat.numel()) % (2 * world)  # DeepSpeed aligns each flat group to 2 * world elements
+        flats.append(torch.cat([flat, torch.zeros(pad)]))
+    for r in range(world):
+        parts = [f.chunk(world)[r].clone() for f in flats]
+        torch.save({"optimizer_state_dict": {"single_partition_of_fp32_groups": parts}},
+                   os.path.join(tag, f"zero_pp_rank_{r}_mp_rank_00_optim_states.pt"))
+
+
+@pytest.mark.parametrize("world", [1, 2, 8])
+def test_zero2_directory_consolidation(tmp_path, world):
+    cfg, P, _, _ = load_case("nopad")
+    sd = to_reference(P, cfg)
+    _write_zero2_dir(str(tmp_path), sd, world, group_split=5)
+    got = consolidate_zero(str(tmp_path))
+    back = from_reference(got, cfg)
+    assert all(torch.equal(back[k], P[k]) for k in P)
+    assert set(load_checkpoint(str(tmp_path))) == set(got)
+
+
+def test_driving_model_state_dict_surface(tmp_path):
+    """DrivingModel.state_dict()/load_state_dict() speak the reference layout (no GPU needed before the engine is
+    built): load the reference fixture, read it back, save/load a flat file like agent_simlingo.py:223."""
+    from safetensors.torch import load_file
+    from simlingo_amd.driving import DrivingModel
+    cfg, P, _, _ = load_case("nopad")
+    m = DrivingModel(vision_model={"variant": "tiny"}, language_model={"variant": "tiny", "lora_dropout": 0.0})
+    res = m.load_state_dict(load_file(os.path.join(GOLDEN, "vla_tiny_refsd.safetensors")))
+    assert res.missing_keys == [] and res.unexpected_keys == []
+    sd = m.state_dict()
+    assert list(sd) == list(KEYS["tiny"]) or set(sd) == set(KEYS["tiny"])
+    path = str(tmp_path / "model.pt")
+    torch.save(sd, path)
+    m2 = DrivingModel(vision_model={"variant": "tiny"}, language_model={"variant": "tiny", "lora_dropout": 0.0})
+    m2.load_state_dict(torch.load(path, weights_only=True))
+    got = m2.vla_params()
+    assert all(torch.equal(got[k], P[k]) for k in P)
+    part = {k: v for k, v in sd.items() if k.startswith("adaptors.driving.")}
+    res = m2.load_state_dict(part, strict=False)
+    assert len(res.missing_keys) > 0 and res.unexpected_keys == []

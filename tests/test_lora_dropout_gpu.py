@@ -38,21 +38,29 @@ def test_dropout_mask_consistency(dev):
     torch.testing.assert_close(y.float(), (x.float() * mask).bfloat16().float())
 
 
-@pytest.mark.parametrize("M,kin,nsites,p", [(300, 256, 3, 0.1), (6384 // 8 + 5, 896, 2, 0.1), (77, 4864 // 4, 1, 0.0),
-                                            (1, 64, 4, 0.1)])
+@pytest.mark.parametrize("M,kin,nsites,p", [(300, 256, 3, 0.1), (6384 // 8 + 5, 896, 2, 0.1), (77, 1280, 1, 0.0),
+                                            (1, 128, 4, 0.1), (6384, 4864, 1, 0.1)])
 def test_lora_down_grouped(dev, M, kin, nsites, p):
-    """slx_lora_down: t[:, 32j:32j+32] = drop_j(x) A_j^T, one launch for the sites sharing x."""
+    """slx_dropout_bits writes the keep masks as bits (bit c&31 of word c>>5) exactly as the host mirror computes
+    them; slx_lora_down: t[:, 32j:32j+32] = drop_j(x) A_j^T from those bits, one launch for the sites sharing x."""
+    from simlingo_amd.dropmask import keep_bits
     g = torch.Generator(device=dev).manual_seed(11)
     xfull = torch.randn(M, kin + 64, device=dev, generator=g).bfloat16()
     x = xfull[:, :kin]  # strided view: ldx != kin, ldmask = kin
     As = [(torch.randn(32, kin, device=dev, generator=g) * 0.1).bfloat16() for _ in range(nsites)]
     seeds = [1234567 + 7919 * j for j in range(nsites)]
     t = torch.full((M, 32 * nsites + 16), 7.0, device=dev).bfloat16()
-    K.lora_down(x, As, t, seeds, p=p)
+    bits = [torch.zeros(M, kin // 32, device=dev, dtype=torch.int32) for _ in range(nsites)]
+    if p > 0:
+        K.dropout_bits([(seeds[j], bits[j], kin, kin) for j in range(nsites)], M, p)
+    K.lora_down(x, As, t, seeds, p=p, bits=bits if p > 0 else None)
     for j in range(nsites):
         mask = torch.from_numpy(keep_scale(seeds[j], M, kin, kin, p)).to(dev) if p > 0 else 1.0
         xd = (x.float() * mask).bfloat16().float()
         torch.testing.assert_close(t[:, 32 * j:32 * (j + 1)].float(), xd @ As[j].float().t(), atol=3e-2, rtol=2e-2)
+        if p > 0:
+            want = torch.from_numpy(keep_bits(seeds[j], M, kin, kin, p).view("int32")).to(dev)
+            assert torch.equal(bits[j], want), j
     assert (t[:, 32 * nsites:].float() == 7.0).all()  # columns past the sites untouched
 
 
@@ -74,18 +82,42 @@ def test_dropmask_dgrad_padded_k64(dev):
         torch.testing.assert_close(dx, ref, atol=2e-2, rtol=2e-2)
 
 
-@pytest.mark.parametrize("M,kin,nsites,p", [(300, 256, 3, 0.1), (1000, 896, 2, 0.1), (130, 640, 1, 0.0),
-                                            (64, 128, 4, 0.1)])
-def test_lora_da_grouped(dev, M, kin, nsites, p):
-    """slx_lora_da: dA_j += dT_j^T drop_j(x) with per-site masks, one launch for the sites sharing x."""
+@pytest.mark.parametrize("M,kin,nsites,p,mode", [(300, 256, 3, 0.1, "f32"), (1000, 896, 2, 0.1, "f32"),
+                                                 (130, 640, 1, 0.0, "f32"), (64, 128, 4, 0.1, "bf16"),
+                                                 (6384, 896, 3, 0.1, "f32"), (6384, 896, 1, 0.1, "bf16"),
+                                                 (6384, 4864, 1, 0.1, "none"), (798, 128, 3, 0.0, "f32"),
+                                                 (798, 896, 2, 0.0, "bf16")])
+def test_lora_bwd_grouped(dev, M, kin, nsites, p, mode):
+    """slx_lora_bwd: dA_j += dT_j^T drop_j(x) and dx += sum_j drop_j'(dT_j A_j) (f32 in place / bf16 out / none),
+    masks read from the keep bits of slx_lora_down, dT read as f32 from a strided view (the dgrad GEMM's extra
+    columns)."""
+    from simlingo_amd.dropmask import keep_bits
     g = torch.Generator(device=dev).manual_seed(13)
     x = torch.randn(M, kin, device=dev, generator=g).bfloat16()
-    dT = torch.randn(M, 32 * nsites + 32, device=dev, generator=g).bfloat16()
+    dtfull = torch.randn(M, 32 * nsites + 64, device=dev, generator=g)
+    dt = dtfull[:, 16:16 + 32 * nsites]
+    As = [(torch.randn(32, kin, device=dev, generator=g) * 0.1).bfloat16() for _ in range(nsites)]
     seeds = [777 + 31 * j for j in range(nsites)]
+    bits = [torch.from_numpy(keep_bits(sd, M, kin, kin, p).view("int32")).to(dev) if p > 0 else None for sd in seeds]
     dAs = [torch.full((32, kin), 0.5, device=dev) for _ in range(nsites)]
-    K.lora_da(x, dT, dAs, seeds, p=p)
+    dx0 = torch.randn(M, kin, device=dev, generator=g)
+    dx = dx0.clone()
+    dxb = torch.empty(M, kin, device=dev, dtype=torch.bfloat16) if mode == "bf16" else None
+    K.lora_bwd(x, dt, As, bits, dAs, dx=None if mode == "none" else dx, dx_bf16=dxb, p=p)
+    dtb = dt.bfloat16().float()
+    ref_dx = dx0.clone()
     for j in range(nsites):
         mask = torch.from_numpy(keep_scale(seeds[j], M, kin, kin, p)).to(dev) if p > 0 else 1.0
         xd = (x.float() * mask).bfloat16().float()
-        ref = 0.5 + dT[:, 32 * j:32 * (j + 1)].float().t() @ xd
-        torch.testing.assert_close(dAs[j], ref, atol=5e-2, rtol=1e-2)
+        torch.testing.assert_close(dAs[j], 0.5 + dtb[:, 32 * j:32 * (j + 1)].t() @ xd, atol=5e-2 * (M / 300) ** 0.5,
+                                   rtol=1e-2)
+        ref_dx += mask * (dtb[:, 32 * j:32 * (j + 1)] @ As[j].float())
+    lora_term = (ref_dx - dx0).abs().max().item()
+    if mode == "f32":  # the kernel sums the same bf16 operands in f32: relative to the LoRA term, ~1e-7
+        assert (dx - ref_dx).abs().max().item() <= 1e-5 * lora_term
+    elif mode == "bf16":
+        torch.testing.assert_close(dxb.float(), ref_dx, atol=3e-2, rtol=2e-2)
+        assert (dxb.float() - ref_dx).abs().max().item() <= 1e-5 * lora_term + (ref_dx.abs().max().item() / 128)
+        assert torch.equal(dx, dx0)  # the f32 base gradient is only read
+    else:
+        assert torch.equal(dx, dx0)
