@@ -55,6 +55,8 @@ def parse():
     ap.add_argument("--n-loss", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--wire", default="f32", choices=["f32", "bf16"],
+                    help="gradient all-reduce wire dtype (bf16: half the xGMI bytes, f32 accumulation kept)")
     return ap.parse_args()
 
 
@@ -116,7 +118,7 @@ def setup_vla(args, dev, world, rank):
     B = args.batch or (8 if full else 4)
     s_text = args.s_text if full else 24
     n_loss = args.n_loss if full else 6
-    eng = VLAEngine(cfg, dev, init_params(cfg, seed=0, lora_b_std=0.02, device=dev))
+    eng = VLAEngine(cfg, dev, init_params(cfg, seed=0, lora_b_std=0.02, device=dev), wire=args.wire)
     ex = make_batch(cfg, B=B, s_text=s_text, n_loss=n_loss, seed=1000 + rank)
     plan = plan_from_example(cfg, ex)
     dplan = plan.to_device(dev)

@@ -38,6 +38,8 @@ class VLAConfig:
     lora_r: int = 32
     lora_alpha: int = 64
     lora_dropout: float = 0.1
+    # ---- vision_model.freeze (encoder/vlm.py:35-44): InternViT frozen, mlp1 still trained ----
+    vit_freeze: bool = False
     # ---- driving adaptor (adaptors.py:96-136), wp_encoder (driving.py:91-96) ----
     n_route: int = 20
     n_speed: int = 10

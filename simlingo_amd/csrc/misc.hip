@@ -275,7 +275,8 @@ __global__ __launch_bounds__(1024) void ce_fwd_kernel(const float* logits, long 
   if (threadIdx.x == 0) {
     const float l = mx + __logf(s);
     lse[r] = l;
-    loss[r] = l - x[labels[r]];
+    const int lab = labels[r];
+    loss[r] = (lab >= 0 && lab < V) ? l - x[lab] : 0.f;  // ignore_index (-1) rows: loss 0, as F.cross_entropy
   }
 }
 // bwd: dlogits[r, v] = (softmax - onehot) * (*gscale); padded columns [V, ldd) zeroed.
@@ -286,7 +287,7 @@ __global__ void ce_bwd_kernel(const float* logits, long ld, const int* labels, c
   const int lab = labels[r];
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < ldd; i += gridDim.x * blockDim.x) {
     float v = 0.f;
-    if (i < V) v = (__expf(logits[r * ld + i] - l) - (i == lab ? 1.f : 0.f)) * g;
+    if (i < V && lab >= 0) v = (__expf(logits[r * ld + i] - l) - (i == lab ? 1.f : 0.f)) * g;  // ignored rows: 0
     dlogits[r * ldd + i] = (bf16)v;
   }
 }

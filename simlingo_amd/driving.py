@@ -69,17 +69,21 @@ class DrivingModel(_Base):
     def __init__(self, cfg_data_module=None, processor=None, cache_dir=None, **cfg):
         super().__init__()
         for key, value in cfg.items():   # driving.py:51-52
-            setattr(self, key, value)
+            if key not in ("vision_model", "language_model"):
+                setattr(self, key, value)
         self.cfg_data_module = cfg_data_module
         self.processor = processor
         self.cache_dir = cache_dir
         vm = cfg.get("vision_model", {"variant": "OpenGVLab/InternVL2-1B"})
         lm = cfg.get("language_model", {"variant": "OpenGVLab/InternVL2-1B"})
-        if _get(vm, "freeze", False):
-            raise NotImplementedError("vision_model.freeze=True is not on the MI355X hot path yet")
+        # speed_wps_mode '1d' reads label.waypoints_1d, which simlingo_training's DrivingLabel does not carry, and
+        # predict_route_as_wps=False leaves DrivingAdaptor.queries unset (adaptors.py:110-133): both fail in the
+        # reference, so only the configuration it can run is accepted
         if _get(cfg, "speed_wps_mode", "2d") != "2d" or not _get(cfg, "predict_route_as_wps", True):
-            raise NotImplementedError("MI355X hot path implements speed_wps_mode='2d', predict_route_as_wps=True")
-        over = dict(lora=bool(_get(lm, "lora", True)), lora_r=int(_get(lm, "lora_r", 32)),
+            raise NotImplementedError("speed_wps_mode='2d' with predict_route_as_wps=True is the configuration "
+                                      "simlingo_training runs (adaptors.py:110-133, 189-199)")
+        over = dict(vit_freeze=bool(_get(vm, "freeze", False)),
+                    lora=bool(_get(lm, "lora", True)), lora_r=int(_get(lm, "lora_r", 32)),
                     lora_alpha=int(_get(lm, "lora_alpha", 64)), lora_dropout=float(_get(lm, "lora_dropout", 0.1)),
                     lr=float(cfg.get("lr", 3e-5)), weight_decay=float(cfg.get("weight_decay", 0.1)),
                     betas=tuple(cfg.get("betas", (0.9, 0.999))), pct_start=float(cfg.get("pct_start", 0.05)))
@@ -93,6 +97,18 @@ class DrivingModel(_Base):
         self.hidden_size = self.vla_cfg.llm_dim
         self._last_predictions = None
         self.predict_language = bool(cfg.get("predict_language", True))   # driving.py:58
+        # inner seams (driving.py:62-96): the reference's submodules, served by the engine (simlingo_amd.vlm/adaptors)
+        from .adaptors import AdaptorList
+        from .vlm import LLM, VLMEncoderModel
+        vkw = dict(vm) if isinstance(vm, dict) else {k: getattr(vm, k) for k in ("variant", "embed_dim", "freeze")
+                                                        if hasattr(vm, k)}
+        lkw = dict(lm) if isinstance(lm, dict) else {k: getattr(lm, k) for k in ("variant", "lora", "lora_alpha",
+                                                                                  "lora_r", "lora_dropout") if hasattr(lm, k)}
+        vkw.pop("_target_", None)
+        lkw.pop("_target_", None)
+        self.vision_model = VLMEncoderModel(cfg_data_module, processor, cache_dir, **vkw)._bind(self)
+        self.language_model = LLM(**lkw)._bind(self)
+        object.__setattr__(self, "adaptors", AdaptorList()._bind(self))
         self.max_new_tokens = int(cfg.get("max_new_tokens", 100))   # driving.py:147
         self._decoder = None
         self.sampled_tokens = None

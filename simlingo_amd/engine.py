@@ -34,6 +34,12 @@ BF16, F32 = torch.bfloat16, torch.float32
 ALIGN = 64  # elements; keeps every parameter view 256-B aligned
 
 
+def _f32_frozen(s) -> bool:
+    """Frozen parameters the kernels read as f32 (1-D vectors and, with vision_model.freeze, the ViT position table
+    added by slx_vit_embed_fwd); every other frozen tensor is a bf16 GEMM operand."""
+    return len(s.shape) == 1 or s.name == "vit.pos"
+
+
 def _pad8(n):
     return (n + 7) // 8 * 8
 
@@ -44,7 +50,7 @@ def _pad64(n):
 
 class VLAEngine(EngineOps):
     def __init__(self, cfg: VLAConfig, device, params: dict[str, torch.Tensor] | None = None, seed: int = 0,
-                 bucket_bytes: int = 32 << 20, precise: bool = False):
+                 bucket_bytes: int = 32 << 20, precise: bool = False, wire: str = "f32"):
         """precise=True: fp32 parity mode — the same launch sequence with f32 activations and weights (the f32
         twins of csrc/precise.hip), forward only; used to hold the forward to the north-star tolerance."""
         from .params import init_params
@@ -80,7 +86,7 @@ class VLAEngine(EngineOps):
                 self.P[s.name].copy_(params[s.name].to(dev))
             else:
                 t = params[s.name].to(dev)
-                if len(s.shape) == 1:
+                if _f32_frozen(s):
                     self.P[s.name] = t.float().contiguous()
                 else:
                     self.W[s.name] = t.to(self.adt).contiguous()
@@ -108,7 +114,7 @@ class VLAEngine(EngineOps):
             e = o + (math.prod(s.shape) + ALIGN - 1) // ALIGN * ALIGN
             a, b = self.group_ranges.get(s.group, (o, e))
             self.group_ranges[s.group] = (min(a, o), max(b, e))
-        self.bucketer = GradBucketer(self.grad, self.group_ranges, bucket_bytes)
+        self.bucketer = GradBucketer(self.grad, self.group_ranges, bucket_bytes, wire=wire)
         self.world = 1
         self.step_seed = 0
         self.saved = None
@@ -128,7 +134,7 @@ class VLAEngine(EngineOps):
                     raise ValueError(f"{s.name}: shape {tuple(t.shape)} != {tuple(s.shape)}")
                 if s.trainable:
                     self.P[s.name].copy_(t.to(self.device, torch.float32))
-                elif len(s.shape) == 1:
+                elif _f32_frozen(s):
                     self.P[s.name].copy_(t.to(self.device, torch.float32))
                 elif s.name == "llm.lm_head":
                     self.W[s.name][: self.cfg.vocab].copy_(t.to(self.device, self.adt))
@@ -146,7 +152,7 @@ class VLAEngine(EngineOps):
         engine's bf16 copies) - the inverse of load_params."""
         out = {}
         for s in self.specs:
-            if s.trainable or len(s.shape) == 1:
+            if s.trainable or _f32_frozen(s):
                 out[s.name] = self.P[s.name].detach().float().cpu().clone()
             elif s.name == "llm.lm_head":
                 out[s.name] = self.W[s.name][: self.cfg.vocab].detach().float().cpu()
@@ -239,53 +245,7 @@ class VLAEngine(EngineOps):
         X = self.encode_inputs(pix, plan, dplan, sv)
         S, d = plan.S, cfg.llm_dim
         Ml = B * S
-        # ---------------- Qwen2 + LoRA ----------------
-        Hq, Hk, Fl = cfg.llm_heads, cfg.llm_kv_heads, cfg.llm_ffn
-        qn, kn = Hq * 64, Hk * 64
-        nqkv = qn + 2 * kn
-        cos, sin = self.rope_tables(S)
-        seql = dplan["seqlens"]
-        llm_saved = []
-        lora = cfg.lora
-        r = cfg.lora_r
-        for i in range(cfg.llm_layers):
-            p = f"llm.{i}."
-            L = {}
-            cat = self.cat[i] if lora else None
-            Pq, Po, Pg, Pd = (128, 64, 64, 64) if lora else (0, 0, 0, 0)
-            hx = self._buf(("hx", i), Ml, d + Pq, zero=lora)
-            h, nrm1 = self._norm(X, self.P[p + "ln1"], None, Ml, d, cfg.rms_eps, rms=True, out=hx[:, :d])
-            if lora:
-                L.update(self._lora_down(hx[:, :d], i, ("q", "k", "v"), hx[:, d:], sv))
-            qkv = self._e(Ml, nqkv)
-            K.mm(hx, cat["qkv"] if lora else self.W[p + "qkv_w"], qkv, bias=self.P[p + "qkv_b"])
-            K.rope(qkv, Ml, S, Hq + Hk, cos, sin)  # q and k heads are the first Hq+Hk head slots
-            ox = self._buf(("ox", i), Ml, qn + Po, zero=lora)
-            o = ox[:, :qn]
-            lse = self._e(B * Hq * S, dtype=F32)
-            K.attn_fwd(qkv[:, :qn], qkv[:, qn:qn + kn], qkv[:, qn + kn:], o, lse, B=B, S=S, Hq=Hq, Hkv=Hk, causal=True,
-                       seqlens=seql)
-            if lora:
-                L.update(self._lora_down(o, i, ("o",), ox[:, qn:], sv))
-            Xm = self._e(Ml, d, dtype=F32)
-            K.mm(ox, cat["o"] if lora else self.W[p + "o_w"], Xm, epi=K.EPI_RESID_LS, resid=X, ldr=d, ls=self.ones_d)
-            h2x = self._buf(("h2x", i), Ml, d + Pg, zero=lora)
-            h2, nrm2 = self._norm(Xm, self.P[p + "ln2"], None, Ml, d, cfg.rms_eps, rms=True, out=h2x[:, :d])
-            if lora:
-                L.update(self._lora_down(h2, i, ("gate", "up"), h2x[:, d:], sv))
-            gu = self._e(Ml, 2 * Fl)
-            K.mm(h2x, cat["gu"] if lora else self.W[p + "gate_up_w"], gu)
-            ax = self._buf(("ax", i), Ml, Fl + Pd, zero=lora)
-            act = ax[:, :Fl]
-            self._swiglu(gu, act, Ml, Fl)
-            if lora:
-                L.update(self._lora_down(act, i, ("down",), ax[:, Fl:], sv))
-            Xo = self._e(Ml, d, dtype=F32)
-            K.mm(ax, cat["down"] if lora else self.W[p + "down_w"], Xo, epi=K.EPI_RESID_LS, resid=Xm, ldr=d,
-                 ls=self.ones_d)
-            llm_saved.append(dict(X=X, hx=hx, n1=nrm1, qkv=qkv, ox=ox, lse=lse, Xm=Xm, h2x=h2x, n2=nrm2, gu=gu, ax=ax,
-                                  lora=L))
-            X = Xo
+        X, llm_saved = self.llm_stack(X, B, S, dplan["seqlens"], sv)
         sv["llm"] = llm_saved
         # final RMSNorm kept in f32: the driving heads read it unrounded (only the LM-head rows are cast to bf16)
         feat, nf = self._norm(X, self.P["llm.norm"], None, Ml, d, cfg.rms_eps, rms=True, out=self._e(Ml, d, dtype=F32))
@@ -332,17 +292,72 @@ class VLAEngine(EngineOps):
         self.saved = sv
         return out4, route_pred, speed_pred
 
-    def encode_inputs(self, pix: torch.Tensor, plan: Plan, dplan: dict, sv: dict) -> torch.Tensor:
-        """InternViT -> pixel_shuffle + mlp1 -> wp_encoder -> token assembly: the LLM input rows X [B*S, d] f32
-        (extract_feature internvl2_model.py:114, replace_placeholder_tokens :17-144, AdaptorList.forward
-        adaptors.py:301-331). Saves what the backward needs into `sv`."""
+    def llm_stack(self, X: torch.Tensor, B: int, S: int, seql: torch.Tensor, sv: dict):
+        """Qwen2 decoder x24 + LoRA (language_model.model, driving.py:217-223) over the assembled rows X [B*S, d] f32,
+        causal with key padding (seql [B] valid leading rows). Returns the last residual stream and the per-layer
+        activations the backward reads (sv["drop"] / sv["step_seed"] select the LoRA dropout masks)."""
         cfg = self.cfg
-        B = plan.B
+        d = cfg.llm_dim
+        Ml = B * S
+        # ---------------- Qwen2 + LoRA ----------------
+        Hq, Hk, Fl = cfg.llm_heads, cfg.llm_kv_heads, cfg.llm_ffn
+        qn, kn = Hq * 64, Hk * 64
+        nqkv = qn + 2 * kn
+        cos, sin = self.rope_tables(S)
+        llm_saved = []
+        lora = cfg.lora
+        r = cfg.lora_r
+        for i in range(cfg.llm_layers):
+            p = f"llm.{i}."
+            L = {}
+            cat = self.cat[i] if lora else None
+            Pq, Po, Pg, Pd = (128, 64, 64, 64) if lora else (0, 0, 0, 0)
+            hx = self._buf(("hx", i), Ml, d + Pq, zero=lora)
+            h, nrm1 = self._norm(X, self.P[p + "ln1"], None, Ml, d, cfg.rms_eps, rms=True, out=hx[:, :d])
+            if lora:
+                L.update(self._lora_down(hx[:, :d], i, ("q", "k", "v"), hx[:, d:], sv))
+            qkv = self._e(Ml, nqkv)
+            K.mm(hx, cat["qkv"] if lora else self.W[p + "qkv_w"], qkv, bias=self.P[p + "qkv_b"])
+            K.rope(qkv, Ml, S, Hq + Hk, cos, sin)  # q and k heads are the first Hq+Hk head slots
+            ox = self._buf(("ox", i), Ml, qn + Po, zero=lora)
+            o = ox[:, :qn]
+            lse = self._e(B * Hq * S, dtype=F32)
+            K.attn_fwd(qkv[:, :qn], qkv[:, qn:qn + kn], qkv[:, qn + kn:], o, lse, B=B, S=S, Hq=Hq, Hkv=Hk, causal=True,
+                       seqlens=seql)
+            if lora:
+                L.update(self._lora_down(o, i, ("o",), ox[:, qn:], sv))
+            Xm = self._e(Ml, d, dtype=F32)
+            K.mm(ox, cat["o"] if lora else self.W[p + "o_w"], Xm, epi=K.EPI_RESID_LS, resid=X, ldr=d, ls=self.ones_d)
+            h2x = self._buf(("h2x", i), Ml, d + Pg, zero=lora)
+            h2, nrm2 = self._norm(Xm, self.P[p + "ln2"], None, Ml, d, cfg.rms_eps, rms=True, out=h2x[:, :d])
+            if lora:
+                L.update(self._lora_down(h2, i, ("gate", "up"), h2x[:, d:], sv))
+            gu = self._e(Ml, 2 * Fl)
+            K.mm(h2x, cat["gu"] if lora else self.W[p + "gate_up_w"], gu)
+            ax = self._buf(("ax", i), Ml, Fl + Pd, zero=lora)
+            act = ax[:, :Fl]
+            self._swiglu(gu, act, Ml, Fl)
+            if lora:
+                L.update(self._lora_down(act, i, ("down",), ax[:, Fl:], sv))
+            Xo = self._e(Ml, d, dtype=F32)
+            K.mm(ax, cat["down"] if lora else self.W[p + "down_w"], Xo, epi=K.EPI_RESID_LS, resid=Xm, ldr=d,
+                 ls=self.ones_d)
+            llm_saved.append(dict(X=X, hx=hx, n1=nrm1, qkv=qkv, ox=ox, lse=lse, Xm=Xm, h2x=h2x, n2=nrm2, gu=gu, ax=ax,
+                                  lora=L))
+            X = Xo
+        return X, llm_saved
+
+    def vit_features(self, pix: torch.Tensor, sv: dict | None = None) -> torch.Tensor:
+        """InternViT (24 layers) -> drop CLS -> pixel_shuffle(0.5) + mlp1 (extract_feature, internvl2_model.py:114):
+        pixel tiles [N, 3, 448, 448] -> image tokens [N*256, d] (bf16, or f32 in parity mode). Saves what the backward
+        reads into `sv`."""
+        cfg = self.cfg
+        sv = {} if sv is None else sv
         pix = pix.reshape(-1, 3, cfg.img_size, cfg.img_size)
         if pix.dtype != F32 or not pix.is_contiguous():
             pix = pix.float().contiguous()
         N = pix.shape[0]
-        sv["N"], sv["B"] = N, B
+        sv["N"] = N
         # ---------------- InternViT ----------------
         D, T, F_, H = cfg.vit_dim, cfg.vit_tokens, cfg.vit_ffn, cfg.vit_heads
         g = cfg.vit_grid
@@ -391,7 +406,19 @@ class VLAEngine(EngineOps):
         K.mm(z, self.W["proj.fc1.w"], a1, bias=self.P["proj.fc1.b"], epi=K.EPI_GELU, aux_out=a1pre, ldaux_out=d)
         img = self._e(Mi, d)
         K.mm(a1, self.W["proj.fc2.w"], img, bias=self.P["proj.fc2.b"])
-        sv.update(z=z, nz=nz, a1pre=a1pre, a1=a1)
+        sv.update(z=z, nz=nz, a1pre=a1pre, a1=a1, Mi=Mi, Mv=Mv)
+        return img
+
+    def encode_inputs(self, pix: torch.Tensor, plan: Plan, dplan: dict, sv: dict) -> torch.Tensor:
+        """InternViT -> pixel_shuffle + mlp1 -> wp_encoder -> token assembly: the LLM input rows X [B*S, d] f32
+        (extract_feature internvl2_model.py:114, replace_placeholder_tokens :17-144, AdaptorList.forward
+        adaptors.py:301-331). Saves what the backward needs into `sv`."""
+        cfg = self.cfg
+        B = plan.B
+        sv["B"] = B
+        img = self.vit_features(pix, sv)
+        d = cfg.llm_dim
+        Mi = sv["Mi"]
         # ---------------- waypoint encoder (placeholder coords) ----------------
         nwp = plan.wp_coords.shape[0]
         wp_out = self._e(max(nwp, 1), d, dtype=F32)
@@ -414,8 +441,27 @@ class VLAEngine(EngineOps):
         X = self._e(Ml, d, dtype=F32)
         K.call("slx_assemble_tokens_f32" if self.precise else "slx_assemble_tokens", K.P(dplan["code"]), Ml, d, K.P(self.W["llm.embed"]), cfg.vocab, K.P(img),
                K.P(wp_out), K.P(self.P["drv.query_route"]), K.P(X), K.stream_ptr())
-        sv.update(nwp=nwp, Mi=Mi, Mv=Mv)
+        sv["nwp"] = nwp
         return X
+
+    def llm_features(self, X: torch.Tensor, B: int, S: int, seql: torch.Tensor, logits: bool = False):
+        """Eval forward of the Qwen2 stack on arbitrary input rows X [B*S, d] f32 (LoRA dropout off): post-norm
+        features [B*S, d] f32 and, if asked, the full-vocabulary logits [B*S, V] f32 (language_model.model(...),
+        driving.py:217-225 / llm.py:126-143)."""
+        cfg = self.cfg
+        d, Ml = cfg.llm_dim, B * S
+        Xl, _ = self.llm_stack(X, B, S, seql, {"step_seed": 0, "drop": 0.0})
+        feat, _ = self._norm(Xl, self.P["llm.norm"], None, Ml, d, cfg.rms_eps, rms=True, out=self._e(Ml, d, dtype=F32))
+        if not logits:
+            return feat, None
+        fb = self._e(Ml, d)
+        if self.precise:
+            fb.copy_(feat)
+        else:
+            K.call("slx_cast_rows", K.P(feat), d, K.P(fb), d, Ml, d, K.stream_ptr())
+        lg = self._e(Ml, self.Vp, dtype=F32)
+        K.mm(fb, self.W["llm.lm_head"][: cfg.vocab], lg)
+        return feat, lg[:, : cfg.vocab]
 
     def _lora_down(self, x, i, sites, t_out, sv):
         """t_out[:, 32j:32j+32] = drop_j(x) A_j^T for the sites sharing x (bf16, written into the extra columns of
@@ -578,6 +624,10 @@ class VLAEngine(EngineOps):
                    param_accumulate=True)
         del dz, da1, dimg
         self._group_done("proj")
+        if cfg.vit_freeze:  # vision_model.freeze: mlp1 is the last trainable module; no InternViT backward at all
+            self.bucketer.mark("backward_end")
+            self.saved = None
+            return
         # ---------------- InternViT layers ----------------
         F_, H, N = cfg.vit_ffn, cfg.vit_heads, sv["N"]
         vws = K.attn_ws(N, T, H, H, self.device)
@@ -628,6 +678,7 @@ class VLAEngine(EngineOps):
         self.G["vit.patch.w"].copy_(dwp[:, : cfg.patch_k])
         self._colsum(dpatch, self.G["vit.patch.b"], 0)
         self._group_done("vit_embed")
+        self.bucketer.mark("backward_end")
         self.saved = None
 
     def _lora_bwd(self, i, sites, dys, tx, x, dtx, dx, sv, swiglu=None, dx_bf16=None):

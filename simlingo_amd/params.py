@@ -81,22 +81,23 @@ def param_specs(cfg: VLAConfig) -> list[PSpec]:
     a(PSpec("proj.fc1.b", (d,), True, "zeros", "proj"))
     a(PSpec("proj.fc2.w", (d, d), True, "normal", "proj"))
     a(PSpec("proj.fc2.b", (d,), True, "zeros", "proj"))
-    # InternViT layers, last first
+    # InternViT layers, last first (vision_model.freeze: requires_grad False for all but mlp1, encoder/vlm.py:36-44)
+    vt = not cfg.vit_freeze
     for i in reversed(range(cfg.vit_layers)):
         p = f"vit.{i}."
         g = f"vit{i}"
-        a(PSpec(p + "ln1.w", (D,), True, "ones", g)); a(PSpec(p + "ln1.b", (D,), True, "zeros", g))
-        a(PSpec(p + "qkv.w", (3 * D, D), True, "normal", g)); a(PSpec(p + "qkv.b", (3 * D,), True, "zeros", g))
-        a(PSpec(p + "proj.w", (D, D), True, "normal", g)); a(PSpec(p + "proj.b", (D,), True, "zeros", g))
-        a(PSpec(p + "ls1", (D,), True, "ls", g))
-        a(PSpec(p + "ln2.w", (D,), True, "ones", g)); a(PSpec(p + "ln2.b", (D,), True, "zeros", g))
-        a(PSpec(p + "fc1.w", (F, D), True, "normal", g)); a(PSpec(p + "fc1.b", (F,), True, "zeros", g))
-        a(PSpec(p + "fc2.w", (D, F), True, "normal", g)); a(PSpec(p + "fc2.b", (D,), True, "zeros", g))
-        a(PSpec(p + "ls2", (D,), True, "ls", g))
-    a(PSpec("vit.cls", (D,), True, "normal", "vit_embed"))
-    a(PSpec("vit.pos", (T, D), True, "normal", "vit_embed"))
-    a(PSpec("vit.patch.w", (D, cfg.patch_k), True, "normal", "vit_embed"))
-    a(PSpec("vit.patch.b", (D,), True, "zeros", "vit_embed"))
+        a(PSpec(p + "ln1.w", (D,), vt, "ones", g)); a(PSpec(p + "ln1.b", (D,), vt, "zeros", g))
+        a(PSpec(p + "qkv.w", (3 * D, D), vt, "normal", g)); a(PSpec(p + "qkv.b", (3 * D,), vt, "zeros", g))
+        a(PSpec(p + "proj.w", (D, D), vt, "normal", g)); a(PSpec(p + "proj.b", (D,), vt, "zeros", g))
+        a(PSpec(p + "ls1", (D,), vt, "ls", g))
+        a(PSpec(p + "ln2.w", (D,), vt, "ones", g)); a(PSpec(p + "ln2.b", (D,), vt, "zeros", g))
+        a(PSpec(p + "fc1.w", (F, D), vt, "normal", g)); a(PSpec(p + "fc1.b", (F,), vt, "zeros", g))
+        a(PSpec(p + "fc2.w", (D, F), vt, "normal", g)); a(PSpec(p + "fc2.b", (D,), vt, "zeros", g))
+        a(PSpec(p + "ls2", (D,), vt, "ls", g))
+    a(PSpec("vit.cls", (D,), vt, "normal", "vit_embed"))
+    a(PSpec("vit.pos", (T, D), vt, "normal", "vit_embed"))
+    a(PSpec("vit.patch.w", (D, cfg.patch_k), vt, "normal", "vit_embed"))
+    a(PSpec("vit.patch.b", (D,), vt, "zeros", "vit_embed"))
     return out
 
 

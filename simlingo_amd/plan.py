@@ -37,6 +37,7 @@ class Plan:
     loss_pos: np.ndarray   # [R] int32 final flat positions whose logits enter the LM loss
     loss_labels: np.ndarray  # [R] int32 next-token labels
     loss_bt: np.ndarray | None = None  # [R, 2] (sample, position in the shifted [B, L-1] label grid) of each loss row
+    perm: np.ndarray | None = None     # [B, S] AdaptorList.forward's valid-first permutation (adaptors.py:322-325)
 
     def to_device(self, device) -> dict:
         t = lambda a, dt=torch.int32: torch.from_numpy(np.ascontiguousarray(a)).to(dt).pin_memory().to(device, non_blocking=True) \
@@ -116,7 +117,7 @@ def build_plan(cfg: VLAConfig, ids, valid, loss_mask, placeholder_values, n_img:
     return Plan(B=B, L=L, S=S, code=code.reshape(-1).astype(np.int32), seqlens=seqlens, n_img=n_img, img_pos=img_pos,
                 wp_coords=np.asarray(wp_coords, dtype=np.float32).reshape(-1, 2), wp_pos=wp_pos,
                 query_pos=query_pos, loss_pos=loss_pos, loss_labels=loss_labels,
-                loss_bt=np.stack([bb, tt], 1).astype(np.int64))
+                loss_bt=np.stack([bb, tt], 1).astype(np.int64), perm=perm.astype(np.int64))
 
 
 def plan_from_example(cfg: VLAConfig, example, inference: bool = False) -> Plan:

@@ -70,3 +70,54 @@ def test_bucketed_allreduce_gloo_world2():
     want = torch.arange(n, dtype=torch.float32) * 3  # sum over ranks (1x + 2x); AdamW applies 1/world
     for r in range(2):
         torch.testing.assert_close(ret[r], want)
+
+
+def _overlap_worker(rank, world, port, n, ranges, wire, ret):
+    """A backward that signals its parameter groups in layout order with ~4 ms of compute between them: the first
+    buckets' all-reduces (gloo runs them on its own thread, as RCCL runs them on its own stream) must complete
+    while the backward is still running."""
+    import time
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.set_num_threads(1)
+    g = torch.arange(n, dtype=torch.float32) * (rank + 1) * 1e-3
+    bk = GradBucketer(g, ranges, bucket_bytes=1 << 16, wire=wire, trace=True)
+    bk.set_distributed(None, world)
+    work = torch.randn(192, 192)
+    for name in sorted(ranges, key=lambda k: ranges[k][0]):
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < 4e-3:  # "backward compute" of this group
+            work = torch.tanh(work @ work.t() * 1e-3)
+            bk.poll()
+        bk.group_done(name)
+    bk.mark("backward_end")
+    bk.wait()
+    ret[rank] = (g.clone(), list(bk.trace), len(bk.buckets))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("wire", ["f32", "bf16"])
+def test_allreduce_overlaps_backward_and_bf16_wire(wire):
+    cfg = tiny_config()
+    ranges, n = group_ranges(cfg)
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ret = mp.Manager().dict()
+    mp.spawn(_overlap_worker, args=(2, port, n, ranges, wire, ret), nprocs=2, join=True)
+    want = torch.arange(n, dtype=torch.float32) * 3e-3
+    for r in range(2):
+        g, trace, nb = ret[r]
+        if wire == "f32":
+            torch.testing.assert_close(g, want)
+        else:  # bf16 on the wire, f32 in the optimizer: bf16 rounding of the summands and the sum
+            torch.testing.assert_close(g, want, rtol=8e-3, atol=1e-6)
+            assert not torch.equal(g, want)  # the wire really was bf16
+        t_end = next(t for ev, _, t in trace if ev == "backward_end")
+        issued = [(b, t) for ev, b, t in trace if ev == "issue"]
+        done = {b: t for ev, b, t in trace if ev == "done"}
+        assert len(issued) == nb > 2
+        # every bucket but the last is launched before the backward ends, and the first ones complete before it ends
+        assert sum(t < t_end for _, t in issued) >= nb - 1
+        assert 0 in done and done[0] < t_end, (done, t_end)

@@ -26,17 +26,19 @@ def _worker(rank, world, port, ret):
         eng = VLAEngine(cfg, dev, seed=5, bucket_bytes=64 << 10)
         if distributed:
             eng.set_distributed(None, world)
+            eng.bucketer.trace_on = True
         ex = make_batch(cfg, B=2, s_text=24, n_loss=4, seed=seed)
         plan = plan_from_example(cfg, ex)
         eng.forward(ex.driving_input.camera_images.to(dev), plan, plan.to_device(dev),
                     ex.driving_label.path.to(dev), ex.driving_label.waypoints.to(dev))
         eng.backward(None)
+        trace = list(eng.bucketer.trace)
         eng.wait_grads()
         torch.cuda.synchronize()
-        return eng.grad.cpu().clone(), len(eng.bucketer.buckets)
+        return eng.grad.cpu().clone(), len(eng.bucketer.buckets), trace
 
-    g_dp, nb = grads(100 + rank, True)
-    ret[rank] = (g_dp, nb)
+    g_dp, nb, trace = grads(100 + rank, True)
+    ret[rank] = (g_dp, nb, trace)
     if rank == 0:
         ret["ref"] = grads(100, False)[0] + grads(101, False)[0]
     dist.barrier()
@@ -52,7 +54,12 @@ def test_dp_allreduce_matches_sum_of_rank_grads(dev):
     mp.spawn(_worker, args=(2, port, ret), nprocs=2, join=True)
     ref = ret["ref"]
     for r in range(2):
-        g, nb = ret[r]
+        g, nb, trace = ret[r]
         assert nb > 1
         err = ((g - ref).norm() / ref.norm()).item()
         assert err < 1e-2, err
+        # the exchange is issued during the backward: every bucket but the last (the patch embedding's) is launched
+        # before the engine's backward returns, while later layers' kernels are still being queued
+        t_end = next(t for ev, _, t in trace if ev == "backward_end")
+        issued = [t for ev, _, t in trace if ev == "issue"]
+        assert len(issued) == nb and sum(t < t_end for t in issued) >= nb - 1

@@ -99,3 +99,41 @@ def test_reference_checkpoint_reproduces_golden_losses(dev):
     for k, v in sd.items():
         tol = 0 if v.dim() == 1 or "lora" in k or "adaptors.driving" in k or "wp_encoder" in k else 4e-3
         assert (back[k].float() - v).abs().max().item() <= tol * max(1.0, v.abs().max().item()), k
+
+
+def test_frozen_vision_model(dev):
+    """vision_model.freeze=True (encoder/vlm.py:35-44): InternViT takes no gradient and no optimizer update, mlp1
+    (proj.*) still trains. The engine skips the whole InternViT backward; the step's losses and every remaining
+    gradient match the oracle (gradients of the frozen set do not exist), and the ViT weights survive optimizer
+    steps bit-identical."""
+    from simlingo_amd.driving import DrivingModel
+    cfg, P, ex, _ = load_case("nopad")
+    m = DrivingModel(vision_model={"variant": "tiny", "freeze": True},
+                     language_model={"variant": "tiny", "lora_dropout": 0.0}, init_params=P)
+    m.max_steps = 10
+    assert m.vla_cfg.vit_freeze
+    eng = m.build_engine(dev)
+    names = [s.name for s in eng.specs if s.trainable]
+    assert not any(n.startswith("vit.") for n in names) and "proj.fc1.w" in names
+    vit_before = {k: v.clone() for k, v in eng.W.items() if k.startswith("vit.")}
+    vit_before["vit.pos"] = eng.P["vit.pos"].clone()
+    opt = m.configure_optimizers()["optimizer"]
+    for step in range(2):
+        out = m.training_step(ex, step)
+        out["loss"].backward()
+        torch.cuda.synchronize()
+        if step == 0:
+            from test_vla_parity_gpu import engine_precision_params
+            ref, grads = O.loss_and_grads(engine_precision_params(eng, P), m.vla_cfg, ex)
+            assert set(grads) == set(names)
+            assert abs(out["loss"].item() - ref["loss"].item()) <= 1e-2 * abs(ref["loss"].item())
+            for k in names:
+                g, r = eng.G[k].float().cpu().reshape(-1), grads[k].reshape(-1)
+                if r.norm() > 1e-12:
+                    cos = torch.nn.functional.cosine_similarity(g, r, dim=0).item()
+                    assert cos >= 0.98, (k, cos)
+        opt.step()
+    torch.cuda.synchronize()
+    for k, v in vit_before.items():
+        cur = eng.P[k] if k == "vit.pos" else eng.W[k]
+        assert torch.equal(cur, v), k
