@@ -21,11 +21,15 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("SLX_OFFLOAD_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
          f"-I{INCLUDE}", f"-I{CSRC}"]
+# Per-source flags. attention.hip: no SLP packing of f32 math (v_pk_mul/add_f32 issue at ~5x the cost of the two
+# scalar ops they replace when placed between MFMAs, MI355X_MICROARCH.md 'price of one filler beside MFMAs').
+PER_FILE = {"attention.hip": ["-fno-slp-vectorize"]}
 
 
 def _needs(obj: Path, deps: list[Path]) -> bool:
     if not obj.exists():
         return True
+    deps = deps + [Path(__file__)]
     t = obj.stat().st_mtime
     return any(d.stat().st_mtime > t for d in deps)
 
@@ -34,7 +38,7 @@ def _compile(src: Path, extra: list[str]) -> Path:
     obj = BUILD_DIR / (src.stem + ".o")
     headers = list(CSRC.glob("*.h")) + list(INCLUDE.glob("*.h"))
     if _needs(obj, [src] + headers):
-        cmd = [HIPCC, *FLAGS, *extra, "-c", str(src), "-o", str(obj)]
+        cmd = [HIPCC, *FLAGS, *PER_FILE.get(src.name, []), *extra, "-c", str(src), "-o", str(obj)]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"hipcc failed for {src.name}:\n{r.stdout}\n{r.stderr}")

@@ -22,6 +22,14 @@
 #include "common.h"
 #include "../../include/slx.h"
 
+// Tuning knobs (A/B builds through tools/attn_ab.py pass -D overrides): blocks per CU of each kernel.
+#ifndef ATTN_FWD_OCC
+#define ATTN_FWD_OCC 2
+#endif
+#ifndef ATTN_DQ_OCC
+#define ATTN_DQ_OCC 2
+#endif
+
 namespace slx {
 
 __device__ __forceinline__ f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 c) {
@@ -98,6 +106,7 @@ __device__ __forceinline__ void store64(char* lds, const uint4 (&r)[2]) {
 }
 
 constexpr float LOG2E = 1.4426950408889634f;
+constexpr float LAZY = 8.0f;  // forward lazy-rescale threshold (log2 units)
 constexpr float MASKED = -INFINITY;
 
 // XCD-aware block order: the hardware deals consecutive block ids round-robin over the 8 XCDs (each
@@ -131,9 +140,12 @@ __device__ __forceinline__ float half_swap_max(float x) {
 // One 64-key tile of the forward for one wave (32 queries, query on the lane): S^T = K Q^T, online
 // softmax in the log2 domain with the scale folded into one FMA per score (max taken on raw scores,
 // c > 0), P^T from the accumulator straight into O^T += V^T P^T. MASK only for boundary tiles.
+// Measured on the InternViT shape (tools/attn_ab.py): the structure itself - MFMAs fed from LDS, one barrier per
+// 64-key tile - runs at ~860 TF with the softmax removed; the softmax costs ~30 %, of which the lean form below
+// (row sum on the MFMA, lazy rescale) recovers ~2 %.
 template <bool MASK>
 __device__ __forceinline__ void fwd_tile(const char* Kl, const char* Vl, const bf16x8 (&qf)[4], f32x16& o0, f32x16& o1,
-                                         float& m, float& l, float c, int key0, int kvlen, int myq, bool causal,
+                                         f32x16& lacc, float& m, float c, int key0, int kvlen, int myq, bool causal,
                                          int lane) {
   const int hl = lane >> 5;
   f32x16 s[2];
@@ -154,27 +166,29 @@ __device__ __forceinline__ void fwd_tile(const char* Kl, const char* Vl, const b
         s[kb][r] = ok ? s[kb][r] : MASKED;
       }
   }
+  // VALU-lean softmax: the row sum comes out of the PV MFMAs (ones x P^T into lacc, so l sums exactly the bf16 P
+  // that O accumulates), and O/l are rescaled only when some lane's max grows by more than LAZY (log2 units):
+  // p = exp2(s c - m) <= 2^LAZY otherwise.
   float mx = s[0][0];
 #pragma unroll
   for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
     for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[kb][r]);
-  mx = half_swap_max(mx);
-  const float mnew = fmaxf(m, mx * c);
-  const float alpha = __builtin_amdgcn_exp2f(m - mnew);
-  m = mnew;
-  float ps = 0.f;
+  mx = half_swap_max(mx) * c;
+  if (__builtin_amdgcn_ballot_w64(mx > m + LAZY)) {
+    const float mnew = fmaxf(m, mx);
+    const float alpha = __builtin_amdgcn_exp2f(m - mnew);
+    m = mnew;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { o0[r] *= alpha; o1[r] *= alpha; lacc[r] *= alpha; }
+  }
 #pragma unroll
   for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[kb][r], c, -mnew));
-      s[kb][r] = p;
-      ps += p;
-    }
-  l = l * alpha + ps;
+    for (int r = 0; r < 16; ++r) s[kb][r] = __builtin_amdgcn_exp2f(__builtin_fmaf(s[kb][r], c, -m));
+  bf16x8 ones;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) { o0[r] *= alpha; o1[r] *= alpha; }
+  for (int j = 0; j < 8; ++j) ones[j] = (bf16)1.0f;
 #pragma unroll
   for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
@@ -182,10 +196,11 @@ __device__ __forceinline__ void fwd_tile(const char* Kl, const char* Vl, const b
       const bf16x8 pb = acc_frag(s[kb], st);
       o0 = mfma32(tr_frag(Vl, kb * 32 + 16 * st, 0, lane), pb, o0);
       o1 = mfma32(tr_frag(Vl, kb * 32 + 16 * st, 32, lane), pb, o1);
+      lacc = mfma32(ones, pb, lacc);
     }
 }
 
-__global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnArgs a) {
+__global__ __launch_bounds__(256, ATTN_FWD_OCC) void attn_fwd_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) char smem[2 * 2 * 8192];
   const BlockCoord bc = attn_block((a.S + 127) / 128, a.Hq, a.Hkv, a.B);
   const int qb = bc.blk, h = bc.h, b = bc.b;
@@ -216,10 +231,10 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnArgs a) {
   if (a.causal) kend = min(kend, qb * 128 + 128);
   const int nt = (kend + 63) / 64;
 
-  f32x16 o0, o1;
+  f32x16 o0, o1, lacc;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) { o0[r] = 0.f; o1[r] = 0.f; }
-  float m = -1e30f, l = 0.f;
+  for (int r = 0; r < 16; ++r) { o0[r] = 0.f; o1[r] = 0.f; lacc[r] = 0.f; }
+  float m = -1e30f;
 
   uint4 rk[2], rv[2];
   load64(kbase, a.ldk, 0, S, rk);
@@ -238,8 +253,8 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnArgs a) {
     if (active) {
       // boundary tiles (past kvlen, or crossing this wave's causal diagonal) take the masked path
       const int kfull = a.causal ? min(kvlen, q0 + 1) : kvlen;
-      if ((t + 1) * 64 <= kfull) fwd_tile<false>(Kl, Vl, qf, o0, o1, m, l, c, t * 64, kvlen, myq, false, lane);
-      else fwd_tile<true>(Kl, Vl, qf, o0, o1, m, l, c, t * 64, kvlen, myq, a.causal, lane);
+      if ((t + 1) * 64 <= kfull) fwd_tile<false>(Kl, Vl, qf, o0, o1, lacc, m, c, t * 64, kvlen, myq, false, lane);
+      else fwd_tile<true>(Kl, Vl, qf, o0, o1, lacc, m, c, t * 64, kvlen, myq, a.causal, lane);
     }
     if (t + 1 < nt) {
       char* nx = smem + ((t + 1) & 1) * 16384;
@@ -249,7 +264,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnArgs a) {
     __syncthreads();
   }
   if (!active || myq >= S) return;
-  const float lt = l + __shfl_xor(l, 32, 64);
+  const float lt = lacc[0];
   const float inv = 1.0f / lt;
   bf16* orow = a.o + ((long)b * S + myq) * a.ldo + h * 64;
 #pragma unroll
@@ -409,7 +424,10 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kv_kernel(AttnArgs a) {
     const float* lse_l = LD + buf * 128;
     // boundary chunks: past S (query tail), this wave's keys past kvlen, or crossing the causal diagonal
     const bool full = (qc + 64 <= S) && (kw0 + 32 <= kvlen) && (!a.causal || kw0 + 31 <= qc);
-    if (full) bwd_kv_chunk<false>(Ql, Dl, lse_l, lse_l + 64, kf, vf, dk0, dk1, dv0, dv1, c, qc, S, mykey, kvlen, false, lane);
+    if (kw0 >= kvlen) {
+      // every key of this wave is padding or past S (e.g. the last key block of InternViT's 1025 tokens): its dK/dV
+      // stay zero, the wave only helps stage
+    } else if (full) bwd_kv_chunk<false>(Ql, Dl, lse_l, lse_l + 64, kf, vf, dk0, dk1, dv0, dv1, c, qc, S, mykey, kvlen, false, lane);
     else bwd_kv_chunk<true>(Ql, Dl, lse_l, lse_l + 64, kf, vf, dk0, dk1, dv0, dv1, c, qc, S, mykey, kvlen, a.causal, lane);
     if (it + 1 < nit) commit(buf ^ 1, rq, rd, ldv);
     __syncthreads();
@@ -490,7 +508,7 @@ __device__ __forceinline__ void bwd_dq_tile(const char* Kl, const char* Vl, cons
     }
 }
 
-__global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnArgs a) {
+__global__ __launch_bounds__(256, ATTN_DQ_OCC) void attn_bwd_dq_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) char smem[2 * 2 * 8192];
   const BlockCoord bc = attn_block((a.S + 127) / 128, a.Hq, a.Hkv, a.B);
   const int qb = bc.blk, h = bc.h, b = bc.b;
