@@ -24,7 +24,7 @@ HIP events on its launch stream during the timed steps, against the 2.5 PFLOP/s 
 per launch from the rocprofv3 FETCH_SIZE / WRITE_SIZE passes recorded in profiles/*_fc1_traffic.json
 (tools/pmc_traffic.py), when one matches the workload.
 cpu_baseline: the oracle (CPU fp32 PyTorch restatement, oracle/) forward+backward of one full-size sample on
-the host cores, rank 0, N = 1 only.
+the host cores (1 warmup + median of 3), rank 0, N = 1 only.
 """
 from __future__ import annotations
 
@@ -78,19 +78,30 @@ def base_gflop(cfg) -> float:
     return (fwd + 2 * fwd - patch) / 1e9
 
 
+def _timed(fn, warmup=1, reps=3):
+    """SURVEY.md §8d CPU protocol: 1 warmup + median of 3."""
+    for _ in range(warmup):
+        fn()
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        fn()
+        ts.append(time.perf_counter() - t0)
+    return sorted(ts)[len(ts) // 2]
+
+
 def cpu_baseline_vla(cfg, s_text, n_loss, threads):
-    """Oracle fwd+bwd of ONE full-size sample on the host (bounded ~10-30 s)."""
+    """Oracle fwd+bwd of ONE full-size sample on the host, 1 warmup + median of 3 (~12 s each)."""
     from oracle import vla_oracle as O
     from simlingo_amd.params import init_params
     from simlingo_amd.synthetic import make_batch
     torch.set_num_threads(threads)
     P = init_params(cfg, seed=0, lora_b_std=0.02)
     ex = make_batch(cfg, B=1, s_text=s_text, n_loss=n_loss, seed=1234)
-    t0 = time.perf_counter()
-    O.loss_and_grads(P, cfg, ex)
-    dt = time.perf_counter() - t0
+    dt = _timed(lambda: O.loss_and_grads(P, cfg, ex))
     return {"value": 1.0 / dt, "unit": "samples/s", "cores": threads, "kind": "port",
-            "sample": f"1 sample fwd+bwd (S_llm={s_text + cfg.img_tokens + cfg.n_queries}), fp32, {dt:.1f} s"}
+            "sample": f"1 sample fwd+bwd (S_llm={s_text + cfg.img_tokens + cfg.n_queries}), fp32, "
+                      f"1 warmup + median of 3: {dt:.1f} s"}
 
 
 def cpu_baseline_base(cfg, threads):
@@ -100,11 +111,9 @@ def cpu_baseline_base(cfg, threads):
     torch.set_num_threads(threads)
     P = init_base_params(cfg, seed=0)
     ex = make_base_batch(cfg, B=1, seed=1234)
-    t0 = time.perf_counter()
-    O.loss_and_grads(P, cfg, ex)
-    dt = time.perf_counter() - t0
+    dt = _timed(lambda: O.loss_and_grads(P, cfg, ex))
     return {"value": 1.0 / dt, "unit": "samples/s", "cores": threads, "kind": "port",
-            "sample": f"1 sample fwd+bwd (S={cfg.seq}, 2 CLIP tiles), fp32, {dt:.1f} s"}
+            "sample": f"1 sample fwd+bwd (S={cfg.seq}, 2 CLIP tiles), fp32, 1 warmup + median of 3: {dt:.1f} s"}
 
 
 def setup_vla(args, dev, world, rank):

@@ -26,6 +26,17 @@ SHAPES = {  # name: (M, N, K, layout)
     "llm_down": (6384, 896, 4864, K.GEMM_NT),
     "llm_gu_dgrad": (6384, 896, 9728, K.GEMM_NN),
     "sq8192": (8192, 8192, 8192, K.GEMM_NT),
+    # weight gradients with a transposed (feature-major) copy of the forward activation X:
+    # TT: dW = dY^T . Xt^T  (A = dY [tok][out] MN-contiguous, B = Xt [in][tok] K-contiguous)
+    # NN: dW^T = Xt . dY     (A = Xt K-contiguous, B = dY [tok][out] MN-contiguous; output transposed)
+    "vit_fc1_wgrad_tt": (4096, 1024, 16400, K.GEMM_TT),
+    "vit_fc1_wgrad_nn": (1024, 4096, 16400, K.GEMM_NN),
+    "vit_fc2_wgrad_tt": (1024, 4096, 16400, K.GEMM_TT),
+    "vit_fc2_wgrad_nn": (4096, 1024, 16400, K.GEMM_NN),
+    "vit_qkv_wgrad_tt": (3072, 1024, 16400, K.GEMM_TT),
+    "vit_qkv_wgrad_nn": (1024, 3072, 16400, K.GEMM_NN),
+    "vit_proj_wgrad_tt": (1024, 1024, 16400, K.GEMM_TT),
+    "vit_proj_wgrad_nn": (1024, 1024, 16400, K.GEMM_NN),
 }
 VARIANTS = [int(v) for v in os.environ.get("VARIANTS", "1,2,3,4,5,6").split(",")]
 dev = torch.device("cuda")
