@@ -94,7 +94,8 @@ __global__ __launch_bounds__(256) void colsum_kernel(const void* xv, long ldx, l
 #pragma unroll
     for (int e = 0; e < 4; ++e) lsv[e] = ls[c0 + e];
   }
-  for (long r = blockIdx.x; live && r < M; r += gridDim.x) {
+#pragma unroll 4
+  for (long r = blockIdx.x; live && r < M; r += gridDim.x) {  // unrolled: 4 rows of loads in flight per thread
     float v[4];
     if (MODE == 0) {
       const bf16x4 t = *reinterpret_cast<const bf16x4*>((const bf16*)xv + r * ldx + c0);
