@@ -128,6 +128,10 @@ typedef struct slx_norm_desc {
   int y_f32;                  /* 1: y rows are f32 (ldy in floats) instead of bf16               */
   void* dx_bf16; int64_t lddx_bf16; /* bwd, optional: bf16 copy of the (accumulated) dx rows, written
                                        in the same pass (the next dgrad GEMM's operand; no cast kernel) */
+  /* bwd, optional (D <= 1024, no pixel shuffle, dx_accumulate): the slx_ls_branch_bwd of the residual branch that
+   * precedes this norm in the backward, applied to the updated dx rows in the same pass: ls_g = bf16(dx * ls),
+   * ls_dls += sum dx * ls_y, ls_dbias += sum dx * ls (InternViT x = x_in + ls * branch(...), ls != NULL)     */
+  const float* ls; const void* ls_y; int64_t ld_ls_y; void* ls_g; int64_t ld_ls_g; float* ls_dls; float* ls_dbias;
 } slx_norm_desc;
 int slx_norm_fwd(const slx_norm_desc* d, slx_stream_t stream);
 int slx_norm_bwd(const slx_norm_desc* d, const float* dy, int64_t lddy, float* dx, int64_t lddx,
@@ -194,7 +198,8 @@ typedef struct {
   const float* dt; int64_t lddt;      /* f32 [M, >= 32*nsites] */
   const void* A[4];                   /* bf16 [32, Kin] per site */
   const uint32_t* bits[4]; int64_t ldbits;
-  float* dA[4];                       /* f32 [32, Kin] per site, accumulated */
+  float* dA[4];                       /* f32 [32, Kin] per site, accumulated; all NULL: dx only (the dA pass can
+                                         then run on another stream: nothing downstream in the backward reads it) */
   float* dx; int64_t lddx;            /* f32 [M, Kin] or NULL (no input gradient) */
   void* dx_bf16; int64_t lddx_bf16;   /* optional bf16 [M, Kin] output instead of updating dx in place */
   float p;

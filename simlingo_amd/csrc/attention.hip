@@ -14,11 +14,11 @@
 // double-buffered through LDS. Scores are computed transposed (S^T = K Q^T) so each lane owns one
 // query column: the row max needs one cross-half shuffle, the P^T accumulator feeds the P.V MFMA
 // directly as its B operand, and V is read with ds_read_b64_tr_b16 in the matching k order.
-// Backward: three launches, no atomics. delta = rowsum(dO*O); a dK/dV pass (one workgroup = 4 waves =
-// 128 keys of one (b, kv-head), sweeping the GQA group's q-heads x 64-query chunks, S and dP recomputed
-// with the key on the lane so their accumulators feed dV^T/dK^T directly); and a dQ pass shaped like the
-// forward (128 queries per workgroup, K/V tiles through LDS, dS^T in registers, dQ^T += K^T dS^T).
-// Summing dQ over key blocks with f32 atomics instead (one kernel) was bound by the ~1.3 TB/s atomic rate.
+// Backward: two launches, no atomics. First a dQ pass shaped like the forward (128 queries per workgroup, K/V tiles
+// through LDS, dS^T in registers, dQ^T += K^T dS^T) that also computes delta = rowsum(dO*O) per query in its prologue
+// and stores it; then a dK/dV pass (one workgroup = 4 waves = 128 keys of one (b, kv-head), sweeping the GQA group's
+// q-heads x 64-query chunks, S and dP recomputed with the key on the lane so their accumulators feed dV^T/dK^T
+// directly). Summing dQ over key blocks with f32 atomics instead (one kernel) was bound by the ~1.3 TB/s atomic rate.
 #include "common.h"
 #include "../../include/slx.h"
 
@@ -282,27 +282,6 @@ __global__ __launch_bounds__(256, ATTN_FWD_OCC) void attn_fwd_kernel(AttnArgs a)
   if (hl == 0 && a.lse) a.lse[((long)b * a.Hq + h) * S + myq] = m + __log2f(lt);
 }
 
-// delta[b,h,q] = sum_d dO[q,d] * O[q,d]   (one thread per (token, head))
-__global__ void attn_bwd_delta_kernel(AttnArgs a) {
-  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long total = (long)a.B * a.S * a.Hq;
-  if (idx >= total) return;
-  const int h = idx % a.Hq;
-  const long tok = idx / a.Hq;
-  const int b = tok / a.S, s = tok % a.S;
-  const bf16* o = a.o + tok * a.ldo + h * 64;
-  const bf16* d = a.dout + tok * a.lddo + h * 64;
-  float acc = 0.f;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const bf16x8 x = *reinterpret_cast<const bf16x8*>(o + 8 * i);
-    const bf16x8 y = *reinterpret_cast<const bf16x8*>(d + 8 * i);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc += (float)x[j] * (float)y[j];
-  }
-  const_cast<float*>(a.delta)[((long)b * a.Hq + h) * a.S + s] = acc;
-}
-
 // ---- backward, dK/dV pass: one workgroup = 4 waves = 128 keys of one (b, kv-head); sweeps every q-head of
 // the group x 64-query chunks (Q, dO, lse, delta staged through LDS). S and dP are computed with the key on
 // the lane, so their accumulators are the B operands of dV^T += dO^T P and dK^T += Q^T dS. dK/dV of the
@@ -529,14 +508,24 @@ __global__ __launch_bounds__(256, ATTN_DQ_OCC) void attn_bwd_dq_kernel(AttnArgs 
     const int qr = min(myq, S - 1);
     const bf16* qrow = a.q + ((long)b * S + qr) * a.ldq + h * 64;
     const bf16* drow = a.dout + ((long)b * S + qr) * a.lddo + h * 64;
+    const bf16* orow = a.o + ((long)b * S + qr) * a.ldo + h * 64;
+    bf16x8 of[4];
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) {
       qf[kk] = *reinterpret_cast<const bf16x8*>(qrow + 16 * kk + 8 * hl);
       df[kk] = *reinterpret_cast<const bf16x8*>(drow + 16 * kk + 8 * hl);
+      of[kk] = *reinterpret_cast<const bf16x8*>(orow + 16 * kk + 8 * hl);
     }
     const long li = ((long)b * a.Hq + h) * S + qr;
     lse = a.lse[li];
-    dlt = a.delta[li];
+    // delta = rowsum(dO * O) of this query (the lane pair l, l^32 holds the two 32-dim halves); written for the
+    // dK/dV pass, which runs after this one
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dlt = __builtin_fmaf((float)df[kk][j], (float)of[kk][j], dlt);
+    dlt += __shfl_xor(dlt, 32, 64);
+    if (hl == 0 && active && myq < S) const_cast<float*>(a.delta)[li] = dlt;
   }
   int kend = kvlen;
   if (a.causal) kend = min(kend, qb * 128 + 128);
@@ -691,12 +680,10 @@ extern "C" int slx_attn_bwd(const slx_attn_desc* d, const slx_attn_bwd_desc* g, 
   a.dv_acc = f32kv ? g->dv_acc : nullptr;
   a.dk = (bf16*)g->dk; a.dv = (bf16*)g->dv; a.lddk = g->lddk; a.lddv = g->lddv;
   const long ntok = (long)a.B * a.S;
-  {
-    const long total = ntok * a.Hq;
-    hipLaunchKernelGGL(attn_bwd_delta_kernel, dim3((total + 255) / 256), dim3(256), 0, st, a);
-    SLX_LAUNCH_CHECK("slx_attn_bwd(delta)");
-  }
   const int nblk = (a.S + 127) / 128;
+  // dQ pass first: it computes delta = rowsum(dO * O) per query in its prologue and stores it for the dK/dV pass
+  hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3(nblk * a.Hq * a.B), dim3(256), 0, st, a);
+  SLX_LAUNCH_CHECK("slx_attn_bwd(dq)");
   {  // split a GQA group's q-heads over workgroups until the dK/dV grid fills the chip (~2 per CU)
     const int G = a.Hq / a.Hkv, base = nblk * a.Hkv * a.B;
     int ns = (512 + base - 1) / base;
@@ -707,8 +694,6 @@ extern "C" int slx_attn_bwd(const slx_attn_desc* d, const slx_attn_bwd_desc* g, 
   }
   hipLaunchKernelGGL(attn_bwd_kv_kernel, dim3(nblk * a.Hkv * a.nsplit * a.B), dim3(256), 0, st, a);
   SLX_LAUNCH_CHECK("slx_attn_bwd(dk/dv)");
-  hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3(nblk * a.Hq * a.B), dim3(256), 0, st, a);
-  SLX_LAUNCH_CHECK("slx_attn_bwd(dq)");
   // finalize: f32 -> bf16, summing head-split partials and applying the RoPE transpose where asked
   auto conv = [&](const float* src, int heads, bf16* dst, long ld, bool rope, int nsplit) -> int {
     if ((rope && g->rope_cos) || nsplit > 1) {

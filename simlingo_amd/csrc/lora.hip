@@ -416,7 +416,7 @@ extern "C" int slx_dropout_bits(const slx_dropout_bits_desc* d, slx_stream_t str
 
 template <int NS>
 static void launch_bwd(const LoraBwdArgs& a, dim3 grid, hipStream_t st) {
-  hipLaunchKernelGGL(lora_da_kernel<NS>, grid, dim3(256), 0, st, a);
+  if (a.dA[0]) hipLaunchKernelGGL(lora_da_kernel<NS>, grid, dim3(256), 0, st, a);
   if (a.dx)
     hipLaunchKernelGGL(lora_dx_kernel<NS>, dim3((unsigned)(a.Kin / 128), (unsigned)((a.M + 63) / 64)), dim3(256), 0, st, a);
 }
@@ -427,6 +427,9 @@ extern "C" int slx_lora_bwd(const slx_lora_bwd_desc* d, slx_stream_t stream) {
   SLX_CHECK_ARG(d->p >= 0.f && d->p < 1.f, "slx_lora_bwd: 0 <= p < 1");
   SLX_CHECK_ARG(d->p == 0.f || (d->bits[0] && d->ldbits >= d->Kin / 32), "slx_lora_bwd: p > 0 needs the keep bits");
   SLX_CHECK_ARG(!d->dx_bf16 || d->dx, "slx_lora_bwd: dx_bf16 needs dx (the f32 base gradient it is added to)");
+  SLX_CHECK_ARG(d->dA[0] || d->dx, "slx_lora_bwd: nothing to do (neither dA nor dx)");
+  for (int i = 1; i < d->nsites; ++i)
+    SLX_CHECK_ARG((d->dA[i] != nullptr) == (d->dA[0] != nullptr), "slx_lora_bwd: dA for all sites or none");
   if (d->M == 0) return 0;
   LoraBwdArgs a;
   memset(&a, 0, sizeof(a));

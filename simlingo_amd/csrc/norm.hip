@@ -34,6 +34,8 @@ struct NormArgs {
   bf16* dxb; long lddxb;  // optional bf16 copy of dx (non-pixel-shuffle rows only)
   float* partial;   // unused (kept for ABI workspace sizing)
   float* dgamma; float* dbeta;
+  // fused layer-scale branch backward on the updated dx (slx_norm_desc.ls*)
+  const float* ls; const bf16* lsy; long ldlsy; bf16* lsg; long ldlsg; float* dls; float* dlsb;
 };
 
 template <int VPT, bool RMS>
@@ -157,13 +159,13 @@ __global__ __launch_bounds__(256) void norm_fwd_wave_kernel(NormArgs a) {
   }
 }
 
-template <bool RMS>
+template <bool RMS, bool LS>
 __global__ __launch_bounds__(256) void norm_bwd_wave_kernel(NormArgs a) {
-  __shared__ float cs[4][2][1024];
+  __shared__ float cs[4][LS ? 4 : 2][1024];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  float pg[16], pb[16];
+  float pg[16], pb[16], pl[16], pq[16];  // pl/pq: layer-scale branch sums (dls, dbias), LS only
 #pragma unroll
-  for (int i = 0; i < 16; ++i) { pg[i] = 0.f; pb[i] = 0.f; }
+  for (int i = 0; i < 16; ++i) { pg[i] = 0.f; pb[i] = 0.f; pl[i] = 0.f; pq[i] = 0.f; }
   for (long row = (long)blockIdx.x * 4 + w; row < a.rows; row += (long)gridDim.x * 4) {
     const float mu = RMS ? 0.f : a.mean[row];
     const float rs = a.rstd[row];
@@ -214,9 +216,23 @@ __global__ __launch_bounds__(256) void norm_bwd_wave_kernel(NormArgs a) {
         for (int e = 0; e < 4; ++e) ob[e] = (bf16)ov[e];
         *reinterpret_cast<bf16x4*>(a.dxb + row * a.lddxb + col) = ob;
       }
+      if constexpr (LS) {  // slx_ls_branch_bwd's per-element work on the row just produced (colsum_kernel<2>)
+        const float4 l4 = *reinterpret_cast<const float4*>(a.ls + col);
+        const bf16x4 yy = *reinterpret_cast<const bf16x4*>(a.lsy + row * a.ldlsy + col);
+        const float lv[4] = {l4.x, l4.y, l4.z, l4.w};
+        bf16x4 go;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float gv = ov[e] * lv[e];
+          go[e] = (bf16)gv;
+          pl[4 * i + e] += ov[e] * (float)yy[e];
+          pq[4 * i + e] += gv;
+        }
+        *reinterpret_cast<bf16x4*>(a.lsg + row * a.ldlsg + col) = go;
+      }
     }
   }
-  if (a.dgamma || a.dbeta) {  // 4 waves' column partials summed through LDS, then contiguous f32 atomics
+  if (a.dgamma || a.dbeta || LS) {  // 4 waves' column partials summed through LDS, then contiguous f32 atomics
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int col = (lane + 64 * i) * 4;
@@ -225,12 +241,20 @@ __global__ __launch_bounds__(256) void norm_bwd_wave_kernel(NormArgs a) {
       for (int e = 0; e < 4; ++e) {
         cs[w][0][col + e] = pg[4 * i + e];
         cs[w][1][col + e] = pb[4 * i + e];
+        if constexpr (LS) {
+          cs[w][LS ? 2 : 0][col + e] = pl[4 * i + e];
+          cs[w][LS ? 3 : 0][col + e] = pq[4 * i + e];
+        }
       }
     }
     __syncthreads();
     for (int c = threadIdx.x; c < a.D; c += 256) {
       if (a.dgamma) atomicAdd(a.dgamma + c, cs[0][0][c] + cs[1][0][c] + cs[2][0][c] + cs[3][0][c]);
       if (a.dbeta) atomicAdd(a.dbeta + c, cs[0][1][c] + cs[1][1][c] + cs[2][1][c] + cs[3][1][c]);
+      if constexpr (LS) {
+        atomicAdd(a.dls + c, cs[0][LS ? 2 : 0][c] + cs[1][LS ? 2 : 0][c] + cs[2][LS ? 2 : 0][c] + cs[3][LS ? 2 : 0][c]);
+        atomicAdd(a.dlsb + c, cs[0][LS ? 3 : 0][c] + cs[1][LS ? 3 : 0][c] + cs[2][LS ? 3 : 0][c] + cs[3][LS ? 3 : 0][c]);
+      }
     }
   }
 }
@@ -354,7 +378,8 @@ static int norm_bwd(NormArgs& a, float* dgamma, float* dbeta, int accumulate, hi
     if (dgamma) hipMemsetAsync(dgamma, 0, a.D * sizeof(float), st);
     if (dbeta) hipMemsetAsync(dbeta, 0, a.D * sizeof(float), st);
   }
-  if (a.D <= 1024) hipLaunchKernelGGL((norm_bwd_wave_kernel<RMS>), dim3(nblk), dim3(256), 0, st, a);
+  if (a.D <= 1024 && a.ls) hipLaunchKernelGGL((norm_bwd_wave_kernel<RMS, true>), dim3(nblk), dim3(256), 0, st, a);
+  else if (a.D <= 1024) hipLaunchKernelGGL((norm_bwd_wave_kernel<RMS, false>), dim3(nblk), dim3(256), 0, st, a);
   else if (a.D <= 2048) hipLaunchKernelGGL((norm_bwd_kernel<8, RMS>), dim3(nblk), dim3(256), 0, st, a);
   else hipLaunchKernelGGL((norm_bwd_kernel<16, RMS>), dim3(nblk), dim3(256), 0, st, a);
   SLX_LAUNCH_CHECK("slx_norm_bwd");
@@ -389,6 +414,12 @@ extern "C" int slx_norm_bwd(const slx_norm_desc* d, const float* dy, int64_t ldd
   a.partial = (dgamma || dbeta) ? partial_ws : nullptr;
   a.dxb = (bf16*)d->dx_bf16; a.lddxb = d->lddx_bf16;
   SLX_CHECK_ARG(!a.dxb || (!a.ps && a.lddxb % 4 == 0), "slx_norm_bwd: dx_bf16 needs plain rows and lddx_bf16 %% 4 == 0");
+  a.ls = d->ls; a.lsy = (const bf16*)d->ls_y; a.ldlsy = d->ld_ls_y; a.lsg = (bf16*)d->ls_g; a.ldlsg = d->ld_ls_g;
+  a.dls = d->ls_dls; a.dlsb = d->ls_dbias;
+  SLX_CHECK_ARG(!a.ls || (a.lsy && a.lsg && a.dls && a.dlsb && !a.ps && d->D <= 1024 && d->D % 4 == 0 && dx_accumulate &&
+                          a.ldlsy % 4 == 0 && a.ldlsg % 4 == 0),
+                "slx_norm_bwd: the fused layer-scale branch needs ls_y, ls_g, ls_dls, ls_dbias, D <= 1024, plain rows, "
+                "dx_accumulate and 4-element strides");
 
   return d->rms ? norm_bwd<true>(a, dgamma, dbeta, param_accumulate, (hipStream_t)stream)
                 : norm_bwd<false>(a, dgamma, dbeta, param_accumulate, (hipStream_t)stream);

@@ -636,9 +636,11 @@ class VLAEngine(EngineOps):
         for i in reversed(range(cfg.vit_layers)):
             p = f"vit.{i}."
             Ls = sv["vit"][i]
-            # x_out = x_mid + ls2 * (fc2(gelu(fc1(ln2(x_mid)))) )
-            K.call("slx_ls_branch_bwd", K.P(dxv), D, K.P(self.P[p + "ls2"]), K.P(Ls["y2"]), D, K.P(g), D, Mv, D,
-                   K.P(self.G[p + "ls2"]), K.P(self.G[p + "fc2.b"]), 1, K.P(self._ws(2 * 256 * D)), K.stream_ptr())
+            # x_out = x_mid + ls2 * (fc2(gelu(fc1(ln2(x_mid)))) ); below the top layer this branch backward ran fused
+            # into the previous LN1 backward (slx_norm_desc.ls*)
+            if i == cfg.vit_layers - 1:
+                K.call("slx_ls_branch_bwd", K.P(dxv), D, K.P(self.P[p + "ls2"]), K.P(Ls["y2"]), D, K.P(g), D, Mv, D,
+                       K.P(self.G[p + "ls2"]), K.P(self.G[p + "fc2.b"]), 1, K.P(self._ws(2 * 256 * D)), K.stream_ptr())
             K.mm(g, Ls["hact"], self.G[p + "fc2.w"], ta=True, tb=False, accumulate=True)
             dh = self._e(Mv, F_)
             K.mm(g, self.W[p + "fc2.w"], dh, tb=False, epi=K.EPI_GELU_BWD, aux=Ls["hpre"], ldaux=F_,
@@ -647,11 +649,11 @@ class VLAEngine(EngineOps):
             dh2 = self._e(Mv, D, dtype=F32)
             K.mm(dh, self.W[p + "fc1.w"], dh2, tb=False)
             del dh
+            # x_mid = x_in + ls1 * proj(attn(ln1(x_in))): its branch backward (g = ls1 * dx_mid, dls1, proj.b grad)
+            # fused into the LN2 backward that produces dx_mid
             K.norm_bwd(Ls["n2"], dh2, dxv, dx_accumulate=True, dgamma=self.G[p + "ln2.w"], dbeta=self.G[p + "ln2.b"],
-                       ws=self._ws(K.norm_ws_floats(D)), param_accumulate=True)
-            # x_mid = x_in + ls1 * proj(attn(ln1(x_in)))
-            K.call("slx_ls_branch_bwd", K.P(dxv), D, K.P(self.P[p + "ls1"]), K.P(Ls["y1"]), D, K.P(g), D, Mv, D,
-                   K.P(self.G[p + "ls1"]), K.P(self.G[p + "proj.b"]), 1, K.P(self._ws(2 * 256 * D)), K.stream_ptr())
+                       ws=self._ws(K.norm_ws_floats(D)), param_accumulate=True,
+                       ls_branch=(self.P[p + "ls1"], Ls["y1"], g, self.G[p + "ls1"], self.G[p + "proj.b"]))
             K.mm(g, Ls["o"], self.G[p + "proj.w"], ta=True, tb=False, accumulate=True)
             do = self._e(Mv, D)
             K.mm(g, self.W[p + "proj.w"], do, tb=False)
@@ -664,8 +666,12 @@ class VLAEngine(EngineOps):
             self._colsum(dqkv, self.G[p + "qkv.b"], 0)
             K.mm(dqkv, self.W[p + "qkv.w"], dh2, tb=False)
             del dqkv
+            nxt = None
+            if i > 0:  # the next (lower) layer's ls2 branch backward, fused onto dx_in
+                q = f"vit.{i - 1}."
+                nxt = (self.P[q + "ls2"], sv["vit"][i - 1]["y2"], g, self.G[q + "ls2"], self.G[q + "fc2.b"])
             K.norm_bwd(Ls["n1"], dh2, dxv, dx_accumulate=True, dgamma=self.G[p + "ln1.w"], dbeta=self.G[p + "ln1.b"],
-                       ws=self._ws(K.norm_ws_floats(D)), param_accumulate=True)
+                       ws=self._ws(K.norm_ws_floats(D)), param_accumulate=True, ls_branch=nxt)
             del dh2
             self._group_done(f"vit{i}")
         # ---------------- embeddings ----------------
@@ -696,12 +702,14 @@ class VLAEngine(EngineOps):
         drop = sv["drop"]
         keep = sv["llm"][i]["lora"]
         bits = [keep[site] for site in sites]
+        As = [self.W[f"llm.{i}.lora.{site}.a"] for site in sites]
         for j, site in enumerate(sites):
             K.mm(dys[j], tx[:, r * j:r * (j + 1)], self.G[f"llm.{i}.lora.{site}.b"], ta=True, tb=False, alpha=s,
                  accumulate=True)
-        K.lora_bwd(x, dtx, [self.W[f"llm.{i}.lora.{site}.a"] for site in sites], bits,
-                   [self.G[f"llm.{i}.lora.{site}.a"] for site in sites], dx=None if swiglu is not None else dx,
-                   dx_bf16=dx_bf16, p=drop)
+        # dA and the dx term in one launch. (Running the parameter-only part - dB GEMMs, dA - on a side stream was
+        # measured 6 ms/step slower: per-call event/stream overhead on the host and slower main-stream GEMMs.)
+        K.lora_bwd(x, dtx, As, bits, [self.G[f"llm.{i}.lora.{site}.a"] for site in sites],
+                   dx=None if swiglu is not None else dx, dx_bf16=dx_bf16, p=drop)
         if swiglu is not None:
             gu, dgu = swiglu
             M = x.shape[0]

@@ -147,16 +147,17 @@ def gemm(A, B, C, M, N, K, layout, lda, ldb, ldc, *, epi=EPI_STORE, alpha=1.0, b
     d.colsum = colsum.data_ptr() if colsum is not None else 0
     if maskbits is not None:
         d.maskbits, d.ldbits = maskbits.data_ptr(), maskbits.stride(0)
-    rw = _rem_ws.get(C.device)
+    sk = (C.device, torch.cuda.current_stream(C.device).cuda_stream)  # one workspace per stream (side-stream GEMMs)
+    rw = _rem_ws.get(sk)
     if rw is None:
-        rw = _rem_ws[C.device] = torch.empty(REM_WS_FLOATS, dtype=torch.float32, device=C.device)
+        rw = _rem_ws[sk] = torch.empty(REM_WS_FLOATS, dtype=torch.float32, device=C.device)
     d.rem_ws, d.rem_ws_floats = rw.data_ptr(), rw.numel()
     if colsum is not None:
         need = (int(M) + 63) // 64 * int(N)
-        ws = _colsum_ws.get(C.device)
+        ws = _colsum_ws.get(sk)
         if ws is None or ws.numel() < need:
             ws = torch.empty(max(need, 1 << 20), dtype=torch.float32, device=C.device)
-            _colsum_ws[C.device] = ws
+            _colsum_ws[sk] = ws
         d.colsum_ws = ws.data_ptr()
     if A.dtype == torch.float32:  # fp32 parity mode (csrc/precise.hip)
         if B.dtype != torch.float32 or C.dtype != torch.float32:
@@ -215,6 +216,8 @@ class NormDesc(ctypes.Structure):
         ("mean", c_vp), ("rstd", c_vp), ("rows", c_i64), ("D", c_int), ("eps", c_float),
         ("pixel_shuffle_grid", c_int), ("tokens_per_image", c_int), ("y_f32", c_int),
         ("dx_bf16", c_vp), ("lddx_bf16", c_i64),
+        ("ls", c_vp), ("ls_y", c_vp), ("ld_ls_y", c_i64), ("ls_g", c_vp), ("ld_ls_g", c_i64), ("ls_dls", c_vp),
+        ("ls_dbias", c_vp),
     ]
 
 
@@ -399,9 +402,17 @@ def norm_fwd(d: NormDesc):
 
 
 def norm_bwd(d: NormDesc, dy, dx, *, dx_accumulate=False, dgamma=None, dbeta=None, param_accumulate=False, ws=None,
-             lddx=None, dx_bf16=None):
-    """dx_bf16: optional bf16 [rows, >= D] view that receives a bf16 copy of the (accumulated) dx in the same pass."""
+             lddx=None, dx_bf16=None, ls_branch=None):
+    """dx_bf16: optional bf16 [rows, >= D] view that receives a bf16 copy of the (accumulated) dx in the same pass.
+    ls_branch = (ls f32 [D], y bf16 [rows, D], g bf16 [rows, D], dls f32 [D], dbias f32 [D]): the layer-scale branch
+    backward (slx_ls_branch_bwd, accumulating) fused onto the updated dx rows."""
     d.dx_bf16, d.lddx_bf16 = (dx_bf16.data_ptr(), dx_bf16.stride(0)) if dx_bf16 is not None else (0, 0)
+    if ls_branch is not None:
+        ls, y, g, dls, dbias = ls_branch
+        d.ls, d.ls_y, d.ld_ls_y, d.ls_g, d.ld_ls_g = ls.data_ptr(), y.data_ptr(), y.stride(0), g.data_ptr(), g.stride(0)
+        d.ls_dls, d.ls_dbias = dls.data_ptr(), dbias.data_ptr()
+    else:
+        d.ls = d.ls_y = d.ls_g = d.ls_dls = d.ls_dbias = 0
     check(lib().slx_norm_bwd(ctypes.byref(d), P(dy), dy.stride(0), P(dx), lddx if lddx is not None else dx.stride(0),
                              int(dx_accumulate), P(dgamma), P(dbeta), int(param_accumulate), P(ws), stream_ptr()),
           "slx_norm_bwd")
@@ -459,8 +470,9 @@ def lora_down(x, As, t, seeds, p=0.0, ldmask=None, bits=None):
 
 
 def lora_bwd(x, dt, As, bits, dAs, dx=None, dx_bf16=None, p=0.0):
-    """peft LoRA backward of the sites sharing x (one launch): dAs[j] (f32 [32, kin]) += dT_j^T drop_j(x) and, if dx
-    (f32 [M, kin]) is given, dx += sum_j drop_j'(dT_j As[j]) in place - or written as bf16(dx + ...) to dx_bf16.
+    """peft LoRA backward of the sites sharing x (one launch): dAs[j] (f32 [32, kin]) += dT_j^T drop_j(x) (dAs=None:
+    skipped) and, if dx (f32 [M, kin]) is given, dx += sum_j drop_j'(dT_j As[j]) in place - or written as
+    bf16(dx + ...) to dx_bf16.
     dt: f32 [M, >= 32 n] (dT_j = columns 32j..); bits[j]: keep bits from lora_down (None when p == 0)."""
     assert x.dtype == torch.bfloat16 and dt.dtype == torch.float32 and 1 <= len(As) <= 4
     M, kin = x.shape
@@ -468,10 +480,13 @@ def lora_bwd(x, dt, As, bits, dAs, dx=None, dx_bf16=None, p=0.0):
     d = LoraBwdDesc()
     d.x, d.ldx, d.M, d.Kin, d.r, d.nsites = P(x).value, x.stride(0), M, kin, 32, len(As)
     d.dt, d.lddt = P(dt).value, dt.stride(0)
-    for j, (a, g) in enumerate(zip(As, dAs)):
+    for j, a in enumerate(As):
         assert a.shape == (32, kin) and a.is_contiguous() and a.dtype == torch.bfloat16
-        assert g.shape == (32, kin) and g.is_contiguous() and g.dtype == torch.float32
-        d.A[j], d.dA[j] = a.data_ptr(), g.data_ptr()
+        d.A[j] = a.data_ptr()
+        if dAs is not None:  # None: dx only
+            g = dAs[j]
+            assert g.shape == (32, kin) and g.is_contiguous() and g.dtype == torch.float32
+            d.dA[j] = g.data_ptr()
         if p > 0:
             assert bits[j] is not None and bits[j].shape[0] == M
             d.bits[j] = bits[j].data_ptr()

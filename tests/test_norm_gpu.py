@@ -95,3 +95,47 @@ def test_norm_bwd_bf16_copy(dev, rms):
     K.norm_bwd(d, dy, dx, dx_accumulate=True, dx_bf16=dxb)
     torch.cuda.synchronize()
     assert torch.equal(dxb, dx.bfloat16())
+
+
+def test_layernorm_bwd_fused_ls_branch(dev):
+    """slx_norm_desc.ls*: the InternViT layer-scale branch backward (g = bf16(dx * ls), dls += sum dx * y,
+    dbias += sum dx * ls) fused onto the rows the LayerNorm backward just updated, against the separate
+    norm backward + slx_ls_branch_bwd of the same inputs."""
+    M, D = 1025 * 3, 1024
+    gen = torch.Generator(device=dev).manual_seed(5)
+    x = torch.randn(M, D, device=dev, generator=gen)
+    gamma, beta = torch.rand(D, device=dev, generator=gen) + 0.5, torch.randn(D, device=dev, generator=gen)
+    y = torch.empty(M, D, device=dev, dtype=torch.bfloat16)
+    mean, rstd = torch.empty(M, device=dev), torch.empty(M, device=dev)
+    d = K.norm_desc(x, gamma, beta, y, mean, rstd, M, D, 1e-6)
+    K.norm_fwd(d)
+    dy = torch.randn(M, D, device=dev, generator=gen)
+    dx0 = torch.randn(M, D, device=dev, generator=gen)
+    ls = torch.rand(D, device=dev, generator=gen) * 0.2
+    yb = torch.randn(M, D, device=dev, generator=gen).bfloat16()
+    outs = []
+    for fused in (False, True):
+        dx = dx0.clone()
+        dgm, dbt = torch.zeros(D, device=dev), torch.zeros(D, device=dev)
+        g = torch.empty(M, D, device=dev, dtype=torch.bfloat16)
+        dls, dbias = torch.full((D,), 0.5, device=dev), torch.full((D,), -0.25, device=dev)  # accumulate onto these
+        ws = torch.empty(K.norm_ws_floats(D), device=dev)
+        if fused:
+            K.norm_bwd(d, dy, dx, dx_accumulate=True, dgamma=dgm, dbeta=dbt, ws=ws, param_accumulate=True,
+                       ls_branch=(ls, yb, g, dls, dbias))
+        else:
+            K.norm_bwd(d, dy, dx, dx_accumulate=True, dgamma=dgm, dbeta=dbt, ws=ws, param_accumulate=True)
+            K.call("slx_ls_branch_bwd", K.P(dx), D, K.P(ls), K.P(yb), D, K.P(g), D, M, D, K.P(dls), K.P(dbias), 1,
+                   K.P(torch.empty(2 * 256 * D, device=dev)), K.stream_ptr())
+        torch.cuda.synchronize()
+        outs.append((dx, g, dls, dbias, dgm, dbt))
+    (dx_s, g_s, dls_s, db_s, gm_s, bt_s), (dx_f, g_f, dls_f, db_f, gm_f, bt_f) = outs
+    assert torch.equal(dx_s, dx_f) and torch.equal(g_s, g_f)
+    ref_dls = 0.5 + (dx_s.double() * yb.double()).sum(0)
+    ref_db = -0.25 + (dx_s.double() * ls.double()).sum(0)
+    for got in (dls_s, dls_f):
+        torch.testing.assert_close(got.double(), ref_dls, rtol=1e-4, atol=1e-3)
+    for got in (db_s, db_f):
+        torch.testing.assert_close(got.double(), ref_db, rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(gm_f, gm_s, rtol=1e-5, atol=1e-4)
+    torch.testing.assert_close(bt_f, bt_s, rtol=1e-5, atol=1e-4)
