@@ -83,6 +83,8 @@ struct AttnArgs {
   float* dk_acc; float* dv_acc;  // [nsplit][B*S, Hkv*64] f32 when GQA/RoPE (finalized), else null: direct bf16
   bf16* dk; bf16* dv; long lddk, lddv;
   int hsplit, nsplit;            // dK/dV pass: q-heads of a GQA group per workgroup, workgroups per group
+  bf16* dq; long lddq;           // dQ pass output: bf16, RoPE^T applied with rcos/rsin (pos = query index) if given
+  const float* rcos; const float* rsin;
 };
 
 // Stage 64 rows x 64 cols (bf16) of a token-major matrix into a swizzled LDS tile (8 KB).
@@ -560,12 +562,27 @@ __global__ __launch_bounds__(256, ATTN_DQ_OCC) void attn_bwd_dq_kernel(AttnArgs 
     __syncthreads();
   }
   if (!active || myq >= S) return;
-  float* qrow = a.dq_acc + ((long)b * S + myq) * (a.Hq * 64) + h * 64;
+  // dQ of this query: dims d and d + 32 (a RoPE pair) sit in dq0[r] / dq1[r] of the same lane, so the inverse
+  // rotation and the bf16 store need no exchange (no f32 workspace, no finalize launch)
+  bf16* qrow = a.dq + ((long)b * S + myq) * a.lddq + h * 64;
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
     const int d = 8 * g + 4 * hl;
-    *reinterpret_cast<float4*>(qrow + d) = make_float4(dq0[4 * g] * a.scale, dq0[4 * g + 1] * a.scale, dq0[4 * g + 2] * a.scale, dq0[4 * g + 3] * a.scale);
-    *reinterpret_cast<float4*>(qrow + 32 + d) = make_float4(dq1[4 * g] * a.scale, dq1[4 * g + 1] * a.scale, dq1[4 * g + 2] * a.scale, dq1[4 * g + 3] * a.scale);
+    bf16x4 v0, v1;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float x0 = dq0[4 * g + e] * a.scale, x1 = dq1[4 * g + e] * a.scale;
+      if (a.rcos) {
+        const float cs = a.rcos[(long)myq * 32 + d + e], sn = a.rsin[(long)myq * 32 + d + e];
+        const float y0 = x0 * cs + x1 * sn, y1 = x1 * cs - x0 * sn;  // RoPE^T (rope_pair, inverse)
+        x0 = y0;
+        x1 = y1;
+      }
+      v0[e] = (bf16)x0;
+      v1[e] = (bf16)x1;
+    }
+    *reinterpret_cast<bf16x4*>(qrow + d) = v0;
+    *reinterpret_cast<bf16x4*>(qrow + 32 + d) = v1;
   }
 }
 
@@ -672,6 +689,8 @@ extern "C" int slx_attn_bwd(const slx_attn_desc* d, const slx_attn_bwd_desc* g, 
   a.dout = (const bf16*)g->dout; a.lddo = g->lddo;
   a.delta = g->delta_ws;
   a.dq_acc = g->dq_acc;
+  a.dq = (bf16*)g->dq; a.lddq = g->lddq; a.rcos = g->rope_cos; a.rsin = g->rope_sin;
+  SLX_CHECK_ARG(a.dq && a.lddq % 4 == 0, "slx_attn_bwd: dq (bf16, lddq %% 4 == 0) is required");
   const bool gqa = d->Hq != d->Hkv;
   const bool f32kv = gqa || g->rope_cos;  // dK needs RoPE^T or the layout differs: finalize from f32
   SLX_CHECK_ARG(a.lse && a.delta && a.dq_acc, "slx_attn_bwd: lse, delta_ws and dq_acc are required");
@@ -713,7 +732,6 @@ extern "C" int slx_attn_bwd(const slx_attn_desc* d, const slx_attn_bwd_desc* g, 
     SLX_LAUNCH_CHECK("slx_attn_bwd(finalize)");
     return 0;
   };
-  if ((rc = conv(a.dq_acc, a.Hq, (bf16*)g->dq, g->lddq, true, 1))) return rc;
   if (f32kv) {
     if ((rc = conv(a.dk_acc, a.Hkv, (bf16*)g->dk, g->lddk, true, a.nsplit))) return rc;
     if ((rc = conv(a.dv_acc, a.Hkv, (bf16*)g->dv, g->lddv, false, a.nsplit))) return rc;

@@ -18,6 +18,7 @@ ap.add_argument("--warmup", type=int, default=2)
 ap.add_argument("--top", type=int, default=45)
 ap.add_argument("--grid", action="store_true", help="split kernels by launch grid (GEMM shape attribution)")
 ap.add_argument("--marker", default="adamw_kernel")
+ap.add_argument("--gaps", type=int, default=0, help="also list the N largest idle gaps between kernels")
 args = ap.parse_args()
 path = args.path
 if os.path.isdir(path):
@@ -49,3 +50,23 @@ print(f"{steps} steady steps: kernel-busy {busy / 1e6 / steps:.2f} ms/step, firs
 for (n, g), (cnt, d) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:args.top]:
     gs = f" grid {g}" if g else ""
     print(f"{d / 1e6 / steps:8.3f} ms/step calls/step {cnt / steps:6.1f} avg {d / cnt / 1e3:8.1f} us{gs}  {n}")
+
+if args.gaps:
+    # idle time between kernels of the steady steps (a kernel may overlap the previous: track the running max end)
+    gaps = []
+    run_end = sel[0][2]
+    prev = sel[0][0]
+    for name, s_, e_, *_ in sel[1:]:
+        if s_ > run_end:
+            gaps.append((s_ - run_end, prev, name))
+        if e_ > run_end:
+            run_end, prev = e_, name
+    idle = sum(g for g, _, _ in gaps)
+    print(f"idle between kernels: {idle / 1e6 / steps:.2f} ms/step over {len(gaps) / steps:.0f} gaps/step")
+    hist = defaultdict(lambda: [0, 0.0])
+    for g, a, b in gaps:
+        k = (a.replace("void ", "").replace("slx::", "")[:60], b.replace("void ", "").replace("slx::", "")[:60])
+        hist[k][0] += 1
+        hist[k][1] += g
+    for (a, b), (n, g) in sorted(hist.items(), key=lambda kv: -kv[1][1])[:args.gaps]:
+        print(f"{g / 1e6 / steps:7.3f} ms/step {n / steps:5.1f}x avg {g / n / 1e3:6.1f} us  {a}  ->  {b}")
