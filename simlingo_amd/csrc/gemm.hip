@@ -1028,25 +1028,26 @@ static double v_cost(const slx_gemm_desc* d, int v, int M, int batch) {
 template <int EPI, typename OutT>
 __global__ __launch_bounds__(256) void rows_epilogue_kernel(GemmArgs p, const float* __restrict__ part, int nsplit,
                                                             long split_stride, int colsum_row) {
-  // block = 64 columns x 4 row lanes; each thread walks rows ty, ty+4, ... summing the split partials
+  // block = 64 columns x 4 row lanes over rows [blockIdx.y * rpb, +rpb) (rpb = M when the colsum partial row is
+  // needed, else 4: one row per thread); each thread sums its rows' split partials, 8 loads in flight
   __shared__ float red[4][64];
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   const int n = blockIdx.x * 64 + tx;
+  const int rpb = p.colsum ? p.M : 4;
+  const int mend = min(p.M, (int)(blockIdx.y + 1) * rpb);
   float cs = 0.f;
   if (n < p.N) {
     OutT* C = reinterpret_cast<OutT*>(p.C);
-    for (int m = ty; m < p.M; m += 4) {
+    for (int m = blockIdx.y * rpb + ty; m < mend; m += 4) {
       const float* q = part + (long)m * p.N + n;
-      float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+      float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
       int y = 0;
-      for (; y + 4 <= nsplit; y += 4) {
-        a0 += q[(long)y * split_stride];
-        a1 += q[(long)(y + 1) * split_stride];
-        a2 += q[(long)(y + 2) * split_stride];
-        a3 += q[(long)(y + 3) * split_stride];
+      for (; y + 8 <= nsplit; y += 8) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) a[u] += q[(long)(y + u) * split_stride];
       }
-      for (; y < nsplit; ++y) a0 += q[(long)y * split_stride];
-      const float acc = (a0 + a1) + (a2 + a3);
+      for (; y < nsplit; ++y) a[0] += q[(long)y * split_stride];
+      const float acc = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
       epilogue_elem<EPI, OutT>(p, C, m, n, acc);
       if constexpr (EPI == EPI_STORE) cs += acc * p.alpha + (p.bias ? p.bias[n] : 0.f);
       else if constexpr (EPI == EPI_GELU_BWD) cs += acc * p.alpha * gelu_erf_grad((float)p.aux[(long)m * p.ldaux + n]);
@@ -1172,7 +1173,8 @@ static int gemm_launch(const slx_gemm_desc* d, int v, hipStream_t st, int mshift
 
 template <int EPI, typename OutT>
 static int launch_rows(GemmArgs& a, const float* part, int nsplit, long split_stride, int colsum_row, hipStream_t st) {
-  hipLaunchKernelGGL((rows_epilogue_kernel<EPI, OutT>), dim3((a.N + 63) / 64), dim3(256), 0, st, a, part, nsplit,
+  const unsigned gy = a.colsum ? 1u : (unsigned)((a.M + 3) / 4);
+  hipLaunchKernelGGL((rows_epilogue_kernel<EPI, OutT>), dim3((a.N + 63) / 64, gy), dim3(256), 0, st, a, part, nsplit,
                      split_stride, colsum_row);
   SLX_LAUNCH_CHECK("slx_gemm_bf16(remainder epilogue)");
   return 0;
