@@ -176,17 +176,21 @@ typedef struct {
 int slx_dropout_bits(const slx_dropout_bits_desc* d, slx_stream_t stream);
 /* LoRA down-projection of the sites sharing one input (peft LoraLayer.forward lora_A(dropout(x)),
  * llm.py:106-119 / peft lora/layer.py): t[:, 32j:32j+32] = drop_j(x) A_j^T, bf16 out; r must be 32, Kin % 32 == 0.
- * p > 0: the keep mask of site j is read from bits[j] ([M][ldbits] uint32, slx_dropout_bits); seed is unused. */
+ * p > 0: the keep mask of site j is read from bits[j] ([M][ldbits] uint32, slx_dropout_bits); seed is unused.
+ * A_j is passed in the packed fragment order slx_lora_pack_a writes (refreshed once per optimizer step).  */
 typedef struct {
   const void* x; int64_t ldx;         /* bf16 [M, Kin] */
   int64_t M; int Kin; int r; int nsites;
-  const void* A[4];                   /* bf16 [r, Kin] per site */
+  const void* A[4];                   /* bf16 packed A_j (slx_lora_pack_a), 32 * Kin elements per site */
   uint64_t seed[4];
   void* t; int64_t ldt;               /* bf16 [M, >= 32*nsites] */
   float p; int64_t ldmask;
   const uint32_t* bits[4]; int64_t ldbits;  /* keep bits per site (p > 0), ldbits >= Kin/32 words per row */
 } slx_lora_down_desc;
 int slx_lora_down(const slx_lora_down_desc* d, slx_stream_t stream);
+/* A [32, Kin] bf16 (row stride lda, the peft lora_A.weight layout) -> Af, the packed fragment order of slx_lora_down:
+ * Af[((2*(k/32) + (k/16)%2) * 64 + r + 32*((k/8)%2)) * 8 + k%8] = A[r][k]. Kin % 32 == 0.                    */
+int slx_lora_pack_a(const void* A, int64_t lda, int Kin, void* Af, slx_stream_t stream);
 /* LoRA backward of the sites sharing one input (peft lora_A backward + the dropout's input gradient):
  *   dA_j[32, Kin] += dT_j^T drop_j(x)                     (f32 atomics)
  *   dx[M, Kin]    += sum_j keep_j/(1-p) * (dT_j A_j)      (if dx; or bf16(dx + ...) written to dx_bf16 instead)
@@ -264,9 +268,10 @@ int slx_llava_merge_fwd(const void* src, int C, int64_t n_img, int npatch_h, int
                         int wu, int pool, const float* newline, void* out, slx_stream_t s);
 int slx_llava_merge_bwd(const float* dout, int C, int64_t n_img, int npatch_h, int npatch_w, int g, int r0, int hu, int c0,
                         int wu, int pool, void* dsrc, slx_stream_t s);
-/* table: n device-resident entries {src f32*, lds, dst*, ldd, rows, cols, float-bits scale, dst_f32}:
- * dst = src * scale (bf16, or f32 in the fp32 parity mode). Packs LoRA B (scaled by lora_alpha/r) into the
- * fused [W | s*B] operands. */
+/* table: n device-resident entries {src f32*, lds, dst*, ldd, rows, cols, float-bits scale, mode}:
+ * dst = src * scale, mode 0 bf16, 1 f32 (the fp32 parity mode), 2 bf16 in slx_lora_pack_a's fragment order
+ * (rows == 32). Packs LoRA B (scaled by lora_alpha/r) into the fused [W | s*B] operands and LoRA A into the
+ * packed copies slx_lora_down reads, once per optimizer step. */
 int slx_pack_scaled(const int64_t* table, int n, slx_stream_t s);
 
 /* ---- KV-cached greedy decode (agent call, BASELINE configs[4]) -------------------------------------

@@ -12,6 +12,7 @@
 typedef __bf16 bf16;
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -101,6 +102,13 @@ __device__ __forceinline__ float silu(float x) { return x / (1.0f + __expf(-x));
 __device__ __forceinline__ float silu_grad(float x) {
   const float s = 1.0f / (1.0f + __expf(-x));
   return s * (1.0f + x * (1.0f - s));
+}
+
+// Packed A (slx_lora_pack_a / slx_pack_scaled mode 2, read by slx_lora_down): the B-operand fragments of v_mfma_f32_32x32x16_bf16 in lane
+// order, Af[((2*st + hh) * 64 + lane) * 8 + j] = A[lane & 31][32*st + 16*hh + 8*(lane >> 5) + j], so a wave reads one
+// contiguous KiB per fragment instead of touching 32 rows of A.
+__device__ __forceinline__ long lora_frag_index(int r, int k) {
+  return ((long)(2 * (k >> 5) + ((k >> 4) & 1)) * 64 + r + 32 * ((k >> 3) & 1)) * 8 + (k & 7);
 }
 
 // Counter-based hash RNG for the LoRA dropout masks: deterministic in (seed, index). One 32-bit hash per PAIR of

@@ -28,23 +28,29 @@ struct LoraDownArgs {
   long ldmask;
 };
 
-// Block = 32 rows x every site, 4 waves taking the k32 column steps w, w+4, w+8, ... (neighbouring waves read
-// neighbouring 64-B segments of a row), two steps per iteration with all loads issued before the MFMAs; the [32 x 32]
-// partials are summed through LDS. v_mfma_f32_32x32x16_bf16 with x rows as the A operand (lane: row l&31, columns
-// 8h..8h+7 and 16+8h..16+8h+7 of the step, h = l >> 5) and A_s rows as the B operand (lane: rank index l&31, the
-// same columns), straight from global memory. The dropout keep mask comes from the bits slx_dropout_bits wrote (one
-// 32-bit word per row and step): no hashing here.
+// Block = 32 rows x every site, 8 waves; wave w takes the step pairs (64 k = one 128-B line per row) w, w+8, ...
+// Per pair: x [32 x 64] is read with coalesced 16-B loads (8 rows x 128 B per instruction), scaled to
+// bf16(x / (1-p)) once and staged in a wave-private LDS tile (16-B chunks XOR-swizzled by row & 7: conflict-free
+// writes and fragment reads); each site then ANDs its keep bits into the fragments (2 ops per element) and runs
+// v_mfma_f32_32x32x16_bf16 against the packed A fragments. The next pair's global loads are issued before the
+// current pair's MFMAs. The 8 waves' [32 x 32] partials are summed through per-wave LDS slices.
 template <int NS>
-__global__ __launch_bounds__(256) void lora_down_kernel(LoraDownArgs a) {
-  __shared__ float red[NS][32][33];  // the 4 waves' partials, summed with LDS float atomics
+struct DownRegs {  // one pair's x pieces and keep words (double-buffered across pairs)
+  uint4 x[4];
+  uint32_t kw[NS][2];
+};
+
+template <int NS>
+__global__ __launch_bounds__(512) void lora_down_kernel(LoraDownArgs a) {
+  __shared__ __attribute__((aligned(16))) char xs[8][32 * 128];
+  __shared__ float red[8][32][33];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, r = lane & 31;
   const int m0 = blockIdx.x * 32;
-  const int gm = m0 + r;
-  const bool rowok = gm < a.M;
-  const bf16* xrow = a.x + (long)(rowok ? gm : 0) * a.ldx + 8 * h;
   const bool drop = a.p > 0.f;
   const float sc = drop ? 1.0f / (1.0f - a.p) : 1.0f;
-  const int nk = a.Kin / 32;
+  const int nk = a.Kin / 32, npair = (nk + 1) / 2;
+  const int srow = lane >> 3, sch = lane & 7;  // staging: row 8i + srow, 16-B chunk sch of the pair
+  char* xw = xs[w];
   f32x16 acc[NS];
 #pragma unroll
   for (int s = 0; s < NS; ++s)
@@ -53,58 +59,121 @@ __global__ __launch_bounds__(256) void lora_down_kernel(LoraDownArgs a) {
   bf16x8 z;
 #pragma unroll
   for (int j = 0; j < 8; ++j) z[j] = (bf16)0.f;
-  for (int s0 = w; s0 < nk; s0 += 8) {
-    bf16x8 xv[2][2], av[2][NS][2];
-    uint32_t kw[2][NS];
+  bf16x8 av[NS][2][2];  // A fragments of the current pair; site s is reloaded for the next pair after its MFMAs
+
+  auto load_x = [&](int pi, DownRegs<NS>& R) {
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {  // steps s0 and s0 + 4: every load first
-      const int st = s0 + 4 * q;
-      const bool ok = st < nk;
-      const int k0 = 32 * st;
-#pragma unroll
-      for (int hh = 0; hh < 2; ++hh)
-        xv[q][hh] = (ok && rowok) ? *reinterpret_cast<const bf16x8*>(xrow + k0 + 16 * hh) : z;
-#pragma unroll
-      for (int s = 0; s < NS; ++s) {
-#pragma unroll
-        for (int hh = 0; hh < 2; ++hh)
-          av[q][s][hh] = ok ? *reinterpret_cast<const bf16x8*>(a.A[s] + (long)r * a.Kin + k0 + 16 * hh + 8 * h) : z;
-        kw[q][s] = (drop && ok && rowok) ? a.bits[s][(long)gm * a.ldbits + st] : 0u;
-      }
+    for (int i = 0; i < 4; ++i) {
+      const int gm = m0 + 8 * i + srow, k = 64 * pi + 8 * sch;
+      R.x[i] = (gm < a.M && k < a.Kin) ? *reinterpret_cast<const uint4*>(a.x + (long)gm * a.ldx + k)
+                                       : make_uint4(0u, 0u, 0u, 0u);
     }
+    const int gm = m0 + r;
 #pragma unroll
-    for (int q = 0; q < 2; ++q)
+    for (int ss = 0; ss < 2; ++ss) {
+      const int st = 2 * pi + ss;
 #pragma unroll
       for (int s = 0; s < NS; ++s)
+        R.kw[s][ss] = (drop && st < nk && gm < a.M) ? a.bits[s][(long)gm * a.ldbits + st] : 0u;
+    }
+  };
+  auto load_a = [&](int pi, int s) {
+#pragma unroll
+    for (int ss = 0; ss < 2; ++ss) {
+      const int st = 2 * pi + ss;
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh)
+        av[s][ss][hh] = st < nk ? *reinterpret_cast<const bf16x8*>(a.A[s] + ((long)(2 * st + hh) * 64 + lane) * 8) : z;
+    }
+  };
+  auto process = [&](const DownRegs<NS>& R, int next) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      uint4 v = R.x[i];
+      if (drop) {  // bf16(x * sc), the rounding of peft's dropout output
+        uint32_t* u = reinterpret_cast<uint32_t*>(&v);
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+          const float lo = __uint_as_float(u[d] << 16) * sc, hi = __uint_as_float(u[d] & 0xFFFF0000u) * sc;
+          bf16x2 o;
+          o[0] = (bf16)lo;
+          o[1] = (bf16)hi;
+          u[d] = __builtin_bit_cast(uint32_t, o);
+        }
+      }
+      const int row = 8 * i + srow;
+      *reinterpret_cast<uint4*>(xw + row * 128 + ((sch ^ (row & 7)) << 4)) = v;
+    }
+    __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // wave-private tile written (LDS is in order per wave)
+    bf16x8 xf[2][2];
+#pragma unroll
+    for (int ss = 0; ss < 2; ++ss)
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh)
+        xf[ss][hh] = *reinterpret_cast<const bf16x8*>(xw + r * 128 + (((4 * ss + 2 * hh + h) ^ (r & 7)) << 4));
+    __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // fragments read before the next pair overwrites the tile
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss)
 #pragma unroll
         for (int hh = 0; hh < 2; ++hh) {
-          bf16x8 xm = xv[q][hh];
+          bf16x8 xm = xf[ss][hh];
           if (drop) {
-            const uint32_t b = (kw[q][s] >> (16 * hh + 8 * h)) & 0xFFu;
+            const uint32_t b = R.kw[s][ss] >> (16 * hh + 8 * h);
+            uint32_t* u = reinterpret_cast<uint32_t*>(&xm);
 #pragma unroll
-            for (int j = 0; j < 8; ++j) xm[j] = (bf16)((float)xv[q][hh][j] * ((b >> j) & 1u ? sc : 0.f));
+            for (int d = 0; d < 4; ++d) {
+              const uint32_t lo = (uint32_t)__builtin_amdgcn_sbfe((int)b, 2 * d, 1);
+              const uint32_t hi = (uint32_t)__builtin_amdgcn_sbfe((int)b, 2 * d + 1, 1);
+              u[d] &= (lo & 0xFFFFu) | (hi & 0xFFFF0000u);
+            }
           }
-          acc[s] = mfma32x32(xm, av[q][s][hh], acc[s]);
+          acc[s] = mfma32x32(xm, av[s][ss][hh], acc[s]);
         }
-  }
-  for (int i = threadIdx.x; i < NS * 32 * 33; i += 256) (&red[0][0][0])[i] = 0.f;
-  __syncthreads();
-#pragma unroll
-  for (int s = 0; s < NS; ++s)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) atomicAdd(&red[s][8 * (i >> 2) + 4 * h + (i & 3)][r], acc[s][i]);
-  __syncthreads();
-  // 32 rows x 32*NS outputs: thread -> (row, 4 columns) of one site per pass
-  for (int i = threadIdx.x; i < 32 * 8 * NS; i += 256) {
-    const int s = i / 256, row = (i >> 3) & 31, c0 = (i & 7) * 4;
-    const int m = m0 + row;
-    if (m < a.M) {
-      bf16x4 o;
-#pragma unroll
-      for (int c = 0; c < 4; ++c) o[c] = (bf16)red[s][row][c0 + c];
-      *reinterpret_cast<bf16x4*>(a.t + (long)m * a.ldt + 32 * s + c0) = o;
+      if (next >= 0) load_a(next, s);
     }
+  };
+
+  DownRegs<NS> R0, R1;
+  if (w < npair) {
+    load_x(w, R0);
+#pragma unroll
+    for (int s = 0; s < NS; ++s) load_a(w, s);
   }
+  for (int pi = w; pi < npair; pi += 16) {
+    const bool more = pi + 8 < npair;
+    if (more) load_x(pi + 8, R1);
+    process(R0, more ? pi + 8 : -1);
+    if (!more) break;
+    const bool more2 = pi + 16 < npair;
+    if (more2) load_x(pi + 16, R0);
+    process(R1, more2 ? pi + 16 : -1);
+  }
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) red[w][8 * (i >> 2) + 4 * h + (i & 3)][r] = acc[s][i];
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int o = threadIdx.x + 512 * q, row = o >> 5, c = o & 31;
+      float v = 0.f;
+#pragma unroll
+      for (int ww = 0; ww < 8; ++ww) v += red[ww][row][c];
+      if (m0 + row < a.M) a.t[(long)(m0 + row) * a.ldt + 32 * s + c] = (bf16)v;
+    }
+    __syncthreads();
+  }
+}
+
+// A [32][Kin] bf16 (row stride lda) -> packed fragment order (lora_frag_index)
+__global__ __launch_bounds__(256) void lora_pack_a_kernel(const bf16* __restrict__ A, long lda, int Kin,
+                                                          bf16* __restrict__ Af) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= 32L * Kin) return;
+  const int rr = (int)(i / Kin), k = (int)(i % Kin);
+  Af[lora_frag_index(rr, k)] = A[(long)rr * lda + k];
 }
 
 // ---- keep bits ---------------------------------------------------------------------------------------------------
@@ -381,12 +450,20 @@ extern "C" int slx_lora_down(const slx_lora_down_desc* d, slx_stream_t stream) {
   dim3 grid((unsigned)((d->M + 31) / 32));
   hipStream_t st = (hipStream_t)stream;
   switch (d->nsites) {
-    case 1: hipLaunchKernelGGL(lora_down_kernel<1>, grid, dim3(256), 0, st, a); break;
-    case 2: hipLaunchKernelGGL(lora_down_kernel<2>, grid, dim3(256), 0, st, a); break;
-    case 3: hipLaunchKernelGGL(lora_down_kernel<3>, grid, dim3(256), 0, st, a); break;
-    default: hipLaunchKernelGGL(lora_down_kernel<4>, grid, dim3(256), 0, st, a); break;
+    case 1: hipLaunchKernelGGL(lora_down_kernel<1>, grid, dim3(512), 0, st, a); break;
+    case 2: hipLaunchKernelGGL(lora_down_kernel<2>, grid, dim3(512), 0, st, a); break;
+    case 3: hipLaunchKernelGGL(lora_down_kernel<3>, grid, dim3(512), 0, st, a); break;
+    default: hipLaunchKernelGGL(lora_down_kernel<4>, grid, dim3(512), 0, st, a); break;
   }
   SLX_LAUNCH_CHECK("slx_lora_down");
+  return 0;
+}
+
+extern "C" int slx_lora_pack_a(const void* A, int64_t lda, int Kin, void* Af, slx_stream_t stream) {
+  SLX_CHECK_ARG(A && Af && Kin > 0 && Kin % 32 == 0 && lda >= Kin, "slx_lora_pack_a: A, Af, Kin %% 32, lda >= Kin");
+  hipLaunchKernelGGL(lora_pack_a_kernel, dim3((unsigned)((32L * Kin + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     (const bf16*)A, (long)lda, Kin, (bf16*)Af);
+  SLX_LAUNCH_CHECK("slx_lora_pack_a");
   return 0;
 }
 

@@ -450,8 +450,9 @@ __global__ void cast_rows_kernel(const float* src, long lds, bf16* dst, long ldd
 }
 
 // Batched 2-D scaled copy f32 -> bf16 (or f32, parity mode): entry e of `tab` =
-// {src, lds, dst, ldd, rows, cols, scale(bits), dst_f32}. Packs every LoRA B (times alpha/r) into the fused
-// [W | s*B] GEMM operands in one launch.
+// {src, lds, dst, ldd, rows, cols, scale(bits), mode}, mode 0 bf16 [rows][ldd], 1 f32 [rows][ldd], 2 bf16 in the
+// packed LoRA-A fragment order of slx_lora_down (rows == 32, ldd unused). Packs every LoRA B (times alpha/r) into the
+// fused [W | s*B] GEMM operands and every LoRA A into its fragment copy in one launch.
 __global__ void pack_scaled_kernel(const long long* tab, int n) {
   const int e = blockIdx.x;
   const long long* t = tab + 8 * (long)e;
@@ -460,11 +461,12 @@ __global__ void pack_scaled_kernel(const long long* tab, int n) {
   const long ldd = t[3];
   const long rows = t[4], cols = t[5];
   const float sc = __int_as_float((int)t[6]);
-  const bool f32 = t[7] != 0;
+  const int mode = (int)t[7];
   for (long i = (long)blockIdx.y * blockDim.x + threadIdx.x; i < rows * cols; i += (long)gridDim.y * blockDim.x) {
     const long r = i / cols, c = i % cols;
     const float v = src[r * lds + c] * sc;
-    if (f32) reinterpret_cast<float*>(t[2])[r * ldd + c] = v;
+    if (mode == 1) reinterpret_cast<float*>(t[2])[r * ldd + c] = v;
+    else if (mode == 2) reinterpret_cast<bf16*>(t[2])[lora_frag_index((int)r, (int)c)] = (bf16)v;
     else reinterpret_cast<bf16*>(t[2])[r * ldd + c] = (bf16)v;
   }
 }

@@ -215,6 +215,11 @@ class VLAEngine(EngineOps):
                 entries.append([a.data_ptr(), a.stride(0), ap.data_ptr(), ap.stride(0), r, a.shape[1],
                                 int(np.float32(1.0).view(np.int32)), int(self.precise)])
                 cats["apad." + site] = ap
+                if not self.precise:  # fragment-ordered copy read by slx_lora_down (mode 2)
+                    af = torch.empty(r * a.shape[1], dtype=torch.bfloat16, device=self.device)
+                    entries.append([a.data_ptr(), a.stride(0), af.data_ptr(), 0, r, a.shape[1],
+                                    int(np.float32(1.0).view(np.int32)), 2])
+                    cats["afrag." + site] = af
             self.cat.append(cats)
         self._pack_tab = torch.tensor(entries, dtype=torch.int64, device=self.device)
         self._pack_n = len(entries)
@@ -476,7 +481,8 @@ class VLAEngine(EngineOps):
                 K.mm(x, self.W[f"llm.{i}.lora.{site}.a"], t_out[:, r * j:r * (j + 1)])
             return {site: None for site in sites}
         bits = [self._lora_bits(i, site, x.shape[0], sv) for site in sites]
-        K.lora_down(x, [self.W[f"llm.{i}.lora.{site}.a"] for site in sites], t_out, seeds, p=sv["drop"], bits=bits)
+        K.lora_down(x, [self.cat[i]["afrag." + site] for site in sites], t_out, seeds, p=sv["drop"], bits=bits,
+                    packed=True)
         return dict(zip(sites, bits))
 
     def _lora_bits(self, i, site, M, sv):

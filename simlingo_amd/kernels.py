@@ -261,6 +261,7 @@ _vp, _i, _I, _f = c_vp, c_int, c_i64, c_float
 for _n, _a in {
     "slx_attn_fwd": [ctypes.POINTER(AttnDesc), _vp],
     "slx_lora_down": [ctypes.POINTER(LoraDownDesc), _vp],
+    "slx_lora_pack_a": [_vp, ctypes.c_int64, ctypes.c_int, _vp, _vp],
     "slx_lora_bwd": [ctypes.POINTER(LoraBwdDesc), _vp],
     "slx_dropout_bits": [ctypes.POINTER(DropoutBitsDesc), _vp],
     "slx_attn_bwd": [ctypes.POINTER(AttnDesc), ctypes.POINTER(AttnBwdDesc), _vp],
@@ -449,16 +450,31 @@ def dropout_bits(jobs, rows, p):
     check(lib().slx_dropout_bits(ctypes.byref(d), stream_ptr()), "slx_dropout_bits")
 
 
-def lora_down(x, As, t, seeds, p=0.0, ldmask=None, bits=None):
+def lora_pack_a(a, out=None):
+    """A [32, kin] bf16 (peft lora_A.weight layout) -> the packed fragment order slx_lora_down reads."""
+    assert a.dtype == torch.bfloat16 and a.dim() == 2 and a.shape[0] == 32 and a.stride(1) == 1
+    out = torch.empty(32 * a.shape[1], device=a.device, dtype=torch.bfloat16) if out is None else out
+    assert out.dtype == torch.bfloat16 and out.is_contiguous() and out.numel() == a.numel()
+    check(lib().slx_lora_pack_a(P(a), a.stride(0), a.shape[1], P(out), stream_ptr()), "slx_lora_pack_a")
+    return out
+
+
+def lora_down(x, As, t, seeds, p=0.0, ldmask=None, bits=None, packed=False):
     """t[:, 32j:32j+32] = drop_j(x) As[j]^T for the sites sharing x (one launch); p > 0: bits[j] (int32
-    [M, >= kin/32]) holds site j's keep mask (dropout_bits); seeds are not used by the kernel."""
+    [M, >= kin/32]) holds site j's keep mask (dropout_bits); seeds are not used by the kernel.
+    packed=True: As[j] are already in slx_lora_pack_a's fragment order (flat, 32 * kin elements); else the [32, kin]
+    matrices are packed here first (one extra launch per site)."""
     assert x.dtype == torch.bfloat16 and t.dtype == torch.bfloat16 and 1 <= len(As) <= 4
     M, kin = x.shape
     assert t.shape[0] == M and t.shape[1] >= 32 * len(As)
+    if not packed:
+        for a in As:
+            assert a.shape == (32, kin)
+        As = [lora_pack_a(a) for a in As]
     d = LoraDownDesc()
-    d.x, d.ldx, d.M, d.Kin, d.r, d.nsites = P(x).value, x.stride(0), M, kin, As[0].shape[0], len(As)
+    d.x, d.ldx, d.M, d.Kin, d.r, d.nsites = P(x).value, x.stride(0), M, kin, 32, len(As)
     for j, a in enumerate(As):
-        assert a.shape == (32, kin) and a.is_contiguous() and a.dtype == torch.bfloat16
+        assert a.numel() == 32 * kin and a.is_contiguous() and a.dtype == torch.bfloat16
         d.A[j] = a.data_ptr()
         d.seed[j] = int(seeds[j]) & ((1 << 64) - 1)
         if bits is not None and bits[j] is not None:

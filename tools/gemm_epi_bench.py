@@ -2,6 +2,8 @@
 fused epilogues (random operands, variants interleaved in one process):
   fc1      16400 x 4096 x 1024 NT, bias + GELU, bf16 out + bf16 pre-activation aux
   fc2bwd   16400 x 4096 x 1024 NN, GELU' against the bf16 aux, bf16 out, fc1.b column sums
+  nn_plain / nn_f32 / fc2bwd_nocs / nt_plain: the same shapes with plain bf16 / f32 stores, GELU' without the column
+           sums, and the fc1 NT shape without bias/GELU (epilogue ablations)
   fc2      16400 x 1024 x 4096 NT, bias + layer-scale residual (f32), f32 out + bf16 branch aux
   proj     16400 x 1024 x 1024 NT, same epilogue as fc2
 VARIANTS=0,2,5,7 (env) selects the variants (0 = the host cost model's choice)."""
@@ -26,6 +28,15 @@ def case(name):
         C, aux, bias = torch.empty(M, N, device=dev, dtype=bf), torch.empty(M, N, device=dev, dtype=bf), torch.randn(N, device=dev)
         return N, Kd, lambda v: K.gemm(A, B, C, M, N, Kd, K.GEMM_NT, Kd, Kd, N, epi=K.EPI_GELU, bias=bias, aux_out=aux,
                                        ldaux_out=N, variant=v)
+    if name in ("nn_plain", "nn_f32", "fc2bwd_nocs", "nt_plain"):  # epilogue ablations of the fc1/fc2-dgrad shapes
+        N, Kd = 4096, 1024
+        bt = (Kd, N) if name != "nt_plain" else (N, Kd)
+        A, B = torch.randn(M, Kd, device=dev).to(bf), (torch.randn(*bt, device=dev) * 0.03).to(bf)
+        C = torch.empty(M, N, device=dev, dtype=torch.float32 if name == "nn_f32" else bf)
+        aux = torch.randn(M, N, device=dev).to(bf)
+        lay, ldb = (K.GEMM_NT, Kd) if name == "nt_plain" else (K.GEMM_NN, N)
+        kw = dict(epi=K.EPI_GELU_BWD, aux=aux, ldaux=N) if name == "fc2bwd_nocs" else {}
+        return N, Kd, lambda v: K.gemm(A, B, C, M, N, Kd, lay, Kd, ldb, N, variant=v, **kw)
     if name == "fc2bwd":
         N, Kd = 4096, 1024
         A, B = torch.randn(M, Kd, device=dev).to(bf), (torch.randn(Kd, N, device=dev) * 0.03).to(bf)
