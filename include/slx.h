@@ -188,9 +188,10 @@ typedef struct {
   const uint32_t* bits[4]; int64_t ldbits;  /* keep bits per site (p > 0), ldbits >= Kin/32 words per row */
 } slx_lora_down_desc;
 int slx_lora_down(const slx_lora_down_desc* d, slx_stream_t stream);
-/* A [32, Kin] bf16 (row stride lda, the peft lora_A.weight layout) -> Af, the packed fragment order of slx_lora_down:
- * Af[((2*(k/32) + (k/16)%2) * 64 + r + 32*((k/8)%2)) * 8 + k%8] = A[r][k]. Kin % 32 == 0.                    */
-int slx_lora_pack_a(const void* A, int64_t lda, int Kin, void* Af, slx_stream_t stream);
+/* A [32, Kin] bf16 (row stride lda, the peft lora_A.weight layout) -> Af, a packed fragment order (Kin % 32 == 0):
+ * layout 0, read by slx_lora_down:        Af[((2*(k/32) + (k/16)%2) * 64 + r + 32*((k/8)%2)) * 8 + k%8] = A[r][k];
+ * layout 1, read by slx_lora_bwd (dx):    Af[((2*(k/32) + r/16) * 64 + k%32 + 32*((r/8)%2)) * 8 + r%8]  = A[r][k]. */
+int slx_lora_pack_a(const void* A, int64_t lda, int Kin, int layout, void* Af, slx_stream_t stream);
 /* LoRA backward of the sites sharing one input (peft lora_A backward + the dropout's input gradient):
  *   dA_j[32, Kin] += dT_j^T drop_j(x)                     (f32 atomics)
  *   dx[M, Kin]    += sum_j keep_j/(1-p) * (dT_j A_j)      (if dx; or bf16(dx + ...) written to dx_bf16 instead)
@@ -200,7 +201,7 @@ typedef struct {
   const void* x; int64_t ldx;         /* bf16 [M, Kin] (undropped forward input) */
   int64_t M; int Kin; int r; int nsites;
   const float* dt; int64_t lddt;      /* f32 [M, >= 32*nsites] */
-  const void* A[4];                   /* bf16 [32, Kin] per site */
+  const void* A[4];                   /* bf16 packed A_j, slx_lora_pack_a layout 1 (read by the dx term only) */
   const uint32_t* bits[4]; int64_t ldbits;
   float* dA[4];                       /* f32 [32, Kin] per site, accumulated; all NULL: dx only (the dA pass can
                                          then run on another stream: nothing downstream in the backward reads it) */
@@ -270,8 +271,8 @@ int slx_llava_merge_bwd(const float* dout, int C, int64_t n_img, int npatch_h, i
                         int wu, int pool, void* dsrc, slx_stream_t s);
 /* table: n device-resident entries {src f32*, lds, dst*, ldd, rows, cols, float-bits scale, mode}:
  * dst = src * scale, mode 0 bf16, 1 f32 (the fp32 parity mode), 2 bf16 in slx_lora_pack_a's fragment order
- * (rows == 32). Packs LoRA B (scaled by lora_alpha/r) into the fused [W | s*B] operands and LoRA A into the
- * packed copies slx_lora_down reads, once per optimizer step. */
+ * (rows == 32), 3 bf16 in layout 1 of slx_lora_pack_a. Packs LoRA B (scaled by lora_alpha/r) into the fused
+ * [W | s*B] operands and LoRA A into the packed copies slx_lora_down / slx_lora_bwd read, once per optimizer step. */
 int slx_pack_scaled(const int64_t* table, int n, slx_stream_t s);
 
 /* ---- KV-cached greedy decode (agent call, BASELINE configs[4]) -------------------------------------

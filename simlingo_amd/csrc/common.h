@@ -111,6 +111,13 @@ __device__ __forceinline__ long lora_frag_index(int r, int k) {
   return ((long)(2 * (k >> 5) + ((k >> 4) & 1)) * 64 + r + 32 * ((k >> 3) & 1)) * 8 + (k & 7);
 }
 
+// Packed A for the dx term of slx_lora_bwd (slx_lora_pack_a layout 1 / slx_pack_scaled mode 3): the A-operand
+// fragments of the transposed tile A^T dT^T, Ax[((2*ct + kb) * 64 + lane) * 8 + i] = A[16*kb + 8*(lane >> 5) + i][32*ct +
+// (lane & 31)].
+__device__ __forceinline__ long lora_dxfrag_index(int r, int k) {
+  return ((long)(2 * (k >> 5) + (r >> 4)) * 64 + (k & 31) + 32 * ((r >> 3) & 1)) * 8 + (r & 7);
+}
+
 // Counter-based hash RNG for the LoRA dropout masks: deterministic in (seed, index). One 32-bit hash per PAIR of
 // consecutive mask indices (idx >> 1); its low / high 16 bits are the uniforms of the even / odd element, and an
 // element is kept iff its uniform >= thr = round(p * 65536) (p = 0.1 -> 6554 / 65536 = 0.100006). The forward

@@ -167,13 +167,14 @@ __global__ __launch_bounds__(512) void lora_down_kernel(LoraDownArgs a) {
   }
 }
 
-// A [32][Kin] bf16 (row stride lda) -> packed fragment order (lora_frag_index)
-__global__ __launch_bounds__(256) void lora_pack_a_kernel(const bf16* __restrict__ A, long lda, int Kin,
+// A [32][Kin] bf16 (row stride lda) -> packed fragment order: layout 0 = slx_lora_down's (lora_frag_index),
+// 1 = the dx kernel's (lora_dxfrag_index)
+__global__ __launch_bounds__(256) void lora_pack_a_kernel(const bf16* __restrict__ A, long lda, int Kin, int layout,
                                                           bf16* __restrict__ Af) {
   const long i = (long)blockIdx.x * 256 + threadIdx.x;
   if (i >= 32L * Kin) return;
   const int rr = (int)(i / Kin), k = (int)(i % Kin);
-  Af[lora_frag_index(rr, k)] = A[(long)rr * lda + k];
+  Af[layout ? lora_dxfrag_index(rr, k) : lora_frag_index(rr, k)] = A[(long)rr * lda + k];
 }
 
 // ---- keep bits ---------------------------------------------------------------------------------------------------
@@ -241,16 +242,17 @@ __device__ __forceinline__ bf16x8 la_tr(const char* lds, int rbase, int cbase, i
 }
 
 // dA_j += dT_j^T drop_j(x): block = 128 columns of x (4 waves x 32) x a chunk of rows walked in 64-row sub-chunks.
-// Per sub-chunk x [64 x 128] and dT [64 x 32*NS] (f32 -> bf16) sit in swizzled LDS tiles and the keep words
-// [NS][64][4] next to them; per 16-row slice dT^T (transposed tile read) x masked x (transposed tile read) on
-// v_mfma_f32_32x32x16_bf16, accumulated in registers over the chunk, one set of f32 atomics per block at the end.
-// The next sub-chunk's global loads are issued into registers before the current one is multiplied.
+// Each staging thread holds 32 consecutive columns of one row, i.e. exactly one keep word per site, so the masks are
+// applied while the sub-chunk is committed to LDS: one tile per site of bf16(x / (1-p)) & keep_j (the rounding of
+// peft's dropout output), plus dT [64 x 32*NS] (f32 -> bf16), all [64][64] panels with the la_sw swizzle. The inner
+// loop is then transposed tile reads + v_mfma_f32_32x32x16_bf16 only (dT^T x masked x per 16-row slice), accumulated
+// in registers over the chunk, one set of f32 atomics per block at the end. The next sub-chunk's global loads are
+// issued into registers before the current one is multiplied.
 template <int NS>
-__global__ __launch_bounds__(256) void lora_da_kernel(LoraBwdArgs a) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * 8192 + 2 * 8192];  // x: 2 x [64][64] | dT: 2 x [64][64]
-  __shared__ uint32_t mk[NS][64][4];
-  char* xs = smem;
-  char* ts = smem + 2 * 8192;
+__global__ __launch_bounds__(256, 2) void lora_da_kernel(LoraBwdArgs a) {
+  constexpr int TP = (32 * NS + 63) / 64;                     // dT panels
+  __shared__ __attribute__((aligned(16))) char smem[(2 * NS + TP) * 8192];  // x_j: NS x 2 panels | dT: TP panels
+  char* ts = smem + 2 * NS * 8192;
   const int c0 = blockIdx.x * 128;
   const int mb = blockIdx.y * a.mchunk, me = min(a.M, mb + a.mchunk);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
@@ -278,29 +280,45 @@ __global__ __launch_bounds__(256) void lora_da_kernel(LoraBwdArgs a) {
         rt[c4][1] = ok ? *reinterpret_cast<const float4*>(a.dt + (long)gm * a.lddt + 8 * c + 4) : z;
       }
     }
-    if (drop) {
 #pragma unroll
-      for (int j = 0; j < NS; ++j) {  // word (row tid>>2, column word tid&3) of site j
-        const int g = mm + (tid >> 2);
-        rm[j] = g < me ? a.bits[j][(long)g * a.ldbits + (c0 >> 5) + (tid & 3)] : 0u;
-      }
-    }
+    for (int j = 0; j < NS; ++j)  // keep word (row srow, columns 32 (tid & 3) ..) of site j
+      rm[j] = drop ? (ok ? a.bits[j][(long)gm * a.ldbits + (c0 >> 5) + (tid & 3)] : 0u) : 0xFFFFFFFFu;
   };
   auto commit = [&]() {
 #pragma unroll
     for (int c4 = 0; c4 < 4; ++c4) {
       const int c = (tid & 3) * 4 + c4;
-      *reinterpret_cast<uint4*>(xs + (c >> 3) * 8192 + la_sw(srow, c & 7)) = rx[c4];
-      if (8 * c < 32 * NS) {
-        bf16x8 u;
-        u[0] = (bf16)rt[c4][0].x; u[1] = (bf16)rt[c4][0].y; u[2] = (bf16)rt[c4][0].z; u[3] = (bf16)rt[c4][0].w;
-        u[4] = (bf16)rt[c4][1].x; u[5] = (bf16)rt[c4][1].y; u[6] = (bf16)rt[c4][1].z; u[7] = (bf16)rt[c4][1].w;
-        *reinterpret_cast<bf16x8*>(ts + (c >> 3) * 8192 + la_sw(srow, c & 7)) = u;
-      }
-    }
-    if (drop) {
+      uint4 v = rx[c4];
+      uint32_t* u = reinterpret_cast<uint32_t*>(&v);
+      if (drop) {
 #pragma unroll
-      for (int j = 0; j < NS; ++j) mk[j][tid >> 2][tid & 3] = rm[j];
+        for (int d = 0; d < 4; ++d) {
+          bf16x2 o;
+          o[0] = (bf16)(__uint_as_float(u[d] << 16) * a.sc);
+          o[1] = (bf16)(__uint_as_float(u[d] & 0xFFFF0000u) * a.sc);
+          u[d] = __builtin_bit_cast(uint32_t, o);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < NS; ++j) {
+        uint4 m = v;
+        if (drop) {
+          uint32_t* mu = reinterpret_cast<uint32_t*>(&m);
+#pragma unroll
+          for (int d = 0; d < 4; ++d) {  // columns 8 c4 + 2d, +1 of this thread's 32 -> bits of rm[j]
+            const uint32_t lo = (uint32_t)__builtin_amdgcn_sbfe((int)rm[j], 8 * c4 + 2 * d, 1);
+            const uint32_t hi = (uint32_t)__builtin_amdgcn_sbfe((int)rm[j], 8 * c4 + 2 * d + 1, 1);
+            mu[d] &= (lo & 0xFFFFu) | (hi & 0xFFFF0000u);
+          }
+        }
+        *reinterpret_cast<uint4*>(smem + (2 * j + (c >> 3)) * 8192 + la_sw(srow, c & 7)) = m;
+      }
+      if (8 * c < 32 * NS) {
+        bf16x8 t;
+        t[0] = (bf16)rt[c4][0].x; t[1] = (bf16)rt[c4][0].y; t[2] = (bf16)rt[c4][0].z; t[3] = (bf16)rt[c4][0].w;
+        t[4] = (bf16)rt[c4][1].x; t[5] = (bf16)rt[c4][1].y; t[6] = (bf16)rt[c4][1].z; t[7] = (bf16)rt[c4][1].w;
+        *reinterpret_cast<bf16x8*>(ts + (c >> 3) * 8192 + la_sw(srow, c & 7)) = t;
+      }
     }
   };
   if (mb < me) {
@@ -312,22 +330,13 @@ __global__ __launch_bounds__(256) void lora_da_kernel(LoraBwdArgs a) {
     const bool more = mm + 64 < me;
     if (more) load(mm + 64);
 #pragma unroll
-    for (int ms = 0; ms < 4; ++ms) {
-      const bf16x8 xb = la_tr(xs + (w >> 1) * 8192, 16 * ms, 32 * (w & 1), lane);
+    for (int ms = 0; ms < 4; ++ms)
 #pragma unroll
       for (int j = 0; j < NS; ++j) {
+        const bf16x8 xm = la_tr(smem + (2 * j + (w >> 1)) * 8192, 16 * ms, 32 * (w & 1), lane);
         const bf16x8 ta = la_tr(ts + ((32 * j) >> 6) * 8192, 16 * ms, (32 * j) & 63, lane);
-        bf16x8 xm = xb;
-        if (drop) {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const int rr = 16 * ms + 8 * (e >> 2) + 4 * h + (e & 3);
-            xm[e] = (bf16)((float)xb[e] * ((mk[j][rr][w] >> (lane & 31)) & 1u ? a.sc : 0.f));
-          }
-        }
         acc[j] = mfma32x32(ta, xm, acc[j]);
       }
-    }
     __syncthreads();
     if (more) {
       commit();
@@ -343,87 +352,92 @@ __global__ __launch_bounds__(256) void lora_da_kernel(LoraBwdArgs a) {
     }
 }
 
-// dx += sum_j keep_j / (1-p) * (dT_j A_j) (f32 in place, or bf16(dx + ...) to dxb): block = 64 rows x 128 columns,
-// 4 waves x 32 columns, two 32-row tiles. A_j [32 x 128] (bf16) and the block's keep words [NS][64][4] are staged in
-// LDS with coalesced loads; v_mfma_f32_32x32x16_bf16 takes dT rows (f32 -> bf16, straight from global) as the A
-// operand and A_j^T (read back from LDS) as the B operand; the keep bits are applied in the accumulator layout.
-// Each lane's 32 dx values are loaded before anything else (the kernel is an HBM stream of dx).
+// dx += sum_j keep_j / (1-p) * (dT_j A_j) (f32 in place, or bf16(dx + ...) to dxb): block = one 32-row tile, 8 waves
+// taking the 32-column tiles w, w+8, ... Each wave computes the TRANSPOSED tile D[col][row] = sum_k A_j[k][col]
+// dT_j[row][k] on v_mfma_f32_32x32x16_bf16 (A operand: the packed dx fragments of A_j, one contiguous KiB each; B
+// operand: the wave's dT rows, f32 -> bf16, loaded once), so each lane owns one row and 4 consecutive columns per
+// register group: dx is read and written with 16-B accesses and the lane's keep bits of a site are one word. The next
+// column tile's loads are issued before the current tile's MFMAs.
 template <int NS>
-__global__ __launch_bounds__(256) void lora_dx_kernel(LoraBwdArgs a) {
-  __shared__ __attribute__((aligned(16))) bf16 As[NS][32][128];
-  __shared__ uint32_t mk[NS][64][4];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
-  const int c0 = blockIdx.x * 128, m0 = blockIdx.y * 64;
-  const int lc = 32 * w + (lane & 31), mycol = c0 + lc;
+struct DxRegs {
+  bf16x8 af[NS][2];
+  float4 dxv[4];
+  uint32_t kw[NS];
+};
+
+template <int NS>
+__global__ __launch_bounds__(512) void lora_dx_kernel(LoraBwdArgs a) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, r = lane & 31;
+  const int row = blockIdx.x * 32 + r;
+  const bool rok = row < a.M;
   const bool drop = a.bits[0] != nullptr;
-  float dxv[2][16];
-#pragma unroll
-  for (int rt = 0; rt < 2; ++rt)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int gm = m0 + 32 * rt + 8 * (i >> 2) + 4 * h + (i & 3);
-      dxv[rt][i] = gm < a.M ? a.dx[(long)gm * a.lddx + mycol] : 0.f;
-    }
-#pragma unroll
-  for (int j = 0; j < NS; ++j) {
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {  // 32 rows x 16 chunks of 16 B = 512 chunks per site
-      const int ci = tid + 256 * q, rr = ci >> 4, cc = ci & 15;
-      *reinterpret_cast<uint4*>(&As[j][rr][8 * cc]) =
-          *reinterpret_cast<const uint4*>(a.A[j] + (long)rr * a.Kin + c0 + 8 * cc);
-    }
-    if (drop) {
-      const int rr = tid >> 2, g = m0 + rr;
-      mk[j][rr][tid & 3] = g < a.M ? a.bits[j][(long)g * a.ldbits + (c0 >> 5) + (tid & 3)] : 0u;
-    }
-  }
-  __syncthreads();
-  bf16x8 af[NS][2];  // B operand: lane holds A_j[r = 16kb + 8h + i][lc]
+  const int nct = a.Kin / 32;
+  bf16x8 tb[NS][2];  // B operand: lane (row r, half h) holds dT_j[row][16 kb + 8 h + i]
 #pragma unroll
   for (int j = 0; j < NS; ++j)
 #pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
+    for (int kb = 0; kb < 2; ++kb) {
+      const float* tp = a.dt + (long)(rok ? row : 0) * a.lddt + 32 * j + 16 * kb + 8 * h;
+      const float4 f0 = rok ? *reinterpret_cast<const float4*>(tp) : make_float4(0.f, 0.f, 0.f, 0.f);
+      const float4 f1 = rok ? *reinterpret_cast<const float4*>(tp + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+      tb[j][kb][0] = (bf16)f0.x; tb[j][kb][1] = (bf16)f0.y; tb[j][kb][2] = (bf16)f0.z; tb[j][kb][3] = (bf16)f0.w;
+      tb[j][kb][4] = (bf16)f1.x; tb[j][kb][5] = (bf16)f1.y; tb[j][kb][6] = (bf16)f1.z; tb[j][kb][7] = (bf16)f1.w;
+    }
+  auto load = [&](int ct, DxRegs<NS>& R) {
 #pragma unroll
-      for (int i = 0; i < 8; ++i) af[j][kb][i] = As[j][16 * kb + 8 * h + i][lc];
+    for (int j = 0; j < NS; ++j) {
 #pragma unroll
-  for (int rt = 0; rt < 2; ++rt) {
-    const int trow = m0 + 32 * rt + (lane & 31);
-    const bool tok = trow < a.M;
-    // one accumulator per site (the keep masks differ per site), all MFMAs first, then the masked sum. (Re-zeroing
-    // one accumulator per site inside the loop miscompiled without dropout: rows 24-31 of each 32-row tile read
-    // stale values, 0.45 relative error - tools/dbg_lora2.py; tests/test_lora_dropout_gpu.py holds it to 1e-5.)
+      for (int kb = 0; kb < 2; ++kb)
+        R.af[j][kb] = *reinterpret_cast<const bf16x8*>(a.A[j] + ((long)(2 * ct + kb) * 64 + lane) * 8);
+      R.kw[j] = (drop && rok) ? a.bits[j][(long)row * a.ldbits + ct] : 0u;
+    }
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+      R.dxv[g] = rok ? *reinterpret_cast<const float4*>(a.dx + (long)row * a.lddx + 32 * ct + 8 * g + 4 * h)
+                     : make_float4(0.f, 0.f, 0.f, 0.f);
+  };
+  auto process = [&](int ct, const DxRegs<NS>& R) {
     f32x16 o[NS];
 #pragma unroll
     for (int j = 0; j < NS; ++j) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) o[j][i] = 0.f;
 #pragma unroll
-      for (int kb = 0; kb < 2; ++kb) {
-        bf16x8 tf;
-        const float* tp = a.dt + (long)trow * a.lddt + 32 * j + 16 * kb + 8 * h;
-        const float4 f0 = tok ? *reinterpret_cast<const float4*>(tp) : make_float4(0.f, 0.f, 0.f, 0.f);
-        const float4 f1 = tok ? *reinterpret_cast<const float4*>(tp + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
-        tf[0] = (bf16)f0.x; tf[1] = (bf16)f0.y; tf[2] = (bf16)f0.z; tf[3] = (bf16)f0.w;
-        tf[4] = (bf16)f1.x; tf[5] = (bf16)f1.y; tf[6] = (bf16)f1.z; tf[7] = (bf16)f1.w;
-        o[j] = mfma32x32(tf, af[j][kb], o[j]);
-      }
+      for (int kb = 0; kb < 2; ++kb) o[j] = mfma32x32(R.af[j][kb], tb[j][kb], o[j]);
     }
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int rr = 32 * rt + 8 * (i >> 2) + 4 * h + (i & 3);
-      float sum = 0.f;
+    for (int g = 0; g < 4; ++g) {
+      float v[4] = {R.dxv[g].x, R.dxv[g].y, R.dxv[g].z, R.dxv[g].w};
 #pragma unroll
-      for (int j = 0; j < NS; ++j) {
-        const float k = drop ? ((mk[j][rr][w] >> (lane & 31)) & 1u ? a.sc : 0.f) : 1.0f;
-        sum += k * o[j][i];
+      for (int e = 0; e < 4; ++e) {  // register 4g+e: column 8g + 4h + e of the tile
+        float sum = 0.f;
+#pragma unroll
+        for (int j = 0; j < NS; ++j) {
+          const float k = drop ? (((R.kw[j] >> (8 * g + 4 * h + e)) & 1u) ? a.sc : 0.f) : 1.0f;
+          sum += k * o[j][4 * g + e];
+        }
+        v[e] += sum;
       }
-      const int gm = m0 + rr;
-      if (gm < a.M) {
-        const float v = dxv[rt][i] + sum;
-        if (a.dxb) a.dxb[(long)gm * a.lddxb + mycol] = (bf16)v;
-        else a.dx[(long)gm * a.lddx + mycol] = v;
+      if (rok) {
+        const int col = 32 * ct + 8 * g + 4 * h;
+        if (a.dxb) {
+          bf16x4 b = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+          *reinterpret_cast<bf16x4*>(a.dxb + (long)row * a.lddxb + col) = b;
+        } else {
+          *reinterpret_cast<float4*>(a.dx + (long)row * a.lddx + col) = make_float4(v[0], v[1], v[2], v[3]);
+        }
       }
     }
+  };
+  DxRegs<NS> R0, R1;
+  if (w < nct) load(w, R0);
+  for (int ct = w; ct < nct; ct += 16) {
+    const bool more = ct + 8 < nct;
+    if (more) load(ct + 8, R1);
+    process(ct, R0);
+    if (!more) break;
+    if (ct + 16 < nct) load(ct + 16, R0);
+    process(ct + 8, R1);
   }
 }
 
@@ -459,10 +473,11 @@ extern "C" int slx_lora_down(const slx_lora_down_desc* d, slx_stream_t stream) {
   return 0;
 }
 
-extern "C" int slx_lora_pack_a(const void* A, int64_t lda, int Kin, void* Af, slx_stream_t stream) {
+extern "C" int slx_lora_pack_a(const void* A, int64_t lda, int Kin, int layout, void* Af, slx_stream_t stream) {
   SLX_CHECK_ARG(A && Af && Kin > 0 && Kin % 32 == 0 && lda >= Kin, "slx_lora_pack_a: A, Af, Kin %% 32, lda >= Kin");
+  SLX_CHECK_ARG(layout == 0 || layout == 1, "slx_lora_pack_a: layout 0 (lora_down) or 1 (lora_bwd dx)");
   hipLaunchKernelGGL(lora_pack_a_kernel, dim3((unsigned)((32L * Kin + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
-                     (const bf16*)A, (long)lda, Kin, (bf16*)Af);
+                     (const bf16*)A, (long)lda, Kin, layout, (bf16*)Af);
   SLX_LAUNCH_CHECK("slx_lora_pack_a");
   return 0;
 }
@@ -494,13 +509,14 @@ extern "C" int slx_dropout_bits(const slx_dropout_bits_desc* d, slx_stream_t str
 template <int NS>
 static void launch_bwd(const LoraBwdArgs& a, dim3 grid, hipStream_t st) {
   if (a.dA[0]) hipLaunchKernelGGL(lora_da_kernel<NS>, grid, dim3(256), 0, st, a);
-  if (a.dx)
-    hipLaunchKernelGGL(lora_dx_kernel<NS>, dim3((unsigned)(a.Kin / 128), (unsigned)((a.M + 63) / 64)), dim3(256), 0, st, a);
+  if (a.dx) hipLaunchKernelGGL(lora_dx_kernel<NS>, dim3((unsigned)((a.M + 31) / 32)), dim3(512), 0, st, a);
 }
 
 extern "C" int slx_lora_bwd(const slx_lora_bwd_desc* d, slx_stream_t stream) {
   SLX_CHECK_ARG(d->nsites >= 1 && d->nsites <= 4 && d->r == 32, "slx_lora_bwd: 1..4 sites of rank 32");
   SLX_CHECK_ARG(d->Kin % 128 == 0 && d->ldx % 8 == 0 && d->lddt % 4 == 0, "slx_lora_bwd: Kin %% 128, ldx %% 8, lddt %% 4");
+  SLX_CHECK_ARG(!d->dx || (d->lddx % 4 == 0 && (!d->dx_bf16 || d->lddx_bf16 % 4 == 0)),
+                "slx_lora_bwd: lddx %% 4 (and lddx_bf16 %% 4): the dx term uses 16-B accesses");
   SLX_CHECK_ARG(d->p >= 0.f && d->p < 1.f, "slx_lora_bwd: 0 <= p < 1");
   SLX_CHECK_ARG(d->p == 0.f || (d->bits[0] && d->ldbits >= d->Kin / 32), "slx_lora_bwd: p > 0 needs the keep bits");
   SLX_CHECK_ARG(!d->dx_bf16 || d->dx, "slx_lora_bwd: dx_bf16 needs dx (the f32 base gradient it is added to)");

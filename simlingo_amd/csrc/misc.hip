@@ -450,8 +450,8 @@ __global__ void cast_rows_kernel(const float* src, long lds, bf16* dst, long ldd
 }
 
 // Batched 2-D scaled copy f32 -> bf16 (or f32, parity mode): entry e of `tab` =
-// {src, lds, dst, ldd, rows, cols, scale(bits), mode}, mode 0 bf16 [rows][ldd], 1 f32 [rows][ldd], 2 bf16 in the
-// packed LoRA-A fragment order of slx_lora_down (rows == 32, ldd unused). Packs every LoRA B (times alpha/r) into the
+// {src, lds, dst, ldd, rows, cols, scale(bits), mode}, mode 0 bf16 [rows][ldd], 1 f32 [rows][ldd], 2 / 3 bf16 in the
+// packed LoRA-A fragment orders of slx_lora_down / slx_lora_bwd's dx term (rows == 32, ldd unused). Packs every LoRA B (times alpha/r) into the
 // fused [W | s*B] GEMM operands and every LoRA A into its fragment copy in one launch.
 __global__ void pack_scaled_kernel(const long long* tab, int n) {
   const int e = blockIdx.x;
@@ -467,6 +467,7 @@ __global__ void pack_scaled_kernel(const long long* tab, int n) {
     const float v = src[r * lds + c] * sc;
     if (mode == 1) reinterpret_cast<float*>(t[2])[r * ldd + c] = v;
     else if (mode == 2) reinterpret_cast<bf16*>(t[2])[lora_frag_index((int)r, (int)c)] = (bf16)v;
+    else if (mode == 3) reinterpret_cast<bf16*>(t[2])[lora_dxfrag_index((int)r, (int)c)] = (bf16)v;
     else reinterpret_cast<bf16*>(t[2])[r * ldd + c] = (bf16)v;
   }
 }

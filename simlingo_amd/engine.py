@@ -215,11 +215,12 @@ class VLAEngine(EngineOps):
                 entries.append([a.data_ptr(), a.stride(0), ap.data_ptr(), ap.stride(0), r, a.shape[1],
                                 int(np.float32(1.0).view(np.int32)), int(self.precise)])
                 cats["apad." + site] = ap
-                if not self.precise:  # fragment-ordered copy read by slx_lora_down (mode 2)
-                    af = torch.empty(r * a.shape[1], dtype=torch.bfloat16, device=self.device)
-                    entries.append([a.data_ptr(), a.stride(0), af.data_ptr(), 0, r, a.shape[1],
-                                    int(np.float32(1.0).view(np.int32)), 2])
-                    cats["afrag." + site] = af
+                if not self.precise:  # fragment-ordered copies read by slx_lora_down (mode 2) and slx_lora_bwd (3)
+                    for mode, key in ((2, "afrag."), (3, "axfrag.")):
+                        af = torch.empty(r * a.shape[1], dtype=torch.bfloat16, device=self.device)
+                        entries.append([a.data_ptr(), a.stride(0), af.data_ptr(), 0, r, a.shape[1],
+                                        int(np.float32(1.0).view(np.int32)), mode])
+                        cats[key + site] = af
             self.cat.append(cats)
         self._pack_tab = torch.tensor(entries, dtype=torch.int64, device=self.device)
         self._pack_n = len(entries)
@@ -708,14 +709,14 @@ class VLAEngine(EngineOps):
         drop = sv["drop"]
         keep = sv["llm"][i]["lora"]
         bits = [keep[site] for site in sites]
-        As = [self.W[f"llm.{i}.lora.{site}.a"] for site in sites]
+        As = [self.cat[i]["axfrag." + site] for site in sites]
         for j, site in enumerate(sites):
             K.mm(dys[j], tx[:, r * j:r * (j + 1)], self.G[f"llm.{i}.lora.{site}.b"], ta=True, tb=False, alpha=s,
                  accumulate=True)
         # dA and the dx term in one launch. (Running the parameter-only part - dB GEMMs, dA - on a side stream was
         # measured 6 ms/step slower: per-call event/stream overhead on the host and slower main-stream GEMMs.)
         K.lora_bwd(x, dtx, As, bits, [self.G[f"llm.{i}.lora.{site}.a"] for site in sites],
-                   dx=None if swiglu is not None else dx, dx_bf16=dx_bf16, p=drop)
+                   dx=None if swiglu is not None else dx, dx_bf16=dx_bf16, p=drop, packed=True)
         if swiglu is not None:
             gu, dgu = swiglu
             M = x.shape[0]

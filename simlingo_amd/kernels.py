@@ -261,7 +261,7 @@ _vp, _i, _I, _f = c_vp, c_int, c_i64, c_float
 for _n, _a in {
     "slx_attn_fwd": [ctypes.POINTER(AttnDesc), _vp],
     "slx_lora_down": [ctypes.POINTER(LoraDownDesc), _vp],
-    "slx_lora_pack_a": [_vp, ctypes.c_int64, ctypes.c_int, _vp, _vp],
+    "slx_lora_pack_a": [_vp, ctypes.c_int64, ctypes.c_int, ctypes.c_int, _vp, _vp],
     "slx_lora_bwd": [ctypes.POINTER(LoraBwdDesc), _vp],
     "slx_dropout_bits": [ctypes.POINTER(DropoutBitsDesc), _vp],
     "slx_attn_bwd": [ctypes.POINTER(AttnDesc), ctypes.POINTER(AttnBwdDesc), _vp],
@@ -450,12 +450,13 @@ def dropout_bits(jobs, rows, p):
     check(lib().slx_dropout_bits(ctypes.byref(d), stream_ptr()), "slx_dropout_bits")
 
 
-def lora_pack_a(a, out=None):
-    """A [32, kin] bf16 (peft lora_A.weight layout) -> the packed fragment order slx_lora_down reads."""
+def lora_pack_a(a, layout=0, out=None):
+    """A [32, kin] bf16 (peft lora_A.weight layout) -> a packed fragment order: layout 0 is read by slx_lora_down,
+    layout 1 by slx_lora_bwd's dx term."""
     assert a.dtype == torch.bfloat16 and a.dim() == 2 and a.shape[0] == 32 and a.stride(1) == 1
     out = torch.empty(32 * a.shape[1], device=a.device, dtype=torch.bfloat16) if out is None else out
     assert out.dtype == torch.bfloat16 and out.is_contiguous() and out.numel() == a.numel()
-    check(lib().slx_lora_pack_a(P(a), a.stride(0), a.shape[1], P(out), stream_ptr()), "slx_lora_pack_a")
+    check(lib().slx_lora_pack_a(P(a), a.stride(0), a.shape[1], int(layout), P(out), stream_ptr()), "slx_lora_pack_a")
     return out
 
 
@@ -470,7 +471,7 @@ def lora_down(x, As, t, seeds, p=0.0, ldmask=None, bits=None, packed=False):
     if not packed:
         for a in As:
             assert a.shape == (32, kin)
-        As = [lora_pack_a(a) for a in As]
+        As = [lora_pack_a(a, 0) for a in As]
     d = LoraDownDesc()
     d.x, d.ldx, d.M, d.Kin, d.r, d.nsites = P(x).value, x.stride(0), M, kin, 32, len(As)
     for j, a in enumerate(As):
@@ -485,19 +486,25 @@ def lora_down(x, As, t, seeds, p=0.0, ldmask=None, bits=None, packed=False):
     check(lib().slx_lora_down(ctypes.byref(d), stream_ptr()), "slx_lora_down")
 
 
-def lora_bwd(x, dt, As, bits, dAs, dx=None, dx_bf16=None, p=0.0):
+def lora_bwd(x, dt, As, bits, dAs, dx=None, dx_bf16=None, p=0.0, packed=False):
     """peft LoRA backward of the sites sharing x (one launch): dAs[j] (f32 [32, kin]) += dT_j^T drop_j(x) (dAs=None:
     skipped) and, if dx (f32 [M, kin]) is given, dx += sum_j drop_j'(dT_j As[j]) in place - or written as
     bf16(dx + ...) to dx_bf16.
-    dt: f32 [M, >= 32 n] (dT_j = columns 32j..); bits[j]: keep bits from lora_down (None when p == 0)."""
+    dt: f32 [M, >= 32 n] (dT_j = columns 32j..); bits[j]: keep bits from lora_down (None when p == 0).
+    As: [32, kin] matrices (packed here into slx_lora_pack_a layout 1 when dx is asked for), or with packed=True the
+    layout-1 copies themselves (only the dx term reads A)."""
     assert x.dtype == torch.bfloat16 and dt.dtype == torch.float32 and 1 <= len(As) <= 4
     M, kin = x.shape
     assert dt.shape[0] == M and dt.shape[1] >= 32 * len(As) and dt.stride(1) == 1
     d = LoraBwdDesc()
     d.x, d.ldx, d.M, d.Kin, d.r, d.nsites = P(x).value, x.stride(0), M, kin, 32, len(As)
     d.dt, d.lddt = P(dt).value, dt.stride(0)
+    if not packed:
+        for a in As:
+            assert a.shape == (32, kin) and a.dtype == torch.bfloat16
+        As = [lora_pack_a(a, 1) for a in As] if dx is not None else As
     for j, a in enumerate(As):
-        assert a.shape == (32, kin) and a.is_contiguous() and a.dtype == torch.bfloat16
+        assert a.numel() == 32 * kin and a.is_contiguous() and a.dtype == torch.bfloat16
         d.A[j] = a.data_ptr()
         if dAs is not None:  # None: dx only
             g = dAs[j]

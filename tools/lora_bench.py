@@ -39,8 +39,9 @@ for name, (kin, ns) in GROUPS.items():
     dt = torch.randn(M, 32 * ns, device=dev)
     dAs = [torch.zeros(32, kin, device=dev) for _ in range(ns)]
     dx = torch.zeros(M, kin, device=dev)
-    tb = t_ms(lambda: K.lora_bwd(x, dt, As, bits, dAs, dx=dx, p=0.1))
-    ta = t_ms(lambda: K.lora_bwd(x, dt, As, bits, dAs, p=0.1))
+    Ax = [K.lora_pack_a(a, 1) for a in As]
+    tb = t_ms(lambda: K.lora_bwd(x, dt, Ax, bits, dAs, dx=dx, p=0.1, packed=True))
+    ta = t_ms(lambda: K.lora_bwd(x, dt, Ax, bits, dAs, p=0.1, packed=True))
     xb = M * kin * 2 / 1e9
     bb = ns * M * kin / 8 / 1e9
     print(f"{name:5s} kin {kin} ns {ns}: down {td * 1e3:6.1f} us ({(xb + bb) / td:5.2f} TB/s) | dA {ta * 1e3:6.1f} us "
