@@ -105,6 +105,9 @@ typedef struct slx_attn_bwd_desc {
   float* dq_acc;                /* [B*S, Hq*64] f32 workspace (fully overwritten)        */
   float* dk_acc; float* dv_acc; /* [B*S, Hq*64] f32 workspaces, required for GQA or RoPE */
   const float* rope_cos; const float* rope_sin; /* [S, 32] tables: apply RoPE^T to dq/dk */
+  float* dbias_q; float* dbias_k; float* dbias_v; /* optional [Hq*64] / [Hkv*64] f32: += column sums of dq / dk / dv
+                                   over all B*S rows (the q/k/v bias gradients of InternViT's qkv Linear,
+                                   qkv_bias=True); dk/dv sums need Hq == Hkv and no RoPE                      */
 } slx_attn_bwd_desc;
 int slx_attn_fwd(const slx_attn_desc* d, slx_stream_t stream);
 int slx_attn_bwd(const slx_attn_desc* d, const slx_attn_bwd_desc* g, slx_stream_t stream);

@@ -82,6 +82,7 @@ struct AttnArgs {
   float* dq_acc;               // [B*S, Hq*64] f32, written by the dQ pass (finalized to bf16 + RoPE^T)
   float* dk_acc; float* dv_acc;  // [nsplit][B*S, Hkv*64] f32 when GQA/RoPE (finalized), else null: direct bf16
   bf16* dk; bf16* dv; long lddk, lddv;
+  float* dbq; float* dbk; float* dbv;  // optional bias-gradient column sums of dq / dk / dv (f32, accumulated)
   int hsplit, nsplit;            // dK/dV pass: q-heads of a GQA group per workgroup, workgroups per group
   bf16* dq; long lddq;           // dQ pass output: bf16, RoPE^T applied with rcos/rsin (pos = query index) if given
   const float* rcos; const float* rsin;
@@ -334,6 +335,34 @@ __device__ __forceinline__ void bwd_kv_chunk(const char* Ql, const char* Dl, con
   }
 }
 
+// dst[0..63] += column sums over the block's 128 rows (4 waves x 32 lanes) of a [row x 64] gradient tile, for the
+// q/k/v bias gradients (InternViT qkv.b): lane (row l & 31, half hl) holds dims 8g + 4hl + e in v0[4g + e] and
+// 32 + 8g + 4hl + e in v1[4g + e] (rows that do not exist pass zeros). Each wave transposes its 32 rows through a
+// wave-private [32][64] f32 LDS tile (float4 groups XOR-swizzled by row & 15), lane = dim sums its column, and the 4
+// wave partials meet in `red`: one f32 atomic per dim and block. All 256 threads must call it; `lds` >= 32 KiB.
+__device__ __forceinline__ void block_colsum64(char* lds, float* red, const float (&v0)[16], const float (&v1)[16],
+                                               float* dst, int lane, int w) {
+  __syncthreads();  // the tile area is free (main loop done, or the previous call's reads finished)
+  float* t = reinterpret_cast<float*>(lds) + w * 2048;
+  const int q = lane & 31, hl = lane >> 5;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const int c4 = 2 * g + hl;
+    *reinterpret_cast<float4*>(t + q * 64 + ((c4 ^ (q & 15)) << 2)) =
+        make_float4(v0[4 * g], v0[4 * g + 1], v0[4 * g + 2], v0[4 * g + 3]);
+    *reinterpret_cast<float4*>(t + q * 64 + (((8 + c4) ^ (q & 15)) << 2)) =
+        make_float4(v1[4 * g], v1[4 * g + 1], v1[4 * g + 2], v1[4 * g + 3]);
+  }
+  __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // wave-private tile written (LDS is in order per wave)
+  float sum = 0.f;
+  const int c4 = lane >> 2, e = lane & 3;
+#pragma unroll
+  for (int r = 0; r < 32; ++r) sum += t[r * 64 + ((c4 ^ (r & 15)) << 2) + e];
+  red[w * 64 + lane] = sum;
+  __syncthreads();
+  if (w == 0) atomicAdd(dst + lane, red[lane] + red[64 + lane] + red[128 + lane] + red[192 + lane]);
+}
+
 __global__ __launch_bounds__(256, 2) void attn_bwd_kv_kernel(AttnArgs a) {
   // LDS: Q chunk x2 (8 KB each) | dO chunk x2 | lse,delta x2
   __shared__ __attribute__((aligned(16))) char smem[2 * 8192 + 2 * 8192 + 2 * 2 * 64 * 4];
@@ -414,12 +443,16 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kv_kernel(AttnArgs a) {
     __syncthreads();
   }
 
-  if (mykey >= S) return;
+  const bool kvalid = mykey < S;
+  float ck0[16], ck1[16], cv0[16], cv1[16];  // the stored bf16 values, for the bias column sums
   // accumulators: column = key (lane), rows = d
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
     const int d = 8 * g + 4 * hl;
-    if (a.dk_acc) {  // f32 partial of this head split; the finalize sums splits, applies RoPE^T, casts
+    if (!kvalid) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) ck0[4 * g + e] = ck1[4 * g + e] = cv0[4 * g + e] = cv1[4 * g + e] = 0.f;
+    } else if (a.dk_acc) {  // f32 partial of this head split; the finalize sums splits, applies RoPE^T, casts
       const long off = (long)sp * a.B * S * (a.Hkv * 64) + ((long)b * S + mykey) * (a.Hkv * 64) + hk * 64;
       float* kp = a.dk_acc + off;
       float* vp = a.dv_acc + off;
@@ -437,12 +470,21 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kv_kernel(AttnArgs a) {
         k1v[e] = (bf16)(dk1[4 * g + e] * a.scale);
         v0v[e] = (bf16)dv0[4 * g + e];
         v1v[e] = (bf16)dv1[4 * g + e];
+        ck0[4 * g + e] = (float)k0v[e];
+        ck1[4 * g + e] = (float)k1v[e];
+        cv0[4 * g + e] = (float)v0v[e];
+        cv1[4 * g + e] = (float)v1v[e];
       }
       *reinterpret_cast<bf16x4*>(kp + d) = k0v;
       *reinterpret_cast<bf16x4*>(kp + 32 + d) = k1v;
       *reinterpret_cast<bf16x4*>(vp + d) = v0v;
       *reinterpret_cast<bf16x4*>(vp + 32 + d) = v1v;
     }
+  }
+  if (a.dbk) {  // bf16 path only (the host refuses bias sums with the f32 GQA/RoPE finalize)
+    __shared__ float red[256];
+    block_colsum64(smem, red, ck0, ck1, a.dbk + hk * 64, lane, w);
+    block_colsum64(smem, red, cv0, cv1, a.dbv + hk * 64, lane, w);
   }
 }
 
@@ -561,10 +603,11 @@ __global__ __launch_bounds__(256, ATTN_DQ_OCC) void attn_bwd_dq_kernel(AttnArgs 
     }
     __syncthreads();
   }
-  if (!active || myq >= S) return;
+  const bool qvalid = active && myq < S;
+  float c0[16], c1[16];  // the stored bf16 values, for the bias column sums
   // dQ of this query: dims d and d + 32 (a RoPE pair) sit in dq0[r] / dq1[r] of the same lane, so the inverse
   // rotation and the bf16 store need no exchange (no f32 workspace, no finalize launch)
-  bf16* qrow = a.dq + ((long)b * S + myq) * a.lddq + h * 64;
+  bf16* qrow = a.dq + ((long)b * S + (qvalid ? myq : 0)) * a.lddq + h * 64;
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
     const int d = 8 * g + 4 * hl;
@@ -580,9 +623,17 @@ __global__ __launch_bounds__(256, ATTN_DQ_OCC) void attn_bwd_dq_kernel(AttnArgs 
       }
       v0[e] = (bf16)x0;
       v1[e] = (bf16)x1;
+      c0[4 * g + e] = qvalid ? (float)v0[e] : 0.f;
+      c1[4 * g + e] = qvalid ? (float)v1[e] : 0.f;
     }
-    *reinterpret_cast<bf16x4*>(qrow + d) = v0;
-    *reinterpret_cast<bf16x4*>(qrow + 32 + d) = v1;
+    if (qvalid) {
+      *reinterpret_cast<bf16x4*>(qrow + d) = v0;
+      *reinterpret_cast<bf16x4*>(qrow + 32 + d) = v1;
+    }
+  }
+  if (a.dbq) {
+    __shared__ float red[256];
+    block_colsum64(smem, red, c0, c1, a.dbq + h * 64, lane, w);
   }
 }
 
@@ -698,6 +749,9 @@ extern "C" int slx_attn_bwd(const slx_attn_desc* d, const slx_attn_bwd_desc* g, 
   a.dk_acc = f32kv ? g->dk_acc : nullptr;
   a.dv_acc = f32kv ? g->dv_acc : nullptr;
   a.dk = (bf16*)g->dk; a.dv = (bf16*)g->dv; a.lddk = g->lddk; a.lddv = g->lddv;
+  a.dbq = g->dbias_q; a.dbk = g->dbias_k; a.dbv = g->dbias_v;
+  SLX_CHECK_ARG((a.dbk == nullptr) == (a.dbv == nullptr), "slx_attn_bwd: dbias_k and dbias_v go together");
+  SLX_CHECK_ARG(!a.dbk || !f32kv, "slx_attn_bwd: dk/dv bias sums need the bf16 dK/dV path (no GQA, no RoPE)");
   const long ntok = (long)a.B * a.S;
   const int nblk = (a.S + 127) / 128;
   // dQ pass first: it computes delta = rowsum(dO * O) per query in its prologue and stores it for the dK/dV pass

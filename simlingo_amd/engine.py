@@ -667,10 +667,10 @@ class VLAEngine(EngineOps):
             qkv = Ls["qkv"]
             dqkv = self._e(Mv, 3 * D)
             K.attn_bwd(qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], Ls["o"], Ls["lse"], do,
-                       dqkv[:, :D], dqkv[:, D:2 * D], dqkv[:, 2 * D:], vws, B=N, S=T, Hq=H, Hkv=H, causal=False)
+                       dqkv[:, :D], dqkv[:, D:2 * D], dqkv[:, 2 * D:], vws, B=N, S=T, Hq=H, Hkv=H, causal=False,
+                       dbias=self.G[p + "qkv.b"])  # qkv.b grad = column sums of dq | dk | dv, in the same kernels
             del do
             K.mm(dqkv, Ls["h1"], self.G[p + "qkv.w"], ta=True, tb=False, accumulate=True)
-            self._colsum(dqkv, self.G[p + "qkv.b"], 0)
             K.mm(dqkv, self.W[p + "qkv.w"], dh2, tb=False)
             del dqkv
             nxt = None

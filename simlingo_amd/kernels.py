@@ -206,7 +206,7 @@ class AttnBwdDesc(ctypes.Structure):
     _fields_ = [
         ("dout", c_vp), ("lddo", c_i64), ("dq", c_vp), ("lddq", c_i64), ("dk", c_vp), ("lddk", c_i64),
         ("dv", c_vp), ("lddv", c_i64), ("delta_ws", c_vp), ("dq_acc", c_vp), ("dk_acc", c_vp), ("dv_acc", c_vp),
-        ("rope_cos", c_vp), ("rope_sin", c_vp),
+        ("rope_cos", c_vp), ("rope_sin", c_vp), ("dbias_q", c_vp), ("dbias_k", c_vp), ("dbias_v", c_vp),
     ]
 
 
@@ -336,8 +336,9 @@ def attn_fwd(q, k, v, o, lse, **kw):
     check(getattr(lib(), name)(ctypes.byref(d), stream_ptr()), name)
 
 
-def attn_bwd(q, k, v, o, lse, dout, dq, dk, dv, ws, *, rope_cos=None, rope_sin=None, **kw):
-    """ws: attn_ws(...) f32 buffers (delta, dq_acc, and dk_acc/dv_acc for GQA or RoPE)."""
+def attn_bwd(q, k, v, o, lse, dout, dq, dk, dv, ws, *, rope_cos=None, rope_sin=None, dbias=None, **kw):
+    """ws: attn_ws(...) f32 buffers (delta, dq_acc, and dk_acc/dv_acc for GQA or RoPE).
+    dbias: optional f32 [3 * Hq * 64] (q | k | v bias gradients) += column sums of dq, dk, dv (no GQA, no RoPE)."""
     d = attn_desc(q, k, v, o, lse, **kw)
     g = AttnBwdDesc()
     g.dout, g.lddo = dout.data_ptr(), dout.stride(0)
@@ -350,6 +351,10 @@ def attn_bwd(q, k, v, o, lse, dout, dq, dk, dv, ws, *, rope_cos=None, rope_sin=N
     g.dv_acc = ws["dv_acc"].data_ptr() if "dv_acc" in ws else 0
     g.rope_cos = rope_cos.data_ptr() if rope_cos is not None else 0
     g.rope_sin = rope_sin.data_ptr() if rope_sin is not None else 0
+    if dbias is not None:
+        n = d.Hq * 64
+        assert dbias.dtype == torch.float32 and dbias.is_contiguous() and dbias.numel() == 3 * n
+        g.dbias_q, g.dbias_k, g.dbias_v = dbias.data_ptr(), dbias.data_ptr() + 4 * n, dbias.data_ptr() + 8 * n
     check(lib().slx_attn_bwd(ctypes.byref(d), ctypes.byref(g), stream_ptr()), "slx_attn_bwd")
 
 

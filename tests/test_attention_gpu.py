@@ -59,11 +59,17 @@ def test_attention_fwd_bwd(dev, B, S, Hq, Hkv, causal, lens):
     dqkv = torch.zeros_like(qkv)
     dq, dk, dv = dqkv[:, : Hq * 64], dqkv[:, Hq * 64: (Hq + Hkv) * 64], dqkv[:, (Hq + Hkv) * 64:]
     ws = K.attn_ws(B, S, Hq, Hkv, dev)
-    K.attn_bwd(q, k, v, o, lse, dout, dq, dk, dv, ws, B=B, S=S, Hq=Hq, Hkv=Hkv, causal=causal, seqlens=seql)
+    # the q/k/v bias-gradient column sums ride along where dK/dV take the bf16 path (no GQA; RoPE is not used here)
+    dbias = torch.full((3 * Hq * 64,), 0.25, device=dev) if Hq == Hkv else None
+    K.attn_bwd(q, k, v, o, lse, dout, dq, dk, dv, ws, B=B, S=S, Hq=Hq, Hkv=Hkv, causal=causal, seqlens=seql,
+               dbias=dbias)
     for name, got, want in (("dq", dq, qr.grad), ("dk", dk, kr.grad), ("dv", dv, vr.grad)):
         scale = want.abs().max().item() + 1e-6
         e = (got.float() - want).abs().max().item()
         assert e < 3e-2 * scale + 1e-2, f"{name}: max err {e} (scale {scale})"
+    if dbias is not None:  # sums of the stored bf16 gradients over all B*S rows, f32 accumulation
+        want = 0.25 + dqkv.float().sum(0)
+        torch.testing.assert_close(dbias, want, atol=1e-3 * (B * S) ** 0.5, rtol=1e-4)
 
 
 def test_rope_roundtrip_and_values(dev):

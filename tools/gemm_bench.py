@@ -37,6 +37,10 @@ SHAPES = {  # name: (M, N, K, layout)
     "vit_qkv_wgrad_nn": (1024, 3072, 16400, K.GEMM_NN),
     "vit_proj_wgrad_tt": (1024, 1024, 16400, K.GEMM_TT),
     "vit_proj_wgrad_nn": (1024, 1024, 16400, K.GEMM_NN),
+    # NT: both operands token-contiguous copies (dY^T and X^T, tokens padded to 16448 = 257 * 64)
+    "vit_fc1_wgrad_nt": (4096, 1024, 16448, K.GEMM_NT),
+    "vit_fc2_wgrad_nt": (1024, 4096, 16448, K.GEMM_NT),
+    "vit_qkv_wgrad_nt": (3072, 1024, 16448, K.GEMM_NT),
 }
 VARIANTS = [int(v) for v in os.environ.get("VARIANTS", "1,2,3,4,5,6").split(",")]
 dev = torch.device("cuda")
