@@ -135,6 +135,8 @@ typedef struct slx_norm_desc {
    * precedes this norm in the backward, applied to the updated dx rows in the same pass: ls_g = bf16(dx * ls),
    * ls_dls += sum dx * ls_y, ls_dbias += sum dx * ls (InternViT x = x_in + ls * branch(...), ls != NULL)     */
   const float* ls; const void* ls_y; int64_t ld_ls_y; void* ls_g; int64_t ld_ls_g; float* ls_dls; float* ls_dbias;
+  int dy_bf16;                /* bwd: 1 = the dy argument of slx_norm_bwd points to bf16 rows (lddy in elements):
+                                 the bf16 gradient a bf16 Linear's backward hands LayerNorm under autocast      */
 } slx_norm_desc;
 int slx_norm_fwd(const slx_norm_desc* d, slx_stream_t stream);
 int slx_norm_bwd(const slx_norm_desc* d, const float* dy, int64_t lddy, float* dx, int64_t lddx,

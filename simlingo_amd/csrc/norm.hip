@@ -29,7 +29,7 @@ struct NormArgs {
   int y_f32;                              // y holds f32 rows (CLIP pre_layrnorm feeds the f32 residual; for
                                           // RMS, the f32 parity mode: input dtype f32, no bf16 cast of x_hat)
   // bwd
-  const float* dy; long lddy;
+  const float* dy; long lddy; int dy_bf16;  // dy_bf16: dy points to bf16 rows (slx_norm_desc.dy_bf16)
   float* dx; long lddx; int dx_accumulate;
   bf16* dxb; long lddxb;  // optional bf16 copy of dx (non-pixel-shuffle rows only)
   float* partial;   // unused (kept for ABI workspace sizing)
@@ -37,6 +37,16 @@ struct NormArgs {
   // fused layer-scale branch backward on the updated dx (slx_norm_desc.ls*)
   const float* ls; const bf16* lsy; long ldlsy; bf16* lsg; long ldlsg; float* dls; float* dlsb;
 };
+
+// 4 consecutive dy values of a row (f32 rows, or bf16 rows when a.dy_bf16; DYB: decided at compile time)
+template <int DYB = -1>
+__device__ __forceinline__ float4 load_dy4(const NormArgs& a, long row, int col) {
+  if (DYB == 1 || (DYB < 0 && a.dy_bf16)) {
+    const bf16x4 b = *reinterpret_cast<const bf16x4*>(reinterpret_cast<const bf16*>(a.dy) + row * a.lddy + col);
+    return make_float4((float)b[0], (float)b[1], (float)b[2], (float)b[3]);
+  }
+  return *reinterpret_cast<const float4*>(a.dy + row * a.lddy + col);
+}
 
 template <int VPT, bool RMS>
 __global__ __launch_bounds__(256) void norm_fwd_kernel(NormArgs a) {
@@ -159,7 +169,7 @@ __global__ __launch_bounds__(256) void norm_fwd_wave_kernel(NormArgs a) {
   }
 }
 
-template <bool RMS, bool LS>
+template <bool RMS, bool LS, bool DYB>
 __global__ __launch_bounds__(256) void norm_bwd_wave_kernel(NormArgs a) {
   __shared__ float cs[4][LS ? 4 : 2][1024];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -179,7 +189,7 @@ __global__ __launch_bounds__(256) void norm_bwd_wave_kernel(NormArgs a) {
         const float* src = a.ps ? a.x + ps_src_row(row, col / a.C, a.G, a.tok_per_img) * a.ldx + (col % a.C)
                                 : a.x + row * a.ldx + col;
         t = *reinterpret_cast<const float4*>(src);
-        d = *reinterpret_cast<const float4*>(a.dy + row * a.lddy + col);
+        d = load_dy4<DYB ? 1 : 0>(a, row, col);
         g = *reinterpret_cast<const float4*>(a.gamma + col);
       }
       const float tv[4] = {t.x, t.y, t.z, t.w}, dv[4] = {d.x, d.y, d.z, d.w}, gv[4] = {g.x, g.y, g.z, g.w};
@@ -286,7 +296,7 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(NormArgs a) {
       if (a.ps) src = a.x + ps_src_row(row, col / a.C, a.G, a.tok_per_img) * a.ldx + (col % a.C);
       else src = a.x + row * a.ldx + col;
       const float4 t = *reinterpret_cast<const float4*>(src);
-      const float4 d = *reinterpret_cast<const float4*>(a.dy + row * a.lddy + col);
+      const float4 d = load_dy4(a, row, col);
       const float tv[4] = {t.x, t.y, t.z, t.w}, dv[4] = {d.x, d.y, d.z, d.w};
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -378,8 +388,13 @@ static int norm_bwd(NormArgs& a, float* dgamma, float* dbeta, int accumulate, hi
     if (dgamma) hipMemsetAsync(dgamma, 0, a.D * sizeof(float), st);
     if (dbeta) hipMemsetAsync(dbeta, 0, a.D * sizeof(float), st);
   }
-  if (a.D <= 1024 && a.ls) hipLaunchKernelGGL((norm_bwd_wave_kernel<RMS, true>), dim3(nblk), dim3(256), 0, st, a);
-  else if (a.D <= 1024) hipLaunchKernelGGL((norm_bwd_wave_kernel<RMS, false>), dim3(nblk), dim3(256), 0, st, a);
+  if (a.D <= 1024 && a.ls) {
+    if (a.dy_bf16) hipLaunchKernelGGL((norm_bwd_wave_kernel<RMS, true, true>), dim3(nblk), dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((norm_bwd_wave_kernel<RMS, true, false>), dim3(nblk), dim3(256), 0, st, a);
+  } else if (a.D <= 1024) {
+    if (a.dy_bf16) hipLaunchKernelGGL((norm_bwd_wave_kernel<RMS, false, true>), dim3(nblk), dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((norm_bwd_wave_kernel<RMS, false, false>), dim3(nblk), dim3(256), 0, st, a);
+  }
   else if (a.D <= 2048) hipLaunchKernelGGL((norm_bwd_kernel<8, RMS>), dim3(nblk), dim3(256), 0, st, a);
   else hipLaunchKernelGGL((norm_bwd_kernel<16, RMS>), dim3(nblk), dim3(256), 0, st, a);
   SLX_LAUNCH_CHECK("slx_norm_bwd");
@@ -411,6 +426,8 @@ extern "C" int slx_norm_bwd(const slx_norm_desc* d, const float* dy, int64_t ldd
   NormArgs a;
   fill(a, d);
   a.dy = dy; a.lddy = lddy; a.dx = dx; a.lddx = lddx; a.dx_accumulate = dx_accumulate;
+  a.dy_bf16 = d->dy_bf16;
+  SLX_CHECK_ARG(!a.dy_bf16 || lddy % 4 == 0, "slx_norm_bwd: bf16 dy needs lddy %% 4 == 0");
   a.partial = (dgamma || dbeta) ? partial_ws : nullptr;
   a.dxb = (bf16*)d->dx_bf16; a.lddxb = d->lddx_bf16;
   SLX_CHECK_ARG(!a.dxb || (!a.ps && a.lddxb % 4 == 0), "slx_norm_bwd: dx_bf16 needs plain rows and lddx_bf16 %% 4 == 0");

@@ -653,7 +653,7 @@ class VLAEngine(EngineOps):
             K.mm(g, self.W[p + "fc2.w"], dh, tb=False, epi=K.EPI_GELU_BWD, aux=Ls["hpre"], ldaux=F_,
                  colsum=self.G[p + "fc1.b"])  # fc1.b grad = column sums of dh, in the same epilogue
             K.mm(dh, Ls["h2"], self.G[p + "fc1.w"], ta=True, tb=False, accumulate=True)
-            dh2 = self._e(Mv, D, dtype=F32)
+            dh2 = self._e(Mv, D)  # bf16: the gradient a bf16 Linear backward hands the fp32 LayerNorm under autocast
             K.mm(dh, self.W[p + "fc1.w"], dh2, tb=False)
             del dh
             # x_mid = x_in + ls1 * proj(attn(ln1(x_in))): its branch backward (g = ls1 * dx_mid, dls1, proj.b grad)

@@ -217,7 +217,7 @@ class NormDesc(ctypes.Structure):
         ("pixel_shuffle_grid", c_int), ("tokens_per_image", c_int), ("y_f32", c_int),
         ("dx_bf16", c_vp), ("lddx_bf16", c_i64),
         ("ls", c_vp), ("ls_y", c_vp), ("ld_ls_y", c_i64), ("ls_g", c_vp), ("ld_ls_g", c_i64), ("ls_dls", c_vp),
-        ("ls_dbias", c_vp),
+        ("ls_dbias", c_vp), ("dy_bf16", c_int),
     ]
 
 
@@ -409,10 +409,13 @@ def norm_fwd(d: NormDesc):
 
 def norm_bwd(d: NormDesc, dy, dx, *, dx_accumulate=False, dgamma=None, dbeta=None, param_accumulate=False, ws=None,
              lddx=None, dx_bf16=None, ls_branch=None):
-    """dx_bf16: optional bf16 [rows, >= D] view that receives a bf16 copy of the (accumulated) dx in the same pass.
+    """dy: f32 or bf16 rows. dx_bf16: optional bf16 [rows, >= D] view that receives a bf16 copy of the (accumulated) dx
+    in the same pass.
     ls_branch = (ls f32 [D], y bf16 [rows, D], g bf16 [rows, D], dls f32 [D], dbias f32 [D]): the layer-scale branch
     backward (slx_ls_branch_bwd, accumulating) fused onto the updated dx rows."""
     d.dx_bf16, d.lddx_bf16 = (dx_bf16.data_ptr(), dx_bf16.stride(0)) if dx_bf16 is not None else (0, 0)
+    assert dy.dtype in (torch.float32, torch.bfloat16)
+    d.dy_bf16 = int(dy.dtype == torch.bfloat16)
     if ls_branch is not None:
         ls, y, g, dls, dbias = ls_branch
         d.ls, d.ls_y, d.ld_ls_y, d.ls_g, d.ld_ls_g = ls.data_ptr(), y.data_ptr(), y.stride(0), g.data_ptr(), g.stride(0)

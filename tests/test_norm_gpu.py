@@ -139,3 +139,36 @@ def test_layernorm_bwd_fused_ls_branch(dev):
         torch.testing.assert_close(got.double(), ref_db, rtol=1e-4, atol=1e-3)
     torch.testing.assert_close(gm_f, gm_s, rtol=1e-5, atol=1e-4)
     torch.testing.assert_close(bt_f, bt_s, rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("rms,fused_ls", [(False, True), (False, False), (True, False)])
+def test_norm_bwd_bf16_dy(dev, rms, fused_ls):
+    """slx_norm_desc.dy_bf16: a bf16 dy (what the InternViT fc1 / qkv dgrad GEMMs now hand LayerNorm) gives exactly the
+    result of the f32 dy holding the same values, for the wave kernel with and without the fused ls branch."""
+    M, D = 1025 * 2 + 7, 1024
+    gen = torch.Generator(device=dev).manual_seed(9)
+    x = torch.randn(M, D, device=dev, generator=gen)
+    gamma, beta = torch.rand(D, device=dev, generator=gen) + 0.5, torch.randn(D, device=dev, generator=gen)
+    y = torch.empty(M, D, device=dev, dtype=torch.bfloat16)
+    mean, rstd = torch.empty(M, device=dev), torch.empty(M, device=dev)
+    d = K.norm_desc(x, gamma, None if rms else beta, y, mean, rstd, M, D, 1e-6, rms=rms)
+    K.norm_fwd(d)
+    dyb = torch.randn(M, D, device=dev, generator=gen).bfloat16()
+    dx0 = torch.randn(M, D, device=dev, generator=gen)
+    ls = torch.rand(D, device=dev, generator=gen) * 0.2
+    yb = torch.randn(M, D, device=dev, generator=gen).bfloat16()
+    outs = []
+    for dy in (dyb.float(), dyb):
+        dx = dx0.clone()
+        dgm, dbt = torch.zeros(D, device=dev), torch.zeros(D, device=dev)
+        g = torch.empty(M, D, device=dev, dtype=torch.bfloat16)
+        dls, dbias = torch.zeros(D, device=dev), torch.zeros(D, device=dev)
+        K.norm_bwd(d, dy, dx, dx_accumulate=True, dgamma=dgm, dbeta=None if rms else dbt,
+                   ws=torch.empty(K.norm_ws_floats(D), device=dev), param_accumulate=True,
+                   ls_branch=(ls, yb, g, dls, dbias) if fused_ls else None)
+        torch.cuda.synchronize()
+        outs.append((dx, dgm, dbt, g, dls, dbias))
+    (dx_f, gm_f, bt_f, g_f, dls_f, db_f), (dx_b, gm_b, bt_b, g_b, dls_b, db_b) = outs
+    assert torch.equal(dx_f, dx_b) and torch.equal(g_f, g_b)
+    for a, b in ((gm_f, gm_b), (bt_f, bt_b), (dls_f, dls_b), (db_f, db_b)):  # cross-block sums: order may differ
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-4)
