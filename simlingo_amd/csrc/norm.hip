@@ -181,6 +181,23 @@ __global__ __launch_bounds__(256) void norm_bwd_wave_kernel(NormArgs a) {
     const float rs = a.rstd[row];
     float xh[16], gd[16];
     float s1 = 0.f, s2 = 0.f;
+    // the row's accumulate input (dx) and layer-scale branch rows are loaded with x / dy, so a row costs one memory
+    // round trip instead of two
+    float4 dxo[4];
+    bf16x4 lyv[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int col = (lane + 64 * i) * 4;
+      dxo[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (col < a.D && a.dx_accumulate) {
+        const float* dsrc = a.ps ? a.dx + ps_src_row(row, col / a.C, a.G, a.tok_per_img) * a.lddx + (col % a.C)
+                                 : a.dx + row * a.lddx + col;
+        dxo[i] = *reinterpret_cast<const float4*>(dsrc);
+      }
+      if constexpr (LS) {
+        if (col < a.D) lyv[i] = *reinterpret_cast<const bf16x4*>(a.lsy + row * a.ldlsy + col);
+      }
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int col = (lane + 64 * i) * 4;
@@ -216,8 +233,7 @@ __global__ __launch_bounds__(256) void norm_bwd_wave_kernel(NormArgs a) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) ov[e] = rs * (gd[4 * i + e] - m1 - xh[4 * i + e] * m2);
       if (a.dx_accumulate) {
-        const float4 q = *reinterpret_cast<const float4*>(dst);
-        ov[0] += q.x; ov[1] += q.y; ov[2] += q.z; ov[3] += q.w;
+        ov[0] += dxo[i].x; ov[1] += dxo[i].y; ov[2] += dxo[i].z; ov[3] += dxo[i].w;
       }
       *reinterpret_cast<float4*>(dst) = make_float4(ov[0], ov[1], ov[2], ov[3]);
       if (a.dxb) {
@@ -228,7 +244,7 @@ __global__ __launch_bounds__(256) void norm_bwd_wave_kernel(NormArgs a) {
       }
       if constexpr (LS) {  // slx_ls_branch_bwd's per-element work on the row just produced (colsum_kernel<2>)
         const float4 l4 = *reinterpret_cast<const float4*>(a.ls + col);
-        const bf16x4 yy = *reinterpret_cast<const bf16x4*>(a.lsy + row * a.ldlsy + col);
+        const bf16x4 yy = lyv[i];
         const float lv[4] = {l4.x, l4.y, l4.z, l4.w};
         bf16x4 go;
 #pragma unroll
