@@ -995,7 +995,9 @@ static int split_for(const slx_gemm_desc* d, int v, int M, int batch) {
   const int tiles = ((M + v_tile_m(v) - 1) / v_tile_m(v)) * ((d->N + v_tile_n(v) - 1) / v_tile_n(v)) * batch;
   const int ksteps = (d->K + BK - 1) / BK;
   const int slots = v_slots(v);
-  if (!(d->epilogue == SLX_EPI_STORE && d->out_f32 && batch == 1 && tiles <= slots / 2 && ksteps >= 8)) return 1;
+  // (batched launches split too when they accumulate into C: no per-batch pre-zeroing needed; grid z = batch)
+  if (!(d->epilogue == SLX_EPI_STORE && d->out_f32 && (batch == 1 || d->accumulate) && tiles <= slots / 2 &&
+        ksteps >= 8)) return 1;
   if (d->ksplit_max < 0 || d->colsum) return 1;
   int sp = slots / tiles;  // floor: never more blocks than one round holds
   sp = sp < ksteps / 4 ? sp : ksteps / 4;

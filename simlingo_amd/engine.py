@@ -710,9 +710,24 @@ class VLAEngine(EngineOps):
         keep = sv["llm"][i]["lora"]
         bits = [keep[site] for site in sites]
         As = [self.cat[i]["axfrag." + site] for site in sites]
-        for j, site in enumerate(sites):
-            K.mm(dys[j], tx[:, r * j:r * (j + 1)], self.G[f"llm.{i}.lora.{site}.b"], ta=True, tb=False, alpha=s,
-                 accumulate=True)
+        # dB_j = s dy_j^T t_j. Sites of equal width whose dy columns are adjacent (k|v, gate|up) and whose B-gradient
+        # slices sit a fixed stride apart in the flat buffer (a, b interleaved per site) run as one batched split-K
+        # launch instead of one each.
+        j = 0
+        while j < len(sites):
+            gb = self.G[f"llm.{i}.lora.{sites[j]}.b"]
+            if j + 1 < len(sites):
+                gn = self.G[f"llm.{i}.lora.{sites[j + 1]}.b"]
+                out = dys[j].shape[1]
+                if (dys[j + 1].shape[1] == out and dys[j + 1].data_ptr() == dys[j].data_ptr() + 2 * out
+                        and gn.shape == gb.shape and gn.data_ptr() > gb.data_ptr()):
+                    sC = (gn.data_ptr() - gb.data_ptr()) // 4
+                    K.gemm(dys[j], tx[:, r * j:], gb, out, r, dys[j].shape[0], K.GEMM_TN, dys[j].stride(0),
+                           tx.stride(0), r, alpha=s, accumulate=True, batch=2, sA=out, sB=r, sC=sC)
+                    j += 2
+                    continue
+            K.mm(dys[j], tx[:, r * j:r * (j + 1)], gb, ta=True, tb=False, alpha=s, accumulate=True)
+            j += 1
         # dA and the dx term in one launch. (Running the parameter-only part - dB GEMMs, dA - on a side stream was
         # measured 6 ms/step slower: per-call event/stream overhead on the host and slower main-stream GEMMs.)
         K.lora_bwd(x, dtx, As, bits, [self.G[f"llm.{i}.lora.{site}.a"] for site in sites],

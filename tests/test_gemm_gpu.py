@@ -257,3 +257,25 @@ def test_gemm_colsum_bias_grad(dev, epi, M):
         ref = pre
     torch.testing.assert_close(out.float(), ref, atol=3e-2 * Kd ** 0.5 / 16, rtol=2e-2)
     torch.testing.assert_close(cs, 0.5 + ref.sum(0), atol=2e-3 * M ** 0.5, rtol=1e-3)
+
+
+def test_batched_splitk_accumulate_tn(dev):
+    """Batched TN weight-gradient GEMM with split-K f32 atomics accumulating into C (the LoRA dB pairs k|v and
+    gate|up: A = adjacent column blocks of dy, B = adjacent 32-column blocks of t, C = B-gradient slices sC apart)."""
+    g = torch.Generator(device=dev).manual_seed(21)
+    M, out, r = 3000, 640, 32
+    dy = torch.randn(M, 2 * out + 16, device=dev, generator=g).bfloat16()
+    t = torch.randn(M, 2 * r + 64, device=dev, generator=g).bfloat16()
+    flat = torch.zeros(3 * out * r + 4096, device=dev)
+    sC = out * r + 1024
+    C0, C1 = flat[:out * r].view(out, r), flat[sC:sC + out * r].view(out, r)
+    C0.fill_(0.5)
+    C1.fill_(-0.25)
+    K.gemm(dy, t, C0, out, r, M, K.GEMM_TN, dy.stride(0), t.stride(0), r, alpha=2.0, accumulate=True, batch=2,
+           sA=out, sB=r, sC=sC)
+    torch.cuda.synchronize()
+    want0 = 0.5 + 2.0 * dy[:, :out].float().t() @ t[:, :r].float()
+    want1 = -0.25 + 2.0 * dy[:, out:2 * out].float().t() @ t[:, r:2 * r].float()
+    torch.testing.assert_close(C0, want0, atol=2e-2, rtol=1e-3)
+    torch.testing.assert_close(C1, want1, atol=2e-2, rtol=1e-3)
+    assert torch.all(flat[out * r:sC] == 0) and torch.all(flat[sC + out * r:] == 0)  # nothing written between
