@@ -607,7 +607,8 @@ __global__ __launch_bounds__(256, ATTN_DQ_OCC) void attn_bwd_dq_kernel(AttnArgs 
   float c0[16], c1[16];  // the stored bf16 values, for the bias column sums
   // dQ of this query: dims d and d + 32 (a RoPE pair) sit in dq0[r] / dq1[r] of the same lane, so the inverse
   // rotation and the bf16 store need no exchange (no f32 workspace, no finalize launch)
-  bf16* qrow = a.dq + ((long)b * S + (qvalid ? myq : 0)) * a.lddq + h * 64;
+  const long qi = qvalid ? myq : 0;  // rows past S (no store) index row 0 of dq and of the RoPE tables
+  bf16* qrow = a.dq + ((long)b * S + qi) * a.lddq + h * 64;
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
     const int d = 8 * g + 4 * hl;
@@ -616,7 +617,7 @@ __global__ __launch_bounds__(256, ATTN_DQ_OCC) void attn_bwd_dq_kernel(AttnArgs 
     for (int e = 0; e < 4; ++e) {
       float x0 = dq0[4 * g + e] * a.scale, x1 = dq1[4 * g + e] * a.scale;
       if (a.rcos) {
-        const float cs = a.rcos[(long)myq * 32 + d + e], sn = a.rsin[(long)myq * 32 + d + e];
+        const float cs = a.rcos[qi * 32 + d + e], sn = a.rsin[qi * 32 + d + e];
         const float y0 = x0 * cs + x1 * sn, y1 = x1 * cs - x0 * sn;  // RoPE^T (rope_pair, inverse)
         x0 = y0;
         x1 = y1;
