@@ -78,6 +78,7 @@ typedef struct slx_gemm_desc {
   float* rem_ws; int64_t rem_ws_floats; /* optional scratch for the M % 256 remainder rows (<= 64 of them):
                        split-K f32 partials [splits][rem][N], then one epilogue pass; without it (or if
                        it is too small) the remainder runs as a latency-bound 16..64-row tile           */
+  int resid_bf16;   /* DROPMASK_SWIGLU: resid holds bf16 rows (the bf16 base gradient of a bf16 Linear backward)  */
 } slx_gemm_desc;
 int slx_gemm_bf16(const slx_gemm_desc* d, slx_stream_t stream);
 
@@ -205,7 +206,7 @@ int slx_lora_pack_a(const void* A, int64_t lda, int Kin, int layout, void* Af, s
 typedef struct {
   const void* x; int64_t ldx;         /* bf16 [M, Kin] (undropped forward input) */
   int64_t M; int Kin; int r; int nsites;
-  const float* dt; int64_t lddt;      /* f32 [M, >= 32*nsites] */
+  const float* dt; int64_t lddt;      /* f32 [M, >= 32*nsites] (bf16 with dt_bf16) */
   const void* A[4];                   /* bf16 packed A_j, slx_lora_pack_a layout 1 (read by the dx term only) */
   const uint32_t* bits[4]; int64_t ldbits;
   float* dA[4];                       /* f32 [32, Kin] per site, accumulated; all NULL: dx only (the dA pass can
@@ -213,6 +214,7 @@ typedef struct {
   float* dx; int64_t lddx;            /* f32 [M, Kin] or NULL (no input gradient) */
   void* dx_bf16; int64_t lddx_bf16;   /* optional bf16 [M, Kin] output instead of updating dx in place */
   float p;
+  int dt_bf16;                        /* 1: dt points to bf16 rows (lddt % 8 == 0), e.g. the bf16 dgrad GEMM output */
 } slx_lora_bwd_desc;
 int slx_lora_bwd(const slx_lora_bwd_desc* d, slx_stream_t stream);
 

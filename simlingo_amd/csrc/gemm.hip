@@ -29,7 +29,8 @@ namespace slx {
 constexpr int BM = 128, BN = 128, BK = 64, NT = 256;
 
 enum { EPI_STORE = 0, EPI_GELU = 1, EPI_RESID_LS = 2, EPI_GELU_BWD = 3, EPI_SWIGLU_BWD = 4, EPI_DROPMASK = 5,
-       EPI_DROPMASK_SWIGLU = 6, EPI_QGELU = 7, EPI_QGELU_BWD = 8 };
+       EPI_DROPMASK_SWIGLU = 6, EPI_QGELU = 7, EPI_QGELU_BWD = 8,
+       EPI_DROPMASK_SWIGLU_B = 9 /* internal: DROPMASK_SWIGLU with a bf16 resid (slx_gemm_desc.resid_bf16) */ };
 
 // CLIP quick_gelu x*sigmoid(1.702x) (transformers ACT2FN["quick_gelu"], the LLaVA-NeXT vision tower)
 __device__ __forceinline__ float qgelu(float x) { return x / (1.0f + __expf(-1.702f * x)); }
@@ -54,6 +55,7 @@ struct GemmArgs {
   long ldaux_out;
   const float* resid;
   long ldr;
+  int resid_bf16;  // DROPMASK_SWIGLU: resid points to bf16 rows
   int accumulate;
   unsigned long long seed;
   float drop_p;
@@ -222,9 +224,12 @@ __device__ __forceinline__ void epilogue_elem(const GemmArgs& p, OutT* __restric
     v *= epi_keep(p, m, n);
     if (p.accumulate) v += (float)C[ci];
     C[ci] = (OutT)v;
-  } else if constexpr (EPI == EPI_DROPMASK_SWIGLU) {
+  } else if constexpr (EPI == EPI_DROPMASK_SWIGLU || EPI == EPI_DROPMASK_SWIGLU_B) {
     if (p.drop_p > 0.f) v *= epi_keep(p, m, n);
-    const float d = v + p.resid[(long)m * p.ldr + n];
+    const long ri = (long)m * p.ldr + n;
+    float d = v;
+    if constexpr (EPI == EPI_DROPMASK_SWIGLU_B) d += (float)reinterpret_cast<const bf16*>(p.resid)[ri];
+    else d += p.resid[ri];
     const long ai = (long)m * p.ldaux + n;
     const float g = (float)p.aux[ai], u = (float)p.aux[ai + p.N];
     C[ci] = (OutT)(d * u * silu_grad(g));
@@ -331,7 +336,7 @@ __device__ __forceinline__ void epilogue_vec8(const GemmArgs& p, OutT* __restric
     for (int e = 0; e < 8; ++e) { o[e] = v[e] * u[e] * silu_grad(g[e]); u[e] = v[e] * silu(g[e]); }
     st8(C + ci, o);
     st8(C + ci + p.N, u);
-  } else if constexpr (EPI == EPI_DROPMASK_SWIGLU) {
+  } else if constexpr (EPI == EPI_DROPMASK_SWIGLU || EPI == EPI_DROPMASK_SWIGLU_B) {
     if (p.drop_p > 0.f) {
       const uint32_t kb = epi_keep8(p, m, n);
       const float sc = 1.0f / (1.0f - p.drop_p);
@@ -339,7 +344,8 @@ __device__ __forceinline__ void epilogue_vec8(const GemmArgs& p, OutT* __restric
       for (int e = 0; e < 8; ++e) v[e] *= (kb >> e) & 1u ? sc : 0.f;
     }
     float r[8], g[8], u[8];
-    ld8(p.resid + (long)m * p.ldr + n, r);
+    if constexpr (EPI == EPI_DROPMASK_SWIGLU_B) ld8(reinterpret_cast<const bf16*>(p.resid) + (long)m * p.ldr + n, r);
+    else ld8(p.resid + (long)m * p.ldr + n, r);
     ld8(p.aux + (long)m * p.ldaux + n, g);
     ld8(p.aux + (long)m * p.ldaux + p.N + n, u);
 #pragma unroll
@@ -1095,7 +1101,7 @@ static int gemm_launch(const slx_gemm_desc* d, int v, hipStream_t st, int mshift
   a.bias = d->bias; a.ls = d->ls;
   a.aux = (const bf16*)d->aux; a.ldaux = d->ldaux;
   a.aux_out = (bf16*)d->aux_out; a.ldaux_out = d->ldaux_out;
-  a.resid = d->resid; a.ldr = d->ldr;
+  a.resid = d->resid; a.ldr = d->ldr; a.resid_bf16 = d->resid_bf16;
   a.accumulate = d->accumulate;
   a.seed = d->seed; a.drop_p = d->drop_p; a.ldmask = d->ldmask;
   a.drop_operand = d->drop_operand;
@@ -1166,7 +1172,9 @@ static int gemm_launch(const slx_gemm_desc* d, int v, hipStream_t st, int mshift
       return launch_any<true, false, EPI_DROPMASK, float>(a, batch, st, v);
     case SLX_EPI_DROPMASK_SWIGLU:
       SLX_CHECK_ARG(!d->out_f32 && d->layout == SLX_GEMM_NN && d->aux && d->resid,
-                    "slx_gemm_bf16: DROPMASK_SWIGLU needs NN, bf16 out, aux (gate|up), resid (f32 base grad)");
+                    "slx_gemm_bf16: DROPMASK_SWIGLU needs NN, bf16 out, aux (gate|up), resid (f32 or bf16 base grad)");
+      SLX_CHECK_ARG(!d->resid_bf16 || d->epilogue == SLX_EPI_DROPMASK_SWIGLU, "slx_gemm_bf16: resid_bf16 is for DROPMASK_SWIGLU");
+      if (d->resid_bf16) return launch_any<true, false, EPI_DROPMASK_SWIGLU_B, bf16>(a, batch, st, v);
       return launch_any<true, false, EPI_DROPMASK_SWIGLU, bf16>(a, batch, st, v);
   }
   set_error("slx_gemm_bf16: bad epilogue %d", d->epilogue);

@@ -220,6 +220,7 @@ struct LoraBwdArgs {
   bf16* dxb; long lddxb;
   float sc;       // 1 / (1 - p)
   int mchunk;
+  int dt_bf16;    // dt holds bf16 rows
 };
 
 __device__ __forceinline__ int la_sw(int row, int chunk) {
@@ -248,7 +249,7 @@ __device__ __forceinline__ bf16x8 la_tr(const char* lds, int rbase, int cbase, i
 // loop is then transposed tile reads + v_mfma_f32_32x32x16_bf16 only (dT^T x masked x per 16-row slice), accumulated
 // in registers over the chunk, one set of f32 atomics per block at the end. The next sub-chunk's global loads are
 // issued into registers before the current one is multiplied.
-template <int NS>
+template <int NS, bool DTB>  // DTB: dt rows are bf16
 __global__ __launch_bounds__(256, 2) void lora_da_kernel(LoraBwdArgs a) {
   constexpr int TP = (32 * NS + 63) / 64;                     // dT panels
   __shared__ __attribute__((aligned(16))) char smem[(2 * NS + TP) * 8192];  // x_j: NS x 2 panels | dT: TP panels
@@ -276,8 +277,14 @@ __global__ __launch_bounds__(256, 2) void lora_da_kernel(LoraBwdArgs a) {
       rx[c4] = ok ? *reinterpret_cast<const uint4*>(a.x + (long)gm * a.ldx + c0 + 8 * c) : make_uint4(0u, 0u, 0u, 0u);
       if (8 * c < 32 * NS) {
         const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-        rt[c4][0] = ok ? *reinterpret_cast<const float4*>(a.dt + (long)gm * a.lddt + 8 * c) : z;
-        rt[c4][1] = ok ? *reinterpret_cast<const float4*>(a.dt + (long)gm * a.lddt + 8 * c + 4) : z;
+        if constexpr (DTB) {  // 8 bf16 in the bits of rt[c4][0]
+          const uint4 u = ok ? *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16*>(a.dt) + (long)gm * a.lddt + 8 * c)
+                             : make_uint4(0u, 0u, 0u, 0u);
+          rt[c4][0] = __builtin_bit_cast(float4, u);
+        } else {
+          rt[c4][0] = ok ? *reinterpret_cast<const float4*>(a.dt + (long)gm * a.lddt + 8 * c) : z;
+          rt[c4][1] = ok ? *reinterpret_cast<const float4*>(a.dt + (long)gm * a.lddt + 8 * c + 4) : z;
+        }
       }
     }
 #pragma unroll
@@ -315,8 +322,12 @@ __global__ __launch_bounds__(256, 2) void lora_da_kernel(LoraBwdArgs a) {
       }
       if (8 * c < 32 * NS) {
         bf16x8 t;
-        t[0] = (bf16)rt[c4][0].x; t[1] = (bf16)rt[c4][0].y; t[2] = (bf16)rt[c4][0].z; t[3] = (bf16)rt[c4][0].w;
-        t[4] = (bf16)rt[c4][1].x; t[5] = (bf16)rt[c4][1].y; t[6] = (bf16)rt[c4][1].z; t[7] = (bf16)rt[c4][1].w;
+        if constexpr (DTB) {
+          t = __builtin_bit_cast(bf16x8, rt[c4][0]);
+        } else {
+          t[0] = (bf16)rt[c4][0].x; t[1] = (bf16)rt[c4][0].y; t[2] = (bf16)rt[c4][0].z; t[3] = (bf16)rt[c4][0].w;
+          t[4] = (bf16)rt[c4][1].x; t[5] = (bf16)rt[c4][1].y; t[6] = (bf16)rt[c4][1].z; t[7] = (bf16)rt[c4][1].w;
+        }
         *reinterpret_cast<bf16x8*>(ts + (c >> 3) * 8192 + la_sw(srow, c & 7)) = t;
       }
     }
@@ -365,7 +376,7 @@ struct DxRegs {
   uint32_t kw[NS];
 };
 
-template <int NS>
+template <int NS, bool DTB>  // DTB: dt rows are bf16
 __global__ __launch_bounds__(512) void lora_dx_kernel(LoraBwdArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, r = lane & 31;
   const int row = blockIdx.x * 32 + r;
@@ -377,11 +388,19 @@ __global__ __launch_bounds__(512) void lora_dx_kernel(LoraBwdArgs a) {
   for (int j = 0; j < NS; ++j)
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {
-      const float* tp = a.dt + (long)(rok ? row : 0) * a.lddt + 32 * j + 16 * kb + 8 * h;
-      const float4 f0 = rok ? *reinterpret_cast<const float4*>(tp) : make_float4(0.f, 0.f, 0.f, 0.f);
-      const float4 f1 = rok ? *reinterpret_cast<const float4*>(tp + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
-      tb[j][kb][0] = (bf16)f0.x; tb[j][kb][1] = (bf16)f0.y; tb[j][kb][2] = (bf16)f0.z; tb[j][kb][3] = (bf16)f0.w;
-      tb[j][kb][4] = (bf16)f1.x; tb[j][kb][5] = (bf16)f1.y; tb[j][kb][6] = (bf16)f1.z; tb[j][kb][7] = (bf16)f1.w;
+      const long off = (long)(rok ? row : 0) * a.lddt + 32 * j + 16 * kb + 8 * h;
+      if constexpr (DTB) {
+        bf16x8 z;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) z[e] = (bf16)0.f;
+        tb[j][kb] = rok ? *reinterpret_cast<const bf16x8*>(reinterpret_cast<const bf16*>(a.dt) + off) : z;
+      } else {
+        const float* tp = a.dt + off;
+        const float4 f0 = rok ? *reinterpret_cast<const float4*>(tp) : make_float4(0.f, 0.f, 0.f, 0.f);
+        const float4 f1 = rok ? *reinterpret_cast<const float4*>(tp + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+        tb[j][kb][0] = (bf16)f0.x; tb[j][kb][1] = (bf16)f0.y; tb[j][kb][2] = (bf16)f0.z; tb[j][kb][3] = (bf16)f0.w;
+        tb[j][kb][4] = (bf16)f1.x; tb[j][kb][5] = (bf16)f1.y; tb[j][kb][6] = (bf16)f1.z; tb[j][kb][7] = (bf16)f1.w;
+      }
     }
   auto load = [&](int ct, DxRegs<NS>& R) {
 #pragma unroll
@@ -506,10 +525,15 @@ extern "C" int slx_dropout_bits(const slx_dropout_bits_desc* d, slx_stream_t str
   return 0;
 }
 
+template <int NS, bool DTB>
+static void launch_bwd_t(const LoraBwdArgs& a, dim3 grid, hipStream_t st) {
+  if (a.dA[0]) hipLaunchKernelGGL((lora_da_kernel<NS, DTB>), grid, dim3(256), 0, st, a);
+  if (a.dx) hipLaunchKernelGGL((lora_dx_kernel<NS, DTB>), dim3((unsigned)((a.M + 31) / 32)), dim3(512), 0, st, a);
+}
 template <int NS>
 static void launch_bwd(const LoraBwdArgs& a, dim3 grid, hipStream_t st) {
-  if (a.dA[0]) hipLaunchKernelGGL(lora_da_kernel<NS>, grid, dim3(256), 0, st, a);
-  if (a.dx) hipLaunchKernelGGL(lora_dx_kernel<NS>, dim3((unsigned)((a.M + 31) / 32)), dim3(512), 0, st, a);
+  if (a.dt_bf16) launch_bwd_t<NS, true>(a, grid, st);
+  else launch_bwd_t<NS, false>(a, grid, st);
 }
 
 extern "C" int slx_lora_bwd(const slx_lora_bwd_desc* d, slx_stream_t stream) {
@@ -527,7 +551,8 @@ extern "C" int slx_lora_bwd(const slx_lora_bwd_desc* d, slx_stream_t stream) {
   LoraBwdArgs a;
   memset(&a, 0, sizeof(a));
   a.x = (const bf16*)d->x; a.ldx = d->ldx; a.M = (int)d->M; a.Kin = d->Kin; a.nsites = d->nsites;
-  a.dt = d->dt; a.lddt = d->lddt;
+  a.dt = d->dt; a.lddt = d->lddt; a.dt_bf16 = d->dt_bf16;
+  SLX_CHECK_ARG(!d->dt_bf16 || d->lddt % 8 == 0, "slx_lora_bwd: bf16 dt needs lddt %% 8 (16-B row loads)");
   for (int i = 0; i < 4; ++i) {
     a.A[i] = (const bf16*)(i < d->nsites ? d->A[i] : d->A[0]);
     a.bits[i] = (d->p > 0.f && i < d->nsites) ? d->bits[i] : nullptr;

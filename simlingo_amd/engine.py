@@ -558,7 +558,9 @@ class VLAEngine(EngineOps):
             Pq, Po, Pg, Pd = (128, 64, 64, 64) if lora else (0, 0, 0, 0)
             hx, ox, h2x, ax = Ls["hx"], Ls["ox"], Ls["h2x"], Ls["ax"]
             # down projection: Xo = Xm + [act | t_d] . [Wd | s B_d]^T   (dxb = bf16(dX), from the last norm backward)
-            dax = self._e(Ml, Fl + Pd, dtype=F32)
+            # bf16 with LoRA: the gradient of act that a bf16 Linear backward produces under autocast (read once by the
+            # SwiGLU epilogue and, columns Fl.., as the dT operand); f32 for the plain slx_swiglu_bwd path
+            dax = self._e(Ml, Fl + Pd, dtype=BF16 if lora else F32)
             K.mm(dxb, cat["down"] if lora else self.W[p + "down_w"], dax, tb=False)
             dgu = self._e(Ml, 2 * Fl)
             if lora:  # the down-site dropout dgrad and the SwiGLU backward share one GEMM epilogue
@@ -736,8 +738,12 @@ class VLAEngine(EngineOps):
             gu, dgu = swiglu
             M = x.shape[0]
             F = gu.shape[1] // 2
-            dT = self._buf(("dT_down",), M, 64)  # bf16 K=64 operand: dt_down | 32 zero columns (W_cat padding)
-            K.call("slx_cast_rows", K.P(dtx), dtx.stride(0), K.P(dT), dT.stride(0), M, 64, K.stream_ptr())
+            if dtx.dtype == torch.bfloat16:  # the K=64 operand straight from the bf16 dgrad output (64 columns)
+                assert dtx.shape[1] == 64
+                dT = dtx
+            else:
+                dT = self._buf(("dT_down",), M, 64)  # bf16 K=64 operand: dt_down | 32 zero columns (W_cat padding)
+                K.call("slx_cast_rows", K.P(dtx), dtx.stride(0), K.P(dT), dT.stride(0), M, 64, K.stream_ptr())
             K.gemm(dT, self.cat[i]["apad.down"], dgu, M, F, 64, K.GEMM_NN, dT.stride(0), x.shape[1], dgu.stride(0),
                    epi=K.EPI_DROPMASK_SWIGLU, resid=dx, ldr=dx.stride(0), aux=gu, ldaux=gu.stride(0),
                    seed=lora_site_seed(sv["step_seed"], i, LORA_SITES.index("down")), drop_p=drop,

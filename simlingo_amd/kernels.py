@@ -40,7 +40,7 @@ class GemmDesc(ctypes.Structure):
         ("seed", c_u64), ("drop_p", c_float), ("ldmask", c_i64),
         ("ksplit_max", c_int), ("variant", c_int), ("drop_operand", c_int),
         ("colsum", c_vp), ("colsum_ws", c_vp), ("maskbits", c_vp), ("ldbits", c_i64), ("rem_ws", c_vp),
-        ("rem_ws_floats", c_i64),
+        ("rem_ws_floats", c_i64), ("resid_bf16", c_int),
     ]
 
 
@@ -138,6 +138,7 @@ def gemm(A, B, C, M, N, K, layout, lda, ldb, ldc, *, epi=EPI_STORE, alpha=1.0, b
     d.aux_out = aux_out.data_ptr() if aux_out is not None else 0
     d.ldaux_out = int(ldaux_out)
     d.resid = resid.data_ptr() if resid is not None else 0
+    d.resid_bf16 = int(resid is not None and resid.dtype == torch.bfloat16)
     d.ldr = int(ldr)
     d.accumulate = 1 if accumulate else 0
     d.seed, d.drop_p, d.ldmask = int(seed) & ((1 << 64) - 1), float(drop_p), int(ldmask)
@@ -253,7 +254,7 @@ class LoraBwdDesc(ctypes.Structure):
     _fields_ = [
         ("x", c_vp), ("ldx", c_i64), ("M", c_i64), ("Kin", c_int), ("r", c_int), ("nsites", c_int),
         ("dt", c_vp), ("lddt", c_i64), ("A", c_vp * 4), ("bits", c_vp * 4), ("ldbits", c_i64), ("dA", c_vp * 4),
-        ("dx", c_vp), ("lddx", c_i64), ("dx_bf16", c_vp), ("lddx_bf16", c_i64), ("p", c_float),
+        ("dx", c_vp), ("lddx", c_i64), ("dx_bf16", c_vp), ("lddx_bf16", c_i64), ("p", c_float), ("dt_bf16", c_int),
     ]
 
 
@@ -498,13 +499,14 @@ def lora_bwd(x, dt, As, bits, dAs, dx=None, dx_bf16=None, p=0.0, packed=False):
     """peft LoRA backward of the sites sharing x (one launch): dAs[j] (f32 [32, kin]) += dT_j^T drop_j(x) (dAs=None:
     skipped) and, if dx (f32 [M, kin]) is given, dx += sum_j drop_j'(dT_j As[j]) in place - or written as
     bf16(dx + ...) to dx_bf16.
-    dt: f32 [M, >= 32 n] (dT_j = columns 32j..); bits[j]: keep bits from lora_down (None when p == 0).
+    dt: f32 or bf16 [M, >= 32 n] (dT_j = columns 32j..); bits[j]: keep bits from lora_down (None when p == 0).
     As: [32, kin] matrices (packed here into slx_lora_pack_a layout 1 when dx is asked for), or with packed=True the
     layout-1 copies themselves (only the dx term reads A)."""
-    assert x.dtype == torch.bfloat16 and dt.dtype == torch.float32 and 1 <= len(As) <= 4
+    assert x.dtype == torch.bfloat16 and dt.dtype in (torch.float32, torch.bfloat16) and 1 <= len(As) <= 4
     M, kin = x.shape
     assert dt.shape[0] == M and dt.shape[1] >= 32 * len(As) and dt.stride(1) == 1
     d = LoraBwdDesc()
+    d.dt_bf16 = int(dt.dtype == torch.bfloat16)
     d.x, d.ldx, d.M, d.Kin, d.r, d.nsites = P(x).value, x.stride(0), M, kin, 32, len(As)
     d.dt, d.lddt = P(dt).value, dt.stride(0)
     if not packed:

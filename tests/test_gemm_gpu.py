@@ -205,26 +205,32 @@ def test_gemm_v3_overlapped_last_tile(dev):
     torch.testing.assert_close(acc, 1.0 + x.float() @ w.float().t(), atol=2e-3, rtol=2e-3)
 
 
-@pytest.mark.parametrize("p,use_bits", [(0.0, False), (0.1, False), (0.1, True)])
-def test_gemm_dropmask_swiglu_epilogue(dev, p, use_bits):
+@pytest.mark.parametrize("p,use_bits,resid_bf16", [(0.0, False, False), (0.1, False, False), (0.1, True, False),
+                                                   (0.1, True, True)])
+def test_gemm_dropmask_swiglu_epilogue(dev, p, use_bits, resid_bf16):
     """EPI_DROPMASK_SWIGLU: dgu = SwiGLU'(gu) applied to (resid + keep * dT.A): the Qwen2 down-projection LoRA
-    dropout dgrad fused into the SwiGLU backward (engine._lora_bwd, swiglu=...)."""
+    dropout dgrad fused into the SwiGLU backward (engine._lora_bwd, swiglu=...). resid_bf16: the base gradient as the
+    bf16 dgrad output (slx_gemm_desc.resid_bf16), dT read from its trailing 64 columns as the engine does."""
     from simlingo_amd.dropmask import keep_scale
     M, F, seed = 300, 256, 4242
     g = torch.Generator(device=dev).manual_seed(3)
     dT = torch.randn(M, 64, device=dev, generator=g).bfloat16()
     A = (torch.randn(64, F, device=dev, generator=g) * 0.1).bfloat16()
     base = torch.randn(M, F + 64, device=dev, generator=g)
+    if resid_bf16:
+        base = base.bfloat16()
+        base[:, F:] = dT
+        dT = base[:, F:]
     gu = torch.randn(M, 2 * F, device=dev, generator=g).bfloat16()
     dgu = torch.empty(M, 2 * F, device=dev, dtype=torch.bfloat16)
     bits = None
     if use_bits:  # the keep bits slx_lora_down stores (host mirror), read instead of the hash
         from simlingo_amd.dropmask import keep_bits
         bits = torch.from_numpy(keep_bits(seed, M, F, F, p).view("int32")).to(dev)
-    K.gemm(dT, A, dgu, M, F, 64, K.GEMM_NN, 64, F, 2 * F, epi=K.EPI_DROPMASK_SWIGLU, resid=base, ldr=F + 64, aux=gu,
-           ldaux=2 * F, seed=seed if not use_bits else seed + 1, drop_p=p, ldmask=F, maskbits=bits)
+    K.gemm(dT, A, dgu, M, F, 64, K.GEMM_NN, dT.stride(0), F, 2 * F, epi=K.EPI_DROPMASK_SWIGLU, resid=base,
+           ldr=F + 64, aux=gu, ldaux=2 * F, seed=seed if not use_bits else seed + 1, drop_p=p, ldmask=F, maskbits=bits)
     mask = torch.from_numpy(keep_scale(seed, M, F, F, p)).to(dev) if p > 0 else 1.0
-    d = base[:, :F] + mask * (dT.float() @ A.float())
+    d = base[:, :F].float() + mask * (dT.float() @ A.float())
     gg, uu = gu.float()[:, :F].requires_grad_(), gu.float()[:, F:].requires_grad_()
     (torch.nn.functional.silu(gg) * uu).backward(d)
     torch.testing.assert_close(dgu[:, :F].float(), gg.grad, atol=3e-2, rtol=2e-2)

@@ -87,7 +87,8 @@ def test_dropmask_dgrad_padded_k64(dev):
                                                  (6384, 896, 3, 0.1, "f32"), (6384, 896, 1, 0.1, "bf16"),
                                                  (6384, 4864, 1, 0.1, "none"), (798, 128, 3, 0.0, "f32"),
                                                  (798, 896, 2, 0.0, "bf16")])
-def test_lora_bwd_grouped(dev, M, kin, nsites, p, mode):
+@pytest.mark.parametrize("dt_bf16", [False, True])
+def test_lora_bwd_grouped(dev, M, kin, nsites, p, mode, dt_bf16):
     """slx_lora_bwd: dA_j += dT_j^T drop_j(x) and dx += sum_j drop_j'(dT_j A_j) (f32 in place / bf16 out / none),
     masks read from the keep bits of slx_lora_down, dT read as f32 from a strided view (the dgrad GEMM's extra
     columns)."""
@@ -95,6 +96,8 @@ def test_lora_bwd_grouped(dev, M, kin, nsites, p, mode):
     g = torch.Generator(device=dev).manual_seed(13)
     x = torch.randn(M, kin, device=dev, generator=g).bfloat16()
     dtfull = torch.randn(M, 32 * nsites + 64, device=dev, generator=g)
+    if dt_bf16:  # slx_lora_bwd_desc.dt_bf16: dT as the bf16 dgrad output columns (16-B aligned rows)
+        dtfull = dtfull.bfloat16()
     dt = dtfull[:, 16:16 + 32 * nsites]
     As = [(torch.randn(32, kin, device=dev, generator=g) * 0.1).bfloat16() for _ in range(nsites)]
     seeds = [777 + 31 * j for j in range(nsites)]
