@@ -81,6 +81,11 @@ typedef struct slx_gemm_desc {
   int resid_bf16;   /* DROPMASK_SWIGLU: resid holds bf16 rows (the bf16 base gradient of a bf16 Linear backward)  */
 } slx_gemm_desc;
 int slx_gemm_bf16(const slx_gemm_desc* d, slx_stream_t stream);
+/* Two independent accumulating f32 STORE GEMMs (same layout and K, no bias / colsum / batch) in one launch:
+ * the InternViT weight-gradient pairs (fc2.w + fc1.w, proj.w + qkv.w; the torch autograd wgrad GEMMs of
+ * internvl2 InternMLP / InternAttention, K = tokens) share one round of 256 split-K blocks.
+ * d1->ksplit_max caps the split count (0 = automatic).                                                     */
+int slx_gemm_bf16_pair(const slx_gemm_desc* d1, const slx_gemm_desc* d2, slx_stream_t stream);
 
 /* ---- Attention (head_dim 64) ----------------------------------------------------------------
  * Replaces flash-attn 2.7.0.post2 (README.md:67-68) inside the InternVL2-1B remote code:
@@ -315,7 +320,9 @@ int slx_dec_begin(slx_dec_state* st, unsigned long long* keys, const void* embed
                   slx_stream_t s);
 int slx_dec_gemv(const slx_dec_gemv_desc* d, slx_stream_t s);
 /* one query row (cache row state->pos) over cache rows [0, pos]; q/k rotated with cos/sin row pos;
- * split over keys (slx_dec_attn_nsplit(lmax) workgroups per kv head, partials in ws) + combine;
+ * split over keys (slx_dec_attn_nsplit(lmax) workgroups per kv head, partials in ws), merged in the
+ * same launch by the last-arriving workgroup of each kv head (arrival counters at the end of ws: ws
+ * must be zeroed once before first use; every call leaves the counters at 0 again);
  * out bf16 [Hq*64]; lmax = cache rows allocated (the split count is fixed by it: graph-safe)      */
 int slx_dec_attn_nsplit(int lmax);
 int slx_dec_attn_ws_floats(int Hq, int Hkv, int lmax);

@@ -785,19 +785,19 @@ __device__ __forceinline__ void v3_mfma(f32x4 (&acc)[8][4], int mh, int nh, cons
   __builtin_amdgcn_s_setprio(0);
 }
 
+// XCD-bijective block order: blocks dealt round-robin over the 8 XCDs get contiguous tile ranges per XCD
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int q = nwg >> 3, r = nwg & 7, xcd = bid & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+}
+
+// One 256x256 output tile (tile index bid of p's grid after the XCD remap), K range of split blockIdx.y, batch z.
 template <bool AK, bool BKc, int EPI, typename OutT>
-__global__ __launch_bounds__(512, 1) void gemm_bf16_v3_kernel(GemmArgs p) {
+__device__ __forceinline__ void v3_tile(const GemmArgs& p, int bid, long z, char* smem) {
   constexpr int NW = 8;
   constexpr int A_BYTES = V3_BM * BK * 2, B_BYTES = V3_BN * BK * 2;
   constexpr int STAGE = A_BYTES + B_BYTES;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tilesM = p.tilesM, tilesN = p.tilesN;
-  const int nwg = tilesM * tilesN;
-  int bid = blockIdx.x;
-  {
-    const int q = nwg >> 3, r = nwg & 7, xcd = bid & 7;
-    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-  }
   constexpr int GROUP = 4;
   const int npg = GROUP * tilesN;
   const int gid = bid / npg;
@@ -808,7 +808,6 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_v3_kernel(GemmArgs p) {
   // mshift_last: the partial last M tile is shifted up to end at M, so every tile is full; the rows it shares with
   // the previous tile are recomputed bit-identically (same K order) and stored twice with the same values.
   const int m0 = (p.mshift_last && tm == tilesM - 1) ? p.M - V3_BM : tm * V3_BM, n0 = tn * V3_BN;
-  const long z = blockIdx.z;
   const bf16* A = p.A + z * p.sA;
   const bf16* B = p.B + z * p.sB;
   OutT* __restrict__ C = reinterpret_cast<OutT*>(p.C) + z * p.sC;
@@ -908,6 +907,24 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_v3_kernel(GemmArgs p) {
     epilogue_tile64<EPI, OutT>(p, C, ep, lane, m0 + arow + 64 * mh, n0 + bcol);
     __builtin_amdgcn_s_waitcnt(0xC07F);
   }
+}
+
+template <bool AK, bool BKc, int EPI, typename OutT>
+__global__ __launch_bounds__(512, 1) void gemm_bf16_v3_kernel(GemmArgs p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  v3_tile<AK, BKc, EPI, OutT>(p, xcd_remap(blockIdx.x, p.tilesM * p.tilesN), blockIdx.z, smem);
+}
+
+// Two independent GEMMs of one layout (f32 outputs accumulated, same K and split count) in one launch: grid.x
+// covers both tile sets, so two under-filled weight-gradient grids (InternViT fc2 + fc1, proj + qkv) fill the chip
+// together instead of leaving CUs idle one after the other.
+template <bool AK, bool BKc>
+__global__ __launch_bounds__(512, 1) void gemm_bf16_v3_pair_kernel(GemmArgs p, GemmArgs q) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int n1 = p.tilesM * p.tilesN;
+  const int bid = xcd_remap(blockIdx.x, n1 + q.tilesM * q.tilesN);
+  if (bid < n1) v3_tile<AK, BKc, EPI_STORE, float>(p, bid, 0, smem);
+  else v3_tile<AK, BKc, EPI_STORE, float>(q, bid - n1, 0, smem);
 }
 
 template <bool AK, bool BKc, int EPI, typename OutT>
@@ -1316,4 +1333,73 @@ extern "C" int slx_gemm_bf16(const slx_gemm_desc* d, slx_stream_t stream) {
   const int rc = gemm_launch(d, v, st);
   if (rc) return rc;
   return d->colsum ? colsum_reduce(d, st) : 0;
+}
+
+// Two accumulating f32-output GEMMs of one layout and one K in a single v3 launch (gemm_bf16_v3_pair_kernel): the
+// InternViT weight gradients come in pairs whose separate grids under-fill the chip (fc1/fc2: 64 tiles of 256^2
+// each, qkv/proj: 48 + 16 tiles, K = 16400 tokens); together they split K over one full round of 256 blocks.
+static void pair_args(const slx_gemm_desc* d, GemmArgs& a) {
+  memset(&a, 0, sizeof(a));
+  a.A = (const bf16*)d->A; a.B = (const bf16*)d->B; a.C = d->C;
+  a.lda = d->lda; a.ldb = d->ldb; a.ldc = d->ldc;
+  a.M = d->M; a.N = d->N; a.K = d->K;
+  a.alpha = d->alpha;
+  a.accumulate = 1;
+  a.vec_ok = d->ldc % 8 == 0 && ((uintptr_t)d->C % 16) == 0;
+  a.tilesM = (d->M + V3_BM - 1) / V3_BM;
+  a.tilesN = (d->N + V3_BN - 1) / V3_BN;
+}
+
+template <bool AK, bool BKc>
+static int launch_pair(GemmArgs& a, GemmArgs& b, hipStream_t st) {
+  constexpr int LDS_RING = 2 * (V3_BM * BK * 2 + V3_BN * BK * 2);
+  constexpr int LDS_EP = 8 * 64 * EP_LD * 4;
+  constexpr int LDS = LDS_RING > LDS_EP ? LDS_RING : LDS_EP;
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)gemm_bf16_v3_pair_kernel<AK, BKc>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    attr = true;
+  }
+  dim3 grid(a.tilesM * a.tilesN + b.tilesM * b.tilesN, a.ksplit);
+  hipLaunchKernelGGL((gemm_bf16_v3_pair_kernel<AK, BKc>), grid, dim3(512), LDS, st, a, b);
+  SLX_LAUNCH_CHECK("slx_gemm_bf16_pair");
+  return 0;
+}
+
+extern "C" int slx_gemm_bf16_pair(const slx_gemm_desc* d1, const slx_gemm_desc* d2, slx_stream_t stream) {
+  SLX_CHECK_ARG(d1 && d2, "slx_gemm_bf16_pair: null desc");
+  SLX_CHECK_ARG(d1->layout == d2->layout && d1->K == d2->K, "slx_gemm_bf16_pair: the two GEMMs need one layout and one K");
+  for (const slx_gemm_desc* d : {d1, d2}) {
+    SLX_CHECK_ARG(d->M > 0 && d->N > 0 && d->K > 0 && d->batch <= 1, "slx_gemm_bf16_pair: positive dims, no batch");
+    SLX_CHECK_ARG(d->epilogue == SLX_EPI_STORE && d->out_f32 && d->accumulate && !d->colsum && !d->bias &&
+                  d->drop_operand == 0, "slx_gemm_bf16_pair: f32 accumulate STORE only (no bias / colsum / dropout)");
+    const bool ak = d->layout == SLX_GEMM_NT || d->layout == SLX_GEMM_NN;
+    const bool bk = d->layout == SLX_GEMM_NT || d->layout == SLX_GEMM_TT;
+    SLX_CHECK_ARG((ak ? d->K : d->M) % 8 == 0 && (bk ? d->K : d->N) % 8 == 0 && d->lda % 8 == 0 && d->ldb % 8 == 0 &&
+                  ((uintptr_t)d->A & 15) == 0 && ((uintptr_t)d->B & 15) == 0,
+                  "slx_gemm_bf16_pair: 16-B aligned operands with contiguous dims and leading dims multiples of 8");
+    SLX_CHECK_ARG((!ak || d->K % BK == 0) && (!bk || d->K % BK == 0), "slx_gemm_bf16_pair: K-contiguous operands need K %% %d == 0", BK);
+  }
+  GemmArgs a, b;
+  pair_args(d1, a);
+  pair_args(d2, b);
+  const int tiles = a.tilesM * a.tilesN + b.tilesM * b.tilesN;
+  const int ksteps = (d1->K + BK - 1) / BK;
+  int sp = 256 / tiles;  // one round of 256 blocks
+  if (sp > ksteps / 4) sp = ksteps / 4;
+  if (d1->ksplit_max > 0 && sp > d1->ksplit_max) sp = d1->ksplit_max;
+  if (sp < 1) sp = 1;
+  const int per = ((ksteps + sp - 1) / sp) * BK;
+  sp = (d1->K + per - 1) / per;
+  a.ksplit = b.ksplit = sp;
+  a.kchunk = b.kchunk = sp > 1 ? per : d1->K;
+  hipStream_t st = (hipStream_t)stream;
+  switch (d1->layout) {
+    case SLX_GEMM_NT: return launch_pair<true, true>(a, b, st);
+    case SLX_GEMM_NN: return launch_pair<true, false>(a, b, st);
+    case SLX_GEMM_TN: return launch_pair<false, false>(a, b, st);
+    case SLX_GEMM_TT: return launch_pair<false, true>(a, b, st);
+  }
+  set_error("slx_gemm_bf16_pair: bad layout %d", d1->layout);
+  return -22;
 }

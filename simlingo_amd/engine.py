@@ -17,6 +17,7 @@ All arithmetic is in libslx_hip.so; torch only allocates and supplies the stream
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -31,6 +32,8 @@ from .params import LORA_SITES, lora_io, param_specs
 from .plan import Plan
 
 BF16, F32 = torch.bfloat16, torch.float32
+# InternViT weight gradients as paired launches (slx_gemm_bf16_pair); SLX_PAIR_WGRAD=0 runs them one by one (A/B)
+PAIR_WGRAD = os.environ.get("SLX_PAIR_WGRAD", "1") != "0"
 ALIGN = 64  # elements; keeps every parameter view 256-B aligned
 
 
@@ -650,11 +653,15 @@ class VLAEngine(EngineOps):
             if i == cfg.vit_layers - 1:
                 K.call("slx_ls_branch_bwd", K.P(dxv), D, K.P(self.P[p + "ls2"]), K.P(Ls["y2"]), D, K.P(g), D, Mv, D,
                        K.P(self.G[p + "ls2"]), K.P(self.G[p + "fc2.b"]), 1, K.P(self._ws(2 * 256 * D)), K.stream_ptr())
-            K.mm(g, Ls["hact"], self.G[p + "fc2.w"], ta=True, tb=False, accumulate=True)
+            if not PAIR_WGRAD:
+                K.mm(g, Ls["hact"], self.G[p + "fc2.w"], ta=True, tb=False, accumulate=True)
             dh = self._e(Mv, F_)
             K.mm(g, self.W[p + "fc2.w"], dh, tb=False, epi=K.EPI_GELU_BWD, aux=Ls["hpre"], ldaux=F_,
                  colsum=self.G[p + "fc1.b"])  # fc1.b grad = column sums of dh, in the same epilogue
-            K.mm(dh, Ls["h2"], self.G[p + "fc1.w"], ta=True, tb=False, accumulate=True)
+            if PAIR_WGRAD:  # fc2.w and fc1.w gradients as one launch (two under-filled grids fill the chip together)
+                K.mm_pair((g, Ls["hact"], self.G[p + "fc2.w"]), (dh, Ls["h2"], self.G[p + "fc1.w"]))
+            else:
+                K.mm(dh, Ls["h2"], self.G[p + "fc1.w"], ta=True, tb=False, accumulate=True)
             dh2 = self._e(Mv, D)  # bf16: the gradient a bf16 Linear backward hands the fp32 LayerNorm under autocast
             K.mm(dh, self.W[p + "fc1.w"], dh2, tb=False)
             del dh
@@ -663,7 +670,8 @@ class VLAEngine(EngineOps):
             K.norm_bwd(Ls["n2"], dh2, dxv, dx_accumulate=True, dgamma=self.G[p + "ln2.w"], dbeta=self.G[p + "ln2.b"],
                        ws=self._ws(K.norm_ws_floats(D)), param_accumulate=True,
                        ls_branch=(self.P[p + "ls1"], Ls["y1"], g, self.G[p + "ls1"], self.G[p + "proj.b"]))
-            K.mm(g, Ls["o"], self.G[p + "proj.w"], ta=True, tb=False, accumulate=True)
+            if not PAIR_WGRAD:
+                K.mm(g, Ls["o"], self.G[p + "proj.w"], ta=True, tb=False, accumulate=True)
             do = self._e(Mv, D)
             K.mm(g, self.W[p + "proj.w"], do, tb=False)
             qkv = Ls["qkv"]
@@ -672,7 +680,10 @@ class VLAEngine(EngineOps):
                        dqkv[:, :D], dqkv[:, D:2 * D], dqkv[:, 2 * D:], vws, B=N, S=T, Hq=H, Hkv=H, causal=False,
                        dbias=self.G[p + "qkv.b"])  # qkv.b grad = column sums of dq | dk | dv, in the same kernels
             del do
-            K.mm(dqkv, Ls["h1"], self.G[p + "qkv.w"], ta=True, tb=False, accumulate=True)
+            if PAIR_WGRAD:  # proj.w (g still holds ls1 * dx_mid) and qkv.w gradients as one launch
+                K.mm_pair((g, Ls["o"], self.G[p + "proj.w"]), (dqkv, Ls["h1"], self.G[p + "qkv.w"]))
+            else:
+                K.mm(dqkv, Ls["h1"], self.G[p + "qkv.w"], ta=True, tb=False, accumulate=True)
             K.mm(dqkv, self.W[p + "qkv.w"], dh2, tb=False)
             del dqkv
             nxt = None

@@ -49,6 +49,7 @@ _SIGS: dict[str, list] = {
     "slx_abi_version": [],
     "slx_device_sync": [],
     "slx_gemm_bf16": [ctypes.POINTER(GemmDesc), c_vp],
+    "slx_gemm_bf16_pair": [ctypes.POINTER(GemmDesc), ctypes.POINTER(GemmDesc), c_vp],
 }
 _RESTYPE = {"slx_last_error": ctypes.c_char_p}
 
@@ -118,10 +119,20 @@ _rem_ws: dict = {}     # per-device split-K scratch of the M-remainder rows (str
 REM_WS_FLOATS = 16 << 20  # 64 MB: 32 splits x 64 rows x 8192 columns
 
 
-def gemm(A, B, C, M, N, K, layout, lda, ldb, ldc, *, epi=EPI_STORE, alpha=1.0, bias=None, ls=None,
-         aux=None, ldaux=0, aux_out=None, ldaux_out=0, resid=None, ldr=0, accumulate=False,
-         seed=0, drop_p=0.0, ldmask=0, batch=1, sA=0, sB=0, sC=0, ksplit_max=0, variant=None, drop_operand=0,
-         colsum=None, maskbits=None):
+def gemm(A, B, C, M, N, K, layout, lda, ldb, ldc, **kw):
+    d = _gemm_desc(A, B, C, M, N, K, layout, lda, ldb, ldc, **kw)
+    if A.dtype == torch.float32:  # fp32 parity mode (csrc/precise.hip)
+        if B.dtype != torch.float32 or C.dtype != torch.float32:
+            raise RuntimeError("fp32 parity-mode GEMM needs f32 A, B and C")
+        check(lib().slx_gemm_f32(ctypes.byref(d), stream_ptr()), "slx_gemm_f32")
+        return
+    check(lib().slx_gemm_bf16(ctypes.byref(d), stream_ptr()), "slx_gemm_bf16")
+
+
+def _gemm_desc(A, B, C, M, N, K, layout, lda, ldb, ldc, *, epi=EPI_STORE, alpha=1.0, bias=None, ls=None,
+               aux=None, ldaux=0, aux_out=None, ldaux_out=0, resid=None, ldr=0, accumulate=False,
+               seed=0, drop_p=0.0, ldmask=0, batch=1, sA=0, sB=0, sC=0, ksplit_max=0, variant=None, drop_operand=0,
+               colsum=None, maskbits=None):
     _require_cuda(A, B, C)
     d = GemmDesc()
     d.layout, d.epilogue = layout, epi
@@ -160,12 +171,7 @@ def gemm(A, B, C, M, N, K, layout, lda, ldb, ldc, *, epi=EPI_STORE, alpha=1.0, b
             ws = torch.empty(max(need, 1 << 20), dtype=torch.float32, device=C.device)
             _colsum_ws[sk] = ws
         d.colsum_ws = ws.data_ptr()
-    if A.dtype == torch.float32:  # fp32 parity mode (csrc/precise.hip)
-        if B.dtype != torch.float32 or C.dtype != torch.float32:
-            raise RuntimeError("fp32 parity-mode GEMM needs f32 A, B and C")
-        check(lib().slx_gemm_f32(ctypes.byref(d), stream_ptr()), "slx_gemm_f32")
-        return
-    check(lib().slx_gemm_bf16(ctypes.byref(d), stream_ptr()), "slx_gemm_bf16")
+    return d
 
 
 def linear(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor, bias=None, **kw):
@@ -532,6 +538,28 @@ def lora_bwd(x, dt, As, bits, dAs, dx=None, dx_bf16=None, p=0.0, packed=False):
         d.dx_bf16, d.lddx_bf16 = dx_bf16.data_ptr(), dx_bf16.stride(0)
     d.p = float(p)
     check(lib().slx_lora_bwd(ctypes.byref(d), stream_ptr()), "slx_lora_bwd")
+
+
+def _mm_dims(A, B, C, ta, tb):
+    if ta:
+        Kd, M = A.shape
+    else:
+        M, Kd = A.shape
+    N = B.shape[0] if tb else B.shape[1]
+    layout = {(False, True): GEMM_NT, (False, False): GEMM_NN, (True, False): GEMM_TN, (True, True): GEMM_TT}[(ta, tb)]
+    assert C.shape[0] >= M and C.shape[1] >= N, (C.shape, M, N)
+    return M, N, Kd, layout
+
+
+def mm_pair(g1, g2, *, ta=True, tb=False, alpha=1.0, ksplit_max=0):
+    """Two accumulating f32 GEMMs C_i += op(A_i) @ op(B_i) (g_i = (A_i, B_i, C_i), same layout and K) in one
+    launch (slx_gemm_bf16_pair): the InternViT weight-gradient pairs."""
+    ds = []
+    for A, B, C in (g1, g2):
+        M, N, Kd, layout = _mm_dims(A, B, C, ta, tb)
+        ds.append(_gemm_desc(A, B, C, M, N, Kd, layout, A.stride(0), B.stride(0), C.stride(0), alpha=alpha,
+                             accumulate=True, ksplit_max=ksplit_max))
+    check(lib().slx_gemm_bf16_pair(ctypes.byref(ds[0]), ctypes.byref(ds[1]), stream_ptr()), "slx_gemm_bf16_pair")
 
 
 def mm(A, B, C, *, ta=False, tb=True, **kw):

@@ -285,3 +285,24 @@ def test_batched_splitk_accumulate_tn(dev):
     torch.testing.assert_close(C0, want0, atol=2e-2, rtol=1e-3)
     torch.testing.assert_close(C1, want1, atol=2e-2, rtol=1e-3)
     assert torch.all(flat[out * r:sC] == 0) and torch.all(flat[sC + out * r:] == 0)  # nothing written between
+
+
+@pytest.mark.parametrize("shapes,split", [(((1024, 512), (512, 1024)), 0), (((768, 256), (256, 264)), 3),
+                                          (((136, 64), (256, 200)), 1)])
+def test_gemm_pair_wgrad(dev, shapes, split):
+    """slx_gemm_bf16_pair: two accumulating TN weight-gradient GEMMs (dW_i += dY_i^T X_i) in one launch, each vs
+    torch fp32 on the same bf16 operands (M-remainder tiles, split-K on and off)."""
+    T = 1040
+    g = torch.Generator(device=dev).manual_seed(sum(sum(s) for s in shapes) + split)
+    ops, refs = [], []
+    for (N, Kd) in shapes:
+        dy = torch.randn(T, N, device=dev, generator=g).bfloat16()
+        x = torch.randn(T, Kd, device=dev, generator=g).bfloat16()
+        C = torch.randn(N, Kd, device=dev, generator=g)
+        refs.append(C + dy.float().t() @ x.float())
+        ops.append((dy, x, C))
+    K.mm_pair(ops[0], ops[1], ksplit_max=split)
+    for (_, _, C), ref in zip(ops, refs):
+        assert (C - ref).abs().max().item() < 2e-3 * T ** 0.5
+    with pytest.raises(RuntimeError, match="one layout and one K"):
+        K.mm_pair(ops[0], (ops[1][0][:512], ops[1][1][:512], ops[1][2]))
