@@ -325,6 +325,9 @@ int slx_dec_gemv(const slx_dec_gemv_desc* d, slx_stream_t s);
  * must be zeroed once before first use; every call leaves the counters at 0 again);
  * out bf16 [Hq*64]; lmax = cache rows allocated (the split count is fixed by it: graph-safe)      */
 int slx_dec_attn_nsplit(int lmax);
+/* tools only: record phase timestamps (wall_clock64 ticks) of the next slx_dec_attn launches into buf
+ * (>= 64 + Hkv * nsplit int64); NULL turns tracing off                                                  */
+void slx_dec_attn_set_trace(long long* buf);
 int slx_dec_attn_ws_floats(int Hq, int Hkv, int lmax);
 int slx_dec_attn(void* cache, int64_t ld, int Hq, int Hkv, const float* cos_tab, const float* sin_tab, int lmax,
                  float* ws, void* out, const slx_dec_state* st, slx_stream_t s);

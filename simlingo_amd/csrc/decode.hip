@@ -88,16 +88,34 @@ struct GemvArgs {
 };
 
 // One wave owns R output rows (SWIGLU: R gate + R up rows) of a row group; lane l holds 16-B chunks
-// l, l+64, ... (CPL per row) of each row. The first row group's weight loads are issued before the
-// RMSNorm prologue, so the weight stream and the x/norm round trip overlap (the layer is latency-bound).
+// l, l+64, ... (CPL per row) of each row. Load order is the latency schedule of a batch-1 layer: the
+// x vector (f32 residual row for the fused RMSNorm, or the bf16 input) first, then the first row
+// group's weight stream, and only then the scalar done-flag check, so the norm waits for x alone
+// (in-order vmcnt) and the flag / x / weight round trips all overlap.
+constexpr int kGemvXPer = 8;  // x elements per thread held in registers (K <= 2048 with X, K <= 8192 with xb)
 template <int MODE, int R, int CPL>
 __global__ __launch_bounds__(256) void dec_gemv_kernel(GemvArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   bf16* xs = reinterpret_cast<bf16*>(smem_raw);
   __shared__ float red[16];
-  if (a.st && a.st->done) return;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int K = a.K, nch = K >> 3;
+  float xv[kGemvXPer], gv[kGemvXPer];
+  uint4 xq[kGemvXPer / 2];
+  if (a.X) {
+#pragma unroll
+    for (int i = 0; i < kGemvXPer; ++i) {
+      const int j = tid + 256 * i;
+      xv[i] = j < K ? a.X[j] : 0.f;
+      gv[i] = j < K ? a.gamma[j] : 0.f;
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < kGemvXPer / 2; ++i) {
+      const int j = (tid + 256 * i) * 8;
+      xq[i] = j < K ? *reinterpret_cast<const uint4*>(a.xb + j) : make_uint4(0u, 0u, 0u, 0u);
+    }
+  }
   constexpr int NR = MODE == GV_SWIGLU ? 2 * R : R;
   const int nrg = (a.N + 4 * R - 1) / (4 * R);
   uint4 w[NR][CPL];
@@ -120,13 +138,23 @@ __global__ __launch_bounds__(256) void dec_gemv_kernel(GemvArgs a) {
   };
   int rg = blockIdx.x;
   if (rg < nrg) issue(rg);
+  if (a.st && a.st->done) return;
   if (a.X) {
     float ss = 0.f;
-    for (int j = tid; j < K; j += 256) { const float v = a.X[j]; ss += v * v; }
+#pragma unroll
+    for (int i = 0; i < kGemvXPer; ++i) ss += xv[i] * xv[i];
     const float rs = rsqrtf(block_sum(ss, red) / K + a.eps);
-    for (int j = tid; j < K; j += 256) xs[j] = (bf16)((float)(bf16)(a.X[j] * rs) * a.gamma[j]);
+#pragma unroll
+    for (int i = 0; i < kGemvXPer; ++i) {
+      const int j = tid + 256 * i;
+      if (j < K) xs[j] = (bf16)((float)(bf16)(xv[i] * rs) * gv[i]);
+    }
   } else {
-    for (int j = tid * 8; j < K; j += 256 * 8) *reinterpret_cast<uint4*>(xs + j) = *reinterpret_cast<const uint4*>(a.xb + j);
+#pragma unroll
+    for (int i = 0; i < kGemvXPer / 2; ++i) {
+      const int j = (tid + 256 * i) * 8;
+      if (j < K) *reinterpret_cast<uint4*>(xs + j) = xq[i];
+    }
   }
   __syncthreads();
   unsigned long long best = 0ull;  // ARGMAX: running best of this wave over its row groups
@@ -181,189 +209,247 @@ __global__ __launch_bounds__(256) void dec_gemv_kernel(GemvArgs a) {
   }
 }
 
-// ---- attention of the new token over the cache: split over keys, then a combine -------------------
+// ---- attention of the new token over the cache: split over keys, combined in the same launch -------
 // cache row layout: [q (Hq*64) | k (Hkv*64) | v (Hkv*64)]; rows 0..pos-1 hold rotated k; row pos holds
 // the fresh q/k/v of this token. Grid (Hkv, nsplit): workgroup (g, s) takes keys [s*c, (s+1)*c) of kv
-// head g (c = ceil((pos+1)/nsplit) <= 128) for the G = Hq/Hkv query heads sharing it, and writes its
-// partial softmax state (max, sum, unnormalised output) to a workspace; dec_attn_combine_kernel merges
-// the nsplit partials (flash-decoding). The workgroup holding row pos rotates that k row and writes it
-// back for the following steps; every workgroup rotates the q rows it needs itself.
+// head g (c = ceil((pos+1)/nsplit) <= 128) for the G = Hq/Hkv query heads sharing it and publishes its
+// partial softmax state (max, sum, unnormalised output) to a workspace; the workgroup whose arrival on
+// kv head g's counter comes last merges the nsplit partials (flash-decoding) and resets the counter, so
+// the split and the merge cost one launch. Hand-off (MI355X_MICROARCH.md, inter-workgroup visibility,
+// table row 1): partials stored and loaded with agent-scope (sc1) accesses, every storing wave waits
+// vmcnt(0) before the workgroup barrier, one lane adds to the counter, the last adder's workgroup reads
+// behind an LDS flag. The workgroup holding row pos rotates that k row and writes it back for the
+// following steps; every workgroup rotates the q rows it needs itself.
 constexpr int kAttnChunk = 128;
+constexpr int kAttnCntStride = 32;  // one counter per kv head, 128 B apart, after the partials
 
 struct DecAttnArgs {
   bf16* cache; long ld; int Hq, Hkv;
   const float* cos; const float* sin;  // [S_max, 32]
-  float* ws;                           // [Hkv][nsplit][G * (2 + 64)]
+  float* ws;                           // [Hkv][nsplit][G * (2 + 64)] partials, then Hkv counters
   bf16* out;                           // [Hq*64]
   const slx_dec_state* st;
   float scale;
+  long long* trace;  // tools only (slx_dec_attn_set_trace): phase timestamps of workgroup (0, 0) and the merger
 };
 
-__global__ __launch_bounds__(256) void dec_attn_split_kernel(DecAttnArgs a) {
-  __shared__ float qs[8 * 64], ks[64], ps[8][kAttnChunk], red[4][8][64], mh[8];
+__device__ __forceinline__ void tr(const DecAttnArgs& a, int slot) {
+  if (a.trace && threadIdx.x == 0) a.trace[slot] = (long long)wall_clock64();
+}
+
+__device__ __forceinline__ void st_agent(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_agent(float* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// wave-wide max / sum through DPP (within 16-lane rows) + readlane of the 4 row results (no LDS round trips)
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+template <bool MAX>
+__device__ __forceinline__ float wave_reduce(float x) {
+  auto op = [](float u, float v) { return MAX ? fmaxf(u, v) : u + v; };
+  x = op(x, dpp_f<0xB1>(x));   // quad_perm [1,0,3,2]
+  x = op(x, dpp_f<0x4E>(x));   // quad_perm [2,3,0,1]
+  x = op(x, dpp_f<0x141>(x));  // row_half_mirror
+  x = op(x, dpp_f<0x140>(x));  // row_mirror
+  const float r0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 0));
+  const float r1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 16));
+  const float r2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 32));
+  const float r3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 48));
+  return op(op(r0, r1), op(r2, r3));
+}
+
+// Latency schedule (phase timestamps measured with tools/dec_attn_trace.py): one round trip for the cache rows
+// (K and V of this split staged in LDS, q of the G heads rotated into LDS), scores spread over all 256 threads as
+// (head, key) pairs, the partial softmax per head on one wave with DPP reductions, P.V with lane = output dim, the
+// partial published with agent-scope stores, then one arrival; the last arriver loads every split's (m, l, o) for
+// its lanes in one round trip and merges in registers.
+__global__ __launch_bounds__(256) void dec_attn_kernel(DecAttnArgs a) {
+  __shared__ __attribute__((aligned(16))) float ps[8][kAttnChunk];
+  __shared__ __attribute__((aligned(16))) float qs[8 * 64];
+  __shared__ float mh[8], lh[8];
+  __shared__ __attribute__((aligned(16))) bf16 ksm[kAttnChunk * 64];  // this split's K rows (rotated)
+  __shared__ __attribute__((aligned(16))) bf16 vs[kAttnChunk * 64];   // this split's V rows
+  __shared__ int last_s;
+  const bool t0 = a.trace && blockIdx.x == 0 && blockIdx.y == 0;
+  if (a.trace && threadIdx.x == 0) a.trace[64 + blockIdx.y * gridDim.x + blockIdx.x] = (long long)wall_clock64();
+  if (t0) tr(a, 0);
   if (a.st->done) return;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int pos = a.st->pos, L = pos + 1;
   const int g = blockIdx.x, sp = blockIdx.y, ns = gridDim.y, G = a.Hq / a.Hkv;
+  if (t0) tr(a, 1);
   const int c = (L + ns - 1) / ns;
   const int j0 = sp * c, j1 = min(L, j0 + c), n = max(0, j1 - j0);
   const int qn = a.Hq * 64, kn = a.Hkv * 64;
   float* part = a.ws + ((long)g * ns + sp) * (G * 66);
-  if (n == 0) {  // empty split: neutral partial
-    if (tid < G) { part[tid] = -INFINITY; part[G + tid] = 0.f; }
-    for (int i = tid; i < G * 64; i += 256) part[2 * G + i] = 0.f;
-    return;
-  }
-  bf16* row = a.cache + (long)pos * a.ld;
-  const float* cs = a.cos + (long)pos * 32;
-  const float* sn = a.sin + (long)pos * 32;
-  // every global read of this workgroup is issued up front (one latency round trip): the K row of
-  // this thread's key, and the V chunks of its key slots
-  const int d8 = lane & 7, jj = tid >> 3;
-  bf16x8 kt[8];
-  if (tid < n && j0 + tid != pos) {
-    const bf16* kr = a.cache + (long)(j0 + tid) * a.ld + qn + g * 64;
+  int* cnt = reinterpret_cast<int*>(a.ws + (long)a.Hkv * ns * (G * 66)) + g * kAttnCntStride;
+  if (n > 0) {
+    bf16* row = a.cache + (long)pos * a.ld;
+    const float* cs = a.cos + (long)pos * 32;
+    const float* sn = a.sin + (long)pos * 32;
+    // every global read is issued up front (one latency round trip): 16-B chunks of the K and V rows of the
+    // split (key t = tid/8 + 32 i, chunk tid%8), the q rows and the RoPE row
+    const int d8 = lane & 7, jj = tid >> 3;
+    const bf16* kb = a.cache + qn + g * 64 + 8 * d8;
+    const bf16* vb = a.cache + qn + kn + g * 64 + 8 * d8;
+    bf16x8 kt[kAttnChunk / 32], vt[kAttnChunk / 32];
 #pragma unroll
-    for (int q8 = 0; q8 < 8; ++q8) kt[q8] = *reinterpret_cast<const bf16x8*>(kr + 8 * q8);
-  }
-  const bf16* vb = a.cache + qn + kn + g * 64 + 8 * d8;
-  bf16x8 vt[kAttnChunk / 32];
-#pragma unroll
-  for (int i = 0; i < kAttnChunk / 32; ++i) {
-    const int t = jj + 32 * i;
-    if (t < n) vt[i] = *reinterpret_cast<const bf16x8*>(vb + (long)(j0 + t) * a.ld);
-  }
-  if (tid < 32 * G) {  // rotate_half RoPE of the G query heads (bf16-rounded like the stored rows)
-    const int h = tid >> 5, j = tid & 31;
-    const bf16* q = row + (g * G + h) * 64;
-    const float q0 = (float)q[j], q1 = (float)q[j + 32];
-    qs[h * 64 + j] = (float)(bf16)(q0 * cs[j] - q1 * sn[j]);
-    qs[h * 64 + j + 32] = (float)(bf16)(q1 * cs[j] + q0 * sn[j]);
-  }
-  if (tid < 32 && j1 == L) {  // k of this token: rotated, written back once
-    const int j = tid;
-    bf16* k = row + qn + g * 64;
-    const float k0 = (float)k[j], k1 = (float)k[j + 32];
-    const bf16 r0 = (bf16)(k0 * cs[j] - k1 * sn[j]), r1 = (bf16)(k1 * cs[j] + k0 * sn[j]);
-    k[j] = r0;
-    k[j + 32] = r1;
-    ks[j] = (float)r0;
-    ks[j + 32] = (float)r1;
-  }
-  __syncthreads();
-  // scores: one key per thread (n <= 128)
-  if (tid < n) {
-    const int j = j0 + tid;
-    float kv[64];
-    if (j == pos) {
-#pragma unroll
-      for (int d = 0; d < 64; ++d) kv[d] = ks[d];
-    } else {
-#pragma unroll
-      for (int q8 = 0; q8 < 8; ++q8)
-#pragma unroll
-        for (int e = 0; e < 8; ++e) kv[8 * q8 + e] = (float)kt[q8][e];
-    }
-    for (int h = 0; h < G; ++h) {
-      float s = 0.f;
-#pragma unroll
-      for (int d = 0; d < 64; ++d) s = __builtin_fmaf(qs[h * 64 + d], kv[d], s);
-      ps[h][tid] = s * a.scale;
-    }
-  }
-  __syncthreads();
-  // partial softmax: wave w takes heads w and w + 4
-  for (int h = wave; h < G; h += 4) {
-    float m = -INFINITY;
-    for (int t = lane; t < n; t += 64) m = fmaxf(m, ps[h][t]);
-    m = warp_max(m);
-    float l = 0.f;
-    for (int t = lane; t < n; t += 64) {
-      const float e = __expf(ps[h][t] - m);
-      ps[h][t] = e;
-      l += e;
-    }
-    l = warp_sum(l);
-    if (lane == 0) { mh[h] = m; part[h] = m; part[G + h] = l; }
-  }
-  __syncthreads();
-  // unnormalised P V: lane (d8 = lane & 7) owns 8 dims, key slots jj = tid >> 3 (32 of them)
-  float acc[8][8];
-#pragma unroll
-  for (int h = 0; h < 8; ++h)
-#pragma unroll
-    for (int e = 0; e < 8; ++e) acc[h][e] = 0.f;
-#pragma unroll
-  for (int i = 0; i < kAttnChunk / 32; ++i) {
-    const int t = jj + 32 * i;
-    if (t < n) {
-      const bf16x8 v = vt[i];
-#pragma unroll
-      for (int h = 0; h < 8; ++h) {
-        if (h < G) {
-          const float p = ps[h][t];
-#pragma unroll
-          for (int e = 0; e < 8; ++e) acc[h][e] = __builtin_fmaf(p, (float)v[e], acc[h][e]);
-        }
+    for (int i = 0; i < kAttnChunk / 32; ++i) {
+      const int t = jj + 32 * i;
+      if (t < n) {
+        kt[i] = *reinterpret_cast<const bf16x8*>(kb + (long)(j0 + t) * a.ld);
+        vt[i] = *reinterpret_cast<const bf16x8*>(vb + (long)(j0 + t) * a.ld);
       }
     }
-  }
-  // reduce the 8 key slots of a wave (lane bits 3..5), then the 4 waves through LDS
-#pragma unroll
-  for (int h = 0; h < 8; ++h)
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      float v = acc[h][e];
-      v += __shfl_xor(v, 8, 64);
-      v += __shfl_xor(v, 16, 64);
-      v += __shfl_xor(v, 32, 64);
-      acc[h][e] = v;
+    if (tid < 32 * G) {  // rotate_half RoPE of the G query heads (bf16-rounded like the stored rows)
+      const int h = tid >> 5, j = tid & 31;
+      const bf16* q = row + (g * G + h) * 64;
+      const float q0 = (float)q[j], q1 = (float)q[j + 32];
+      qs[h * 64 + j] = (float)(bf16)(q0 * cs[j] - q1 * sn[j]);
+      qs[h * 64 + j + 32] = (float)(bf16)(q1 * cs[j] + q0 * sn[j]);
     }
-  if (lane < 8) {
+    if (tid < 32 && j1 == L) {  // k of this token: rotated, written back once (and into this split's K tile)
+      const int j = tid;
+      bf16* k = row + qn + g * 64;
+      const float k0 = (float)k[j], k1 = (float)k[j + 32];
+      const bf16 r0 = (bf16)(k0 * cs[j] - k1 * sn[j]), r1 = (bf16)(k1 * cs[j] + k0 * sn[j]);
+      k[j] = r0;
+      k[j + 32] = r1;
+      const int tp = pos - j0, sw = tp & 7;  // K tile chunks XOR-swizzled by row (conflict-free score reads)
+      ksm[tp * 64 + 8 * ((j >> 3) ^ sw) + (j & 7)] = r0;
+      ksm[tp * 64 + 8 * (((j + 32) >> 3) ^ sw) + (j & 7)] = r1;
+    }
 #pragma unroll
-    for (int h = 0; h < 8; ++h)
-      if (h < G)
+    for (int i = 0; i < kAttnChunk / 32; ++i) {
+      const int t = jj + 32 * i;
+      if (t < n) {
+        if (j0 + t != pos) *reinterpret_cast<bf16x8*>(ksm + t * 64 + 8 * (d8 ^ (t & 7))) = kt[i];
+        *reinterpret_cast<bf16x8*>(vs + t * 64 + 8 * d8) = vt[i];
+      }
+    }
+    __syncthreads();
+    if (t0) tr(a, 2);
+    // scores: (head, key) pairs over all threads
+    for (int i = tid; i < G * n; i += 256) {
+      const int h = i / n, t = i - h * n;
+      const float4* q4 = reinterpret_cast<const float4*>(qs + h * 64);
+      const bf16x8* k8 = reinterpret_cast<const bf16x8*>(ksm + t * 64);
+      float acc[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int e = 0; e < 8; ++e) red[wave][h][8 * lane + e] = acc[h][e];
+      for (int c8 = 0; c8 < 8; ++c8) {
+        const bf16x8 kv = k8[c8 ^ (t & 7)];
+        const float4 qa = q4[2 * c8], qb = q4[2 * c8 + 1];
+        acc[0] = __builtin_fmaf(qa.x, (float)kv[0], acc[0]);
+        acc[1] = __builtin_fmaf(qa.y, (float)kv[1], acc[1]);
+        acc[2] = __builtin_fmaf(qa.z, (float)kv[2], acc[2]);
+        acc[3] = __builtin_fmaf(qa.w, (float)kv[3], acc[3]);
+        acc[0] = __builtin_fmaf(qb.x, (float)kv[4], acc[0]);
+        acc[1] = __builtin_fmaf(qb.y, (float)kv[5], acc[1]);
+        acc[2] = __builtin_fmaf(qb.z, (float)kv[6], acc[2]);
+        acc[3] = __builtin_fmaf(qb.w, (float)kv[7], acc[3]);
+      }
+      ps[h][t] = ((acc[0] + acc[1]) + (acc[2] + acc[3])) * a.scale;
+    }
+    __syncthreads();
+    if (t0) tr(a, 3);
+    // partial softmax: wave w takes heads w and w + 4 (n <= 128: two keys per lane)
+    for (int h = wave; h < G; h += 4) {
+      const float x0 = lane < n ? ps[h][lane] : -INFINITY;
+      const float x1 = lane + 64 < n ? ps[h][lane + 64] : -INFINITY;
+      const float m = wave_reduce<true>(fmaxf(x0, x1));
+      const float e0 = lane < n ? __expf(x0 - m) : 0.f;
+      const float e1 = lane + 64 < n ? __expf(x1 - m) : 0.f;
+      if (lane < n) ps[h][lane] = e0;
+      if (lane + 64 < n) ps[h][lane + 64] = e1;
+      const float l = wave_reduce<false>(e0 + e1);
+      if (lane == 0) { mh[h] = m; lh[h] = l; }
+    }
+    __syncthreads();
+    if (t0) tr(a, 4);
+    // unnormalised P V: lanes 0-31 of wave w take head w, lanes 32-63 head w + 4, two output dims per lane
+    // (8 keys per step, LDS reads of a step issued together)
+    {
+      const int h = wave + 4 * (lane >> 5), dd = 2 * (lane & 31);
+      if (h < G) {
+        float ax[2] = {0.f, 0.f}, ay[2] = {0.f, 0.f};
+        int t = 0;
+        for (; t + 8 <= n; t += 8) {
+          const float4 p0 = *reinterpret_cast<const float4*>(&ps[h][t]);
+          const float4 p1 = *reinterpret_cast<const float4*>(&ps[h][t + 4]);
+          const float pp[8] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w};
+          uint32_t v[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const uint32_t*>(vs + (t + u) * 64 + dd);
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            ax[u & 1] = __builtin_fmaf(pp[u], __uint_as_float(v[u] << 16), ax[u & 1]);
+            ay[u & 1] = __builtin_fmaf(pp[u], __uint_as_float(v[u] & 0xFFFF0000u), ay[u & 1]);
+          }
+        }
+        for (; t < n; ++t) {
+          const uint32_t v = *reinterpret_cast<const uint32_t*>(vs + t * 64 + dd);
+          ax[0] = __builtin_fmaf(ps[h][t], __uint_as_float(v << 16), ax[0]);
+          ay[0] = __builtin_fmaf(ps[h][t], __uint_as_float(v & 0xFFFF0000u), ay[0]);
+        }
+        st_agent(part + 2 * G + h * 64 + dd, ax[0] + ax[1]);
+        st_agent(part + 2 * G + h * 64 + dd + 1, ay[0] + ay[1]);
+      }
+    }
+  } else {  // empty split: neutral partial
+    for (int i = tid; i < G * 64; i += 256) st_agent(part + 2 * G + i, 0.f);
+    if (tid < G) { mh[tid] = -INFINITY; lh[tid] = 0.f; }
+    __syncthreads();
   }
+  if (tid < G) { st_agent(part + tid, mh[tid]); st_agent(part + G + tid, lh[tid]); }
+  // publish, then arrive (one lane, after every storing wave's vmcnt(0) and a workgroup barrier)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  for (int i = tid; i < G * 64; i += 256) {
-    const int h = i >> 6, d = i & 63;
-    part[2 * G + i] = red[0][h][d] + red[1][h][d] + red[2][h][d] + red[3][h][d];
-  }
-}
-
-__global__ __launch_bounds__(512) void dec_attn_combine_kernel(DecAttnArgs a, int ns) {
-  if (a.st->done) return;
-  const int g = blockIdx.x, G = a.Hq / a.Hkv, t = threadIdx.x;
-  if (t >= G * 64) return;
-  const int h = t >> 6, d = t & 63;
-  const float* base = a.ws + (long)g * ns * (G * 66);
-  constexpr int MAXS = 64;
-  float m[MAXS], l[MAXS], o[MAXS];
+  if (t0) tr(a, 5);
+  if (tid == 0) last_s = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ns - 1;
+  __syncthreads();
+  if (t0) tr(a, 6);
+  if (!last_s) return;
+  if (a.trace) tr(a, 8);
+  // the last arriver merges the ns partials of kv head g: lane = dim of heads wave, wave + 4; every (m, l, o)
+  // of its splits is loaded at once (kMergeBatch splits per round trip), the weights computed per lane
+  float* base = a.ws + (long)g * ns * (G * 66);
+  constexpr int kMergeBatch = 16;
+  for (int h = wave; h < G; h += 4) {
+    float M = -INFINITY, den = 0.f, num = 0.f;
+    for (int s0 = 0; s0 < ns; s0 += kMergeBatch) {
+      float m[kMergeBatch], l[kMergeBatch], o[kMergeBatch];
 #pragma unroll
-  for (int s = 0; s < MAXS; ++s) {  // all partials loaded at once (ns <= 64), then merged
-    if (s < ns) {
-      const float* p = base + s * (G * 66);
-      m[s] = p[h];
-      l[s] = p[G + h];
-      o[s] = p[2 * G + h * 64 + d];
+      for (int u = 0; u < kMergeBatch; ++u) {
+        float* p = base + (s0 + u) * (G * 66);
+        const bool ok = s0 + u < ns;
+        m[u] = ok ? ld_agent(p + h) : -INFINITY;
+        l[u] = ok ? ld_agent(p + G + h) : 0.f;
+        o[u] = ok ? ld_agent(p + 2 * G + h * 64 + lane) : 0.f;
+      }
+      float Mb = M;
+#pragma unroll
+      for (int u = 0; u < kMergeBatch; ++u) Mb = fmaxf(Mb, m[u]);
+      const float r = M == -INFINITY ? 0.f : __expf(M - Mb);  // rescale the running sums to the new max
+      den *= r;
+      num *= r;
+#pragma unroll
+      for (int u = 0; u < kMergeBatch; ++u) {
+        const float w = m[u] == -INFINITY ? 0.f : __expf(m[u] - Mb);
+        den = __builtin_fmaf(w, l[u], den);
+        num = __builtin_fmaf(w, o[u], num);
+      }
+      M = Mb;
     }
+    a.out[(g * G + h) * 64 + lane] = (bf16)(num / den);
   }
-  float M = -INFINITY;
-#pragma unroll
-  for (int s = 0; s < MAXS; ++s)
-    if (s < ns) M = fmaxf(M, m[s]);
-  float num = 0.f, den = 0.f;
-#pragma unroll
-  for (int s = 0; s < MAXS; ++s) {
-    if (s < ns) {
-      const float w = m[s] == -INFINITY ? 0.f : __expf(m[s] - M);
-      num = __builtin_fmaf(w, o[s], num);
-      den = __builtin_fmaf(w, l[s], den);
-    }
-  }
-  a.out[(g * G + h) * 64 + d] = (bf16)(num / den);
+  if (a.trace) tr(a, 9);
+  if (tid == 0) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (a.trace) { __syncthreads(); tr(a, 10); }
 }
 
 template <int MODE, int R>
@@ -414,6 +500,7 @@ int slx_dec_gemv(const slx_dec_gemv_desc* d, slx_stream_t s) {
   SLX_CHECK_ARG(d && d->W, "slx_dec_gemv: null desc/W");
   SLX_CHECK_ARG(d->K % 8 == 0 && d->ldw % 8 == 0 && ((uintptr_t)d->W & 15) == 0, "slx_dec_gemv: K, ldw %% 8, W 16-B aligned");
   SLX_CHECK_ARG(d->K <= 8192, "slx_dec_gemv: K <= 8192 (16 chunks of 16 B per lane)");
+  SLX_CHECK_ARG(!d->X || d->K <= 256 * kGemvXPer, "slx_dec_gemv: K <= %d with the fused RMSNorm", 256 * kGemvXPer);
   SLX_CHECK_ARG((d->X && d->gamma) || (d->xb && ((uintptr_t)d->xb & 15) == 0), "slx_dec_gemv: need X+gamma or 16-B aligned xb");
   GemvArgs a;
   a.W = (const bf16*)d->W; a.ldw = d->ldw; a.N = d->N; a.K = d->K;
@@ -430,10 +517,14 @@ int slx_dec_gemv(const slx_dec_gemv_desc* d, slx_stream_t s) {
   return -22;
 }
 
-int slx_dec_attn_nsplit(int lmax) { return (lmax + kAttnChunk - 1) / kAttnChunk > 16 ? (lmax + kAttnChunk - 1) / kAttnChunk : 16; }
+static long long* g_dec_trace = nullptr;
+// tools only: phase timestamps (wall_clock64 ticks) of the next slx_dec_attn launches; NULL turns tracing off
+void slx_dec_attn_set_trace(long long* buf) { g_dec_trace = buf; }
+
+int slx_dec_attn_nsplit(int lmax) { return (lmax + kAttnChunk - 1) / kAttnChunk > 8 ? (lmax + kAttnChunk - 1) / kAttnChunk : 8; }
 
 int slx_dec_attn_ws_floats(int Hq, int Hkv, int lmax) {
-  return Hkv > 0 ? Hkv * slx_dec_attn_nsplit(lmax) * (Hq / Hkv) * 66 : 0;
+  return Hkv > 0 ? Hkv * slx_dec_attn_nsplit(lmax) * (Hq / Hkv) * 66 + Hkv * kAttnCntStride : 0;
 }
 
 int slx_dec_attn(void* cache, int64_t ld, int Hq, int Hkv, const float* cos_tab, const float* sin_tab, int lmax,
@@ -441,13 +532,12 @@ int slx_dec_attn(void* cache, int64_t ld, int Hq, int Hkv, const float* cos_tab,
   SLX_CHECK_ARG(cache && cos_tab && sin_tab && ws && out && st, "slx_dec_attn: null argument");
   SLX_CHECK_ARG(Hkv > 0 && Hq % Hkv == 0 && Hq / Hkv <= 8, "slx_dec_attn: Hq/Hkv must be an integer <= 8");
   SLX_CHECK_ARG(ld % 8 == 0 && ((uintptr_t)cache & 15) == 0, "slx_dec_attn: cache rows must be 16-B aligned");
-  SLX_CHECK_ARG(lmax > 0 && lmax <= 64 * kAttnChunk, "slx_dec_attn: lmax <= 8192");
+  SLX_CHECK_ARG(lmax > 0 && lmax <= 64 * kAttnChunk, "slx_dec_attn: lmax <= 8192");  // ns <= 64: ns * G <= 512
   const int ns = slx_dec_attn_nsplit(lmax);
-  DecAttnArgs a{(bf16*)cache, ld, Hq, Hkv, cos_tab, sin_tab, ws, (bf16*)out, st, 0.125f};
-  hipLaunchKernelGGL(dec_attn_split_kernel, dim3(Hkv, ns), dim3(256), 0, (hipStream_t)s, a);
-  SLX_LAUNCH_CHECK("slx_dec_attn(split)");
-  hipLaunchKernelGGL(dec_attn_combine_kernel, dim3(Hkv), dim3(512), 0, (hipStream_t)s, a, ns);
-  SLX_LAUNCH_CHECK("slx_dec_attn(combine)");
+  DecAttnArgs a{(bf16*)cache, ld, Hq, Hkv, cos_tab, sin_tab, ws, (bf16*)out, st, 0.125f, g_dec_trace};
+  SLX_CHECK_ARG(((uintptr_t)ws & 3) == 0, "slx_dec_attn: ws must be 4-B aligned (and zeroed once: it holds the counters)");
+  hipLaunchKernelGGL(dec_attn_kernel, dim3(Hkv, ns), dim3(256), 0, (hipStream_t)s, a);
+  SLX_LAUNCH_CHECK("slx_dec_attn");
   return 0;
 }
 

@@ -171,6 +171,159 @@ __global__ __launch_bounds__(256) void norm_fwd_wave_kernel(NormArgs a) {
 
 template <bool RMS, bool LS, bool DYB>
 __global__ __launch_bounds__(256) void norm_bwd_wave_kernel(NormArgs a) {
+  // column sums (dgamma, dbeta; dls, dbias of the layer-scale branch) accumulate in wave-private LDS rows: each lane
+  // owns its 16 columns, so there are no conflicts and no barriers until the end, and the 64 accumulator registers go
+  // to the second row in flight instead
+  __shared__ __attribute__((aligned(16))) float cs[4][LS ? 4 : 2][1024];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  constexpr int NACC = LS ? 4 : 2;
+#pragma unroll
+  for (int q = 0; q < NACC; ++q)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int col = (lane + 64 * i) * 4;
+      if (col < 1024) *reinterpret_cast<float4*>(&cs[w][q][col]) = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  auto acc4 = [&](int q, int col, const float (&v)[4]) {
+    float4* p = reinterpret_cast<float4*>(&cs[w][q][col]);
+    float4 c = *p;
+    c.x += v[0]; c.y += v[1]; c.z += v[2]; c.w += v[3];
+    *p = c;
+  };
+  // Software-pipelined rows: the next row's loads (x, dy, the accumulated dx row, the layer-scale branch row and its
+  // mean / rstd) are issued before the current row's reductions and stores, so each wave keeps two rows of HBM traffic
+  // in flight (the kernel is HBM-bound; gamma and ls are loaded once per wave).
+  struct RowIn {
+    float mu, rs;
+    float4 t[4], dxo[4];
+    float4 d[4];
+    bf16x4 lyv[4];
+  };
+  // gamma / ls of this lane's columns: re-read per row (L1 hits) ahead of the next row's loads, so their wait does
+  // not cover the next row's traffic (in-order vmcnt) and they hold no registers across the row
+  auto load_cols = [&](float4 (&gm)[4], float4 (&lsv)[4]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int col = (lane + 64 * i) * 4;
+      gm[i] = col < a.D ? *reinterpret_cast<const float4*>(a.gamma + col) : make_float4(0.f, 0.f, 0.f, 0.f);
+      if constexpr (LS) lsv[i] = col < a.D ? *reinterpret_cast<const float4*>(a.ls + col) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  auto load_row = [&](long row, RowIn& r) {
+    r.mu = RMS ? 0.f : a.mean[row];
+    r.rs = a.rstd[row];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int col = (lane + 64 * i) * 4;
+      r.dxo[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+      r.t[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+      r.d[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (col < a.D) {
+        if (a.dx_accumulate) {
+          const float* dsrc = a.ps ? a.dx + ps_src_row(row, col / a.C, a.G, a.tok_per_img) * a.lddx + (col % a.C)
+                                   : a.dx + row * a.lddx + col;
+          r.dxo[i] = *reinterpret_cast<const float4*>(dsrc);
+        }
+        if constexpr (LS) r.lyv[i] = *reinterpret_cast<const bf16x4*>(a.lsy + row * a.ldlsy + col);
+        const float* src = a.ps ? a.x + ps_src_row(row, col / a.C, a.G, a.tok_per_img) * a.ldx + (col % a.C)
+                                : a.x + row * a.ldx + col;
+        r.t[i] = *reinterpret_cast<const float4*>(src);
+        r.d[i] = load_dy4<DYB ? 1 : 0>(a, row, col);
+      }
+    }
+  };
+  const long stride = (long)gridDim.x * 4;
+  long row = (long)blockIdx.x * 4 + w;
+  RowIn cur;
+  if (row < a.rows) load_row(row, cur);
+  for (; row < a.rows; row += stride) {
+    float4 gm[4], lsv[4];
+    load_cols(gm, lsv);
+    RowIn nxt;
+    if (row + stride < a.rows) load_row(row + stride, nxt);
+    const float mu = cur.mu, rs = cur.rs;
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int col = (lane + 64 * i) * 4;
+      const float4 t = cur.t[i], d = cur.d[i], g = gm[i];
+      const float tv[4] = {t.x, t.y, t.z, t.w}, dv[4] = {d.x, d.y, d.z, d.w}, gv[4] = {g.x, g.y, g.z, g.w};
+      float ag[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float xh = col < a.D ? (tv[e] - mu) * rs : 0.f;
+        const float gd = dv[e] * gv[e];
+        s1 += gd;
+        s2 += gd * xh;
+        ag[e] = dv[e] * (RMS ? (float)(bf16)xh : xh);
+      }
+      if (col < a.D) {
+        acc4(0, col, ag);
+        acc4(1, col, dv);
+      }
+    }
+    const float m1 = RMS ? 0.f : warp_sum(s1) / a.D;
+    const float m2 = warp_sum(s2) / a.D;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int col = (lane + 64 * i) * 4;
+      if (col >= a.D) continue;
+      float* dst = a.ps ? a.dx + ps_src_row(row, col / a.C, a.G, a.tok_per_img) * a.lddx + (col % a.C)
+                        : a.dx + row * a.lddx + col;
+      float ov[4];
+      {  // x_hat and g*dy recomputed from the row's registers (cheaper than keeping 32 of them live)
+        const float4 t = cur.t[i], d = cur.d[i], g = gm[i];
+        const float tv[4] = {t.x, t.y, t.z, t.w}, dv[4] = {d.x, d.y, d.z, d.w}, gv[4] = {g.x, g.y, g.z, g.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) ov[e] = rs * (dv[e] * gv[e] - m1 - ((tv[e] - mu) * rs) * m2);
+      }
+      if (a.dx_accumulate) {
+        ov[0] += cur.dxo[i].x; ov[1] += cur.dxo[i].y; ov[2] += cur.dxo[i].z; ov[3] += cur.dxo[i].w;
+      }
+      *reinterpret_cast<float4*>(dst) = make_float4(ov[0], ov[1], ov[2], ov[3]);
+      if (a.dxb) {
+        bf16x4 ob;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) ob[e] = (bf16)ov[e];
+        *reinterpret_cast<bf16x4*>(a.dxb + row * a.lddxb + col) = ob;
+      }
+      if constexpr (LS) {  // slx_ls_branch_bwd's per-element work on the row just produced (colsum_kernel<2>)
+        const float4 l4 = lsv[i];
+        const bf16x4 yy = cur.lyv[i];
+        const float lv[4] = {l4.x, l4.y, l4.z, l4.w};
+        bf16x4 go;
+        float al[4], aq[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float gv = ov[e] * lv[e];
+          go[e] = (bf16)gv;
+          al[e] = ov[e] * (float)yy[e];
+          aq[e] = gv;
+        }
+        acc4(LS ? 2 : 0, col, al);
+        acc4(LS ? 3 : 0, col, aq);
+        *reinterpret_cast<bf16x4*>(a.lsg + row * a.ldlsg + col) = go;
+      }
+    }
+    cur = nxt;
+  }
+  if (a.dgamma || a.dbeta || LS) {  // 4 waves' column partials summed through LDS, then contiguous f32 atomics
+    __syncthreads();
+    for (int c = threadIdx.x; c < a.D; c += 256) {
+      if (a.dgamma) atomicAdd(a.dgamma + c, cs[0][0][c] + cs[1][0][c] + cs[2][0][c] + cs[3][0][c]);
+      if (a.dbeta) atomicAdd(a.dbeta + c, cs[0][1][c] + cs[1][1][c] + cs[2][1][c] + cs[3][1][c]);
+      if constexpr (LS) {
+        atomicAdd(a.dls + c, cs[0][LS ? 2 : 0][c] + cs[1][LS ? 2 : 0][c] + cs[2][LS ? 2 : 0][c] + cs[3][LS ? 2 : 0][c]);
+        atomicAdd(a.dlsb + c, cs[0][LS ? 3 : 0][c] + cs[1][LS ? 3 : 0][c] + cs[2][LS ? 3 : 0][c] + cs[3][LS ? 3 : 0][c]);
+      }
+    }
+  }
+}
+
+// One row at a time per wave, column sums in registers: the form for few rows per wave (Qwen2 RMSNorm, 6384 rows),
+// where norm_bwd_wave_kernel's second row in flight does not pay for its LDS accumulators.
+template <bool RMS, bool LS, bool DYB>
+__global__ __launch_bounds__(256) void norm_bwd_row_kernel(NormArgs a) {
   __shared__ float cs[4][LS ? 4 : 2][1024];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   float pg[16], pb[16], pl[16], pq[16];  // pl/pq: layer-scale branch sums (dls, dbias), LS only
@@ -407,9 +560,12 @@ static int norm_bwd(NormArgs& a, float* dgamma, float* dbeta, int accumulate, hi
   if (a.D <= 1024 && a.ls) {
     if (a.dy_bf16) hipLaunchKernelGGL((norm_bwd_wave_kernel<RMS, true, true>), dim3(nblk), dim3(256), 0, st, a);
     else hipLaunchKernelGGL((norm_bwd_wave_kernel<RMS, true, false>), dim3(nblk), dim3(256), 0, st, a);
-  } else if (a.D <= 1024) {
+  } else if (a.D <= 1024 && a.rows >= 16 * nblk) {  // >= 4 rows per wave: two rows in flight per wave pay off
     if (a.dy_bf16) hipLaunchKernelGGL((norm_bwd_wave_kernel<RMS, false, true>), dim3(nblk), dim3(256), 0, st, a);
     else hipLaunchKernelGGL((norm_bwd_wave_kernel<RMS, false, false>), dim3(nblk), dim3(256), 0, st, a);
+  } else if (a.D <= 1024) {
+    if (a.dy_bf16) hipLaunchKernelGGL((norm_bwd_row_kernel<RMS, false, true>), dim3(nblk), dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((norm_bwd_row_kernel<RMS, false, false>), dim3(nblk), dim3(256), 0, st, a);
   }
   else if (a.D <= 2048) hipLaunchKernelGGL((norm_bwd_kernel<8, RMS>), dim3(nblk), dim3(256), 0, st, a);
   else hipLaunchKernelGGL((norm_bwd_kernel<16, RMS>), dim3(nblk), dim3(256), 0, st, a);
