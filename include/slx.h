@@ -328,6 +328,9 @@ int slx_dec_attn_nsplit(int lmax);
 /* tools only: record phase timestamps (wall_clock64 ticks) of the next slx_dec_attn launches into buf
  * (>= 64 + Hkv * nsplit int64); NULL turns tracing off                                                  */
 void slx_dec_attn_set_trace(long long* buf);
+/* tests / tools only: 1 = use the split form even for caches of <= 1024 rows (which otherwise run one MFMA
+ * workgroup per kv head, no split)                                                                        */
+void slx_dec_attn_force_split(int on);
 int slx_dec_attn_ws_floats(int Hq, int Hkv, int lmax);
 int slx_dec_attn(void* cache, int64_t ld, int Hq, int Hkv, const float* cos_tab, const float* sin_tab, int lmax,
                  float* ws, void* out, const slx_dec_state* st, slx_stream_t s);

@@ -116,14 +116,31 @@ constexpr float MASKED = -INFINITY;
 // with its own L2). Map the physical id to a logical one so every XCD gets a contiguous logical range,
 // and order logical ids (b, kv-head, q-head in group, 128-row block) fastest-last: all blocks that read
 // one (b, kv-head)'s K/V (or Q/dO in backward) then share one L2 instead of fetching it eight times.
+// Causal launches (Qwen2) instead deal the blocks heaviest-first in dispatch order, with the row block as the slowest
+// logical dimension (order 1: highest query block first, for the forward / dQ passes; order 2: lowest key block first,
+// for the dK/dV pass): a query block's work grows with its index, and the last blocks dispatched should be the light
+// ones, not a mix that leaves a few heavy blocks running alone at the tail. Every XCD gets the same mix (round-robin
+// dealing); the whole K/V of a 798-token batch (3.3 MB) fits one XCD's L2 anyway.
 struct BlockCoord { int blk, h, b; };
-__device__ __forceinline__ BlockCoord attn_block(int nblk, int Hq, int Hkv, int B) {
+__device__ __forceinline__ BlockCoord attn_block(int nblk, int Hq, int Hkv, int B, int order = 0) {
   const int nwg = nblk * Hq * B;
   int bid = blockIdx.x;
-  const int q = nwg >> 3, r = nwg & 7, xcd = bid & 7;
-  bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
   const int G = Hq / Hkv;
   BlockCoord c;
+  if (order != 0) {
+    const int per = Hq * B;
+    const int r = bid / per;
+    c.blk = order == 1 ? nblk - 1 - r : r;
+    int t = bid - r * per;
+    const int hg = t % G;
+    t /= G;
+    const int hk = t % Hkv;
+    c.b = t / Hkv;
+    c.h = hk * G + hg;
+    return c;
+  }
+  const int q = nwg >> 3, r = nwg & 7, xcd = bid & 7;
+  bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
   c.blk = bid % nblk;
   int t = bid / nblk;
   const int hg = t % G;
@@ -205,7 +222,7 @@ __device__ __forceinline__ void fwd_tile(const char* Kl, const char* Vl, const b
 
 __global__ __launch_bounds__(256, ATTN_FWD_OCC) void attn_fwd_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) char smem[2 * 2 * 8192];
-  const BlockCoord bc = attn_block((a.S + 127) / 128, a.Hq, a.Hkv, a.B);
+  const BlockCoord bc = attn_block((a.S + 127) / 128, a.Hq, a.Hkv, a.B, a.causal ? 1 : 0);
   const int qb = bc.blk, h = bc.h, b = bc.b;
   const int hk = h / (a.Hq / a.Hkv);
   const int S = a.S;
@@ -370,7 +387,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kv_kernel(AttnArgs a) {
   char* Dc = smem + 2 * 8192;
   float* LD = reinterpret_cast<float*>(Dc + 2 * 8192);  // [buf][lse 64 | delta 64]
 
-  const BlockCoord bc = attn_block((a.S + 127) / 128, a.Hkv * a.nsplit, a.Hkv * a.nsplit, a.B);
+  const BlockCoord bc = attn_block((a.S + 127) / 128, a.Hkv * a.nsplit, a.Hkv * a.nsplit, a.B, a.causal ? 2 : 0);
   const int kblk = bc.blk, hk = bc.h / a.nsplit, sp = bc.h % a.nsplit, b = bc.b;
   const int G = a.Hq / a.Hkv;
   const int hg0 = sp * a.hsplit;
@@ -533,7 +550,7 @@ __device__ __forceinline__ void bwd_dq_tile(const char* Kl, const char* Vl, cons
 
 __global__ __launch_bounds__(256, ATTN_DQ_OCC) void attn_bwd_dq_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) char smem[2 * 2 * 8192];
-  const BlockCoord bc = attn_block((a.S + 127) / 128, a.Hq, a.Hkv, a.B);
+  const BlockCoord bc = attn_block((a.S + 127) / 128, a.Hq, a.Hkv, a.B, a.causal ? 1 : 0);
   const int qb = bc.blk, h = bc.h, b = bc.b;
   const int hk = h / (a.Hq / a.Hkv);
   const int S = a.S;
@@ -702,6 +719,198 @@ __global__ void f32_to_bf16_rows_kernel(const float* src, long lds, bf16* dst, l
 #pragma unroll
   for (int j = 0; j < 8; ++j) v[j] = (bf16)s[j];
   *reinterpret_cast<bf16x8*>(dst + t * ldd + c) = v;
+}
+
+
+// ---- decode attention, one workgroup per kv head (agent decode, caches of <= 1024 rows) ---------------------------
+// The new token's G query heads over cache rows [0, pos] of one kv head, without a key split (so no partials, no
+// cross-workgroup merge): 16 waves; wave w owns 32-key blocks w and w + 16. S = K Q^T on the MFMA with K fragments
+// loaded straight from the cache rows (natural order) and the rotated q heads as the B operand (head on the lane,
+// padded to 32 with zero rows); softmax max / sum per head through one LDS exchange each; O^T += V^T P^T with V staged
+// in swizzled LDS and P^T taken from the score accumulator (the training forward's operand forms); the 16 wave
+// partials of O^T summed through LDS. Cache row layout [q (Hq*64) | k (Hkv*64) | v (Hkv*64)], rows < pos hold rotated
+// k; this kernel rotates q and row pos's k (writing that k back for later steps).
+struct DecMfmaArgs {
+  bf16* cache; long ld; int Hq, Hkv;
+  const float* cos; const float* sin;
+  bf16* out;
+  const int* st;  // slx_dec_state: [0] pos, [2] done
+  float scale;
+};
+
+constexpr int kDecKeys = 1024;
+
+__global__ __launch_bounds__(1024) void dec_attn_mfma_kernel(DecMfmaArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* Vl = smem;                          // [kDecKeys][64] bf16, swizzled (128 KB); reused for the O^T partials
+  char* Ql = smem + kDecKeys * 128;         // [32][64] bf16 rotated q heads (rows >= G zero), swizzled
+  float* kpos = reinterpret_cast<float*>(Ql + 32 * 128);  // [64] rotated k of row pos (bf16 values)
+  float* red = kpos + 64;                   // [16 waves][32 heads]
+  float* Mh = red + 16 * 32;                // [32]
+  float* Lh = Mh + 32;                      // [32]
+  if (a.st[2]) return;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hl = lane >> 5;
+  const int pos = a.st[0], L = pos + 1;
+  const int g = blockIdx.x, G = a.Hq / a.Hkv;
+  const int qn = a.Hq * 64, kn = a.Hkv * 64;
+  const int nb = (L + 31) >> 5;  // 32-key blocks
+  const bf16* kcol = a.cache + qn + g * 64;
+  const bf16* vcol = a.cache + qn + kn + g * 64;
+  // ---- every global read up front: K fragments of this wave's blocks, V rows (16-B chunks), q / k rows of pos
+  bf16x8 kf[2][4];
+#pragma unroll
+  for (int bb = 0; bb < 2; ++bb) {
+    const int blk = w + 16 * bb;
+    const int key = min(blk * 32 + (lane & 31), L - 1);
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk)
+      kf[bb][kk] = blk < nb ? *reinterpret_cast<const bf16x8*>(kcol + (long)key * a.ld + 16 * kk + 8 * hl) : bf16x8{};
+  }
+  uint4 vr[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int c = tid + 1024 * i, row = c >> 3;
+    vr[i] = row < L ? *reinterpret_cast<const uint4*>(vcol + (long)row * a.ld + 8 * (c & 7)) : make_uint4(0u, 0u, 0u, 0u);
+  }
+  bf16* prow = a.cache + (long)pos * a.ld;
+  const float* cs = a.cos + (long)pos * 32;
+  const float* sn = a.sin + (long)pos * 32;
+  if (tid < 32 * 32) {  // rotate_half RoPE of the G q heads into Ql (rows >= G: zeros)
+    const int h = tid >> 5, j = tid & 31;
+    float r0 = 0.f, r1 = 0.f;
+    if (h < G) {
+      const bf16* q = prow + (g * G + h) * 64;
+      const float q0 = (float)q[j], q1 = (float)q[j + 32];
+      r0 = q0 * cs[j] - q1 * sn[j];
+      r1 = q1 * cs[j] + q0 * sn[j];
+    }
+    *reinterpret_cast<bf16*>(Ql + sw_elem(h, j)) = (bf16)r0;
+    *reinterpret_cast<bf16*>(Ql + sw_elem(h, j + 32)) = (bf16)r1;
+  }
+  if (w == 15 && lane < 32) {  // k of this token: rotated, written back once
+    const int j = lane;
+    bf16* k = prow + qn + g * 64;
+    const float k0 = (float)k[j], k1 = (float)k[j + 32];
+    const bf16 r0 = (bf16)(k0 * cs[j] - k1 * sn[j]), r1 = (bf16)(k1 * cs[j] + k0 * sn[j]);
+    k[j] = r0;
+    k[j + 32] = r1;
+    kpos[j] = (float)r0;
+    kpos[j + 32] = (float)r1;
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int c = tid + 1024 * i, row = c >> 3;
+    if (row < nb * 32) *reinterpret_cast<uint4*>(Vl + sw_off(row, c & 7)) = vr[i];
+  }
+  __syncthreads();
+  // the lanes holding row pos take the rotated k
+#pragma unroll
+  for (int bb = 0; bb < 2; ++bb) {
+    if (w + 16 * bb == (pos >> 5) && (lane & 31) == (pos & 31)) {
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) kf[bb][kk][j] = (bf16)kpos[16 * kk + 8 * hl + j];
+    }
+  }
+  // ---- scores S[key][head] = K q^T, head on the lane (l & 31), 16 keys per lane and block
+  bf16x8 qf[4];
+#pragma unroll
+  for (int kk = 0; kk < 4; ++kk) qf[kk] = row_frag(Ql, 0, kk, lane);
+  const float c = a.scale * LOG2E;
+  f32x16 s[2];
+  float mx = -INFINITY;
+#pragma unroll
+  for (int bb = 0; bb < 2; ++bb) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s[bb][r] = 0.f;
+    if (w + 16 * bb < nb) {
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) s[bb] = mfma32(kf[bb][kk], qf[kk], s[bb]);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = (w + 16 * bb) * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
+        s[bb][r] = key < L ? s[bb][r] * c : -INFINITY;
+        mx = fmaxf(mx, s[bb][r]);
+      }
+    }
+  }
+  mx = half_swap_max(mx);
+  if (lane < 32) red[w * 32 + lane] = mx;
+  __syncthreads();
+  if (tid < 32) {
+    float m = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) m = fmaxf(m, red[i * 32 + tid]);
+    Mh[tid] = m;
+  }
+  __syncthreads();
+  const float M = Mh[lane & 31];
+  float ls = 0.f;
+  f32x16 o0, o1;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) { o0[r] = 0.f; o1[r] = 0.f; }
+#pragma unroll
+  for (int bb = 0; bb < 2; ++bb) {
+    if (w + 16 * bb < nb) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        s[bb][r] = __builtin_amdgcn_exp2f(s[bb][r] - M);
+        ls += (float)(bf16)s[bb][r];  // the bf16 P the MFMA sums
+      }
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+        const bf16x8 pb = acc_frag(s[bb], st);
+        o0 = mfma32(tr_frag(Vl, (w + 16 * bb) * 32 + 16 * st, 0, lane), pb, o0);
+        o1 = mfma32(tr_frag(Vl, (w + 16 * bb) * 32 + 16 * st, 32, lane), pb, o1);
+      }
+    }
+  }
+  {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(ls), __float_as_uint(ls), false, false);
+    ls = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  }
+  __syncthreads();  // every wave is done with Vl: reuse it for the O^T partials [16][G][64]
+  float* op = reinterpret_cast<float*>(Vl);
+  if (lane < 32) red[w * 32 + lane] = ls;
+  const int h = lane & 31;
+  if (h < G) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int d = 8 * (r >> 2) + 4 * hl + (r & 3);
+      op[(w * G + h) * 64 + d] = o0[r];
+      op[(w * G + h) * 64 + 32 + d] = o1[r];
+    }
+  }
+  __syncthreads();
+  if (tid < 32) {
+    float l = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) l += red[i * 32 + tid];
+    Lh[tid] = l;
+  }
+  __syncthreads();
+  if (tid < G * 64) {
+    const int hh = tid >> 6, d = tid & 63;
+    float acc = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc += op[(i * G + hh) * 64 + d];
+    a.out[(g * G + hh) * 64 + d] = (bf16)(acc / Lh[hh]);
+  }
+}
+
+int dec_attn_mfma_launch(void* cache, long ld, int Hq, int Hkv, const float* cos_tab, const float* sin_tab, void* out,
+                         const void* st, hipStream_t s) {
+  constexpr int LDS = kDecKeys * 128 + 32 * 128 + (64 + 16 * 32 + 32 + 32) * 4;
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)dec_attn_mfma_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    attr = true;
+  }
+  DecMfmaArgs a{(bf16*)cache, ld, Hq, Hkv, cos_tab, sin_tab, (bf16*)out, (const int*)st, 0.125f};
+  hipLaunchKernelGGL(dec_attn_mfma_kernel, dim3(Hkv), dim3(1024), LDS, s, a);
+  SLX_LAUNCH_CHECK("slx_dec_attn(mfma)");
+  return 0;
 }
 
 }  // namespace slx

@@ -18,6 +18,11 @@
 namespace slx {
 
 constexpr int kKeyShards = 64;
+// attention.hip: the single-workgroup-per-kv-head MFMA form for caches of <= 1024 rows
+int dec_attn_mfma_launch(void* cache, long ld, int Hq, int Hkv, const float* cos_tab, const float* sin_tab, void* out,
+                         const void* st, hipStream_t s);
+static long long* g_dec_trace = nullptr;  // tools only (slx_dec_attn_set_trace)
+static int g_dec_force_split = 0;         // tests / tools only (slx_dec_attn_force_split)
 
 // float -> order-preserving u32; key = value << 32 | (0xFFFFFFFF - index): max key = max value, then the
 // smallest index (torch.argmax returns the first maximal element)
@@ -85,6 +90,7 @@ struct GemvArgs {
   unsigned long long* keys;                        // ARGMAX
   int F;                                           // SWIGLU: up rows start at F (= N)
   const slx_dec_state* st;                         // may be null (prefill)
+  long long* trace;                                // tools only (slx_dec_attn_set_trace): workgroup 0's phases
 };
 
 // One wave owns R output rows (SWIGLU: R gate + R up rows) of a row group; lane l holds 16-B chunks
@@ -136,8 +142,11 @@ __global__ __launch_bounds__(256) void dec_gemv_kernel(GemvArgs a) {
       }
     }
   };
+  const bool t0 = a.trace && blockIdx.x == 0 && threadIdx.x == 0;
+  if (a.trace && threadIdx.x == 0) a.trace[128 + blockIdx.x] = (long long)wall_clock64();
   int rg = blockIdx.x;
   if (rg < nrg) issue(rg);
+  if (t0) a.trace[32] = (long long)wall_clock64();
   if (a.st && a.st->done) return;
   if (a.X) {
     float ss = 0.f;
@@ -157,6 +166,7 @@ __global__ __launch_bounds__(256) void dec_gemv_kernel(GemvArgs a) {
     }
   }
   __syncthreads();
+  if (t0) a.trace[33] = (long long)wall_clock64();
   unsigned long long best = 0ull;  // ARGMAX: running best of this wave over its row groups
   for (; rg < nrg; rg += gridDim.x) {
     float acc[NR];
@@ -204,6 +214,7 @@ __global__ __launch_bounds__(256) void dec_gemv_kernel(GemvArgs a) {
       }
     }
   }
+  if (t0) a.trace[34] = (long long)wall_clock64();
   if constexpr (MODE == GV_ARGMAX) {
     if (lane == 0 && best) atomicMax(a.keys + ((blockIdx.x * 4 + wave) & (kKeyShards - 1)), best);
   }
@@ -507,6 +518,7 @@ int slx_dec_gemv(const slx_dec_gemv_desc* d, slx_stream_t s) {
   a.X = d->X; a.gamma = d->gamma; a.eps = d->eps; a.xb = (const bf16*)d->xb; a.bias = d->bias;
   a.out = (bf16*)d->out; a.out_ld = d->out_ld; a.resid = d->resid; a.keys = d->keys; a.F = d->N;
   a.st = d->state;
+  a.trace = g_dec_trace;
   switch (d->mode) {
     case SLX_DEC_STORE_ROW: SLX_CHECK_ARG(d->out != nullptr, "slx_dec_gemv: out"); return gemv_launch(GV_STORE_ROW, a, (hipStream_t)s);
     case SLX_DEC_RESID: SLX_CHECK_ARG(d->resid != nullptr, "slx_dec_gemv: resid"); return gemv_launch(GV_RESID, a, (hipStream_t)s);
@@ -517,9 +529,10 @@ int slx_dec_gemv(const slx_dec_gemv_desc* d, slx_stream_t s) {
   return -22;
 }
 
-static long long* g_dec_trace = nullptr;
-// tools only: phase timestamps (wall_clock64 ticks) of the next slx_dec_attn launches; NULL turns tracing off
+// tools only: phase timestamps (wall_clock64 ticks) of the next slx_dec_attn / slx_dec_gemv launches; NULL = off
 void slx_dec_attn_set_trace(long long* buf) { g_dec_trace = buf; }
+// tests / tools only: 1 = always use the split-K form (the path for caches of more than 1024 rows)
+void slx_dec_attn_force_split(int on) { g_dec_force_split = on; }
 
 int slx_dec_attn_nsplit(int lmax) { return (lmax + kAttnChunk - 1) / kAttnChunk > 8 ? (lmax + kAttnChunk - 1) / kAttnChunk : 8; }
 
@@ -533,6 +546,8 @@ int slx_dec_attn(void* cache, int64_t ld, int Hq, int Hkv, const float* cos_tab,
   SLX_CHECK_ARG(Hkv > 0 && Hq % Hkv == 0 && Hq / Hkv <= 8, "slx_dec_attn: Hq/Hkv must be an integer <= 8");
   SLX_CHECK_ARG(ld % 8 == 0 && ((uintptr_t)cache & 15) == 0, "slx_dec_attn: cache rows must be 16-B aligned");
   SLX_CHECK_ARG(lmax > 0 && lmax <= 64 * kAttnChunk, "slx_dec_attn: lmax <= 8192");  // ns <= 64: ns * G <= 512
+  if (lmax <= 1024 && !g_dec_trace && !g_dec_force_split)  // one workgroup per kv head: no split partials, no merge
+    return dec_attn_mfma_launch(cache, ld, Hq, Hkv, cos_tab, sin_tab, out, st, (hipStream_t)s);
   const int ns = slx_dec_attn_nsplit(lmax);
   DecAttnArgs a{(bf16*)cache, ld, Hq, Hkv, cos_tab, sin_tab, ws, (bf16*)out, st, 0.125f, g_dec_trace};
   SLX_CHECK_ARG(((uintptr_t)ws & 3) == 0, "slx_dec_attn: ws must be 4-B aligned (and zeroed once: it holds the counters)");

@@ -275,7 +275,11 @@ __global__ __launch_bounds__(256) void norm_bwd_wave_kernel(NormArgs a) {
         const float4 t = cur.t[i], d = cur.d[i], g = gm[i];
         const float tv[4] = {t.x, t.y, t.z, t.w}, dv[4] = {d.x, d.y, d.z, d.w}, gv[4] = {g.x, g.y, g.z, g.w};
 #pragma unroll
-        for (int e = 0; e < 4; ++e) ov[e] = rs * (dv[e] * gv[e] - m1 - ((tv[e] - mu) * rs) * m2);
+        for (int e = 0; e < 4; ++e) {
+          const float xh = (tv[e] - mu) * rs;
+          const float gd = __fmul_rn(dv[e], gv[e]);  // a rounded product, as norm_bwd_row_kernel keeps it (no FMA fusion)
+          ov[e] = rs * (gd - m1 - xh * m2);
+        }
       }
       if (a.dx_accumulate) {
         ov[0] += cur.dxo[i].x; ov[1] += cur.dxo[i].y; ov[2] += cur.dxo[i].z; ov[3] += cur.dxo[i].w;
@@ -557,10 +561,14 @@ static int norm_bwd(NormArgs& a, float* dgamma, float* dbeta, int accumulate, hi
     if (dgamma) hipMemsetAsync(dgamma, 0, a.D * sizeof(float), st);
     if (dbeta) hipMemsetAsync(dbeta, 0, a.D * sizeof(float), st);
   }
-  if (a.D <= 1024 && a.ls) {
+  const bool two_rows = a.rows >= 16 * nblk;  // >= 4 rows per wave: two rows in flight per wave pay off
+  if (a.D <= 1024 && a.ls && two_rows) {
     if (a.dy_bf16) hipLaunchKernelGGL((norm_bwd_wave_kernel<RMS, true, true>), dim3(nblk), dim3(256), 0, st, a);
     else hipLaunchKernelGGL((norm_bwd_wave_kernel<RMS, true, false>), dim3(nblk), dim3(256), 0, st, a);
-  } else if (a.D <= 1024 && a.rows >= 16 * nblk) {  // >= 4 rows per wave: two rows in flight per wave pay off
+  } else if (a.D <= 1024 && a.ls) {
+    if (a.dy_bf16) hipLaunchKernelGGL((norm_bwd_row_kernel<RMS, true, true>), dim3(nblk), dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((norm_bwd_row_kernel<RMS, true, false>), dim3(nblk), dim3(256), 0, st, a);
+  } else if (a.D <= 1024 && two_rows) {
     if (a.dy_bf16) hipLaunchKernelGGL((norm_bwd_wave_kernel<RMS, false, true>), dim3(nblk), dim3(256), 0, st, a);
     else hipLaunchKernelGGL((norm_bwd_wave_kernel<RMS, false, false>), dim3(nblk), dim3(256), 0, st, a);
   } else if (a.D <= 1024) {

@@ -113,3 +113,52 @@ def test_driving_model_forward_surface(dev):
     m.predict_language = False
     sp1, rp1, lang1 = m(ex)
     assert lang1 == [] and sp1.shape == sp.shape
+
+
+@pytest.mark.parametrize("pos", [0, 31, 300, 1000])
+def test_dec_attn_forms_vs_torch(dev, pos):
+    """slx_dec_attn at the agent geometry (14 q / 2 kv heads): the single-workgroup MFMA form (caches <= 1024 rows) and
+    the split form with its last-arriver merge, each vs a torch fp32 softmax attention of the same bf16 rows (q and
+    row pos's k rotated with the same tables); the k row written back must be the rotated one."""
+    import ctypes
+    from simlingo_amd import decode  # noqa: F401
+    from simlingo_amd import kernels as K
+    K.register("slx_dec_attn_force_split", [ctypes.c_int])
+    Hq, Hkv, lmax = 14, 2, 1024
+    ld = (Hq + 2 * Hkv) * 64
+    gen = torch.Generator(device=dev).manual_seed(pos)
+    cache0 = torch.randn(lmax, ld, device=dev, generator=gen).bfloat16()
+    cos, sin = K.rope_tables(lmax, 1e6, dev)
+    st = torch.tensor([pos, 0, 0, 100, -1, 0, 0, 0], dtype=torch.int32, device=dev)
+
+    def rope(x):  # [n, 64] f32 -> rotate_half with row `pos` of the tables, rounded to bf16
+        c, s_ = cos[pos], sin[pos]
+        x0, x1 = x[:, :32], x[:, 32:]
+        return torch.cat([x0 * c - x1 * s_, x1 * c + x0 * s_], 1).bfloat16().float()
+
+    c0 = cache0.float()
+    ref = torch.empty(Hq, 64, device=dev)
+    G = Hq // Hkv
+    for g in range(Hkv):
+        k = c0[:pos + 1, Hq * 64 + 64 * g: Hq * 64 + 64 * (g + 1)].clone()
+        k[pos] = rope(k[pos:pos + 1])[0]
+        v = c0[:pos + 1, (Hq + Hkv) * 64 + 64 * g: (Hq + Hkv) * 64 + 64 * (g + 1)]
+        q = rope(c0[pos, 64 * G * g: 64 * G * (g + 1)].reshape(G, 64))
+        ref[G * g: G * (g + 1)] = torch.softmax(q @ k.t() * 0.125, -1) @ v
+    lib = K.lib()
+    for split in (0, 1):
+        cache = cache0.clone()
+        ws = torch.zeros(lib.slx_dec_attn_ws_floats(Hq, Hkv, lmax), device=dev)
+        out = torch.empty(Hq * 64, dtype=torch.bfloat16, device=dev)
+        lib.slx_dec_attn_force_split(split)
+        try:
+            K.check(lib.slx_dec_attn(K.P(cache), ld, Hq, Hkv, K.P(cos), K.P(sin), lmax, K.P(ws), K.P(out), K.P(st),
+                                     K.stream_ptr()), "slx_dec_attn")
+            torch.cuda.synchronize()
+        finally:
+            lib.slx_dec_attn_force_split(0)
+        err = (out.float().reshape(Hq, 64) - ref).abs().max().item()
+        assert err <= 2e-2 * ref.abs().max().item() + 1e-3, (split, err)
+        for g in range(Hkv):
+            krow = cache[pos, Hq * 64 + 64 * g: Hq * 64 + 64 * (g + 1)].float()
+            assert torch.equal(krow, rope(c0[pos:pos + 1, Hq * 64 + 64 * g: Hq * 64 + 64 * (g + 1)])[0]), split

@@ -97,11 +97,13 @@ def test_norm_bwd_bf16_copy(dev, rms):
     assert torch.equal(dxb, dx.bfloat16())
 
 
-def test_layernorm_bwd_fused_ls_branch(dev):
+@pytest.mark.parametrize("M", [1025 * 3, 16400])
+def test_layernorm_bwd_fused_ls_branch(dev, M):
     """slx_norm_desc.ls*: the InternViT layer-scale branch backward (g = bf16(dx * ls), dls += sum dx * y,
     dbias += sum dx * ls) fused onto the rows the LayerNorm backward just updated, against the separate
-    norm backward + slx_ls_branch_bwd of the same inputs."""
-    M, D = 1025 * 3, 1024
+    norm backward + slx_ls_branch_bwd of the same inputs (3075 rows: one row per wave at a time; 16400 rows, the
+    InternViT step's: two rows in flight per wave)."""
+    D = 1024
     gen = torch.Generator(device=dev).manual_seed(5)
     x = torch.randn(M, D, device=dev, generator=gen)
     gamma, beta = torch.rand(D, device=dev, generator=gen) + 0.5, torch.randn(D, device=dev, generator=gen)

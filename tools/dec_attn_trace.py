@@ -28,16 +28,21 @@ def call():
                              K.stream_ptr()), "slx_dec_attn")
 
 
-for _ in range(20):
-    call()
-torch.cuda.synchronize()
+K.register("slx_dec_attn_force_split", [ctypes.c_int])
 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-e0.record()
-for _ in range(200):
-    call()
-e1.record()
-torch.cuda.synchronize()
-print(f"slx_dec_attn: {e0.elapsed_time(e1) / 200 * 1e3:.2f} us per launch (back to back, incl. boundaries)")
+for split in (0, 1):
+    lib.slx_dec_attn_force_split(split)
+    for _ in range(20):
+        call()
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(200):
+        call()
+    e1.record()
+    torch.cuda.synchronize()
+    form = "split + last-arriver merge" if split else "one workgroup per kv head (MFMA)"
+    print(f"slx_dec_attn [{form}]: {e0.elapsed_time(e1) / 200 * 1e3:.2f} us per launch (back to back, incl. boundaries)")
+lib.slx_dec_attn_force_split(0)
 tr = torch.zeros(64 + 256, dtype=torch.int64, device=dev)
 for rep in range(3):
     tr.zero_()
@@ -54,3 +59,46 @@ for rep in range(3):
              "m/l loaded", "merged"]
     print(f"rep {rep}: workgroup starts span {(max(starts) - base) * 0.01:.2f} us over {len(starts)} workgroups")
     print("   " + "  ".join(f"{n}={us(t[i])}" for i, n in enumerate(names) if n != "-"))
+
+# ---- the layer's GEMVs (QKV with the fused RMSNorm, down + residual) -------------------------------------------------
+from simlingo_amd.decode import DEC_RESID, DEC_STORE_ROW, _gemv_desc  # noqa: E402
+
+d, F = 896, 4864
+X = torch.randn(d, device=dev)
+gamma = torch.rand(d, device=dev) + 0.5
+Wqkv = (torch.randn(ld, d, device=dev) * 0.02).bfloat16()
+bias = torch.randn(ld, device=dev)
+Wd = (torch.randn(d, F, device=dev) * 0.02).bfloat16()
+act = torch.randn(F, device=dev).bfloat16()
+gemvs = {
+    "qkv (N 1152, K 896, norm fused)": _gemv_desc(DEC_STORE_ROW, Wqkv, ld, d, X=X, gamma=gamma, eps=1e-6, bias=bias,
+                                                  out=cache, out_ld=ld, state=st),
+    "down (N 896, K 4864, + resid)": _gemv_desc(DEC_RESID, Wd, d, F, xb=act, resid=X.clone(), state=st),
+}
+for name, desc in gemvs.items():
+    def gcall(desc=desc):
+        K.check(lib.slx_dec_gemv(ctypes.byref(desc), K.stream_ptr()), "slx_dec_gemv")
+    for _ in range(20):
+        gcall()
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(200):
+        gcall()
+    e1.record()
+    torch.cuda.synchronize()
+    print(f"{name}: {e0.elapsed_time(e1) / 200 * 1e3:.2f} us per launch (back to back)")
+    big = torch.zeros(128 + 4096, dtype=torch.int64, device=dev)
+    for rep in range(2):
+        big.zero_()
+        torch.empty(64 << 20, dtype=torch.uint8, device=dev).fill_(1)  # evict: the weights come from HBM as in a step
+        torch.cuda.synchronize()
+        lib.slx_dec_attn_set_trace(ctypes.c_void_p(big.data_ptr()))
+        gcall()
+        torch.cuda.synchronize()
+        lib.slx_dec_attn_set_trace(ctypes.c_void_p(0))
+        t = big.cpu().tolist()
+        starts = [v for v in t[128:] if v]
+        base = min(starts)
+        print(f"   rep {rep}: {len(starts)} workgroups start over {(max(starts) - base) * 0.01:.2f} us; workgroup 0: "
+              f"loads issued {(t[32] - base) * 0.01:.2f}, x ready {(t[33] - base) * 0.01:.2f}, "
+              f"rows done {(t[34] - base) * 0.01:.2f} us")

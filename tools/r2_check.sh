@@ -9,6 +9,7 @@ tail -2 gpurun_out/${TAG}_tests.log
 timeout -k 10 120 python3 tools/dec_attn_trace.py 680 > gpurun_out/${TAG}_dectrace.txt 2>&1
 cat gpurun_out/${TAG}_dectrace.txt
 timeout -k 10 120 python3 tools/norm_bench.py > gpurun_out/${TAG}_norm.txt 2>&1
+timeout -k 10 120 python3 tools/attn_bench.py >> gpurun_out/${TAG}_norm.txt 2>&1
 cat gpurun_out/${TAG}_norm.txt
 timeout -k 10 300 python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err
 cat gpurun_out/${TAG}_bench.json
