@@ -12,6 +12,8 @@
 // the next step's begin kernel). All per-step scalars (position, #generated, done) live in a device
 // slx_dec_state so one decode step can be captured once in a hipGraph and replayed; a step after
 // the EOS token early-exits in every kernel.
+#include <cstdlib>
+
 #include "common.h"
 #include "../../include/slx.h"
 
@@ -474,16 +476,27 @@ static void gemv_cpl(GemvArgs& a, dim3 grid, size_t lds, hipStream_t st) {
 }
 
 static int gemv_launch(int mode, GemvArgs& a, hipStream_t st) {
-  // rows per wave: 4 for the LM head (argmax) / very tall weights, 2 for gate|up, else 1 (more workgroups
-  // in flight for the latency-bound 896-row projections)
-  const int R = mode == GV_ARGMAX ? 4 : (mode == GV_SWIGLU || a.N >= 4096) ? 2 : 1;
+  // rows per wave: 4 for the LM head (argmax) and the q|k|v row GEMV (0.5 us faster than 1: a quarter of the
+  // workgroups to dispatch, tools/gemv_ab.sh), 2 for gate|up, else 1 (the 896-row residual GEMVs measured fastest
+  // with more workgroups in flight)
+  static const int r_env = [] { const char* e = getenv("SLX_DEC_GEMV_R"); return e ? atoi(e) : 0; }();  // tools: A/B
+  int R = mode == GV_ARGMAX || mode == GV_STORE_ROW ? 4 : (mode == GV_SWIGLU || a.N >= 4096) ? 2 : 1;
+  if (r_env == 1 || r_env == 2 || r_env == 4) R = mode == GV_ARGMAX ? 4 : (mode == GV_SWIGLU ? 2 : r_env);
   const int rows_per_block = 4 * R;
   const int groups = (a.N + rows_per_block - 1) / rows_per_block;
   const dim3 grid(groups < 2048 ? groups : 2048);  // grid-stride over row groups: the norm prologue amortised
   const size_t lds = (size_t)a.K * 2;
   switch (mode) {
-    case GV_STORE_ROW: if (R == 2) gemv_cpl<GV_STORE_ROW, 2>(a, grid, lds, st); else gemv_cpl<GV_STORE_ROW, 1>(a, grid, lds, st); break;
-    case GV_RESID: if (R == 2) gemv_cpl<GV_RESID, 2>(a, grid, lds, st); else gemv_cpl<GV_RESID, 1>(a, grid, lds, st); break;
+    case GV_STORE_ROW:
+      if (R == 4) gemv_cpl<GV_STORE_ROW, 4>(a, grid, lds, st);
+      else if (R == 2) gemv_cpl<GV_STORE_ROW, 2>(a, grid, lds, st);
+      else gemv_cpl<GV_STORE_ROW, 1>(a, grid, lds, st);
+      break;
+    case GV_RESID:
+      if (R == 4) gemv_cpl<GV_RESID, 4>(a, grid, lds, st);
+      else if (R == 2) gemv_cpl<GV_RESID, 2>(a, grid, lds, st);
+      else gemv_cpl<GV_RESID, 1>(a, grid, lds, st);
+      break;
     case GV_SWIGLU: gemv_cpl<GV_SWIGLU, 2>(a, grid, lds, st); break;
     case GV_ARGMAX: gemv_cpl<GV_ARGMAX, 4>(a, grid, lds, st); break;
   }

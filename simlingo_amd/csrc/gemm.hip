@@ -21,6 +21,8 @@
 //    operand panels sit in one XCD's L2.
 #include <cmath>
 
+#include <cstdlib>
+
 #include "common.h"
 #include "../../include/slx.h"
 
@@ -909,10 +911,16 @@ __device__ __forceinline__ void v3_tile(const GemmArgs& p, int bid, long z, char
   }
 }
 
+// gridDim.x < tiles: a persistent grid, each block walks tiles blockIdx.x, + gridDim.x, ... (gridDim.x a multiple of 8,
+// so a block keeps its XCD's tile range); the epilogue stores of one tile drain while the next tile's loads start.
 template <bool AK, bool BKc, int EPI, typename OutT>
 __global__ __launch_bounds__(512, 1) void gemm_bf16_v3_kernel(GemmArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  v3_tile<AK, BKc, EPI, OutT>(p, xcd_remap(blockIdx.x, p.tilesM * p.tilesN), blockIdx.z, smem);
+  const int nwg = p.tilesM * p.tilesN;
+  for (int t = blockIdx.x; t < nwg; t += gridDim.x) {
+    if (t != (int)blockIdx.x) __syncthreads();  // the previous tile's epilogue is done with the LDS
+    v3_tile<AK, BKc, EPI, OutT>(p, xcd_remap(t, nwg), blockIdx.z, smem);
+  }
 }
 
 // Two independent GEMMs of one layout (f32 outputs accumulated, same K and split count) in one launch: grid.x
@@ -939,7 +947,12 @@ static int launch_v3(GemmArgs a, int batch, hipStream_t st) {
   }
   a.tilesM = (a.M + V3_BM - 1) / V3_BM;
   a.tilesN = (a.N + V3_BN - 1) / V3_BN;
-  dim3 grid(a.tilesM * a.tilesN, a.ksplit > 1 ? a.ksplit : 1, batch);
+  // persistent grid (one round of 256 blocks walking the tiles) by default: +0.3 % on the VLA step
+  // (profiles/round2_s3_persist_ab.txt); SLX_GEMM_PERSIST=0 launches one block per tile
+  static const int persist = [] { const char* e = getenv("SLX_GEMM_PERSIST"); return e ? atoi(e) : 1; }();
+  int gx = a.tilesM * a.tilesN;
+  if (persist > 0 && a.ksplit <= 1 && batch == 1 && gx > 256 * persist) gx = 256 * persist;
+  dim3 grid(gx, a.ksplit > 1 ? a.ksplit : 1, batch);
   hipLaunchKernelGGL((gemm_bf16_v3_kernel<AK, BKc, EPI, OutT>), grid, dim3(512), LDS, st, a);
   SLX_LAUNCH_CHECK("slx_gemm_bf16(v3)");
   return 0;
