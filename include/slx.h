@@ -331,6 +331,14 @@ void slx_dec_attn_set_trace(long long* buf);
 /* tests / tools only: 1 = use the split form even for caches of <= 1024 rows (which otherwise run one MFMA
  * workgroup per kv head, no split)                                                                        */
 void slx_dec_attn_force_split(int on);
+/* slx_dec_attn followed by the O projection X[n] += W_o[n, :] . out (the "O GEMV + residual" step), in ONE launch for
+ * caches of <= 1024 rows: the O workgroups stream their W_o rows while the attention runs and take the attention
+ * output through an in-launch hand-off (sync: slx_dec_sync_ints() zeroed ints per call site, reset by every call;
+ * sync[2] != 0 reports a hand-off timeout). Longer caches: the split attention + the O GEMV (two launches).       */
+int slx_dec_sync_ints(void);
+int slx_dec_attn_o(void* cache, int64_t ld, int Hq, int Hkv, const float* cos_tab, const float* sin_tab, int lmax,
+                   float* ws, void* out, const slx_dec_state* st, const void* Wo, int64_t ldwo, int N, int K, float* X,
+                   int* sync, slx_stream_t s);
 int slx_dec_attn_ws_floats(int Hq, int Hkv, int lmax);
 int slx_dec_attn(void* cache, int64_t ld, int Hq, int Hkv, const float* cos_tab, const float* sin_tab, int lmax,
                  float* ws, void* out, const slx_dec_state* st, slx_stream_t s);

@@ -740,18 +740,18 @@ struct DecMfmaArgs {
 
 constexpr int kDecKeys = 1024;
 
-__global__ __launch_bounds__(1024) void dec_attn_mfma_kernel(DecMfmaArgs a) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
+// PUBLISH: the output rows are handed to the O-projection workgroups of the same launch (agent-scope stores).
+template <bool PUBLISH>
+__device__ __forceinline__ void dec_attn_mfma_body(const DecMfmaArgs& a, int g, char* smem) {
   char* Vl = smem;                          // [kDecKeys][64] bf16, swizzled (128 KB); reused for the O^T partials
   char* Ql = smem + kDecKeys * 128;         // [32][64] bf16 rotated q heads (rows >= G zero), swizzled
   float* kpos = reinterpret_cast<float*>(Ql + 32 * 128);  // [64] rotated k of row pos (bf16 values)
   float* red = kpos + 64;                   // [16 waves][32 heads]
   float* Mh = red + 16 * 32;                // [32]
   float* Lh = Mh + 32;                      // [32]
-  if (a.st[2]) return;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hl = lane >> 5;
   const int pos = a.st[0], L = pos + 1;
-  const int g = blockIdx.x, G = a.Hq / a.Hkv;
+  const int G = a.Hq / a.Hkv;
   const int qn = a.Hq * 64, kn = a.Hkv * 64;
   const int nb = (L + 31) >> 5;  // 32-key blocks
   const bf16* kcol = a.cache + qn + g * 64;
@@ -895,8 +895,120 @@ __global__ __launch_bounds__(1024) void dec_attn_mfma_kernel(DecMfmaArgs a) {
     float acc = 0.f;
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc += op[(i * G + hh) * 64 + d];
-    a.out[(g * G + hh) * 64 + d] = (bf16)(acc / Lh[hh]);
+    const bf16 o = (bf16)(acc / Lh[hh]);
+    if constexpr (PUBLISH)
+      __hip_atomic_store(reinterpret_cast<unsigned short*>(a.out) + (g * G + hh) * 64 + d, __builtin_bit_cast(unsigned short, o),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else
+      a.out[(g * G + hh) * 64 + d] = o;
   }
+}
+
+__global__ __launch_bounds__(1024) void dec_attn_mfma_kernel(DecMfmaArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  if (a.st[2]) return;
+  dec_attn_mfma_body<false>(a, blockIdx.x, smem);
+}
+
+// Attention + O projection in one launch: workgroups [0, Hkv) run the attention above and publish their rows of the
+// attention output; workgroups [Hkv, Hkv + nO) own 16 rows of W_o each (one per wave), load their weight rows at
+// launch (the weight latency overlaps the attention), wait for the Hkv publications on a counter, then read the output
+// row and add W_o rows . out into the f32 residual. Every workgroup of this launch is resident at once (2 + 56 of 1024
+// threads on 256 CUs), and the wait is bounded, so a lost publication cannot hang the queue (the row is then skipped
+// and the error counter set). Hand-off: agent-scope stores, vmcnt(0), workgroup barrier, one agent-scope add; the
+// waiters poll with agent-scope loads and s_sleep, then load the published bytes with agent-scope loads
+// (MI355X_MICROARCH.md, inter-workgroup visibility, table row 1). sync[0] counts arrivals, sync[1] finished O
+// workgroups (the last one resets both), sync[2] is a sticky timeout flag.
+struct DecOArgs {
+  const bf16* W; long ldw; int N; int K;  // W_o [N][K] bf16 (LoRA merged)
+  float* X;                               // residual row, X[n] += (W_o out)[n]
+  int* sync;
+};
+
+__global__ __launch_bounds__(1024) void dec_attn_o_kernel(DecMfmaArgs a, DecOArgs o) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  if (a.st[2]) return;
+  const int nA = a.Hkv;
+  if ((int)blockIdx.x < nA) {
+    dec_attn_mfma_body<true>(a, blockIdx.x, smem);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(o.sync, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int n = ((int)blockIdx.x - nA) * 16 + w;
+  const int nch = o.K >> 3;
+  uint4 wv[2];
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const int ch = lane + 64 * c;
+    wv[c] = (n < o.N && ch < nch) ? *reinterpret_cast<const uint4*>(o.W + (long)n * o.ldw + 8 * ch) : make_uint4(0u, 0u, 0u, 0u);
+  }
+  __shared__ int ok_s;
+  if (tid == 0) {
+    int ok = 0;
+    for (int it = 0; it < (1 << 20); ++it) {  // bounded: ~1 s at most, far beyond a healthy attention (~10 us)
+      if (__hip_atomic_load(o.sync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= nA) { ok = 1; break; }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    if (!ok) __hip_atomic_store(o.sync + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    ok_s = ok;
+  }
+  __syncthreads();
+  bf16* xs = reinterpret_cast<bf16*>(smem);
+  if (ok_s) {
+    for (int c = tid; c < nch; c += 1024) {  // the attention output row: agent-scope 4-B loads
+      const unsigned* src = reinterpret_cast<const unsigned*>(a.out + 8 * c);
+      uint4 v;
+      v.x = __hip_atomic_load(const_cast<unsigned*>(src), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      v.y = __hip_atomic_load(const_cast<unsigned*>(src + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      v.z = __hip_atomic_load(const_cast<unsigned*>(src + 2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      v.w = __hip_atomic_load(const_cast<unsigned*>(src + 3), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *reinterpret_cast<uint4*>(xs + 8 * c) = v;
+    }
+  }
+  __syncthreads();
+  if (ok_s && n < o.N) {
+    float acc = 0.f;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int ch = lane + 64 * c;
+      if (ch < nch) {
+        const bf16x8 wb = __builtin_bit_cast(bf16x8, wv[c]);
+        const bf16x8 x = *reinterpret_cast<const bf16x8*>(xs + 8 * ch);
+        float sc = 0.f;  // the summation order of dec_gemv_kernel's dot8 (so both O paths round alike)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) sc = __builtin_fmaf((float)wb[e], (float)x[e], sc);
+        acc += sc;
+      }
+    }
+    acc = warp_sum(acc);
+    if (lane == 0) o.X[n] += acc;
+  }
+  __syncthreads();
+  if (tid == 0) {  // the last O workgroup resets the counters for this layer's next step
+    const int nO = (int)gridDim.x - nA;
+    if (__hip_atomic_fetch_add(o.sync + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nO - 1) {
+      __hip_atomic_store(o.sync, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(o.sync + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+int dec_attn_o_launch(void* cache, long ld, int Hq, int Hkv, const float* cos_tab, const float* sin_tab, void* out,
+                      const void* st, const void* Wo, long ldwo, int N, int K, float* X, int* sync, hipStream_t s) {
+  constexpr int LDS = kDecKeys * 128 + 32 * 128 + (64 + 16 * 32 + 32 + 32) * 4;
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)dec_attn_o_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    attr = true;
+  }
+  DecMfmaArgs a{(bf16*)cache, ld, Hq, Hkv, cos_tab, sin_tab, (bf16*)out, (const int*)st, 0.125f};
+  DecOArgs o{(const bf16*)Wo, ldwo, N, K, X, sync};
+  hipLaunchKernelGGL(dec_attn_o_kernel, dim3(Hkv + (N + 15) / 16), dim3(1024), LDS, s, a, o);
+  SLX_LAUNCH_CHECK("slx_dec_attn_o");
+  return 0;
 }
 
 int dec_attn_mfma_launch(void* cache, long ld, int Hq, int Hkv, const float* cos_tab, const float* sin_tab, void* out,

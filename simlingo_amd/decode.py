@@ -26,6 +26,7 @@ quirk (it only arises for padded batches, never in the bs=1 agent) is not reprod
 from __future__ import annotations
 
 import ctypes
+import os
 
 import numpy as np
 import torch
@@ -33,6 +34,9 @@ import torch
 from . import kernels as K
 
 BF16, F32 = torch.bfloat16, torch.float32
+# attention + O projection as one launch (slx_dec_attn_o) instead of slx_dec_attn + the O GEMV: off by default, it
+# measured 35 us per token SLOWER (tools/fuse_o_ab.sh, profiles/round2_s3_fuse_o_ab.txt); SLX_DEC_FUSE_O=1 turns it on
+FUSE_O = os.environ.get("SLX_DEC_FUSE_O", "0") == "1"
 DEC_STORE_ROW, DEC_RESID, DEC_SWIGLU, DEC_ARGMAX = 0, 1, 2, 3
 
 
@@ -50,6 +54,9 @@ K.register("slx_dec_gemv", [ctypes.POINTER(DecGemvDesc), K.c_vp])
 K.register("slx_dec_attn_nsplit", [K.c_int])
 K.register("slx_dec_attn_ws_floats", [K.c_int, K.c_int, K.c_int])
 K.register("slx_dec_attn", [K.c_vp, K.c_i64, K.c_int, K.c_int, K.c_vp, K.c_vp, K.c_int, K.c_vp, K.c_vp, K.c_vp, K.c_vp])
+K.register("slx_dec_sync_ints", [])
+K.register("slx_dec_attn_o", [K.c_vp, K.c_i64, K.c_int, K.c_int, K.c_vp, K.c_vp, K.c_int, K.c_vp, K.c_vp, K.c_vp, K.c_vp,
+                              K.c_i64, K.c_int, K.c_int, K.c_vp, K.c_vp, K.c_vp])
 
 
 def _gemv_desc(mode, W, N, Kd, *, X=None, gamma=None, eps=0.0, xb=None, bias=None, out=None, out_ld=0, resid=None,
@@ -91,6 +98,9 @@ class GreedyDecoder:
         self.ones_d = torch.ones(d, dtype=F32, device=dev)
         nws = K.lib().slx_dec_attn_ws_floats(cfg.llm_heads, cfg.llm_kv_heads, self.max_len)
         self.attn_ws = torch.zeros(max(nws, 1), dtype=F32, device=dev)
+        # attention + O projection hand-off counters, one 128-B line per layer (slx_dec_attn_o resets them per call)
+        assert K.lib().slx_dec_sync_ints() <= 32
+        self.sync = torch.zeros(cfg.llm_layers, 32, dtype=torch.int32, device=dev)
         self._build_step_descs()
         self.graph = None
         if use_graph:
@@ -156,12 +166,19 @@ class GreedyDecoder:
         self._begin()
         s = K.stream_ptr()
         lib = K.lib()
-        for qkv, cache, o, gu, down in self._steps:
+        for i, (qkv, cache, o, gu, down) in enumerate(self._steps):
             K.check(lib.slx_dec_gemv(ctypes.byref(qkv), s), "slx_dec_gemv")
-            K.check(lib.slx_dec_attn(K.P(cache), cache.stride(0), cfg.llm_heads, cfg.llm_kv_heads, K.P(self.cos),
-                                     K.P(self.sin), self.max_len, K.P(self.attn_ws), K.P(self.obuf), K.P(self.state), s),
-                    "slx_dec_attn")
-            K.check(lib.slx_dec_gemv(ctypes.byref(o), s), "slx_dec_gemv")
+            if FUSE_O:  # attention + O projection (+ residual): one launch for caches of <= 1024 rows
+                wo = self.Wm[i]["o_w"]
+                K.check(lib.slx_dec_attn_o(K.P(cache), cache.stride(0), cfg.llm_heads, cfg.llm_kv_heads, K.P(self.cos),
+                                           K.P(self.sin), self.max_len, K.P(self.attn_ws), K.P(self.obuf),
+                                           K.P(self.state), K.P(wo), wo.stride(0), cfg.llm_dim, self.qn, K.P(self.X),
+                                           K.P(self.sync[i]), s), "slx_dec_attn_o")
+            else:
+                K.check(lib.slx_dec_attn(K.P(cache), cache.stride(0), cfg.llm_heads, cfg.llm_kv_heads, K.P(self.cos),
+                                         K.P(self.sin), self.max_len, K.P(self.attn_ws), K.P(self.obuf),
+                                         K.P(self.state), s), "slx_dec_attn")
+                K.check(lib.slx_dec_gemv(ctypes.byref(o), s), "slx_dec_gemv")
             K.check(lib.slx_dec_gemv(ctypes.byref(gu), s), "slx_dec_gemv")
             K.check(lib.slx_dec_gemv(ctypes.byref(down), s), "slx_dec_gemv")
         K.check(lib.slx_dec_gemv(ctypes.byref(self._head), s), "slx_dec_gemv")
