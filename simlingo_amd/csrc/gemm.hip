@@ -74,6 +74,12 @@ struct GemmArgs {
   long split_stride; // split-K: 0 = f32 atomics into C; > 0 = split y stores its partial to C + y * split_stride
   const uint32_t* maskbits;  // DROPMASK epilogues: keep bits [M][ldbits] (slx_lora_down), else the hash
   long ldbits;
+  // v3 with the M-remainder folded in (rows [rem_r0, M), at most 64): split-K partials + last-arriver epilogue
+  int rem_r0;        // 0 = no folded remainder
+  int rem_nsplit;    // K splits per 256-column group
+  int rem_kc;        // K per split (multiple of 32)
+  float* rem_part;   // [rem_nsplit][M - rem_r0][N] f32 partials
+  int* rem_cnt;      // [ceil(N / 256)] arrival counters, zero on entry, reset by each group's last arriver
 };
 
 // Dropout applied while loading an operand (LoRA dropout, regenerated bit-exactly in backward):
@@ -911,11 +917,126 @@ __device__ __forceinline__ void v3_tile(const GemmArgs& p, int bid, long z, char
   }
 }
 
+// The M remainder (rows [rem_r0, M) past the last whole 256-row tile: InternViT's 16 class-token rows of 16 x 1025,
+// CLIP's 64 of 64 x 577) inside the v3 launch instead of two extra launches. Work unit u (one block, before its tiles)
+// = 256-column group u % ncg x K split u / ncg: 8 waves x 32 columns, 16-row MFMA blocks, operands straight from
+// global (A K-contiguous). The partial is published with agent-scope stores; the group's last arriver sums the splits
+// with agent-scope loads and runs the real epilogue (and the colsum partial row) on those rows, then resets the
+// counter (MI355X_MICROARCH.md inter-workgroup visibility, table row 1). No block ever waits on another.
+template <bool BKc, int EPI, typename OutT>
+__device__ __forceinline__ void v3_remainder(const GemmArgs& p, int u) {
+  __shared__ int last_s;
+  __shared__ float csred[256];
+  const int rem = p.M - p.rem_r0, r0 = p.rem_r0;
+  const int ncg = (p.N + 255) / 256, cg = u % ncg, sp = u / ncg;
+  const int n0 = cg * 256, k0 = sp * p.rem_kc, k1 = min(p.K, k0 + p.rem_kc);
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int nrb = (rem + 15) >> 4;
+  f32x4 acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int k = k0; k < k1; k += 32) {
+    const int kk = k + 8 * (lane >> 4);
+    bf16x8 af[4], bfr[2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = r0 + 16 * i + (lane & 15);
+      bf16x8 z = {};
+      if (i < nrb && m < p.M && kk < k1) z = *reinterpret_cast<const bf16x8*>(p.A + (long)m * p.lda + kk);
+      af[i] = z;
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int n = n0 + 32 * w + 16 * j + (lane & 15);
+      bf16x8 z = {};
+      if (n < p.N && kk < k1) {
+        if (BKc) {
+          z = *reinterpret_cast<const bf16x8*>(p.B + (long)n * p.ldb + kk);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) z[e] = p.B[(long)(kk + e) * p.ldb + n];
+        }
+      }
+      bfr[j] = z;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (i < nrb)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+  }
+  // publish: C layout of 16x16x32 is col = lane & 15, row = 4 (lane >> 4) + r
+  float* part = p.rem_part + (long)sp * rem * p.N;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = 16 * i + 4 * (lane >> 4) + r, n = n0 + 32 * w + 16 * j + (lane & 15);
+        if (m < rem && n < p.N)
+          __hip_atomic_store(part + (long)m * p.N + n, acc[i][j][r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0)
+    last_s = __hip_atomic_fetch_add(p.rem_cnt + cg, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == p.rem_nsplit - 1;
+  __syncthreads();
+  if (!last_s) return;
+  // last arriver: column n0 + (tid & 255), rows tid >> 8, + 2, ...; four rows x up to 16 splits (64 agent-scope loads)
+  // in flight per thread, so the group's epilogue costs a round trip or two, not one per split
+  OutT* C = reinterpret_cast<OutT*>(p.C);
+  const int n = n0 + (tid & 255);
+  float cs = 0.f;
+  if (n < p.N) {
+    const long ss = (long)rem * p.N;
+    for (int mb = tid >> 8; mb < rem; mb += 8) {
+      float v[4][16];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int m = mb + 2 * i;
+#pragma unroll
+        for (int y = 0; y < 16; ++y)
+          v[i][y] = (m < rem && y < p.rem_nsplit)
+                        ? __hip_atomic_load(p.rem_part + y * ss + (long)m * p.N + n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                        : 0.f;
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int m = mb + 2 * i;
+        if (m >= rem) continue;
+        float a8[8];
+#pragma unroll
+        for (int y = 0; y < 8; ++y) a8[y] = v[i][y] + v[i][y + 8];
+        const float a = ((a8[0] + a8[1]) + (a8[2] + a8[3])) + ((a8[4] + a8[5]) + (a8[6] + a8[7]));
+        epilogue_elem<EPI, OutT>(p, C, r0 + m, n, a);
+        if constexpr (EPI == EPI_STORE) cs += a * p.alpha + (p.bias ? p.bias[n] : 0.f);
+        else if constexpr (EPI == EPI_GELU_BWD) cs += a * p.alpha * gelu_erf_grad((float)p.aux[(long)(r0 + m) * p.ldaux + n]);
+        else if constexpr (EPI == EPI_QGELU_BWD) cs += a * p.alpha * qgelu_grad((float)p.aux[(long)(r0 + m) * p.ldaux + n]);
+      }
+    }
+  }
+  if (p.colsum) {  // the colsum partial row of these rows (row r0 / 64 of colsum_ws, as the remainder kernel wrote it)
+    if (tid >= 256) csred[tid - 256] = cs;
+    __syncthreads();
+    if (tid < 256 && n < p.N) p.colsum_ws[(long)(r0 / 64) * p.N + n] = cs + csred[tid];
+  }
+  if (tid == 0) __hip_atomic_store(p.rem_cnt + cg, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // gridDim.x < tiles: a persistent grid, each block walks tiles blockIdx.x, + gridDim.x, ... (gridDim.x a multiple of 8,
 // so a block keeps its XCD's tile range); the epilogue stores of one tile drain while the next tile's loads start.
 template <bool AK, bool BKc, int EPI, typename OutT>
 __global__ __launch_bounds__(512, 1) void gemm_bf16_v3_kernel(GemmArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  if constexpr (AK) {
+    if (p.rem_r0 > 0 && (int)blockIdx.x < p.rem_nsplit * ((p.N + 255) / 256)) {
+      v3_remainder<BKc, EPI, OutT>(p, blockIdx.x);
+      __syncthreads();
+    }
+  }
   const int nwg = p.tilesM * p.tilesN;
   for (int t = blockIdx.x; t < nwg; t += gridDim.x) {
     if (t != (int)blockIdx.x) __syncthreads();  // the previous tile's epilogue is done with the LDS
@@ -945,13 +1066,25 @@ static int launch_v3(GemmArgs a, int batch, hipStream_t st) {
     hipFuncSetAttribute((const void*)gemm_bf16_v3_kernel<AK, BKc, EPI, OutT>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
     attr = true;
   }
-  a.tilesM = (a.M + V3_BM - 1) / V3_BM;
+  a.tilesM = a.rem_r0 > 0 ? a.rem_r0 / V3_BM : (a.M + V3_BM - 1) / V3_BM;  // folded remainder rows are not tiles
   a.tilesN = (a.N + V3_BN - 1) / V3_BN;
   // persistent grid (one round of 256 blocks walking the tiles) by default: +0.3 % on the VLA step
   // (profiles/round2_s3_persist_ab.txt); SLX_GEMM_PERSIST=0 launches one block per tile
   static const int persist = [] { const char* e = getenv("SLX_GEMM_PERSIST"); return e ? atoi(e) : 1; }();
   int gx = a.tilesM * a.tilesN;
   if (persist > 0 && a.ksplit <= 1 && batch == 1 && gx > 256 * persist) gx = 256 * persist;
+  if (a.rem_r0 > 0) {  // the folded remainder's work units (one per block, ahead of its tiles)
+    const int ncg = (a.N + 255) / 256, k32 = (a.K + 31) / 32;
+    int sp = gx / ncg;
+    sp = sp < k32 / 2 ? sp : k32 / 2;  // >= 2 MFMA K-steps per split
+    static const int smax = [] { const char* e = getenv("SLX_GEMM_FOLD_SPLIT"); const int v = e ? atoi(e) : 16;
+                                 return v >= 1 && v <= 16 ? v : 16; }();
+    sp = sp < smax ? sp : smax;  // <= 16 splits: the last arriver sums them with one batch of loads per 4 rows
+    sp = sp < 1 ? 1 : sp;
+    a.rem_kc = ((k32 + sp - 1) / sp) * 32;
+    a.rem_nsplit = (a.K + a.rem_kc - 1) / a.rem_kc;
+    if (a.rem_nsplit * ncg > gx) gx = a.rem_nsplit * ncg;
+  }
   dim3 grid(gx, a.ksplit > 1 ? a.ksplit : 1, batch);
   hipLaunchKernelGGL((gemm_bf16_v3_kernel<AK, BKc, EPI, OutT>), grid, dim3(512), LDS, st, a);
   SLX_LAUNCH_CHECK("slx_gemm_bf16(v3)");
@@ -1119,10 +1252,20 @@ static int colsum_reduce(const slx_gemm_desc* d, hipStream_t st) {
   return 0;
 }
 
+constexpr long kRemCntInts = 4096;  // arrival counters at the end of rem_ws (zeroed once by the caller)
+// SLX_GEMM_FOLD_REM=0: the M remainder as its own split-K launch + epilogue launch (A/B)
+static bool fold_off() {
+  static const bool off = [] { const char* e = getenv("SLX_GEMM_FOLD_REM"); return e && atoi(e) == 0; }();
+  return off;
+}
+
 static int gemm_launch(const slx_gemm_desc* d, int v, hipStream_t st, int mshift_last = 0, int colsum_row0 = 0,
-                       int force_split = 0, long split_stride = 0) {
+                       int force_split = 0, long split_stride = 0, int rem_r0 = 0) {
   GemmArgs a;
   a.split_stride = split_stride;
+  a.rem_r0 = rem_r0; a.rem_nsplit = 0; a.rem_kc = 0;
+  a.rem_part = rem_r0 ? d->rem_ws : nullptr;
+  a.rem_cnt = rem_r0 ? reinterpret_cast<int*>(d->rem_ws + d->rem_ws_floats - kRemCntInts) : nullptr;
   a.A = (const bf16*)d->A; a.B = (const bf16*)d->B; a.C = d->C;
   a.lda = d->lda; a.ldb = d->ldb; a.ldc = d->ldc;
   a.sA = d->sA; a.sB = d->sB; a.sC = d->sC;
@@ -1155,7 +1298,7 @@ static int gemm_launch(const slx_gemm_desc* d, int v, hipStream_t st, int mshift
   a.ksplit = 1;
   a.kchunk = d->K;
   {  // split-K for under-filled grids (weight gradients): f32 atomics, >= 4 K-steps per split
-    int sp = force_split > 0 ? force_split : split_for(d, v, d->M, batch);
+    int sp = rem_r0 ? 1 : force_split > 0 ? force_split : split_for(d, v, d->M, batch);  // (no split-K with a fold)
     const int ksteps = (d->K + BK - 1) / BK;
     if (sp > 1) {
       const int per = ((ksteps + sp - 1) / sp) * BK;
@@ -1233,7 +1376,7 @@ static int gemm_remainder(const slx_gemm_desc* d, int r0, hipStream_t st) {
   const int kchunk = ((ksteps + sp - 1) / sp);
   sp = (ksteps + kchunk - 1) / kchunk;
   const long stride = (long)rem * d->N;
-  if (!d->rem_ws || d->rem_ws_floats < stride * sp) return 1;
+  if (!d->rem_ws || d->rem_ws_floats - kRemCntInts < stride * sp) return 1;
   slx_gemm_desc t = *d;
   t.M = rem;
   t.A = ak ? (const void*)((const bf16*)d->A + (long)r0 * d->lda) : (const void*)((const bf16*)d->A + r0);
@@ -1337,6 +1480,13 @@ extern "C" int slx_gemm_bf16(const slx_gemm_desc* d, slx_stream_t stream) {
     // (a few latency-bound blocks walking all of K on the 4-stage ring). Serial on the caller's stream: running
     // them next to the main grid (side stream) measured slower - v3 holds one 139 KB block per CU and whole rounds
     // of 256 blocks, so any CU taken by a side kernel delays a main block.
+    // A K-contiguous (the activation-row GEMMs that have a remainder): fold the remainder rows into the v3 launch
+    const int ncg = (d->N + 255) / 256;
+    if (ak && !fold_off() && d->rem_ws && d->rem_ws_floats - kRemCntInts >= 16L * rem * d->N && ncg <= kRemCntInts) {
+      const int rc = gemm_launch(d, 7, st, 0, 0, 0, 0, m.M);
+      if (rc) return rc;
+      return d->colsum ? colsum_reduce(d, st) : 0;
+    }
     int rc = gemm_launch(&m, 7, st);
     if (!rc) rc = gemm_remainder(d, m.M, st);
     if (rc == 1) rc = gemm_launch(&t, 4, st, 0, row0);

@@ -162,7 +162,8 @@ def _gemm_desc(A, B, C, M, N, K, layout, lda, ldb, ldc, *, epi=EPI_STORE, alpha=
     sk = (C.device, torch.cuda.current_stream(C.device).cuda_stream)  # one workspace per stream (side-stream GEMMs)
     rw = _rem_ws.get(sk)
     if rw is None:
-        rw = _rem_ws[sk] = torch.empty(REM_WS_FLOATS, dtype=torch.float32, device=C.device)
+        # zeroed once: the last 4096 words are the folded-remainder arrival counters (reset by every GEMM that uses them)
+        rw = _rem_ws[sk] = torch.zeros(REM_WS_FLOATS, dtype=torch.float32, device=C.device)
     d.rem_ws, d.rem_ws_floats = rw.data_ptr(), rw.numel()
     if colsum is not None:
         need = (int(M) + 63) // 64 * int(N)

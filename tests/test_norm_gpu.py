@@ -139,8 +139,10 @@ def test_layernorm_bwd_fused_ls_branch(dev, M):
         torch.testing.assert_close(got.double(), ref_dls, rtol=1e-4, atol=1e-3)
     for got in (db_s, db_f):
         torch.testing.assert_close(got.double(), ref_db, rtol=1e-4, atol=1e-3)
-    torch.testing.assert_close(gm_f, gm_s, rtol=1e-5, atol=1e-4)
-    torch.testing.assert_close(bt_f, bt_s, rtol=1e-5, atol=1e-4)
+    # (column sums over M rows accumulated by f32 atomics in a run-dependent order: the bound scales with M)
+    tol = 1e-4 * M / 3075
+    torch.testing.assert_close(gm_f, gm_s, rtol=1e-5, atol=tol)
+    torch.testing.assert_close(bt_f, bt_s, rtol=1e-5, atol=tol)
 
 
 @pytest.mark.parametrize("rms,fused_ls", [(False, True), (False, False), (True, False)])
