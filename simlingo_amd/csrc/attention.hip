@@ -19,6 +19,8 @@
 // and stores it; then a dK/dV pass (one workgroup = 4 waves = 128 keys of one (b, kv-head), sweeping the GQA group's
 // q-heads x 64-query chunks, S and dP recomputed with the key on the lane so their accumulators feed dV^T/dK^T
 // directly). Summing dQ over key blocks with f32 atomics instead (one kernel) was bound by the ~1.3 TB/s atomic rate.
+#include <cstdlib>
+
 #include "common.h"
 #include "../../include/slx.h"
 
@@ -86,6 +88,7 @@ struct AttnArgs {
   int hsplit, nsplit;            // dK/dV pass: q-heads of a GQA group per workgroup, workgroups per group
   bf16* dq; long lddq;           // dQ pass output: bf16, RoPE^T applied with rcos/rsin (pos = query index) if given
   const float* rcos; const float* rsin;
+  int tail_first;                // non-causal: each XCD's partial last row blocks dispatched first (SLX_ATTN_TAIL_FIRST)
 };
 
 // Stage 64 rows x 64 cols (bf16) of a token-major matrix into a swizzled LDS tile (8 KB).
@@ -122,7 +125,7 @@ constexpr float MASKED = -INFINITY;
 // ones, not a mix that leaves a few heavy blocks running alone at the tail. Every XCD gets the same mix (round-robin
 // dealing); the whole K/V of a 798-token batch (3.3 MB) fits one XCD's L2 anyway.
 struct BlockCoord { int blk, h, b; };
-__device__ __forceinline__ BlockCoord attn_block(int nblk, int Hq, int Hkv, int B, int order = 0) {
+__device__ __forceinline__ BlockCoord attn_block(int nblk, int Hq, int Hkv, int B, int order = 0, int tail_first = 0) {
   const int nwg = nblk * Hq * B;
   int bid = blockIdx.x;
   const int G = Hq / Hkv;
@@ -141,6 +144,13 @@ __device__ __forceinline__ BlockCoord attn_block(int nblk, int Hq, int Hkv, int 
   }
   const int q = nwg >> 3, r = nwg & 7, xcd = bid & 7;
   bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  if (tail_first && r == 0 && q % nblk == 0 && nblk > 1) {
+    // within the XCD's range (whole (b, h) groups): its groups' last, partial row blocks first, then the rest
+    const int base = (bid / q) * q, j = bid - base, npair = q / nblk;
+    const int pair = j < npair ? j : (j - npair) / (nblk - 1);
+    const int blk = j < npair ? nblk - 1 : (j - npair) % (nblk - 1);
+    bid = base + pair * nblk + blk;
+  }
   c.blk = bid % nblk;
   int t = bid / nblk;
   const int hg = t % G;
@@ -222,7 +232,7 @@ __device__ __forceinline__ void fwd_tile(const char* Kl, const char* Vl, const b
 
 __global__ __launch_bounds__(256, ATTN_FWD_OCC) void attn_fwd_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) char smem[2 * 2 * 8192];
-  const BlockCoord bc = attn_block((a.S + 127) / 128, a.Hq, a.Hkv, a.B, a.causal ? 1 : 0);
+  const BlockCoord bc = attn_block((a.S + 127) / 128, a.Hq, a.Hkv, a.B, a.causal ? 1 : 0, a.tail_first);
   const int qb = bc.blk, h = bc.h, b = bc.b;
   const int hk = h / (a.Hq / a.Hkv);
   const int S = a.S;
@@ -387,7 +397,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kv_kernel(AttnArgs a) {
   char* Dc = smem + 2 * 8192;
   float* LD = reinterpret_cast<float*>(Dc + 2 * 8192);  // [buf][lse 64 | delta 64]
 
-  const BlockCoord bc = attn_block((a.S + 127) / 128, a.Hkv * a.nsplit, a.Hkv * a.nsplit, a.B, a.causal ? 2 : 0);
+  const BlockCoord bc = attn_block((a.S + 127) / 128, a.Hkv * a.nsplit, a.Hkv * a.nsplit, a.B, a.causal ? 2 : 0, a.tail_first);
   const int kblk = bc.blk, hk = bc.h / a.nsplit, sp = bc.h % a.nsplit, b = bc.b;
   const int G = a.Hq / a.Hkv;
   const int hg0 = sp * a.hsplit;
@@ -550,7 +560,7 @@ __device__ __forceinline__ void bwd_dq_tile(const char* Kl, const char* Vl, cons
 
 __global__ __launch_bounds__(256, ATTN_DQ_OCC) void attn_bwd_dq_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) char smem[2 * 2 * 8192];
-  const BlockCoord bc = attn_block((a.S + 127) / 128, a.Hq, a.Hkv, a.B, a.causal ? 1 : 0);
+  const BlockCoord bc = attn_block((a.S + 127) / 128, a.Hq, a.Hkv, a.B, a.causal ? 1 : 0, a.tail_first);
   const int qb = bc.blk, h = bc.h, b = bc.b;
   const int hk = h / (a.Hq / a.Hkv);
   const int S = a.S;
@@ -1039,6 +1049,8 @@ static int fill_common(AttnArgs& a, const slx_attn_desc* d) {
   a.ldq = d->ldq; a.ldk = d->ldk; a.ldv = d->ldv; a.ldo = d->ldo;
   a.B = d->B; a.S = d->S; a.Hq = d->Hq; a.Hkv = d->Hkv;
   a.seqlens = d->seqlens; a.causal = d->causal; a.scale = d->scale;
+  static const int tf = [] { const char* e = getenv("SLX_ATTN_TAIL_FIRST"); return e ? atoi(e) : 0; }();
+  a.tail_first = (!d->causal && d->S % 128 != 0) ? tf : 0;
   return 0;
 }
 

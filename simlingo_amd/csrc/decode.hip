@@ -485,6 +485,8 @@ static int gemv_launch(int mode, GemvArgs& a, hipStream_t st) {
   static const int r_env = [] { const char* e = getenv("SLX_DEC_GEMV_R"); return e ? atoi(e) : 0; }();  // tools: A/B
   int R = mode == GV_ARGMAX || mode == GV_STORE_ROW ? 4 : (mode == GV_SWIGLU || a.N >= 4096) ? 2 : 1;
   if (r_env == 1 || r_env == 2 || r_env == 4) R = mode == GV_ARGMAX ? 4 : (mode == GV_SWIGLU ? 2 : r_env);
+  static const int rsw_env = [] { const char* e = getenv("SLX_DEC_GEMV_RSW"); return e ? atoi(e) : 0; }();  // A/B
+  if (mode == GV_SWIGLU && (rsw_env == 1 || rsw_env == 2 || rsw_env == 4)) R = rsw_env;
   const int rows_per_block = 4 * R;
   const int groups = (a.N + rows_per_block - 1) / rows_per_block;
   const dim3 grid(groups < 2048 ? groups : 2048);  // grid-stride over row groups: the norm prologue amortised
@@ -500,7 +502,11 @@ static int gemv_launch(int mode, GemvArgs& a, hipStream_t st) {
       else if (R == 2) gemv_cpl<GV_RESID, 2>(a, grid, lds, st);
       else gemv_cpl<GV_RESID, 1>(a, grid, lds, st);
       break;
-    case GV_SWIGLU: gemv_cpl<GV_SWIGLU, 2>(a, grid, lds, st); break;
+    case GV_SWIGLU:
+      if (R == 4) gemv_cpl<GV_SWIGLU, 4>(a, grid, lds, st);
+      else if (R == 1) gemv_cpl<GV_SWIGLU, 1>(a, grid, lds, st);
+      else gemv_cpl<GV_SWIGLU, 2>(a, grid, lds, st);
+      break;
     case GV_ARGMAX: gemv_cpl<GV_ARGMAX, 4>(a, grid, lds, st); break;
   }
   SLX_LAUNCH_CHECK("slx_dec_gemv");
