@@ -1049,7 +1049,8 @@ static int fill_common(AttnArgs& a, const slx_attn_desc* d) {
   a.ldq = d->ldq; a.ldk = d->ldk; a.ldv = d->ldv; a.ldo = d->ldo;
   a.B = d->B; a.S = d->S; a.Hq = d->Hq; a.Hkv = d->Hkv;
   a.seqlens = d->seqlens; a.causal = d->causal; a.scale = d->scale;
-  static const int tf = [] { const char* e = getenv("SLX_ATTN_TAIL_FIRST"); return e ? atoi(e) : 0; }();
+  // default on: +0.1-0.2 % on the VLA step (profiles/round2_s3_tail_swiglu_ab.txt)
+  static const int tf = [] { const char* e = getenv("SLX_ATTN_TAIL_FIRST"); return e ? atoi(e) : 1; }();
   a.tail_first = (!d->causal && d->S % 128 != 0) ? tf : 0;
   return 0;
 }

@@ -480,10 +480,11 @@ static void gemv_cpl(GemvArgs& a, dim3 grid, size_t lds, hipStream_t st) {
 
 static int gemv_launch(int mode, GemvArgs& a, hipStream_t st) {
   // rows per wave: 4 for the LM head (argmax) and the q|k|v row GEMV (0.5 us faster than 1: a quarter of the
-  // workgroups to dispatch, tools/gemv_ab.sh), 2 for gate|up, else 1 (the 896-row residual GEMVs measured fastest
-  // with more workgroups in flight)
+  // workgroups to dispatch, tools/gemv_ab.sh), else 1: the 896-row residual GEMVs and gate|up (1 gate + 1 up row per
+  // wave: 0.795 vs 0.805 ms/token with 2, profiles/round2_s3_tail_swiglu_ab.txt) measured fastest with more
+  // workgroups in flight
   static const int r_env = [] { const char* e = getenv("SLX_DEC_GEMV_R"); return e ? atoi(e) : 0; }();  // tools: A/B
-  int R = mode == GV_ARGMAX || mode == GV_STORE_ROW ? 4 : (mode == GV_SWIGLU || a.N >= 4096) ? 2 : 1;
+  int R = mode == GV_ARGMAX || mode == GV_STORE_ROW ? 4 : (mode != GV_SWIGLU && a.N >= 4096) ? 2 : 1;
   if (r_env == 1 || r_env == 2 || r_env == 4) R = mode == GV_ARGMAX ? 4 : (mode == GV_SWIGLU ? 2 : r_env);
   static const int rsw_env = [] { const char* e = getenv("SLX_DEC_GEMV_RSW"); return e ? atoi(e) : 0; }();  // A/B
   if (mode == GV_SWIGLU && (rsw_env == 1 || rsw_env == 2 || rsw_env == 4)) R = rsw_env;
