@@ -76,8 +76,10 @@ typedef struct slx_gemm_desc {
   const uint32_t* maskbits; int64_t ldbits; /* DROPMASK epilogues: keep bits [M][ldbits] written by
                        slx_lora_down (bit n&31 of word n>>5); NULL = regenerate from (seed, drop_p, ldmask)  */
   float* rem_ws; int64_t rem_ws_floats; /* optional scratch for the M % 256 remainder rows (<= 64 of them):
-                       split-K f32 partials [splits][rem][N], then one epilogue pass; without it (or if
-                       it is too small) the remainder runs as a latency-bound 16..64-row tile           */
+                       split-K f32 partials [splits][rem][N] summed by the v3 launch itself (A K-contiguous)
+                       or by one epilogue pass; its LAST 4096 words are arrival counters that must be zero
+                       before first use (every call leaves them zero; one workspace per stream). Without it
+                       (or if it is too small) the remainder runs as a latency-bound 16..64-row tile      */
   int resid_bf16;   /* DROPMASK_SWIGLU: resid holds bf16 rows (the bf16 base gradient of a bf16 Linear backward)  */
 } slx_gemm_desc;
 int slx_gemm_bf16(const slx_gemm_desc* d, slx_stream_t stream);
