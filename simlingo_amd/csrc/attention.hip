@@ -1092,9 +1092,12 @@ extern "C" int slx_attn_bwd(const slx_attn_desc* d, const slx_attn_bwd_desc* g, 
   // dQ pass first: it computes delta = rowsum(dO * O) per query in its prologue and stores it for the dK/dV pass
   hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3(nblk * a.Hq * a.B), dim3(256), 0, st, a);
   SLX_LAUNCH_CHECK("slx_attn_bwd(dq)");
-  {  // split a GQA group's q-heads over workgroups until the dK/dV grid fills the chip (~2 per CU)
-    const int G = a.Hq / a.Hkv, base = nblk * a.Hkv * a.B;
-    int ns = (512 + base - 1) / base;
+  {  // split a GQA group's q-heads over workgroups: one q-head per workgroup (Qwen2: 7 x 112 = 784 workgroups; with the
+     // heaviest-first order +0.25 % on the step over the 4-way split that just fills the chip,
+     // profiles/round2_s3_kv_gu_ab.txt); SLX_ATTN_KV_NS overrides (A/B)
+    const int G = a.Hq / a.Hkv;
+    static const int ns_env = [] { const char* e = getenv("SLX_ATTN_KV_NS"); return e ? atoi(e) : 0; }();
+    int ns = ns_env > 0 ? ns_env : G;
     ns = ns < 1 ? 1 : (ns > G ? G : ns);
     if (!f32kv) ns = 1;
     a.hsplit = (G + ns - 1) / ns;
