@@ -34,6 +34,9 @@ from .plan import Plan
 BF16, F32 = torch.bfloat16, torch.float32
 # InternViT weight gradients as paired launches (slx_gemm_bf16_pair); SLX_PAIR_WGRAD=0 runs them one by one (A/B)
 PAIR_WGRAD = os.environ.get("SLX_PAIR_WGRAD", "1") != "0"
+# main loop of the K = 64 LoRA GEMM that carries the SwiGLU backward epilogue (an HBM-bound elementwise pass): v2 128^2
+# tiles, two blocks per CU, +0.1-0.15 % over the cost model's v3 (profiles/round2_s3_swiglu_bwd_ab.txt)
+SWIGLU_BWD_VARIANT = int(os.environ.get("SLX_SWIGLU_BWD_VARIANT", "2"))
 ALIGN = 64  # elements; keeps every parameter view 256-B aligned
 
 
@@ -758,7 +761,7 @@ class VLAEngine(EngineOps):
             K.gemm(dT, self.cat[i]["apad.down"], dgu, M, F, 64, K.GEMM_NN, dT.stride(0), x.shape[1], dgu.stride(0),
                    epi=K.EPI_DROPMASK_SWIGLU, resid=dx, ldr=dx.stride(0), aux=gu, ldaux=gu.stride(0),
                    seed=lora_site_seed(sv["step_seed"], i, LORA_SITES.index("down")), drop_p=drop,
-                   ldmask=x.shape[1], maskbits=bits[0])
+                   ldmask=x.shape[1], maskbits=bits[0], variant=SWIGLU_BWD_VARIANT)
 
 
     # ==========================================================================================
