@@ -55,8 +55,12 @@ def parse():
     ap.add_argument("--n-loss", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
-    ap.add_argument("--wire", default="f32", choices=["f32", "bf16"],
-                    help="gradient all-reduce wire dtype (bf16: half the xGMI bytes, f32 accumulation kept)")
+    ap.add_argument("--wire", default="auto", choices=["auto", "f32", "bf16"],
+                    help="gradient all-reduce wire dtype (bf16: half the xGMI bytes, f32 accumulation kept; "
+                         "auto = bf16 at N > 1, SURVEY.md §8e)")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="skip the config-4 (S_text 512, 128 loss tokens) step and the config-5 agent latency that "
+                         "the N = 1 vla line carries as extra keys")
     return ap.parse_args()
 
 
@@ -127,7 +131,7 @@ def setup_vla(args, dev, world, rank):
     B = args.batch or (8 if full else 4)
     s_text = args.s_text if full else 24
     n_loss = args.n_loss if full else 6
-    eng = VLAEngine(cfg, dev, init_params(cfg, seed=0, lora_b_std=0.02, device=dev), wire=args.wire)
+    eng = VLAEngine(cfg, dev, init_params(cfg, seed=0, lora_b_std=0.02, device=dev), wire=args.wire_eff)
     ex = make_batch(cfg, B=B, s_text=s_text, n_loss=n_loss, seed=1000 + rank)
     plan = plan_from_example(cfg, ex)
     dplan = plan.to_device(dev)
@@ -149,7 +153,14 @@ def setup_vla(args, dev, world, rank):
                     "model": "InternVL2-1B geometry, random init" if full else "tiny", "seq_len": plan.S,
                     "s_text": s_text, "loss_tokens_per_sample": n_loss},
         probe=dict(M=2 * B * cfg.vit_tokens, N=cfg.vit_ffn, K=cfg.vit_dim, kernel="slx gemm_bf16 NT+gelu (InternViT fc1)",
-                   tag="vla_b8") if full else None,
+                   tag="vla_b8",
+                   # the step's dominant kernel: the InternViT fc2.w + fc1.w weight-gradient pair (one launch, TN,
+                   # K = tokens), 2 x 2 x M x N x K FLOP
+                   pair=dict(site="vit.wgrad_fc", flop=2 * 2.0 * (2 * B * cfg.vit_tokens) * cfg.vit_ffn * cfg.vit_dim,
+                             kernel="slx gemm_bf16_pair TN (InternViT fc2.w + fc1.w weight gradients)",
+                             # dY (bf16) + GELU output + dH + LN2 output, f32 dW read + write: per launch
+                             algorithmic_bytes=int((2 * B * cfg.vit_tokens) * 2 * (2 * cfg.vit_dim + 2 * cfg.vit_ffn)
+                                                   + 2 * 2 * 4 * cfg.vit_ffn * cfg.vit_dim))) if full else None,
         cpu=(lambda: cpu_baseline_vla(cfg, s_text, n_loss, args.cpu_threads)) if full else None)
 
 
@@ -186,6 +197,55 @@ def setup_base(args, dev, world, rank):
         cpu=(lambda: cpu_baseline_base(cfg, args.cpu_threads)) if full else None)
 
 
+VLA_C4_GFLOP_PER_SAMPLE = 6185.6  # SURVEY.md §8d config 4 (S_text 512, 128 loss tokens, S_llm 1054)
+
+
+def config4_step(args, dev, steps=5, warmup=2):
+    """BASELINE.json configs[3] on one GPU: the VLA step with mixed action + text loss at S_text = 512 (S_llm = 1054)
+    and 128 LM-loss tokens per sample, B = 8, same protocol as the headline line (fwd + bwd + clip + AdamW)."""
+    from simlingo_amd.config import full_config
+    from simlingo_amd.engine import VLAEngine
+    from simlingo_amd.params import init_params
+    from simlingo_amd.plan import plan_from_example
+    from simlingo_amd.synthetic import make_batch
+    cfg = full_config()
+    B = 8
+    eng = VLAEngine(cfg, dev, init_params(cfg, seed=0, lora_b_std=0.02, device=dev))
+    ex = make_batch(cfg, B=B, s_text=512, n_loss=128, seed=1000)
+    plan = plan_from_example(cfg, ex)
+    dplan = plan.to_device(dev)
+    pix, path, wps = ex.driving_input.camera_images.to(dev), ex.driving_label.path.to(dev), ex.driving_label.waypoints.to(dev)
+
+    def step(i):
+        out4, _, _ = eng.forward(pix, plan, dplan, path, wps, training=True)
+        eng.backward(None)
+        eng.adamw_step(cfg.lr, i + 1, betas=cfg.betas, eps=cfg.eps, weight_decay=cfg.weight_decay, max_norm=cfg.grad_clip)
+        return out4
+    for i in range(warmup):
+        step(i)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        out4 = step(warmup + i)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    v = B * steps / dt
+    del eng
+    return {"workload": "config 4: S_text 512 (S_llm 1054), 128 LM-loss tokens/sample, B=8, 1 GPU", "value": round(v, 3),
+            "unit": "samples/s", "ms_per_step": round(dt / steps * 1e3, 3), "steps": steps, "warmup": warmup,
+            "seq_len": plan.S, "gflop_per_sample": VLA_C4_GFLOP_PER_SAMPLE,
+            "step_mfma_frac": round(v * VLA_C4_GFLOP_PER_SAMPLE / 1e3 / PEAK_BF16_TFLOPS, 4),
+            "loss_last": round(out4[0].item(), 5)}
+
+
+def agent_latency(dev, frames=5, new_tokens=100, s_text=64):
+    """BASELINE.json configs[4]: team_code/agent_simlingo.py:797's DrivingModel.forward at bs = 1 (bench_infer.py's
+    protocol: InternViT + assembly, prefill, KV-cached greedy decode of max_new_tokens, driving forward; median
+    frame of `frames`)."""
+    import bench_infer
+    return bench_infer.measure(dev, frames=frames, warmup=1, new_tokens=new_tokens, s_text=s_text)
+
+
 def traffic_record(tag, flop_M):
     """PMC-measured HBM bytes per FC1 launch (profiles/*_{tag}_fc1_traffic.json, newest first)."""
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", f"*{tag}_fc1_traffic.json")), reverse=True):
@@ -208,6 +268,7 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
+    args.wire_eff = ("bf16" if world > 1 else "f32") if args.wire == "auto" else args.wire
     w = (setup_base if args.config.startswith("base") else setup_vla)(args, dev, world, rank)
     eng, step, B = w["eng"], w["step"], w["B"]
     if world > 1:
@@ -228,8 +289,11 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    eng.probe_site = "vit.fc1" if w["probe"] else None
-    eng.probe_events = []
+    pr = w["probe"]
+    eng.probe_site = ({"vit.fc1"} | ({pr["pair"]["site"]} if pr.get("pair") else set())) if pr else None
+    eng.probe_events = {}
+    if world > 1:
+        eng.bucketer.timing = True  # device-clock exposed-communication tail (ddp.GradBucketer.comm_summary)
     t0 = time.perf_counter()
     for i in range(args.steps):
         out4 = step(args.warmup + i)
@@ -259,20 +323,48 @@ def main():
         res["gflop_per_sample"] = round(gf, 1)
         res["step_mfma_frac"] = round(value * gf / 1e3 / (world * PEAK_BF16_TFLOPS), 4)
         res["step_tflops_per_gpu"] = round(value * gf / 1e3 / world, 1)
-    pr = w["probe"]
-    if pr and eng.probe_events:
-        ms = [a.elapsed_time(b) for a, b in eng.probe_events]
+    if pr and eng.probe_events.get("vit.fc1"):
+        ms = [a.elapsed_time(b) for a, b in eng.probe_events["vit.fc1"]]
         avg_ms = sum(ms) / len(ms)
         flop = 2.0 * pr["M"] * pr["N"] * pr["K"]
         ach = flop / (avg_ms * 1e-3) / 1e12
         rec, src = traffic_record(pr["tag"], pr["M"])
-        res["roofline"] = {"bound": "mfma", "kernel": pr["kernel"], "achieved": round(ach, 1), "peak": PEAK_BF16_TFLOPS,
-                           "unit": "TFLOP/s", "frac": round(ach / PEAK_BF16_TFLOPS, 4),
-                           "traffic": rec["traffic_bytes"] if rec else None,
-                           "flop_per_launch": flop, "avg_launch_ms": round(avg_ms, 4), "launches": len(ms)}
+        fc1 = {"bound": "mfma", "kernel": pr["kernel"], "achieved": round(ach, 1), "peak": PEAK_BF16_TFLOPS,
+               "unit": "TFLOP/s", "frac": round(ach / PEAK_BF16_TFLOPS, 4),
+               "traffic": rec["traffic_bytes"] if rec else None,
+               "flop_per_launch": flop, "avg_launch_ms": round(avg_ms, 4), "launches": len(ms)}
         if rec:
-            res["roofline"]["traffic_source"] = src
-            res["roofline"]["algorithmic_bytes"] = rec.get("algorithmic_bytes")
+            fc1["traffic_source"] = src
+            fc1["algorithmic_bytes"] = rec.get("algorithmic_bytes")
+        res["roofline"] = fc1
+        pp = pr.get("pair")
+        if pp and eng.probe_events.get(pp["site"]):  # the dominant kernel becomes `roofline`, FC1 stays beside it
+            ms = [a.elapsed_time(b) for a, b in eng.probe_events[pp["site"]]]
+            avg_ms = sum(ms) / len(ms)
+            ach = pp["flop"] / (avg_ms * 1e-3) / 1e12
+            prec, psrc = traffic_record(pr["tag"] + "_pair", pr["M"])
+            res["roofline"] = {"bound": "mfma", "kernel": pp["kernel"], "achieved": round(ach, 1),
+                               "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s", "frac": round(ach / PEAK_BF16_TFLOPS, 4),
+                               "traffic": prec["traffic_bytes"] if prec else None, "flop_per_launch": pp["flop"],
+                               "avg_launch_ms": round(avg_ms, 4), "launches": len(ms),
+                               "algorithmic_bytes": pp["algorithmic_bytes"]}
+            if prec:
+                res["roofline"]["traffic_source"] = psrc
+            res["roofline_fc1"] = fc1
+    if world > 1:
+        cs = eng.bucketer.comm_summary()
+        if cs:
+            res["comm_exposed_ms"] = cs.pop("comm_exposed_ms")
+            res["comm"] = cs
+    if rank == 0 and world == 1 and args.config == "vla" and not args.no_extras:
+        try:
+            res["config4"] = config4_step(args, dev)
+        except Exception as e:  # the bench line must still be printed
+            res["config4"] = {"error": repr(e)[:200]}
+        try:
+            res["agent"] = agent_latency(dev)
+        except Exception as e:
+            res["agent"] = {"error": repr(e)[:200]}
     if rank == 0 and world == 1 and w["cpu"] and not args.no_cpu_baseline:
         try:
             res["cpu_baseline"] = w["cpu"]()

@@ -25,13 +25,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--frames", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--new-tokens", type=int, default=100)
-    ap.add_argument("--s-text", type=int, default=64)
-    args = ap.parse_args()
+def measure(dev, frames=5, warmup=1, new_tokens=100, s_text=64) -> dict:
     from simlingo_amd.config import full_config
     from simlingo_amd.decode import GreedyDecoder
     from simlingo_amd.engine import VLAEngine
@@ -39,11 +33,10 @@ def main():
     from simlingo_amd.plan import plan_from_example
     from simlingo_amd.synthetic import make_batch
 
-    dev = torch.device("cuda", 0)
     cfg = full_config()
     eng = VLAEngine(cfg, dev, init_params(cfg, seed=0, lora_b_std=0.02, device=dev))
-    dec = GreedyDecoder(eng, max_len=1024, max_new_tokens=args.new_tokens, eos_id=cfg.eos_id)
-    ex = make_batch(cfg, B=1, s_text=args.s_text, n_loss=1, seed=7)
+    dec = GreedyDecoder(eng, max_len=1024, max_new_tokens=new_tokens, eos_id=cfg.eos_id)
+    ex = make_batch(cfg, B=1, s_text=s_text, n_loss=1, seed=7)
     pix = ex.driving_input.camera_images.to(dev)
     NQ = cfg.n_queries
 
@@ -64,10 +57,10 @@ def main():
         return [ev[0].elapsed_time(ev[1]), ev[1].elapsed_time(ev[2]), ev[2].elapsed_time(ev[3])], len(toks), nv, \
             dict(dec.last_timing)
 
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         frame()
     rows = []
-    for _ in range(args.frames):
+    for _ in range(frames):
         t0 = time.perf_counter()
         ph, n, nv, tm = frame()
         rows.append(((time.perf_counter() - t0) * 1e3, ph, n, tm))
@@ -76,19 +69,30 @@ def main():
     step_ms = tm["decode_ms"] / max(tm["decode_steps"], 1)
     d, F = cfg.llm_dim, cfg.llm_ffn
     w_bytes = cfg.llm_layers * 2 * (dec.nqkv * d + d * dec.qn + 2 * F * d + d * F) + 2 * cfg.vocab * d
-    res = {
+    return {
         "metric": "closed-loop agent latency per frame (DrivingModel.forward, greedy decode)", "value": round(wall, 2),
         "unit": "ms", "higher_is_better": False, "n_gpus": 1, "batch": 1, "dtype": "bf16", "data": "synthetic",
         "config": {"workload": "InternViT-300M x2 tiles + Qwen2-0.5B (LoRA merged) greedy decode + driving forward",
-                   "prompt_tokens": nv, "new_tokens": n, "max_new_tokens": args.new_tokens},
+                   "prompt_tokens": nv, "new_tokens": n, "max_new_tokens": new_tokens},
         "phases_ms": {"encode_vit_assembly": round(ph[0], 2), "prefill": round(tm["prefill_ms"], 2),
                       "decode": round(tm["decode_ms"], 2), "driving_forward": round(ph[2], 2)},
         "decode_ms_per_token": round(step_ms, 4),
         "decode_roofline": {"bound": "hbm", "bytes_per_token": w_bytes,
                             "achieved": round(w_bytes / (step_ms * 1e-3) / 1e9, 1), "peak": 8000.0, "unit": "GB/s",
                             "frac": round(w_bytes / (step_ms * 1e-3) / 8e12, 4)},
-        "frames": args.frames,
+        "frames": frames,
     }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--frames", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--new-tokens", type=int, default=100)
+    ap.add_argument("--s-text", type=int, default=64)
+    args = ap.parse_args()
+    res = measure(torch.device("cuda", 0), frames=args.frames, warmup=args.warmup, new_tokens=args.new_tokens,
+                  s_text=args.s_text)
     print(json.dumps(res), flush=True)
 
 

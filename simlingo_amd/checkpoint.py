@@ -172,6 +172,65 @@ def from_reference(sd, cfg: VLAConfig, strict: bool = True) -> dict:
     return P
 
 
+# ---- weights-only loading of DeepSpeed / Lightning checkpoint files ---------------------------------------------------
+# A real ZeRO-2 checkpoint of the reference (train.py:160-168, DeepSpeed 0.16.2 under Lightning 2.4) pickles more than
+# tensors: the optimizer state holds a LossScaler / DynamicLossScaler instance, a ZeroStageEnum and, per group, an
+# OrderedDict of tensor_fragment.fragment_address records; the model-states file holds ds_config and Lightning's
+# client state (hyper_parameters, possibly omegaconf containers). torch's weights-only unpickler rejects every such
+# global. They are mapped here to INERT stand-ins: a stand-in records its constructor arguments and pickled state and
+# runs nothing (the real class is never imported, no code from the file executes). Only globals under the known
+# DeepSpeed / Lightning / OmegaConf packages get one; any other global keeps the weights-only error, named.
+_STANDIN_PREFIXES = ("deepspeed.", "pytorch_lightning.", "lightning.", "lightning_fabric.", "omegaconf.")
+
+
+class _Inert:
+    """Inert stand-in for a checkpoint object: keeps args / state as data, executes nothing."""
+    _qualname = "?"
+
+    def __init__(self, *args, **kwargs):
+        self._args, self._kwargs = args, kwargs
+
+    def __setstate__(self, state):
+        self._state = state
+
+    def __repr__(self):
+        return f"<inert {self._qualname}>"
+
+
+def _standin(qualname: str):
+    return type(qualname.rsplit(".", 1)[-1], (_Inert,), {"_qualname": qualname, "__module__": __name__})
+
+
+def safe_load(path: str, max_standins: int = 64):
+    """torch.load(path, weights_only=True), with inert stand-ins for the DeepSpeed / Lightning / OmegaConf globals a
+    reference checkpoint contains. Raises pickle.UnpicklingError naming any other unsupported global."""
+    import pickle
+    extra = []
+    for _ in range(max_standins):
+        try:
+            with torch.serialization.safe_globals(extra):
+                return torch.load(path, map_location="cpu", weights_only=True)
+        except pickle.UnpicklingError as e:
+            # a dict / list subclass (e.g. Lightning's AttributeDict) fills itself with SETITEM(S) / APPEND(S), which the
+            # weights-only unpickler allows only on plain containers: stand in with the plain container instead
+            m = re.search(r"Can only (SETITEMS?|APPENDS?) for .* but got <class '[\w.]*\.(\w+)'>", str(e))
+            if m:
+                i = next((j for j, (c, q) in enumerate(extra) if c.__name__ == m.group(2) and issubclass(c, _Inert)), None)
+                if i is None:
+                    raise
+                extra[i] = (dict if m.group(1).startswith("SETITEM") else list, extra[i][1])
+                continue
+            m = re.search(r"GLOBAL ([\w.]+) was not an allowed global", str(e))
+            if not m:
+                raise
+            name = m.group(1)
+            if not name.startswith(_STANDIN_PREFIXES) or any(q == name for _, q in extra):
+                raise pickle.UnpicklingError(f"{path}: unsupported object {name} in a weights-only load (only "
+                                             f"{', '.join(_STANDIN_PREFIXES)} objects get inert stand-ins)") from None
+            extra.append((_standin(name), name))
+    raise pickle.UnpicklingError(f"{path}: more than {max_standins} non-tensor globals")
+
+
 # ---- DeepSpeed ZeRO stage 1/2 directory -> consolidated fp32 state dict -------------------------------------------
 def consolidate_zero(ckpt_dir: str) -> "OrderedDict[str, torch.Tensor]":
     """Restatement of deepspeed 0.16.2 `utils/zero_to_fp32.get_fp32_state_dict_from_zero_checkpoint` for ZeRO stage
@@ -181,7 +240,7 @@ def consolidate_zero(ckpt_dir: str) -> "OrderedDict[str, torch.Tensor]":
     [OrderedDict(name -> shape)] per optimizer group) and one *_optim_states.pt per data-parallel rank
     (optimizer_state_dict.single_partition_of_fp32_groups: that rank's fp32 slice of each flat group). Each group's
     slices are concatenated in rank order and cut into the named parameters in param_shapes order. Every file is
-    read with torch.load(weights_only=True)."""
+    read by safe_load (weights-only, inert stand-ins for the DeepSpeed / Lightning objects the files hold)."""
     tag_dir = ckpt_dir
     latest = os.path.join(ckpt_dir, "latest")
     if os.path.isfile(latest):
@@ -193,7 +252,7 @@ def consolidate_zero(ckpt_dir: str) -> "OrderedDict[str, torch.Tensor]":
     optim_files = sorted(glob.glob(os.path.join(tag_dir, "*_optim_states.pt")), key=_rank)
     if not model_files or not optim_files:
         raise FileNotFoundError(f"{tag_dir}: no mp_rank_00_model_states.pt / *_optim_states.pt (not a ZeRO dir)")
-    ms = torch.load(model_files[0], map_location="cpu", weights_only=True)
+    ms = safe_load(model_files[0])
     out: "OrderedDict[str, torch.Tensor]" = OrderedDict()
     for k, v in (ms.get("module") or {}).items():  # buffers / frozen params saved in the module state
         out[k] = v.float() if torch.is_tensor(v) and v.is_floating_point() else v
@@ -202,8 +261,7 @@ def consolidate_zero(ckpt_dir: str) -> "OrderedDict[str, torch.Tensor]":
     shapes = ms["param_shapes"]
     if isinstance(shapes, dict):
         shapes = [shapes]
-    parts = [torch.load(p, map_location="cpu", weights_only=True)["optimizer_state_dict"]
-             ["single_partition_of_fp32_groups"] for p in optim_files]
+    parts = [safe_load(p)["optimizer_state_dict"]["single_partition_of_fp32_groups"] for p in optim_files]
     for g, group_shapes in enumerate(shapes):
         flat = torch.cat([rank_parts[g].float().reshape(-1) for rank_parts in parts])
         off = 0
@@ -223,4 +281,4 @@ def load_checkpoint(path: str) -> dict:
     if path.endswith(".safetensors"):
         from safetensors.torch import load_file
         return load_file(path)
-    return torch.load(path, map_location="cpu", weights_only=True)
+    return safe_load(path)

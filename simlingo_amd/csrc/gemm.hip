@@ -620,6 +620,179 @@ __device__ __forceinline__ void epilogue_tile64(const GemmArgs& p, OutT* __restr
   }
 }
 
+// ---- prefetching vector epilogue ------------------------------------------------------------------------------
+// The row loop above finishes one row per lane-octet at a time (2 unrolled), so an epilogue that reads global data
+// (the GELU'/SwiGLU' aux, the layer-scale residual, an accumulated C) pays one dependent load round trip per 2 rows:
+// 4 round trips per 64x64 sub-tile while the CU's MFMAs idle. Here every global load of a batch of rows (all 8 rows
+// of the lane, or 4 when a row needs more than 2 x 16 B) is issued first, then the rows are finished. Invalid rows
+// (past M) load a clamped row and are never stored, so the loads need no branch (a branch around each load makes
+// hipcc wait vmcnt(0) per row, cdna_hip_programming.md §5 'Three .s-level traps' (c)).
+template <int EPI, typename OutT> struct EpiLd { static constexpr int N = 0; };
+template <typename OutT> struct EpiLd<EPI_STORE, OutT> { static constexpr int N = sizeof(OutT) == 4 ? 2 : 1; };  // accumulate
+template <typename OutT> struct EpiLd<EPI_RESID_LS, OutT> { static constexpr int N = 2; };
+template <typename OutT> struct EpiLd<EPI_GELU_BWD, OutT> { static constexpr int N = 1; };
+template <typename OutT> struct EpiLd<EPI_QGELU_BWD, OutT> { static constexpr int N = 1; };
+template <typename OutT> struct EpiLd<EPI_SWIGLU_BWD, OutT> { static constexpr int N = 2; };
+
+__device__ __forceinline__ void unpack_bf8(uint4 u, float (&f)[8]) {
+  const bf16x8 x = __builtin_bit_cast(bf16x8, u);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) f[e] = (float)x[e];
+}
+__device__ __forceinline__ void unpack_f8(uint4 a, uint4 b, float (&f)[8]) {
+  f[0] = __uint_as_float(a.x); f[1] = __uint_as_float(a.y); f[2] = __uint_as_float(a.z); f[3] = __uint_as_float(a.w);
+  f[4] = __uint_as_float(b.x); f[5] = __uint_as_float(b.y); f[6] = __uint_as_float(b.z); f[7] = __uint_as_float(b.w);
+}
+
+template <int EPI, typename OutT, int NL>
+__device__ __forceinline__ void epi_issue(const GemmArgs& p, const OutT* C, int m, int n, uint4 (&L)[NL]) {
+  if constexpr (EPI == EPI_STORE) {
+    const uint4* q = reinterpret_cast<const uint4*>(C + (long)m * p.ldc + n);
+    L[0] = q[0];
+    if constexpr (NL == 2) L[1] = q[1];
+  } else if constexpr (EPI == EPI_RESID_LS) {
+    const uint4* q = reinterpret_cast<const uint4*>(p.resid + (long)m * p.ldr + n);
+    L[0] = q[0];
+    L[1] = q[1];
+  } else if constexpr (EPI == EPI_GELU_BWD || EPI == EPI_QGELU_BWD) {
+    L[0] = *reinterpret_cast<const uint4*>(p.aux + (long)m * p.ldaux + n);
+  } else if constexpr (EPI == EPI_SWIGLU_BWD) {
+    L[0] = *reinterpret_cast<const uint4*>(p.aux + (long)m * p.ldaux + n);
+    L[1] = *reinterpret_cast<const uint4*>(p.aux + (long)m * p.ldaux + p.N + n);
+  }
+}
+
+// epilogue_vec8 with the row's global inputs already in L (same arithmetic, same rounding points)
+template <int EPI, typename OutT, int NL, bool LD>
+__device__ __forceinline__ void epi_finish(const GemmArgs& p, OutT* __restrict__ C, int m, int n, float (&v)[8],
+                                           const uint4 (&L)[NL]) {
+  const long ci = (long)m * p.ldc + n;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] *= p.alpha;
+  if constexpr (EPI == EPI_STORE) {
+    if (p.bias) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += p.bias[n + e];
+    }
+    if constexpr (LD) {
+      float c[8];
+      if constexpr (NL == 2) unpack_f8(L[0], L[1], c);
+      else unpack_bf8(L[0], c);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += c[e];
+    }
+    st8(C + ci, v);
+  } else if constexpr (EPI == EPI_GELU || EPI == EPI_QGELU) {
+    float h[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) h[e] = (float)(bf16)(v[e] + (p.bias ? p.bias[n + e] : 0.f));
+    st8(p.aux_out + (long)m * p.ldaux_out + n, h);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) h[e] = EPI == EPI_GELU ? gelu_erf(h[e]) : qgelu(h[e]);
+    st8(C + ci, h);
+  } else if constexpr (EPI == EPI_RESID_LS) {
+    if (p.bias) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += p.bias[n + e];
+    }
+    if (p.aux_out) st8(p.aux_out + (long)m * p.ldaux_out + n, v);
+    float r[8];
+    unpack_f8(L[0], L[1], r);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) r[e] += p.ls[n + e] * v[e];
+    st8(C + ci, r);
+  } else if constexpr (EPI == EPI_GELU_BWD || EPI == EPI_QGELU_BWD) {
+    float h[8];
+    unpack_bf8(L[0], h);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] *= EPI == EPI_GELU_BWD ? gelu_erf_grad(h[e]) : qgelu_grad(h[e]);
+    st8(C + ci, v);
+  } else if constexpr (EPI == EPI_SWIGLU_BWD) {
+    float g[8], u[8], o[8];
+    unpack_bf8(L[0], g);
+    unpack_bf8(L[1], u);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { o[e] = v[e] * u[e] * silu_grad(g[e]); u[e] = v[e] * silu(g[e]); }
+    st8(C + ci, o);
+    st8(C + ci + p.N, u);
+  }
+}
+
+template <int EPI, typename OutT, bool LD>
+__device__ __forceinline__ void epilogue_tile64_pf_impl(const GemmArgs& p, OutT* __restrict__ C, const float* ep, int lane,
+                                                        int m_base, int n_base) {
+  constexpr int NL = LD ? EpiLd<EPI, OutT>::N : 1;
+  constexpr int PF = NL <= 2 ? 8 : 4;
+  const int cc = (lane & 7) * 8;
+  const int n = n_base + cc;
+  float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int b = 0; b < 8; b += PF) {
+    uint4 L[PF][NL];
+    if constexpr (LD) {
+#pragma unroll
+      for (int q = 0; q < PF; ++q) {
+        const int m = m_base + (b + q) * 8 + (lane >> 3);
+        epi_issue<EPI, OutT, NL>(p, C, m < p.M ? m : p.M - 1, n, L[q]);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < PF; ++q) {
+      const int row = (b + q) * 8 + (lane >> 3);
+      const int m = m_base + row;
+      float v[8];
+      const float4 a0 = *reinterpret_cast<const float4*>(ep + row * EP_LD + cc);
+      const float4 a1 = *reinterpret_cast<const float4*>(ep + row * EP_LD + cc + 4);
+      v[0] = a0.x; v[1] = a0.y; v[2] = a0.z; v[3] = a0.w; v[4] = a1.x; v[5] = a1.y; v[6] = a1.z; v[7] = a1.w;
+      if (m < p.M) {
+        epi_finish<EPI, OutT, NL, LD>(p, C, m, n, v, L[q]);
+        if constexpr (EPI == EPI_STORE || EPI == EPI_GELU_BWD || EPI == EPI_QGELU_BWD) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) cs[e] += v[e];
+        }
+      }
+    }
+  }
+  if constexpr (EPI == EPI_STORE || EPI == EPI_GELU_BWD || EPI == EPI_QGELU_BWD) {
+    if (p.colsum) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        cs[e] += __shfl_xor(cs[e], 8, 64);
+        cs[e] += __shfl_xor(cs[e], 16, 64);
+        cs[e] += __shfl_xor(cs[e], 32, 64);
+      }
+      if (lane < 8 && m_base < p.M) {
+        float* w = p.colsum_ws + (long)(p.colsum_row0 + m_base / 64) * p.N + n;
+        *reinterpret_cast<float4*>(w) = make_float4(cs[0], cs[1], cs[2], cs[3]);
+        *reinterpret_cast<float4*>(w + 4) = make_float4(cs[4], cs[5], cs[6], cs[7]);
+      }
+    }
+  }
+}
+
+// The 64x64 sub-tile epilogue with batched global loads where the epilogue kind allows it, else epilogue_tile64.
+template <int EPI, typename OutT>
+__device__ __forceinline__ void epilogue_tile64_pf(const GemmArgs& p, OutT* __restrict__ C, const float* ep, int lane,
+                                                   int m_base, int n_base) {
+  constexpr bool kPf = EPI == EPI_STORE || EPI == EPI_GELU || EPI == EPI_QGELU || EPI == EPI_RESID_LS ||
+                       EPI == EPI_GELU_BWD || EPI == EPI_QGELU_BWD || EPI == EPI_SWIGLU_BWD;
+  if constexpr (kPf) {
+    const bool whole = p.vec_ok && n_base + 64 <= p.N && !(EPI == EPI_STORE && p.ksplit > 1);  // wave-uniform
+    if (whole) {
+      if constexpr (EPI == EPI_GELU || EPI == EPI_QGELU) {
+        epilogue_tile64_pf_impl<EPI, OutT, false>(p, C, ep, lane, m_base, n_base);
+      } else if constexpr (EPI == EPI_STORE) {
+        if (p.accumulate) epilogue_tile64_pf_impl<EPI, OutT, true>(p, C, ep, lane, m_base, n_base);
+        else epilogue_tile64_pf_impl<EPI, OutT, false>(p, C, ep, lane, m_base, n_base);
+      } else {
+        epilogue_tile64_pf_impl<EPI, OutT, true>(p, C, ep, lane, m_base, n_base);
+      }
+      return;
+    }
+  }
+  epilogue_tile64<EPI, OutT>(p, C, ep, lane, m_base, n_base);
+}
+
 template <bool AK, bool BKc, int EPI, typename OutT, int BMv, int NS>
 __global__ __launch_bounds__(BMv * 2, 1) void gemm_bf16_dma_kernel(GemmArgs p) {
   constexpr int NW = BMv / 32;                 // waves: (BM/64) x 2
@@ -780,6 +953,9 @@ __device__ __forceinline__ void v3_read(const char* As, const char* Bs, int arow
   }
 }
 
+// SW: operands swapped (B fragment as the MFMA's A), so each 16x16 accumulator holds C^T: lane l has
+// C[m = l & 15][n = 4 (l >> 4) + r], four consecutive columns of one row (one 16-B LDS store per block).
+template <bool SW>
 __device__ __forceinline__ void v3_mfma(f32x4 (&acc)[8][4], int mh, int nh, const bf16x8 (&af)[4][2],
                                         const bf16x8 (&bfr)[2][2]) {
   __builtin_amdgcn_s_setprio(1);
@@ -788,8 +964,12 @@ __device__ __forceinline__ void v3_mfma(f32x4 (&acc)[8][4], int mh, int nh, cons
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
-        acc[4 * mh + i][2 * nh + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][s], bfr[j][s], acc[4 * mh + i][2 * nh + j], 0, 0, 0);
+      for (int j = 0; j < 2; ++j) {
+        if constexpr (SW)
+          acc[4 * mh + i][2 * nh + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j][s], af[i][s], acc[4 * mh + i][2 * nh + j], 0, 0, 0);
+        else
+          acc[4 * mh + i][2 * nh + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][s], bfr[j][s], acc[4 * mh + i][2 * nh + j], 0, 0, 0);
+      }
   __builtin_amdgcn_s_setprio(0);
 }
 
@@ -800,7 +980,7 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 }
 
 // One 256x256 output tile (tile index bid of p's grid after the XCD remap), K range of split blockIdx.y, batch z.
-template <bool AK, bool BKc, int EPI, typename OutT>
+template <bool AK, bool BKc, int EPI, typename OutT, bool SW>
 __device__ __forceinline__ void v3_tile(const GemmArgs& p, int bid, long z, char* smem) {
   constexpr int NW = 8;
   constexpr int A_BYTES = V3_BM * BK * 2, B_BYTES = V3_BN * BK * 2;
@@ -873,19 +1053,19 @@ __device__ __forceinline__ void v3_tile(const GemmArgs& p, int bid, long z, char
     if (has1) dma_issue_range<BKc, V3_BN, NW, 0, 2>(rb, st1 + A_BYTES, wave, k1, kend, p.ldb, baseB, krB, okB);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     v3_barrier();
-    v3_mfma(acc, 0, 0, alo, blo);
+    v3_mfma<SW>(acc, 0, 0, alo, blo);
     v3_barrier();
     // ---- q1
     v3_read<AK, BKc>(As, Bs, arow + 64, bcol + 32, lane, ahi, bhi);
     if (has1) dma_issue_range<BKc, V3_BN, NW, 2, 2>(rb, st1 + A_BYTES, wave, k1, kend, p.ldb, baseB, krB, okB);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     v3_barrier();
-    v3_mfma(acc, 0, 1, alo, bhi);
+    v3_mfma<SW>(acc, 0, 1, alo, bhi);
     v3_barrier();
     // ---- q2
     if (has2) dma_issue_range<AK, V3_BM, NW, 0, 2>(ra, st2, wave, k2, kend, p.lda, baseA, krA, okA);
     v3_barrier();
-    v3_mfma(acc, 1, 0, ahi, blo);
+    v3_mfma<SW>(acc, 1, 0, ahi, blo);
     v3_barrier();
     // ---- q3
     if (has2) {
@@ -895,7 +1075,7 @@ __device__ __forceinline__ void v3_tile(const GemmArgs& p, int bid, long z, char
       wait_vm<0>();
     }
     v3_barrier();
-    v3_mfma(acc, 1, 1, ahi, bhi);
+    v3_mfma<SW>(acc, 1, 1, ahi, bhi);
     v3_barrier();
   }
   if (wr == 0) v3_barrier();  // re-align the barrier counts of the two wave groups
@@ -905,14 +1085,23 @@ __device__ __forceinline__ void v3_tile(const GemmArgs& p, int bid, long z, char
   float* ep = reinterpret_cast<float*>(smem) + wave * (64 * EP_LD);
 #pragma unroll
   for (int mh = 0; mh < 2; ++mh) {
+    if constexpr (SW) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < 4; ++j)
+          *reinterpret_cast<f32x4*>(ep + (i * 16 + (lane & 15)) * EP_LD + j * 16 + 4 * (lane >> 4)) = acc[4 * mh + i][j];
+    } else {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) ep[(i * 16 + (lane >> 4) * 4 + r) * EP_LD + j * 16 + (lane & 15)] = acc[4 * mh + i][j][r];
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) ep[(i * 16 + (lane >> 4) * 4 + r) * EP_LD + j * 16 + (lane & 15)] = acc[4 * mh + i][j][r];
+    }
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): wave-private region written
-    epilogue_tile64<EPI, OutT>(p, C, ep, lane, m0 + arow + 64 * mh, n0 + bcol);
+    if constexpr (SW) epilogue_tile64_pf<EPI, OutT>(p, C, ep, lane, m0 + arow + 64 * mh, n0 + bcol);
+    else epilogue_tile64<EPI, OutT>(p, C, ep, lane, m0 + arow + 64 * mh, n0 + bcol);
     __builtin_amdgcn_s_waitcnt(0xC07F);
   }
 }
@@ -923,13 +1112,14 @@ __device__ __forceinline__ void v3_tile(const GemmArgs& p, int bid, long z, char
 // global (A K-contiguous). The partial is published with agent-scope stores; the group's last arriver sums the splits
 // with agent-scope loads and runs the real epilogue (and the colsum partial row) on those rows, then resets the
 // counter (MI355X_MICROARCH.md inter-workgroup visibility, table row 1). No block ever waits on another.
-template <bool BKc, int EPI, typename OutT>
+template <bool BKc, int EPI, typename OutT, int NTH = 512>
 __device__ __forceinline__ void v3_remainder(const GemmArgs& p, int u) {
+  constexpr int CG = NTH / 2;  // columns per work unit: 32 per wave
   __shared__ int last_s;
-  __shared__ float csred[256];
+  __shared__ float csred[CG];
   const int rem = p.M - p.rem_r0, r0 = p.rem_r0;
-  const int ncg = (p.N + 255) / 256, cg = u % ncg, sp = u / ncg;
-  const int n0 = cg * 256, k0 = sp * p.rem_kc, k1 = min(p.K, k0 + p.rem_kc);
+  const int ncg = (p.N + CG - 1) / CG, cg = u % ncg, sp = u / ncg;
+  const int n0 = cg * CG, k0 = sp * p.rem_kc, k1 = min(p.K, k0 + p.rem_kc);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int nrb = (rem + 15) >> 4;
   f32x4 acc[4][2];
@@ -985,14 +1175,14 @@ __device__ __forceinline__ void v3_remainder(const GemmArgs& p, int u) {
     last_s = __hip_atomic_fetch_add(p.rem_cnt + cg, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == p.rem_nsplit - 1;
   __syncthreads();
   if (!last_s) return;
-  // last arriver: column n0 + (tid & 255), rows tid >> 8, + 2, ...; four rows x up to 16 splits (64 agent-scope loads)
+  // last arriver: column n0 + (tid % CG), rows tid / CG, + 2, ...; four rows x up to 16 splits (64 agent-scope loads)
   // in flight per thread, so the group's epilogue costs a round trip or two, not one per split
   OutT* C = reinterpret_cast<OutT*>(p.C);
-  const int n = n0 + (tid & 255);
+  const int n = n0 + (tid % CG);
   float cs = 0.f;
   if (n < p.N) {
     const long ss = (long)rem * p.N;
-    for (int mb = tid >> 8; mb < rem; mb += 8) {
+    for (int mb = tid / CG; mb < rem; mb += 8) {
       float v[4][16];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -1019,16 +1209,16 @@ __device__ __forceinline__ void v3_remainder(const GemmArgs& p, int u) {
     }
   }
   if (p.colsum) {  // the colsum partial row of these rows (row r0 / 64 of colsum_ws, as the remainder kernel wrote it)
-    if (tid >= 256) csred[tid - 256] = cs;
+    if (tid >= CG) csred[tid - CG] = cs;
     __syncthreads();
-    if (tid < 256 && n < p.N) p.colsum_ws[(long)(r0 / 64) * p.N + n] = cs + csred[tid];
+    if (tid < CG && n < p.N) p.colsum_ws[(long)(r0 / 64) * p.N + n] = cs + csred[tid];
   }
   if (tid == 0) __hip_atomic_store(p.rem_cnt + cg, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // gridDim.x < tiles: a persistent grid, each block walks tiles blockIdx.x, + gridDim.x, ... (gridDim.x a multiple of 8,
 // so a block keeps its XCD's tile range); the epilogue stores of one tile drain while the next tile's loads start.
-template <bool AK, bool BKc, int EPI, typename OutT>
+template <bool AK, bool BKc, int EPI, typename OutT, bool SW>
 __global__ __launch_bounds__(512, 1) void gemm_bf16_v3_kernel(GemmArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   if constexpr (AK) {
@@ -1040,30 +1230,257 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_v3_kernel(GemmArgs p) {
   const int nwg = p.tilesM * p.tilesN;
   for (int t = blockIdx.x; t < nwg; t += gridDim.x) {
     if (t != (int)blockIdx.x) __syncthreads();  // the previous tile's epilogue is done with the LDS
-    v3_tile<AK, BKc, EPI, OutT>(p, xcd_remap(t, nwg), blockIdx.z, smem);
+    v3_tile<AK, BKc, EPI, OutT, SW>(p, xcd_remap(t, nwg), blockIdx.z, smem);
   }
 }
 
 // Two independent GEMMs of one layout (f32 outputs accumulated, same K and split count) in one launch: grid.x
 // covers both tile sets, so two under-filled weight-gradient grids (InternViT fc2 + fc1, proj + qkv) fill the chip
 // together instead of leaving CUs idle one after the other.
-template <bool AK, bool BKc>
+template <bool AK, bool BKc, bool SW>
 __global__ __launch_bounds__(512, 1) void gemm_bf16_v3_pair_kernel(GemmArgs p, GemmArgs q) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int n1 = p.tilesM * p.tilesN;
   const int bid = xcd_remap(blockIdx.x, n1 + q.tilesM * q.tilesN);
-  if (bid < n1) v3_tile<AK, BKc, EPI_STORE, float>(p, bid, 0, smem);
-  else v3_tile<AK, BKc, EPI_STORE, float>(q, bid - n1, 0, smem);
+  if (bid < n1) v3_tile<AK, BKc, EPI_STORE, float, SW>(p, bid, 0, smem);
+  else v3_tile<AK, BKc, EPI_STORE, float, SW>(q, bid - n1, 0, smem);
 }
 
-template <bool AK, bool BKc, int EPI, typename OutT>
+// ---------------------------------------------------------------------------------------------
+// v4: TWO workgroups per CU, so one workgroup's epilogue (LDS staging, GELU/GELU' VALU, the output stores and the
+// aux / residual loads) runs while the other's MFMAs keep the matrix pipes busy - v3 holds one 256-thread-pair
+// block per CU and serialises every tile's epilogue behind its main loop (gemm_epi_bench: fc1 GELU 204 us vs 134 us
+// for the same main loop with plain stores). Each workgroup's vmcnt only counts its own stores, so a tile's
+// stores no longer hold the next tile's DMA waits of the whole CU.
+//   tile 256 x 128, BK = 32, 4 waves (2 M x 2 N, each 128 x 64 = 8 x 4 v_mfma_f32_16x16x32_bf16 blocks: v3's
+//   per-wave tile and LDS-read-per-MFMA ratio), 3-stage LDS-DMA ring of 24 KiB (72 KiB per workgroup; two fit
+//   the 160 KiB LDS), counted vmcnt, one raw s_barrier per K-step, persistent grid of 2 x 256 blocks.
+//   K-contiguous operands live in LDS as [rows][32] (64-B rows) with the 16-B chunk XOR-swizzled by
+//   h((row >> 2) & 3), h = {0, 2, 3, 1}: ds_read_b128 of a 16 x 32 fragment is conflict-free in every lane group
+//   (enumerated); MN-contiguous operands keep v2/v3's [k][128-column panel] image (8 KiB panels) and tr-reads.
+constexpr int V4_BM = 256, V4_BN = 128, V4_BK = 32, V4_NS = 3;
+constexpr int V4_ABYTES = V4_BM * V4_BK * 2, V4_BBYTES = V4_BN * V4_BK * 2, V4_STAGE = V4_ABYTES + V4_BBYTES;
+
+__device__ __forceinline__ int v4_h(int row) { return (0x78 >> (2 * ((row >> 2) & 3))) & 3; }
+
+// per-lane source offsets (elements) of the LDS-DMA pieces this wave issues for one stage of an operand
+template <bool KC, int ROWS>
+__device__ __forceinline__ void v4_dma_setup(int lane, int wave, int r0, int rows_total, long ld, long (&base)[ROWS / 64],
+                                             int (&kr)[ROWS / 64], bool (&ok)[ROWS / 64]) {
+  constexpr int PER = ROWS * V4_BK * 2 / 1024 / 4;  // = ROWS / 64
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int o = (wave * PER + i) * 1024 + lane * 16;
+    if (KC) {  // [rows][32]: 64-B rows, chunk swizzle h
+      const int row = o >> 6, pc = (o >> 4) & 3;
+      const int c = pc ^ v4_h(row);
+      ok[i] = r0 + row < rows_total;
+      base[i] = (long)(r0 + row) * ld + 8 * c;
+      kr[i] = 0;
+    } else {   // [panel][32 k][128]: 256-B k-rows, v2's (k & 3 | k >> 3 & 1) swizzle
+      const int panel = o >> 13, o2 = o & 8191;
+      const int k = o2 >> 8, pc = (o2 >> 4) & 15;
+      const int x = (k & 3) | (((k >> 3) & 1) << 2);
+      const int c = pc ^ (2 * x);
+      const int col = r0 + panel * 128 + 8 * c;
+      ok[i] = col < rows_total;
+      base[i] = (long)k * ld + col;
+      kr[i] = k;
+    }
+  }
+}
+
+template <bool KC, int ROWS>
+__device__ __forceinline__ void v4_dma_issue(__amdgpu_buffer_rsrc_t rs, char* lds_tile, int wave, int k0, int K, long ld,
+                                             const long (&base)[ROWS / 64], const int (&kr)[ROWS / 64],
+                                             const bool (&ok)[ROWS / 64]) {
+  constexpr int PER = ROWS / 64;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    unsigned off;
+    if (KC) off = ok[i] ? (unsigned)((base[i] + k0) * 2) : kSent;
+    else off = (ok[i] && k0 + kr[i] < K) ? (unsigned)((base[i] + (long)k0 * ld) * 2) : kSent;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(lds_tile + (wave * PER + i) * 1024),
+                                             16, off, 0, 0, 0);
+  }
+}
+
+template <bool KC>
+__device__ __forceinline__ bf16x8 v4_read_frag(const char* lds, int rb, int lane) {
+  if (KC) {
+    const int row = rb + (lane & 15), c = lane >> 4;
+    return *reinterpret_cast<const bf16x8*>(lds + row * 64 + ((c ^ v4_h(row)) << 4));
+  }
+  return read_frag<false>(lds + (rb >> 7) * 8192, rb & 127, 0, lane);
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm_v4() {
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else static_assert(N < 0, "unsupported vmcnt");
+}
+
+// One 256 x 128 output tile of p's grid (tile index after the XCD remap), K split blockIdx.y, batch z.
+template <bool AK, bool BKc, int EPI, typename OutT, bool SW>
+__device__ __forceinline__ void v4_tile(const GemmArgs& p, int bid, long z, char* smem) {
+  const int tilesM = p.tilesM, tilesN = p.tilesN;
+  constexpr int GROUP = 4;
+  const int npg = GROUP * tilesN;
+  const int gid = bid / npg;
+  const int fm = gid * GROUP;
+  const int gs = min(tilesM - fm, GROUP);
+  const int tm = fm + (bid % npg) % gs;
+  const int tn = (bid % npg) / gs;
+  const int m0 = (p.mshift_last && tm == tilesM - 1) ? p.M - V4_BM : tm * V4_BM, n0 = tn * V4_BN;
+  const bf16* A = p.A + z * p.sA;
+  const bf16* B = p.B + z * p.sB;
+  OutT* __restrict__ C = reinterpret_cast<OutT*>(p.C) + z * p.sC;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 1, wc = wave & 1;
+  int kbeg = 0, kend = p.K;
+  if (p.ksplit > 1) {
+    kbeg = blockIdx.y * p.kchunk;
+    kend = min(p.K, kbeg + p.kchunk);
+  }
+  const int nk = (kend - kbeg + V4_BK - 1) / V4_BK;
+  const long extA = AK ? ((long)(p.M - 1) * p.lda + p.K) : ((long)(p.K - 1) * p.lda + p.M);
+  const long extB = BKc ? ((long)(p.N - 1) * p.ldb + p.K) : ((long)(p.K - 1) * p.ldb + p.N);
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)A, (short)0, (int)(extA * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)B, (short)0, (int)(extB * 2), 0x00020000);
+  long baseA[V4_BM / 64], baseB[V4_BN / 64];
+  int krA[V4_BM / 64], krB[V4_BN / 64];
+  bool okA[V4_BM / 64], okB[V4_BN / 64];
+  v4_dma_setup<AK, V4_BM>(lane, wave, m0, p.M, p.lda, baseA, krA, okA);
+  v4_dma_setup<BKc, V4_BN>(lane, wave, n0, p.N, p.ldb, baseB, krB, okB);
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int st = 0; st < V4_NS - 1; ++st) {
+    if (st < nk) {
+      char* sl = smem + st * V4_STAGE;
+      v4_dma_issue<AK, V4_BM>(ra, sl, wave, kbeg + st * V4_BK, kend, p.lda, baseA, krA, okA);
+      v4_dma_issue<BKc, V4_BN>(rb, sl + V4_ABYTES, wave, kbeg + st * V4_BK, kend, p.ldb, baseB, krB, okB);
+    }
+  }
+  const int arow = wr * 128, bcol = wc * 64;
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 1 < nk) wait_vm_v4<6>();  // stage kt landed; stage kt+1 (6 pieces per wave) may stay in flight
+    else wait_vm_v4<0>();
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();  // every wave's stage-kt pieces landed; every wave finished reading stage kt-1
+    __builtin_amdgcn_sched_barrier(0);
+    if (kt + 2 < nk) {
+      char* sl = smem + ((kt + 2) % V4_NS) * V4_STAGE;
+      v4_dma_issue<AK, V4_BM>(ra, sl, wave, kbeg + (kt + 2) * V4_BK, kend, p.lda, baseA, krA, okA);
+      v4_dma_issue<BKc, V4_BN>(rb, sl + V4_ABYTES, wave, kbeg + (kt + 2) * V4_BK, kend, p.ldb, baseB, krB, okB);
+    }
+    const char* As = smem + (kt % V4_NS) * V4_STAGE;
+    const char* Bs = As + V4_ABYTES;
+    bf16x8 af[8], bfr[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bfr[j] = v4_read_frag<BKc>(Bs, bcol + 16 * j, lane);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) af[i] = v4_read_frag<AK>(As, arow + 16 * i, lane);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if constexpr (SW) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+        else acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      }
+    __builtin_amdgcn_s_setprio(0);
+  }
+  // ---- epilogue: two 64x64 passes per wave through a wave-private LDS region (4 x 17 KiB <= the 72 KiB ring)
+  __syncthreads();
+  float* ep = reinterpret_cast<float*>(smem) + wave * (64 * EP_LD);
+#pragma unroll
+  for (int mh = 0; mh < 2; ++mh) {
+    if constexpr (SW) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          *reinterpret_cast<f32x4*>(ep + (i * 16 + (lane & 15)) * EP_LD + j * 16 + 4 * (lane >> 4)) = acc[4 * mh + i][j];
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) ep[(i * 16 + (lane >> 4) * 4 + r) * EP_LD + j * 16 + (lane & 15)] = acc[4 * mh + i][j][r];
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): wave-private region written
+    if constexpr (SW) epilogue_tile64_pf<EPI, OutT>(p, C, ep, lane, m0 + arow + 64 * mh, n0 + bcol);
+    else epilogue_tile64<EPI, OutT>(p, C, ep, lane, m0 + arow + 64 * mh, n0 + bcol);
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+  }
+}
+
+// Persistent: gridDim.x = 2 x 256 (two resident blocks per CU) walking tiles blockIdx.x + k * gridDim.x in the XCD
+// remapped order; the folded M remainder (as v3, 128-column work units) runs first.
+template <bool AK, bool BKc, int EPI, typename OutT, bool SW>
+__global__ __launch_bounds__(256, 2) void gemm_bf16_v4_kernel(GemmArgs p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  if constexpr (AK) {
+    if (p.rem_r0 > 0 && (int)blockIdx.x < p.rem_nsplit * ((p.N + 127) / 128)) {
+      v3_remainder<BKc, EPI, OutT, 256>(p, blockIdx.x);
+      __syncthreads();
+    }
+  }
+  const int nwg = p.tilesM * p.tilesN;
+  for (int t = blockIdx.x; t < nwg; t += gridDim.x) {
+    if (t != (int)blockIdx.x) __syncthreads();  // the previous tile's epilogue is done with the LDS
+    v4_tile<AK, BKc, EPI, OutT, SW>(p, xcd_remap(t, nwg), blockIdx.z, smem);
+  }
+}
+
+template <bool AK, bool BKc, int EPI, typename OutT, bool SW>
+static int launch_v4(GemmArgs a, int batch, hipStream_t st) {
+  constexpr int LDS_RING = V4_NS * V4_STAGE;
+  constexpr int LDS_EP = 4 * 64 * EP_LD * 4;
+  constexpr int LDS = LDS_RING > LDS_EP ? LDS_RING : LDS_EP;
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)gemm_bf16_v4_kernel<AK, BKc, EPI, OutT, SW>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    attr = true;
+  }
+  a.tilesM = a.rem_r0 > 0 ? a.rem_r0 / V4_BM : (a.M + V4_BM - 1) / V4_BM;
+  a.tilesN = (a.N + V4_BN - 1) / V4_BN;
+  static const int persist = [] { const char* e = getenv("SLX_GEMM_V4_PERSIST"); return e ? atoi(e) : 2; }();
+  int gx = a.tilesM * a.tilesN;
+  if (persist > 0 && a.ksplit <= 1 && batch == 1 && gx > 256 * persist) gx = 256 * persist;
+  if (a.rem_r0 > 0) {
+    const int ncg = (a.N + 127) / 128, k32 = (a.K + 31) / 32;
+    int sp = gx / ncg;
+    sp = sp < k32 / 2 ? sp : k32 / 2;
+    sp = sp < 16 ? sp : 16;
+    sp = sp < 1 ? 1 : sp;
+    a.rem_kc = ((k32 + sp - 1) / sp) * 32;
+    a.rem_nsplit = (a.K + a.rem_kc - 1) / a.rem_kc;
+    if (a.rem_nsplit * ncg > gx) gx = a.rem_nsplit * ncg;
+  }
+  dim3 grid(gx, a.ksplit > 1 ? a.ksplit : 1, batch);
+  hipLaunchKernelGGL((gemm_bf16_v4_kernel<AK, BKc, EPI, OutT, SW>), grid, dim3(256), LDS, st, a);
+  SLX_LAUNCH_CHECK("slx_gemm_bf16(v4)");
+  return 0;
+}
+
+template <bool AK, bool BKc, int EPI, typename OutT, bool SW>
 static int launch_v3(GemmArgs a, int batch, hipStream_t st) {
   constexpr int LDS_RING = 2 * (V3_BM * BK * 2 + V3_BN * BK * 2);
   constexpr int LDS_EP = 8 * 64 * EP_LD * 4;
   constexpr int LDS = LDS_RING > LDS_EP ? LDS_RING : LDS_EP;
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute((const void*)gemm_bf16_v3_kernel<AK, BKc, EPI, OutT>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    hipFuncSetAttribute((const void*)gemm_bf16_v3_kernel<AK, BKc, EPI, OutT, SW>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
     attr = true;
   }
   a.tilesM = a.rem_r0 > 0 ? a.rem_r0 / V3_BM : (a.M + V3_BM - 1) / V3_BM;  // folded remainder rows are not tiles
@@ -1086,7 +1503,7 @@ static int launch_v3(GemmArgs a, int batch, hipStream_t st) {
     if (a.rem_nsplit * ncg > gx) gx = a.rem_nsplit * ncg;
   }
   dim3 grid(gx, a.ksplit > 1 ? a.ksplit : 1, batch);
-  hipLaunchKernelGGL((gemm_bf16_v3_kernel<AK, BKc, EPI, OutT>), grid, dim3(512), LDS, st, a);
+  hipLaunchKernelGGL((gemm_bf16_v3_kernel<AK, BKc, EPI, OutT, SW>), grid, dim3(512), LDS, st, a);
   SLX_LAUNCH_CHECK("slx_gemm_bf16(v3)");
   return 0;
 }
@@ -1118,7 +1535,8 @@ static int launch_v2(GemmArgs a, int batch, hipStream_t st) {
 }
 
 // variant: 1 = v1 register-staged 128x128; 2 = DMA 128x128 NS2; 3 = DMA 128x128 NS3; 4 = DMA 128x128 NS4;
-//          5 = DMA 256x128 NS2; 6 = DMA 256x128 NS3; 7 = v3 256x256 ping-pong; 0 = automatic
+//          5 = DMA 256x128 NS2; 6 = DMA 256x128 NS3; 7 = v3 256x256 ping-pong; 8 = v3 with swapped operands
+//          (row-contiguous accumulators, 16-B LDS staging) and the batched-load epilogue; 0 = automatic
 template <bool AK, bool BKc, int EPI, typename OutT>
 static int launch_any(GemmArgs& a, int batch, hipStream_t st, int variant) {
   const bool dma_ok = (!AK || a.K % BK == 0) && (!BKc || a.K % BK == 0) && (a.ksplit <= 1 || a.kchunk % BK == 0) &&
@@ -1131,7 +1549,10 @@ static int launch_any(GemmArgs& a, int batch, hipStream_t st, int variant) {
     case 4: return launch_v2<AK, BKc, EPI, OutT, 128, 4>(a, batch, st);
     case 5: return launch_v2<AK, BKc, EPI, OutT, 256, 2>(a, batch, st);
     case 6: return launch_v2<AK, BKc, EPI, OutT, 256, 3>(a, batch, st);
-    case 7: return launch_v3<AK, BKc, EPI, OutT>(a, batch, st);
+    case 7: return launch_v3<AK, BKc, EPI, OutT, false>(a, batch, st);
+    case 8: return launch_v3<AK, BKc, EPI, OutT, true>(a, batch, st);
+    case 9: return launch_v4<AK, BKc, EPI, OutT, false>(a, batch, st);
+    case 10: return launch_v4<AK, BKc, EPI, OutT, true>(a, batch, st);
     default: return launch<AK, BKc, EPI, OutT>(a, batch, st);
   }
 }
@@ -1294,11 +1715,11 @@ static int gemm_launch(const slx_gemm_desc* d, int v, hipStream_t st, int mshift
     a.vec_ok = ok ? 1 : 0;
   }
   const int batch = d->batch < 1 ? 1 : d->batch;
-  a.mshift_last = v == 7 ? mshift_last : 0;
+  a.mshift_last = (v >= 7 && v <= 10) ? mshift_last : 0;
   a.ksplit = 1;
   a.kchunk = d->K;
   {  // split-K for under-filled grids (weight gradients): f32 atomics, >= 4 K-steps per split
-    int sp = rem_r0 ? 1 : force_split > 0 ? force_split : split_for(d, v, d->M, batch);  // (no split-K with a fold)
+    int sp = rem_r0 ? 1 : force_split > 0 ? force_split : split_for(d, (v >= 7 && v <= 10) ? 7 : v, d->M, batch);  // (no split-K with a fold)
     const int ksteps = (d->K + BK - 1) / BK;
     if (sp > 1) {
       const int per = ((ksteps + sp - 1) / sp) * BK;
@@ -1439,6 +1860,14 @@ extern "C" int slx_gemm_bf16(const slx_gemm_desc* d, slx_stream_t stream) {
   const int batch = d->batch < 1 ? 1 : d->batch;
   const bool dma_ok = (!ak || d->K % BK == 0) && (!bk || d->K % BK == 0) && d->drop_operand == 0;
   int v = d->variant;
+  // The 256-row family shares the remainder handling (fold / overlapped last tile / peel): 7 = v3, 8 = v3 with
+  // swapped operands + batched-load epilogue, 9 / 10 = v4 (two workgroups per CU) without / with the swap.
+  // SLX_V3_KIND picks the member the automatic choice launches (A/B hook).
+  static const int kind_default = [] { const char* e = getenv("SLX_V3_KIND"); const int k = e ? atoi(e) : 7;
+                                       return k >= 7 && k <= 10 ? k : 7; }();
+  int v3k = kind_default;
+  if (v >= 8 && v <= 10) { v3k = v; v = 7; }
+  else if (v == 7) v3k = 7;
   const int rem = d->M % V3_BM;
   const bool peel_ok = batch == 1 && d->epilogue != SLX_EPI_DROPMASK && d->epilogue != SLX_EPI_DROPMASK_SWIGLU &&
                        d->M > V3_BM && rem > 0 && rem <= 64;
@@ -1460,7 +1889,7 @@ extern "C" int slx_gemm_bf16(const slx_gemm_desc* d, slx_stream_t stream) {
   // 64x16 main grid is exactly 4 rounds of 256, the overlap makes it 5 and the step 5% slower than the peel)
   if (v == 7 && dma_ok && overlap_ok &&
       v_cost(d, 7, d->M, batch) < v_cost(d, 7, d->M - rem, batch) + v_cost(d, 2, rem, batch))
-    return gemm_launch(d, 7, st, 1);  // (overlap_ok excludes colsum: shifted rows would be summed twice)
+    return gemm_launch(d, v3k, st, 1);  // (overlap_ok excludes colsum: shifted rows would be summed twice)
   if (v == 7 && dma_ok && peel_ok) {
     // main block rows on v3, the M remainder on v2 (same stream, same epilogue)
     slx_gemm_desc m = *d, t = *d;
@@ -1483,17 +1912,17 @@ extern "C" int slx_gemm_bf16(const slx_gemm_desc* d, slx_stream_t stream) {
     // A K-contiguous (the activation-row GEMMs that have a remainder): fold the remainder rows into the v3 launch
     const int ncg = (d->N + 255) / 256;
     if (ak && !fold_off() && d->rem_ws && d->rem_ws_floats - kRemCntInts >= 16L * rem * d->N && ncg <= kRemCntInts) {
-      const int rc = gemm_launch(d, 7, st, 0, 0, 0, 0, m.M);
+      const int rc = gemm_launch(d, v3k, st, 0, 0, 0, 0, m.M);
       if (rc) return rc;
       return d->colsum ? colsum_reduce(d, st) : 0;
     }
-    int rc = gemm_launch(&m, 7, st);
+    int rc = gemm_launch(&m, v3k, st);
     if (!rc) rc = gemm_remainder(d, m.M, st);
     if (rc == 1) rc = gemm_launch(&t, 4, st, 0, row0);
     if (rc) return rc;
     return d->colsum ? colsum_reduce(d, st) : 0;
   }
-  const int rc = gemm_launch(d, v, st);
+  const int rc = gemm_launch(d, v == 7 ? v3k : v, st);
   if (rc) return rc;
   return d->colsum ? colsum_reduce(d, st) : 0;
 }
@@ -1513,18 +1942,18 @@ static void pair_args(const slx_gemm_desc* d, GemmArgs& a) {
   a.tilesN = (d->N + V3_BN - 1) / V3_BN;
 }
 
-template <bool AK, bool BKc>
+template <bool AK, bool BKc, bool SW>
 static int launch_pair(GemmArgs& a, GemmArgs& b, hipStream_t st) {
   constexpr int LDS_RING = 2 * (V3_BM * BK * 2 + V3_BN * BK * 2);
   constexpr int LDS_EP = 8 * 64 * EP_LD * 4;
   constexpr int LDS = LDS_RING > LDS_EP ? LDS_RING : LDS_EP;
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute((const void*)gemm_bf16_v3_pair_kernel<AK, BKc>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    hipFuncSetAttribute((const void*)gemm_bf16_v3_pair_kernel<AK, BKc, SW>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
     attr = true;
   }
   dim3 grid(a.tilesM * a.tilesN + b.tilesM * b.tilesN, a.ksplit);
-  hipLaunchKernelGGL((gemm_bf16_v3_pair_kernel<AK, BKc>), grid, dim3(512), LDS, st, a, b);
+  hipLaunchKernelGGL((gemm_bf16_v3_pair_kernel<AK, BKc, SW>), grid, dim3(512), LDS, st, a, b);
   SLX_LAUNCH_CHECK("slx_gemm_bf16_pair");
   return 0;
 }
@@ -1557,11 +1986,13 @@ extern "C" int slx_gemm_bf16_pair(const slx_gemm_desc* d1, const slx_gemm_desc* 
   a.ksplit = b.ksplit = sp;
   a.kchunk = b.kchunk = sp > 1 ? per : d1->K;
   hipStream_t st = (hipStream_t)stream;
+  static const bool sw_default = [] { const char* e = getenv("SLX_V3_KIND"); return e && atoi(e) == 8; }();
+  const bool sw = d1->variant == 8 || (d1->variant == 0 && sw_default);
   switch (d1->layout) {
-    case SLX_GEMM_NT: return launch_pair<true, true>(a, b, st);
-    case SLX_GEMM_NN: return launch_pair<true, false>(a, b, st);
-    case SLX_GEMM_TN: return launch_pair<false, false>(a, b, st);
-    case SLX_GEMM_TT: return launch_pair<false, true>(a, b, st);
+    case SLX_GEMM_NT: return sw ? launch_pair<true, true, true>(a, b, st) : launch_pair<true, true, false>(a, b, st);
+    case SLX_GEMM_NN: return sw ? launch_pair<true, false, true>(a, b, st) : launch_pair<true, false, false>(a, b, st);
+    case SLX_GEMM_TN: return sw ? launch_pair<false, false, true>(a, b, st) : launch_pair<false, false, false>(a, b, st);
+    case SLX_GEMM_TT: return sw ? launch_pair<false, true, true>(a, b, st) : launch_pair<false, true, false>(a, b, st);
   }
   set_error("slx_gemm_bf16_pair: bad layout %d", d1->layout);
   return -22;

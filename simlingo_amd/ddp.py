@@ -13,6 +13,12 @@ bytes: 655 MB instead of 1.31 GB for the full model) and cast back into the f32 
 the optimizer still accumulates in f32. trace=True records (event, bucket, perf_counter) tuples - "issue" when a
 bucket's all-reduce is launched, "backward_end" from the engine, "done" when a handle is found complete - the
 evidence that the exchange overlaps the backward (tests/test_ddp_gloo.py).
+
+timing=True (bench.py at N > 1) times the exchange of every step against the backward on the device clock: an event
+on the compute stream at each bucket's issue and at backward_end, a per-bucket completion event recorded on a side
+stream that waits on the bucket's handle, and an event after the optimizer-side wait. comm_summary() turns them into
+the exposed communication tail (wait done - backward end, ms) and per-bucket issue / done times relative to
+backward_end. Host perf_counter stamps stand in on a CPU (gloo) group.
 """
 from __future__ import annotations
 
@@ -34,7 +40,7 @@ class Bucket:
 
 class GradBucketer:
     def __init__(self, flat_grad: torch.Tensor, group_ranges: dict[str, tuple[int, int]], bucket_bytes: int = 32 << 20,
-                 wire: str = "f32", trace: bool = False):
+                 wire: str = "f32", trace: bool = False, timing: bool = False):
         if wire not in ("f32", "bf16"):
             raise ValueError(f"wire must be 'f32' or 'bf16', got {wire!r}")
         self.flat = flat_grad
@@ -42,6 +48,9 @@ class GradBucketer:
         self.wire_buf = None
         self.trace_on = trace
         self.trace: list[tuple[str, int, float]] = []
+        self.timing = timing
+        self.steps: list[dict] = []   # timing records, one per step: {"issue": {b: t}, "done": {b: t}, "bwd_end", "wait"}
+        self._tstream = None
         order = sorted(group_ranges, key=lambda g: group_ranges[g][0])
         self.buckets: list[Bucket] = []
         cur = None
@@ -78,10 +87,59 @@ class GradBucketer:
             bk.handle = dist.all_reduce(src, group=self.pg, async_op=True)
             if self.trace_on:
                 self.trace.append(("issue", self.buckets.index(bk), time.perf_counter()))
+            if self.timing:
+                self._time_bucket(bk)
+
+    # ---- device-clock timing of the exchange (bench.py) ----------------------------------------------------------
+    def _stamp(self, stream=None):
+        if self.flat.is_cuda:
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record(stream)
+            return ev
+        return time.perf_counter()
+
+    def _cur(self) -> dict:
+        if not self.steps or "wait" in self.steps[-1]:
+            self.steps.append({"issue": {}, "done": {}})
+        return self.steps[-1]
+
+    def _time_bucket(self, bk):
+        rec, i = self._cur(), self.buckets.index(bk)
+        rec["issue"][i] = self._stamp()
+        if self.flat.is_cuda:  # completion on the device clock: a side stream waits on the handle, then stamps
+            if self._tstream is None:
+                self._tstream = torch.cuda.Stream(device=self.flat.device)
+            with torch.cuda.stream(self._tstream):
+                bk.handle.wait()
+                rec["done"][i] = self._stamp(self._tstream)
+
+    def comm_summary(self, skip: int = 0) -> dict | None:
+        """Median over the recorded steps (after `skip`) of the exposed communication tail, plus the per-bucket
+        issue / done times (ms, relative to backward_end) of the median step. Synchronises the device."""
+        recs = [r for r in self.steps[skip:] if "bwd_end" in r and "wait" in r]
+        if not recs:
+            return None
+        if self.flat.is_cuda:
+            torch.cuda.synchronize(self.flat.device)
+            rel = lambda a, b: a.elapsed_time(b)  # noqa: E731  (ms from a to b)
+        else:
+            rel = lambda a, b: (b - a) * 1e3  # noqa: E731
+        rows = []
+        for r in recs:
+            e = r["bwd_end"]
+            rows.append((rel(e, r["wait"]), sorted((b, rel(e, r["issue"][b]), rel(e, r["done"][b]) if b in r["done"]
+                                                    else None) for b in r["issue"])))
+        rows.sort(key=lambda x: x[0])
+        exposed, buckets = rows[len(rows) // 2]
+        return {"comm_exposed_ms": round(exposed, 3), "steps": len(rows), "n_buckets": len(self.buckets),
+                "wire": self.wire, "bucket_issue_done_ms": [[b, round(t0, 3), None if t1 is None else round(t1, 3)]
+                                                            for b, t0, t1 in buckets]}
 
     def mark(self, event: str):
         if self.trace_on:
             self.trace.append((event, -1, time.perf_counter()))
+        if self.timing and event == "backward_end" and self.world > 1:
+            self._cur()["bwd_end"] = self._stamp()
 
     def poll(self):
         """Trace which in-flight all-reduces have completed (test instrumentation)."""
@@ -92,14 +150,20 @@ class GradBucketer:
                     self.trace.append(("done", i, time.perf_counter()))
 
     def wait(self):
-        for bk in self.buckets:
+        waited = False
+        for i, bk in enumerate(self.buckets):
             if bk.handle is not None:
                 bk.handle.wait()
+                waited = True
+                if self.timing and not self.flat.is_cuda:
+                    self._cur()["done"][i] = time.perf_counter()
                 bk.handle = None
                 if self.wire == "bf16":  # back into the f32 gradient the optimizer reads
                     self.flat[bk.start:bk.end].copy_(self.wire_buf[bk.start:bk.end])
             bk.done = 0
             bk._seen = False
+        if self.timing and waited and self.steps and "wait" not in self.steps[-1]:
+            self.steps[-1]["wait"] = self._stamp()
 
     def summary(self) -> list[tuple[int, int, int]]:
         """[(start, end, n_groups)] in launch order."""

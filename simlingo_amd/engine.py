@@ -662,7 +662,8 @@ class VLAEngine(EngineOps):
             K.mm(g, self.W[p + "fc2.w"], dh, tb=False, epi=K.EPI_GELU_BWD, aux=Ls["hpre"], ldaux=F_,
                  colsum=self.G[p + "fc1.b"])  # fc1.b grad = column sums of dh, in the same epilogue
             if PAIR_WGRAD:  # fc2.w and fc1.w gradients as one launch (two under-filled grids fill the chip together)
-                K.mm_pair((g, Ls["hact"], self.G[p + "fc2.w"]), (dh, Ls["h2"], self.G[p + "fc1.w"]))
+                with self._probe("vit.wgrad_fc"):
+                    K.mm_pair((g, Ls["hact"], self.G[p + "fc2.w"]), (dh, Ls["h2"], self.G[p + "fc1.w"]))
             else:
                 K.mm(dh, Ls["h2"], self.G[p + "fc1.w"], ta=True, tb=False, accumulate=True)
             dh2 = self._e(Mv, D)  # bf16: the gradient a bf16 Linear backward hands the fp32 LayerNorm under autocast
@@ -684,7 +685,8 @@ class VLAEngine(EngineOps):
                        dbias=self.G[p + "qkv.b"])  # qkv.b grad = column sums of dq | dk | dv, in the same kernels
             del do
             if PAIR_WGRAD:  # proj.w (g still holds ls1 * dx_mid) and qkv.w gradients as one launch
-                K.mm_pair((g, Ls["o"], self.G[p + "proj.w"]), (dqkv, Ls["h1"], self.G[p + "qkv.w"]))
+                with self._probe("vit.wgrad_attn"):
+                    K.mm_pair((g, Ls["o"], self.G[p + "proj.w"]), (dqkv, Ls["h1"], self.G[p + "qkv.w"]))
             else:
                 K.mm(dqkv, Ls["h1"], self.G[p + "qkv.w"], ta=True, tb=False, accumulate=True)
             K.mm(dqkv, self.W[p + "qkv.w"], dh2, tb=False)

@@ -14,21 +14,30 @@ class EngineOps:
     """Mixin: expects self.device, self.bucketer (GradBucketer), self.world, self.P / self.G dicts."""
 
     def _probe(self, site):
-        """Context manager: HIP events around one call site on the current stream (bench.py)."""
+        """Context manager: HIP events around one call site on the current stream (bench.py). `probe_site` is one
+        site name or a set of them; events go to `probe_events` (a list for a single site, else {site: list})."""
         eng = self
+
+        def on():
+            ps = eng.probe_site
+            return ps == site if isinstance(ps, str) else (ps is not None and site in ps)
 
         class _P:
             def __enter__(self):
-                if eng.probe_site == site:
+                self.on = on()
+                if self.on:
                     self.e0 = torch.cuda.Event(enable_timing=True)
                     self.e0.record()
                 return self
 
             def __exit__(self, *a):
-                if eng.probe_site == site:
+                if self.on:
                     e1 = torch.cuda.Event(enable_timing=True)
                     e1.record()
-                    eng.probe_events.append((self.e0, e1))
+                    if isinstance(eng.probe_events, dict):
+                        eng.probe_events.setdefault(site, []).append((self.e0, e1))
+                    else:
+                        eng.probe_events.append((self.e0, e1))
                 return False
         return _P()
 

@@ -552,14 +552,14 @@ def _mm_dims(A, B, C, ta, tb):
     return M, N, Kd, layout
 
 
-def mm_pair(g1, g2, *, ta=True, tb=False, alpha=1.0, ksplit_max=0):
+def mm_pair(g1, g2, *, ta=True, tb=False, alpha=1.0, ksplit_max=0, variant=None):
     """Two accumulating f32 GEMMs C_i += op(A_i) @ op(B_i) (g_i = (A_i, B_i, C_i), same layout and K) in one
     launch (slx_gemm_bf16_pair): the InternViT weight-gradient pairs."""
     ds = []
     for A, B, C in (g1, g2):
         M, N, Kd, layout = _mm_dims(A, B, C, ta, tb)
         ds.append(_gemm_desc(A, B, C, M, N, Kd, layout, A.stride(0), B.stride(0), C.stride(0), alpha=alpha,
-                             accumulate=True, ksplit_max=ksplit_max))
+                             accumulate=True, ksplit_max=ksplit_max, variant=variant))
     check(lib().slx_gemm_bf16_pair(ctypes.byref(ds[0]), ctypes.byref(ds[1]), stream_ptr()), "slx_gemm_bf16_pair")
 
 

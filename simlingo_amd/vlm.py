@@ -87,20 +87,39 @@ class LingoInternVLModel(_Bound):
     def replace_placeholder_tokens(self, adaptor_dict: dict, pixel_values, placeholder_values, wp_encoder=None) -> dict:
         """Writes the vision features, the wp_encoder rows of the <TARGET_POINT> placeholders and the image merge into
         adaptor_dict['language_inputs'] and ['inputs'] in place (internvl2_model.py:44-142) and returns the dict.
-        placeholder_values / wp_encoder are taken from the example the dict was built from (the engine owns the
-        wp_encoder weights)."""
-        model = self.owner
+
+        placeholder_values: the caller's coordinates are used (the reference reads them here, :80-81); when they
+        differ from those of the example the dict was built from, the token plan is rebuilt from the dict's ids and
+        masks with the caller's values. wp_encoder: a caller-supplied module (WaypointInputAdaptor, called on
+        [1, n, 2] in its own dtype as :80-82 does) produces the placeholder rows; None uses the engine's own
+        wp_encoder weights (the DrivingModel's, which is what the reference's forward_model passes)."""
+        import numpy as np
+        from .plan import build_plan
         eng = self.engine
+        cfg = eng.cfg
         plan, dplan = adaptor_dict["_plan"], adaptor_dict["_dplan"]
+        if placeholder_values is not None:
+            p2 = build_plan(cfg, adaptor_dict["language__ids"], adaptor_dict["language_inputs_mask"],
+                            adaptor_dict["language__ids_mask"], placeholder_values, plan.n_img)
+            if not (np.array_equal(p2.wp_coords, plan.wp_coords) and np.array_equal(p2.code, plan.code)):
+                plan, dplan = p2, p2.to_device(eng.device)
+                adaptor_dict["_plan"], adaptor_dict["_dplan"] = plan, dplan
         X = eng.encode_inputs(pixel_values.to(eng.device), plan, dplan, {})  # [B*S, d] f32, permuted layout
-        B, S, L, d = plan.B, plan.S, plan.L, eng.cfg.llm_dim
+        B, S, L, d = plan.B, plan.S, plan.L, cfg.llm_dim
+        nwp = plan.wp_coords.shape[0]
+        if wp_encoder is not None and nwp:
+            w0 = wp_encoder.mlp[0].weight if hasattr(wp_encoder, "mlp") else next(wp_encoder.parameters())
+            coords = torch.from_numpy(plan.wp_coords).to(w0.device, w0.dtype)
+            rows = wp_encoder(coords.unsqueeze(0)).squeeze(0).to(eng.device, F32)
+            pos = torch.from_numpy(plan.wp_pos.astype(np.int64)).to(eng.device)
+            keep = pos < B * S  # rows the permuted layout does not reference stay out (plan.py wp_pos)
+            X[pos[keep]] = rows[keep]
         adaptor_dict["inputs"].copy_(X.view(B, S, d))
         # language positions p >= perm[b, 0] sit at final position p - perm[b, 0] (internvl2_model.py:139-142)
         lang = adaptor_dict["language_inputs"]
         for b in range(B):
             i0 = int(plan.perm[b, 0])
             lang[b, i0:].copy_(X.view(B, S, d)[b, : L - i0])
-        del model
         return adaptor_dict
 
 

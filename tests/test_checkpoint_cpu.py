@@ -7,6 +7,7 @@ remote code is restated there). The ZeRO-2 directory reader follows deepspeed 0.
 """
 import json
 import os
+import sys
 
 import pytest
 import torch
@@ -87,7 +88,55 @@ def test_fusion_layout():
     assert torch.equal(pw.reshape(pw.shape[0], -1), P["vit.patch.w"])
 
 
-def _write_zero2_dir(root, sd, world, group_split):
+def _fake_classes():
+    """Classes pickled under the module paths DeepSpeed 0.16 / Lightning use (the packages are absent here): registered
+    in sys.modules only while the fixture is written, so loading must go through inert stand-ins."""
+    import enum
+    import types
+    made = []
+
+    def mod(name):
+        parts = name.split(".")
+        for i in range(1, len(parts) + 1):
+            n = ".".join(parts[:i])
+            if n not in sys.modules:
+                sys.modules[n] = types.ModuleType(n)
+                made.append(n)
+        return sys.modules[name]
+
+    m = mod("deepspeed.runtime.fp16.loss_scaler")
+
+    class LossScaler:
+        def __init__(self, scale):
+            self.cur_scale, self.cur_iter = scale, 0
+    LossScaler.__module__, m.LossScaler = m.__name__, LossScaler
+    m = mod("deepspeed.runtime.zero.config")
+
+    class ZeroStageEnum(int, enum.Enum):
+        disabled, optimizer_states, gradients = 0, 1, 2
+    ZeroStageEnum.__module__, m.ZeroStageEnum = m.__name__, ZeroStageEnum
+    m = mod("deepspeed.utils.tensor_fragment")
+
+    class fragment_address:  # noqa: N801 (DeepSpeed's name)
+        def __init__(self, numel, start):
+            self.numel, self.start = numel, start
+    fragment_address.__module__, m.fragment_address = m.__name__, fragment_address
+    m = mod("lightning.fabric.utilities.data")
+
+    class AttributeDict(dict):
+        pass
+    AttributeDict.__module__, m.AttributeDict = m.__name__, AttributeDict
+
+    for c in (LossScaler, ZeroStageEnum, fragment_address, AttributeDict):
+        c.__qualname__ = c.__name__  # picklable by module path + name, like the real classes
+
+    def cleanup():
+        for n in made:
+            sys.modules.pop(n, None)
+    return LossScaler, ZeroStageEnum, fragment_address, AttributeDict, cleanup
+
+
+def _write_zero2_dir(root, sd, world, group_split, ds_objects=False):
     """A ZeRO stage-2 checkpoint as DeepSpeed 0.16 lays it out: <root>/latest -> tag; the tag dir holds
     mp_rank_00_model_states.pt (module = non-trainable state, param_shapes = [OrderedDict] per group) and one
     zero_pp_rank_{r}_mp_rank_00_optim_states.pt per rank with that rank's slice of every flat fp32 group."""
@@ -102,8 +151,15 @@ def _write_zero2_dir(root, sd, world, group_split):
     frozen = [k for k in names if k not in trainable]
     groups = [trainable[:group_split], trainable[group_split:]]
     shapes = [OrderedDict((k, torch.Size(sd[k].shape)) for k in g) for g in groups]
-    torch.save({"module": {k: sd[k].clone() for k in frozen}, "param_shapes": shapes},
-               os.path.join(tag, "mp_rank_00_model_states.pt"))
+    LossScaler = ZeroStageEnum = fragment_address = AttributeDict = None
+    cleanup = lambda: None  # noqa: E731
+    if ds_objects:
+        LossScaler, ZeroStageEnum, fragment_address, AttributeDict, cleanup = _fake_classes()
+    ms = {"module": {k: sd[k].clone() for k in frozen}, "param_shapes": shapes}
+    if ds_objects:  # what DeepSpeed + Lightning add next to the tensors
+        ms.update(ds_config={"zero_optimization": {"stage": 2}, "fp16": {"loss_scale": 32}}, ds_version="0.16.2",
+                  hyper_parameters=AttributeDict(lr=3e-5), global_steps=7)
+    torch.save(ms, os.path.join(tag, "mp_rank_00_model_states.pt"))
     flats = []
     for g in groups:
         flat = torch.cat([sd[k].reshape(-1).float() for k in g])
@@ -111,15 +167,24 @@ def _write_zero2_dir(root, sd, world, group_split):
         flats.append(torch.cat([flat, torch.zeros(pad)]))
     for r in range(world):
         parts = [f.chunk(world)[r].clone() for f in flats]
-        torch.save({"optimizer_state_dict": {"single_partition_of_fp32_groups": parts}},
+        osd = {"single_partition_of_fp32_groups": parts}
+        if ds_objects:
+            osd.update(loss_scaler=LossScaler(32.0), dynamic_loss_scale=False, zero_stage=ZeroStageEnum.gradients,
+                       param_slice_mappings=[OrderedDict((k, fragment_address(sd[k].numel(), 0)) for k in g[:3])
+                                             for g in groups], ds_version="0.16.2")
+        torch.save({"optimizer_state_dict": osd, "ds_config": {"train_micro_batch_size_per_gpu": 8}},
                    os.path.join(tag, f"zero_pp_rank_{r}_mp_rank_00_optim_states.pt"))
+    cleanup()
 
 
-@pytest.mark.parametrize("world", [1, 2, 8])
-def test_zero2_directory_consolidation(tmp_path, world):
+@pytest.mark.parametrize("world,ds_objects", [(1, False), (2, True), (8, False), (8, True)])
+def test_zero2_directory_consolidation(tmp_path, world, ds_objects):
+    """ds_objects: the optimizer / model-state files also pickle DeepSpeed's LossScaler, ZeroStageEnum,
+    fragment_address records and Lightning hparams: loaded weights-only through inert stand-ins."""
     cfg, P, _, _ = load_case("nopad")
     sd = to_reference(P, cfg)
-    _write_zero2_dir(str(tmp_path), sd, world, group_split=5)
+    _write_zero2_dir(str(tmp_path), sd, world, group_split=5, ds_objects=ds_objects)
+    assert not any(k.startswith("deepspeed") for k in sys.modules)
     got = consolidate_zero(str(tmp_path))
     back = from_reference(got, cfg)
     assert all(torch.equal(back[k], P[k]) for k in P)
@@ -146,3 +211,29 @@ def test_driving_model_state_dict_surface(tmp_path):
     part = {k: v for k, v in sd.items() if k.startswith("adaptors.driving.")}
     res = m2.load_state_dict(part, strict=False)
     assert len(res.missing_keys) > 0 and res.unexpected_keys == []
+
+
+def test_safe_load_names_unknown_globals(tmp_path):
+    """A global outside the DeepSpeed / Lightning / OmegaConf packages is never stood in for: the weights-only
+    error names it, and a stand-in never runs the original constructor."""
+    import pickle
+    import types
+    from simlingo_amd.checkpoint import safe_load
+    mod = types.ModuleType("evilpkg")
+
+    class Payload:
+        def __init__(self):
+            self.x = 1
+    Payload.__module__, Payload.__qualname__, mod.Payload = "evilpkg", "Payload", Payload
+    sys.modules["evilpkg"] = mod
+    try:
+        torch.save({"p": Payload(), "t": torch.ones(1)}, str(tmp_path / "x.pt"))
+    finally:
+        sys.modules.pop("evilpkg")
+    with pytest.raises(pickle.UnpicklingError, match="evilpkg.Payload"):
+        safe_load(str(tmp_path / "x.pt"))
+    LossScaler, _, _, _, cleanup = _fake_classes()
+    torch.save({"ls": LossScaler(32.0)}, str(tmp_path / "y.pt"))
+    cleanup()
+    got = safe_load(str(tmp_path / "y.pt"))["ls"]
+    assert type(got).__module__ == "simlingo_amd.checkpoint" and got._state == {"cur_scale": 32.0, "cur_iter": 0}

@@ -82,7 +82,7 @@ def _overlap_worker(rank, world, port, n, ranges, wire, ret):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.set_num_threads(1)
     g = torch.arange(n, dtype=torch.float32) * (rank + 1) * 1e-3
-    bk = GradBucketer(g, ranges, bucket_bytes=1 << 16, wire=wire, trace=True)
+    bk = GradBucketer(g, ranges, bucket_bytes=1 << 16, wire=wire, trace=True, timing=True)
     bk.set_distributed(None, world)
     work = torch.randn(192, 192)
     for name in sorted(ranges, key=lambda k: ranges[k][0]):
@@ -93,7 +93,7 @@ def _overlap_worker(rank, world, port, n, ranges, wire, ret):
         bk.group_done(name)
     bk.mark("backward_end")
     bk.wait()
-    ret[rank] = (g.clone(), list(bk.trace), len(bk.buckets))
+    ret[rank] = (g.clone(), list(bk.trace), len(bk.buckets), bk.comm_summary())
     dist.destroy_process_group()
 
 
@@ -108,7 +108,13 @@ def test_allreduce_overlaps_backward_and_bf16_wire(wire):
     mp.spawn(_overlap_worker, args=(2, port, n, ranges, wire, ret), nprocs=2, join=True)
     want = torch.arange(n, dtype=torch.float32) * 3e-3
     for r in range(2):
-        g, trace, nb = ret[r]
+        g, trace, nb, cs = ret[r]
+        # bench.py's comm keys (device clock on GPUs, host clock here): the exposed tail after backward_end and each
+        # bucket's issue / done time relative to it; the first bucket is issued ~nb * 4 ms before the end
+        assert cs["n_buckets"] == nb and cs["wire"] == wire and cs["steps"] == 1
+        assert 0.0 <= cs["comm_exposed_ms"] < 1e3
+        rows = cs["bucket_issue_done_ms"]
+        assert len(rows) == nb and rows[0][1] < -4.0 and all(d is not None and d >= t for _, t, d in rows)
         if wire == "f32":
             torch.testing.assert_close(g, want)
         else:  # bf16 on the wire, f32 in the optimizer: bf16 rounding of the summands and the sum

@@ -90,7 +90,7 @@ def test_gemm_split_k(dev, M, N, Kd, layout, accumulate):
     assert (C - ref).abs().max().item() < 2e-3 * Kd ** 0.5
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7])
+@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10])
 @pytest.mark.parametrize("layout", [K.GEMM_NT, K.GEMM_NN, K.GEMM_TN, K.GEMM_TT])
 def test_gemm_variants(dev, variant, layout):
     """Every main-loop variant (v1 register-staged, v2 LDS-DMA rings) on ragged M/N and K tails."""
@@ -108,7 +108,7 @@ def test_gemm_variants(dev, variant, layout):
         assert (C.float() - ref).abs().max().item() < tol
 
 
-@pytest.mark.parametrize("variant", [1, 2, 7])
+@pytest.mark.parametrize("variant", [1, 2, 7, 8, 9, 10])
 def test_gemm_unaligned_output_and_all_epilogues(dev, variant):
     """Scalar epilogue fallback (C rows not 16-B aligned) and every epilogue through the DMA kernel."""
     M, N, Kd = 200, 128, 256
@@ -133,9 +133,10 @@ def test_gemm_unaligned_output_and_all_epilogues(dev, variant):
     torch.testing.assert_close(dgu[:, N:].float(), uu.grad, atol=5e-2, rtol=2e-2)
 
 
+@pytest.mark.parametrize("variant", [7, 8, 9, 10])
 @pytest.mark.parametrize("Kd", [64, 128, 192, 1024])
 @pytest.mark.parametrize("layout", [K.GEMM_NT, K.GEMM_NN, K.GEMM_TN])
-def test_gemm_v3_pipeline_depths(dev, Kd, layout):
+def test_gemm_v3_pipeline_depths(dev, Kd, layout, variant):
     """v3 (256x256 ping-pong) prologue/steady-state/drain paths: 1, 2, 3 and 16 K-tiles; multi-tile grid with
     ragged edges; split-K (f32 atomics) on the same kernel."""
     M, N = 600, 520
@@ -147,12 +148,12 @@ def test_gemm_v3_pipeline_depths(dev, Kd, layout):
     ref = a.float() @ b.float()
     for ks in (-1, 0):
         C = torch.full((M, N), 3.0, device=dev)
-        K.gemm(A, B, C, M, N, Kd, layout, A.stride(0), B.stride(0), C.stride(0), variant=7, ksplit_max=ks,
+        K.gemm(A, B, C, M, N, Kd, layout, A.stride(0), B.stride(0), C.stride(0), variant=variant, ksplit_max=ks,
                accumulate=True)
         assert (C - 3.0 - ref).abs().max().item() < 2e-3 * Kd ** 0.5
 
 
-@pytest.mark.parametrize("variant", [0, 7])
+@pytest.mark.parametrize("variant", [0, 7, 8, 9, 10])
 def test_gemm_v3_m_tail_peel_epilogues(dev, variant):
     """M = 2*256 + 16: v3 runs the first 512 rows and the 16-row remainder is peeled into a v2 launch with offset
     C/aux/aux_out/resid pointers (InternViT: 16400 = 64*256 + 16). Fused epilogues must agree across the seam."""
@@ -185,7 +186,8 @@ def test_gemm_v3_m_tail_peel_epilogues(dev, variant):
     torch.testing.assert_close(dx.float(), xx.grad, atol=5e-2, rtol=2e-2)
 
 
-def test_gemm_v3_overlapped_last_tile(dev):
+@pytest.mark.parametrize("variant", [7, 8, 9, 10])
+def test_gemm_v3_overlapped_last_tile(dev, variant):
     """Write-once epilogues run the partial last M tile of v3 shifted to end at M (rows shared with the previous
     tile are recomputed): the shared rows must be bit-identical to a launch without a remainder, the tail rows
     correct; an accumulating launch (C += ...) still takes the peel path and must not double-add."""
@@ -194,14 +196,14 @@ def test_gemm_v3_overlapped_last_tile(dev):
     x = torch.randn(M, Kd, device=dev, generator=g).bfloat16()
     w = (torch.randn(N, Kd, device=dev, generator=g) * 0.1).bfloat16()
     full = torch.empty(M, N, device=dev)
-    K.gemm(x, w, full, M, N, Kd, K.GEMM_NT, Kd, Kd, N, variant=7, ksplit_max=-1)
+    K.gemm(x, w, full, M, N, Kd, K.GEMM_NT, Kd, Kd, N, variant=variant, ksplit_max=-1)
     head = torch.empty(512, N, device=dev)
-    K.gemm(x, w, head, 512, N, Kd, K.GEMM_NT, Kd, Kd, N, variant=7, ksplit_max=-1)
+    K.gemm(x, w, head, 512, N, Kd, K.GEMM_NT, Kd, Kd, N, variant=variant, ksplit_max=-1)
     torch.cuda.synchronize()
     assert torch.equal(full[:512], head)
     torch.testing.assert_close(full, x.float() @ w.float().t(), atol=2e-3, rtol=2e-3)
     acc = torch.ones(M, N, device=dev)
-    K.gemm(x, w, acc, M, N, Kd, K.GEMM_NT, Kd, Kd, N, variant=7, ksplit_max=-1, accumulate=True)
+    K.gemm(x, w, acc, M, N, Kd, K.GEMM_NT, Kd, Kd, N, variant=variant, ksplit_max=-1, accumulate=True)
     torch.testing.assert_close(acc, 1.0 + x.float() @ w.float().t(), atol=2e-3, rtol=2e-3)
 
 
@@ -237,9 +239,10 @@ def test_gemm_dropmask_swiglu_epilogue(dev, p, use_bits, resid_bf16):
     torch.testing.assert_close(dgu[:, F:].float(), uu.grad, atol=3e-2, rtol=2e-2)
 
 
+@pytest.mark.parametrize("variant", [0, 8, 9, 10])
 @pytest.mark.parametrize("epi,M", [(K.EPI_GELU_BWD, 16400), (K.EPI_GELU_BWD, 1000), (K.EPI_QGELU_BWD, 2308),
                                    (K.EPI_STORE, 1000)])
-def test_gemm_colsum_bias_grad(dev, epi, M):
+def test_gemm_colsum_bias_grad(dev, epi, M, variant):
     """colsum: the epilogue adds the column sums of its f32 output into a [N] vector (fc1.b's gradient from the
     GELU_BWD dgrad), including the M % 256 remainder that runs on the side stream."""
     N, Kd = 512, 256
@@ -249,7 +252,7 @@ def test_gemm_colsum_bias_grad(dev, epi, M):
     h = torch.randn(M, N, device=dev, generator=g).bfloat16()
     out = torch.empty(M, N, device=dev, dtype=torch.float32 if epi == K.EPI_STORE else torch.bfloat16)
     cs = torch.full((N,), 0.5, device=dev)
-    K.mm(dy, w, out, tb=False, epi=epi, aux=h if epi != K.EPI_STORE else None, ldaux=N, colsum=cs)
+    K.mm(dy, w, out, tb=False, epi=epi, aux=h if epi != K.EPI_STORE else None, ldaux=N, colsum=cs, variant=variant)
     pre = dy.float() @ w.float()
     if epi == K.EPI_GELU_BWD:
         x = h.float()
@@ -287,9 +290,10 @@ def test_batched_splitk_accumulate_tn(dev):
     assert torch.all(flat[out * r:sC] == 0) and torch.all(flat[sC + out * r:] == 0)  # nothing written between
 
 
+@pytest.mark.parametrize("variant", [7, 8])
 @pytest.mark.parametrize("shapes,split", [(((1024, 512), (512, 1024)), 0), (((768, 256), (256, 264)), 3),
                                           (((136, 64), (256, 200)), 1)])
-def test_gemm_pair_wgrad(dev, shapes, split):
+def test_gemm_pair_wgrad(dev, shapes, split, variant):
     """slx_gemm_bf16_pair: two accumulating TN weight-gradient GEMMs (dW_i += dY_i^T X_i) in one launch, each vs
     torch fp32 on the same bf16 operands (M-remainder tiles, split-K on and off)."""
     T = 1040
@@ -301,7 +305,7 @@ def test_gemm_pair_wgrad(dev, shapes, split):
         C = torch.randn(N, Kd, device=dev, generator=g)
         refs.append(C + dy.float().t() @ x.float())
         ops.append((dy, x, C))
-    K.mm_pair(ops[0], ops[1], ksplit_max=split)
+    K.mm_pair(ops[0], ops[1], ksplit_max=split, variant=variant)
     for (_, _, C), ref in zip(ops, refs):
         assert (C - ref).abs().max().item() < 2e-3 * T ** 0.5
     with pytest.raises(RuntimeError, match="one layout and one K"):

@@ -94,3 +94,48 @@ def test_extract_feature_and_greedy_sample(dev):
         if (top2[0] - top2[1]).item() > 0.2 * std:
             assert t == int(lg[i].argmax()), i
     torch.testing.assert_close(embeds[0, n0:].cpu(), Pe["llm.embed"][toks[0].cpu()])
+
+
+def test_replace_placeholder_tokens_honours_caller_values_and_encoder(dev):
+    """internvl2_model.py:53-91 reads the caller's placeholder_values and calls the caller's wp_encoder: other
+    coordinates move exactly the <TARGET_POINT> rows; a torch WaypointInputAdaptor holding the engine's weights
+    reproduces the engine's own rows; every other row of `inputs` is untouched."""
+    from torch import nn
+    cfg, P, ex, _ = load_case("nopad")
+    model = _model(P, cfg)
+    model.build_engine(dev)
+    enc = model.vision_model.image_encoder
+    di = ex.driving_input
+    base = model.adaptors(ex)
+    enc.replace_placeholder_tokens(base, di.camera_images, di.prompt.placeholder_values, None)
+    pv2 = [{k: np.asarray(v, dtype=np.float32) + 1.5 for k, v in d.items()} for d in di.prompt.placeholder_values]
+    moved = model.adaptors(ex)
+    enc.replace_placeholder_tokens(moved, di.camera_images, pv2, None)
+    plan = moved["_plan"]
+    B, S, d = plan.B, plan.S, cfg.llm_dim
+    pos = torch.from_numpy(plan.wp_pos[plan.wp_pos < B * S].astype(np.int64))
+    assert pos.numel() > 0
+    xb, xm = base["inputs"].reshape(B * S, d).cpu(), moved["inputs"].reshape(B * S, d).cpu()
+    other = torch.ones(B * S, dtype=torch.bool)
+    other[pos] = False
+    assert torch.equal(xb[other], xm[other])
+    assert (xb[pos] - xm[pos]).abs().max().item() > 1e-3
+
+    class WaypointInputAdaptor(nn.Module):  # adaptors.py:64-93 layout
+        def __init__(self):
+            super().__init__()
+            self.mlp = nn.Sequential(nn.Linear(2, cfg.wp_hidden), nn.ReLU(True), nn.Linear(cfg.wp_hidden, cfg.wp_hidden2),
+                                     nn.ReLU(True), nn.Linear(cfg.wp_hidden2, d))
+
+        def forward(self, x):
+            return self.mlp(x)
+    wp = WaypointInputAdaptor().to(dev)
+    with torch.no_grad():
+        for i, j in ((0, 0), (1, 2), (2, 4)):
+            wp.mlp[j].weight.copy_(model.engine.P[f"wp.{i}.w"].float())
+            wp.mlp[j].bias.copy_(model.engine.P[f"wp.{i}.b"].float())
+    ext = model.adaptors(ex)
+    enc.replace_placeholder_tokens(ext, di.camera_images, pv2, wp)
+    xe = ext["inputs"].reshape(B * S, d).cpu()
+    assert torch.equal(xe[other], xm[other])
+    torch.testing.assert_close(xe[pos], xm[pos], atol=1e-4, rtol=1e-4)
