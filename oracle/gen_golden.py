@@ -14,7 +14,10 @@ InternVLMultiModalProjector (mlp1) and Qwen2ForCausalLM (eager attention, rope_t
 absent, so LoRA is the 10-line restatement `LoraLinear` below (y = Wx + b + (alpha/r) B A x).
 DrivingModel.forward_model/forward_loss (driving.py:190-261) need hydra/lightning to import, so
 their 20 lines of glue are restated in `reference_forward_loss` with line references.
-Geometry: tiny_config (head_dim 64). Everything fp32 on the CPU.
+Geometry: tiny_config (head_dim 64), plus one full-width case `full1`: the InternVL2-1B widths
+(InternViT 1024 x 16 heads at T = 1025, mlp1 4096 -> 896, Qwen2 896 with GQA 14/2, FFN 4864, V = 151655, LoRA r32)
+with ONE InternViT and ONE Qwen2 layer, B = 2 with left padding, S_text = 256 (S_llm = 798). Its inputs are not
+stored (make_batch is seeded; a checksum of every input is); its gradients as digests. Everything fp32 on the CPU.
 """
 from __future__ import annotations
 
@@ -41,7 +44,7 @@ from transformers import (InternVLConfig, InternVLVisionConfig, InternVLVisionMo
                           Qwen2ForCausalLM)
 from transformers.models.internvl.modeling_internvl import InternVLModel, InternVLMultiModalProjector  # noqa: E402
 
-from simlingo_amd.config import tiny_config  # noqa: E402
+from simlingo_amd.config import full_config, tiny_config  # noqa: E402
 from simlingo_amd.params import init_params, param_specs  # noqa: E402
 from simlingo_amd.synthetic import make_batch  # noqa: E402
 
@@ -210,10 +213,13 @@ def grad_digest(g):
     return out
 
 
-def generate(name, B, s_text, n_loss, pad, seed):
-    cfg = tiny_config()
+FULL1 = dict(vit_layers=1, llm_layers=1, lora_dropout=0.0)  # the full1 case's geometry (full_config overrides)
+
+
+def generate(name, B, s_text, n_loss, pad, seed, full=False):
+    cfg = full_config(**FULL1) if full else tiny_config()
     torch.manual_seed(seed)
-    P = init_params(cfg, seed=seed, lora_b_std=0.05, std=0.05)
+    P = init_params(cfg, seed=seed, lora_b_std=0.02) if full else init_params(cfg, seed=seed, lora_b_std=0.05, std=0.05)
     ex = make_batch(cfg, B=B, s_text=s_text, n_loss=n_loss, seed=seed + 1, pad=pad)
     enc, adaptors, wp_enc, qwen, mods = build_reference(cfg, P)
     out, loss_dict, feats, adict = reference_forward_loss(enc, adaptors, wp_enc, qwen, to_ref_types(ex))
@@ -260,12 +266,21 @@ def generate(name, B, s_text, n_loss, pad, seed):
     missing = [n for n in trainable if n not in G]
     assert not missing, missing
     di = ex.driving_input
+    if full:  # inputs regenerated by make_batch(seed + 1); checksums pin them
+        inputs = {"in.make_batch": np.asarray([B, s_text, n_loss, seed + 1] + list(pad or [0] * B)),
+                  "in.pixel_cs": param_checksum(di.camera_images),
+                  "in.ids_cs": param_checksum(di.prompt.phrase_ids.double()),
+                  "in.tp_coords": np.stack([pv[cfg.target_point_id] for pv in di.prompt.placeholder_values]),
+                  "in.path": ex.driving_label.path.numpy(), "in.waypoints": ex.driving_label.waypoints.numpy()}
+    else:
+        inputs = {"in.pixel": di.camera_images.numpy(), "in.ids": di.prompt.phrase_ids.numpy(),
+                  "in.valid": di.prompt.phrase_valid.numpy(), "in.loss_mask": di.prompt.loss_masking.numpy(),
+                  "in.tp_coords": np.stack([pv[cfg.target_point_id] for pv in di.prompt.placeholder_values]),
+                  "in.path": ex.driving_label.path.numpy(), "in.waypoints": ex.driving_label.waypoints.numpy()}
     arrays = {
-        "cfg": np.frombuffer(json.dumps({"name": "tiny"}).encode(), dtype=np.uint8),
-        "in.pixel": di.camera_images.numpy(), "in.ids": di.prompt.phrase_ids.numpy(),
-        "in.valid": di.prompt.phrase_valid.numpy(), "in.loss_mask": di.prompt.loss_masking.numpy(),
-        "in.tp_coords": np.stack([pv[cfg.target_point_id] for pv in di.prompt.placeholder_values]),
-        "in.path": ex.driving_label.path.numpy(), "in.waypoints": ex.driving_label.waypoints.numpy(),
+        "cfg": np.frombuffer(json.dumps({"name": "full1" if full else "tiny", **(FULL1 if full else {})}).encode(),
+                             dtype=np.uint8),
+        **inputs,
         "out.loss": out.loss.detach().numpy(),
         "out.language_loss": out.loss_averages["language_loss"].detach().numpy(),
         "out.route_loss": out.loss_averages["route_loss"].detach().numpy(),
@@ -284,13 +299,18 @@ def generate(name, B, s_text, n_loss, pad, seed):
         for kk, vv in grad_digest(v.detach()).items():
             arrays[kk + "." + k] = vv
     os.makedirs(OUT, exist_ok=True)
-    path = os.path.join(OUT, f"vla_tiny_{name}.npz")
+    path = os.path.join(OUT, f"vla_{name}.npz" if full else f"vla_tiny_{name}.npz")
     np.savez_compressed(path, **arrays)
     print(f"wrote {path}: loss={out.loss.item():.6f} lang={arrays['out.language_loss']:.6f} "
           f"route={arrays['out.route_loss']:.6f} speed={arrays['out.speed_wps_loss']:.6f}")
 
 
 if __name__ == "__main__":
-    torch.set_num_threads(4)
-    generate("nopad", B=2, s_text=24, n_loss=6, pad=None, seed=11)
-    generate("leftpad", B=3, s_text=24, n_loss=5, pad=[0, 5, 9], seed=23)
+    torch.set_num_threads(8)
+    which = sys.argv[1:] or ["nopad", "leftpad", "full1"]
+    if "nopad" in which:
+        generate("nopad", B=2, s_text=24, n_loss=6, pad=None, seed=11)
+    if "leftpad" in which:
+        generate("leftpad", B=3, s_text=24, n_loss=5, pad=[0, 5, 9], seed=23)
+    if "full1" in which:  # InternVL2-1B widths, 1 + 1 layers, GQA 14/2, V = 151655, left-padded B = 2, S_llm = 798
+        generate("full1", B=2, s_text=256, n_loss=16, pad=[0, 37], seed=31, full=True)

@@ -89,3 +89,44 @@ def test_full_geometry_step(dev, case, record_property):
     assert max(obs["rel_loss"]) <= 1e-2, obs
     assert obs["route_max"] <= 5e-2 and obs["speed_max"] <= 5e-2, obs
     assert not bad, bad
+
+
+def test_engine_vs_reference_full1_fixture(dev):
+    """The bf16 step against the REFERENCE-generated full-width fixture directly (tests/golden/vla_full1.npz,
+    oracle/gen_golden.py: the reference's AdaptorList / replace_placeholder_tokens / summarise_losses on the
+    transformers InternViT / mlp1 / Qwen2 mirrors; 1 + 1 layers, GQA 14/2, V = 151655, left-padded B = 2, S = 798).
+    Same bf16 gates as above: losses rel <= 1e-2, route / speed points <= 5e-2 m; the stored gradient samples of
+    every trainable tensor cosine >= 0.99 against the engine's."""
+    import sys
+    import os
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from golden_util import grad_entries, load_full_case
+    from simlingo_amd.engine import VLAEngine
+    from simlingo_amd.plan import plan_from_example
+    cfg, P, ex, z = load_full_case("full1")
+    eng = VLAEngine(cfg, dev, P)
+    plan = plan_from_example(cfg, ex)
+    lab = ex.driving_label
+    out4, rp, sp = eng.forward(ex.driving_input.camera_images.to(dev), plan, plan.to_device(dev), lab.path.to(dev),
+                               lab.waypoints.to(dev), training=True)
+    eng.backward(None)
+    torch.cuda.synchronize()
+    want = np.asarray([float(z["out.loss"]), float(z["out.language_loss"]), float(z["out.route_loss"]),
+                       float(z["out.speed_wps_loss"])])
+    got = out4.cpu().numpy()
+    assert np.all(np.abs(got - want) <= 1e-2 * np.abs(want)), (got, want)
+    assert np.abs(rp.cpu().numpy() - z["out.route_pred"]).max() <= 5e-2
+    assert np.abs(sp.cpu().numpy() - z["out.speed_pred"]).max() <= 5e-2
+    bad = []
+    for name in eng.G:
+        if "gs." + name not in z:
+            continue
+        idx, ref = grad_entries(z, name)
+        e = eng.G[name].detach().float().cpu().reshape(-1)[torch.from_numpy(np.asarray(idx))]
+        r = torch.from_numpy(np.asarray(ref)).float()
+        if r.norm() < 1e-12:
+            continue
+        cos = torch.nn.functional.cosine_similarity(e, r, dim=0).item()
+        if cos < 0.99:
+            bad.append((name, round(cos, 4)))
+    assert not bad, bad

@@ -310,3 +310,46 @@ def test_gemm_pair_wgrad(dev, shapes, split, variant):
         assert (C - ref).abs().max().item() < 2e-3 * T ** 0.5
     with pytest.raises(RuntimeError, match="one layout and one K"):
         K.mm_pair(ops[0], (ops[1][0][:512], ops[1][1][:512], ops[1][2]))
+
+
+@pytest.mark.parametrize("variant", [7, 8])
+@pytest.mark.parametrize("split", [2])
+def test_gemm_splitk_in_launch_reduction(dev, split, variant):
+    """Split-K f32 weight-gradient GEMMs on the 256x256 kernel reduce their partials inside the launch (the last
+    arriving split of each tile sums the others' slabs in split order): bitwise identical across calls whatever the
+    arrival order, equal to the f32-atomics path within rounding, counters left zero (repeated calls agree), and
+    the same through slx_gemm_bf16_pair."""
+    T, M, N = 4096, 768, 520
+    g = torch.Generator(device=dev).manual_seed(split * 7 + variant)
+    dy = torch.randn(T, M, device=dev, generator=g).bfloat16()
+    x = torch.randn(T, N, device=dev, generator=g).bfloat16()
+    c0 = torch.randn(M, N, device=dev, generator=g)
+    ref = c0 + dy.float().t() @ x.float()
+    outs = []
+    for _ in range(3):
+        C = c0.clone()
+        K.gemm(dy, x, C, M, N, T, K.GEMM_TN, M, N, N, accumulate=True, ksplit_max=split, variant=variant)
+        outs.append(C)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+    assert (outs[0] - ref).abs().max().item() < 2e-3 * T ** 0.5
+    Ca = c0.clone()
+    K.gemm(dy, x, Ca, M, N, T, K.GEMM_TN, M, N, N, accumulate=True, ksplit_max=split, variant=variant, split_ws=False)
+    torch.testing.assert_close(outs[0], Ca, atol=1e-3 * T ** 0.5, rtol=1e-5)
+    # non-accumulating: C is written, not added to (no pre-zeroing needed on the reduction path)
+    Cz = torch.full((M, N), float("nan"), device=dev)
+    K.gemm(dy, x, Cz, M, N, T, K.GEMM_TN, M, N, N, ksplit_max=split, variant=variant)
+    torch.testing.assert_close(Cz, ref - c0, atol=2e-3 * T ** 0.5, rtol=1e-4)
+    # pair launch
+    dy2 = torch.randn(T, 256, device=dev, generator=g).bfloat16()
+    x2 = torch.randn(T, 1024, device=dev, generator=g).bfloat16()
+    p1, p2 = [], []
+    for _ in range(2):
+        C1, C2 = c0.clone(), torch.zeros(256, 1024, device=dev)
+        K.mm_pair((dy, x, C1), (dy2, x2, C2), ksplit_max=split, variant=variant)
+        p1.append(C1)
+        p2.append(C2)
+    torch.cuda.synchronize()
+    assert torch.equal(p1[0], p1[1]) and torch.equal(p2[0], p2[1])
+    assert (p1[0] - ref).abs().max().item() < 2e-3 * T ** 0.5
+    assert (p2[0] - dy2.float().t() @ x2.float()).abs().max().item() < 2e-3 * T ** 0.5

@@ -7,8 +7,11 @@ from golden_util import CASES, grad_entries, load_case
 from oracle import vla_oracle as O
 
 
-@pytest.mark.parametrize("case", CASES)
+@pytest.mark.parametrize("case", CASES + ["full1"])
 def test_oracle_matches_reference_fixture(case):
+    """Tiny cases + `full1`: the InternVL2-1B widths (InternViT 1024/16 heads at T = 1025, GQA 14/2,
+    FFN 4864, the 151,655-way CE, LoRA r32) with one layer of each stack, left-padded B = 2 at S_llm = 798, against
+    the reference's own AdaptorList / replace_placeholder_tokens / summarise_losses on the transformers mirrors."""
     cfg, P, ex, z = load_case(case)
     out, grads = O.loss_and_grads(P, cfg, ex)
     for k in ("loss", "language_loss", "route_loss", "speed_wps_loss"):
