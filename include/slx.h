@@ -81,6 +81,11 @@ typedef struct slx_gemm_desc {
                        before first use (every call leaves them zero; one workspace per stream). Without it
                        (or if it is too small) the remainder runs as a latency-bound 16..64-row tile      */
   int resid_bf16;   /* DROPMASK_SWIGLU: resid holds bf16 rows (the bf16 base gradient of a bf16 Linear backward)  */
+  float* split_ws; int64_t split_ws_floats; /* optional scratch for split-K f32 STORE GEMMs on the 256x256 kernel
+                       (weight gradients, slx_gemm_bf16_pair): [tiles][ksplit][65536] f32 partial slabs summed inside
+                       the launch by each tile's last-arriving split (deterministic split order) instead of f32
+                       atomics into C; its LAST 16384 words are arrival counters that must be zero before first use
+                       (every call leaves them zero; one workspace per stream). NULL = atomics                     */
 } slx_gemm_desc;
 int slx_gemm_bf16(const slx_gemm_desc* d, slx_stream_t stream);
 /* Two independent accumulating f32 STORE GEMMs (same layout and K, no bias / colsum / batch) in one launch:

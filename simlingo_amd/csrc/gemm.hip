@@ -80,6 +80,10 @@ struct GemmArgs {
   int rem_kc;        // K per split (multiple of 32)
   float* rem_part;   // [rem_nsplit][M - rem_r0][N] f32 partials
   int* rem_cnt;      // [ceil(N / 256)] arrival counters, zero on entry, reset by each group's last arriver
+  // v3 split-K reduced inside the launch (f32 STORE): per tile one [ksplit][256*256] f32 slab set + 2 counters
+  float* split_ws;   // null = split-K partials go to C with f32 atomics
+  int* split_cnt;    // [2 * tiles] arrival / published counters, zero on entry, reset by each tile's last arriver
+  int split_tile0;   // tile-index offset of this GEMM in the shared workspace (slx_gemm_bf16_pair's second GEMM)
 };
 
 // Dropout applied while loading an operand (LoRA dropout, regenerated bit-exactly in backward):
@@ -190,11 +194,12 @@ __device__ __forceinline__ bf16x8 read_frag(const char* lds, int rb, int s, int 
 }
 
 template <int EPI, typename OutT>
-__device__ __forceinline__ void epilogue_elem(const GemmArgs& p, OutT* __restrict__ C, int m, int n, float acc) {
+__device__ __forceinline__ void epilogue_elem(const GemmArgs& p, OutT* __restrict__ C, int m, int n, float acc,
+                                              bool reduced = false) {
   float v = acc * p.alpha;
   const long ci = (long)m * p.ldc + n;
   if constexpr (EPI == EPI_STORE) {
-    if (p.ksplit > 1) {  // split-K: every split adds its partial; split 0 adds the bias
+    if (p.ksplit > 1 && !reduced) {  // split-K: every split adds its partial; split 0 adds the bias
       if (p.bias && blockIdx.y == 0) v += p.bias[n];
       atomicAdd(reinterpret_cast<float*>(C) + ci, v);
       return;
@@ -272,12 +277,13 @@ __device__ __forceinline__ void st8(T* p, const float (&v)[8]) {
 }
 
 template <int EPI, typename OutT>
-__device__ __forceinline__ void epilogue_vec8(const GemmArgs& p, OutT* __restrict__ C, int m, int n, float (&v)[8]) {
+__device__ __forceinline__ void epilogue_vec8(const GemmArgs& p, OutT* __restrict__ C, int m, int n, float (&v)[8],
+                                              bool reduced = false) {
   const long ci = (long)m * p.ldc + n;
 #pragma unroll
   for (int e = 0; e < 8; ++e) v[e] *= p.alpha;
   if constexpr (EPI == EPI_STORE) {
-    if (p.ksplit > 1) {
+    if (p.ksplit > 1 && !reduced) {
       if (p.bias && blockIdx.y == 0) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] += p.bias[n + e];
@@ -556,9 +562,9 @@ __device__ __forceinline__ void wait_vm() {
 // LDS-staged epilogue of one 64x64 f32 sub-tile held in `ep` (row stride EP_LD), rows m_base.., cols n_base..
 template <int EPI, typename OutT>
 __device__ __forceinline__ void epilogue_tile64(const GemmArgs& p, OutT* __restrict__ C, const float* ep, int lane,
-                                                int m_base, int n_base) {
+                                                int m_base, int n_base, bool reduced = false) {
   if constexpr (EPI == EPI_STORE) {
-    if (p.ksplit > 1) {  // split-K partials: one 64-float row (256 contiguous bytes) per atomic wave-instruction
+    if (p.ksplit > 1 && !reduced) {  // split-K partials: one 64-float row (256 contiguous bytes) per atomic wave-instruction
       const int n1 = n_base + lane;
       const float bv = (p.bias && blockIdx.y == 0 && n1 < p.N) ? p.bias[n1] : 0.f;
       float* Cf = reinterpret_cast<float*>(C);
@@ -591,7 +597,7 @@ __device__ __forceinline__ void epilogue_tile64(const GemmArgs& p, OutT* __restr
     const float4 a1 = *reinterpret_cast<const float4*>(ep + row * EP_LD + cc + 4);
     v[0] = a0.x; v[1] = a0.y; v[2] = a0.z; v[3] = a0.w; v[4] = a1.x; v[5] = a1.y; v[6] = a1.z; v[7] = a1.w;
     if (vec_ok) {
-      epilogue_vec8<EPI, OutT>(p, C, m, n, v);
+      epilogue_vec8<EPI, OutT>(p, C, m, n, v, reduced);
       if constexpr (EPI == EPI_STORE || EPI == EPI_GELU_BWD || EPI == EPI_QGELU_BWD) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) cs[e] += v[e];
@@ -599,7 +605,7 @@ __device__ __forceinline__ void epilogue_tile64(const GemmArgs& p, OutT* __restr
     } else {
 #pragma unroll
       for (int e = 0; e < 8; ++e)
-        if (n + e < p.N) epilogue_elem<EPI, OutT>(p, C, m, n + e, v[e]);
+        if (n + e < p.N) epilogue_elem<EPI, OutT>(p, C, m, n + e, v[e], reduced);
     }
   }
   if constexpr (EPI == EPI_STORE || EPI == EPI_GELU_BWD || EPI == EPI_QGELU_BWD) {
@@ -773,11 +779,11 @@ __device__ __forceinline__ void epilogue_tile64_pf_impl(const GemmArgs& p, OutT*
 // The 64x64 sub-tile epilogue with batched global loads where the epilogue kind allows it, else epilogue_tile64.
 template <int EPI, typename OutT>
 __device__ __forceinline__ void epilogue_tile64_pf(const GemmArgs& p, OutT* __restrict__ C, const float* ep, int lane,
-                                                   int m_base, int n_base) {
+                                                   int m_base, int n_base, bool reduced = false) {
   constexpr bool kPf = EPI == EPI_STORE || EPI == EPI_GELU || EPI == EPI_QGELU || EPI == EPI_RESID_LS ||
                        EPI == EPI_GELU_BWD || EPI == EPI_QGELU_BWD || EPI == EPI_SWIGLU_BWD;
   if constexpr (kPf) {
-    const bool whole = p.vec_ok && n_base + 64 <= p.N && !(EPI == EPI_STORE && p.ksplit > 1);  // wave-uniform
+    const bool whole = p.vec_ok && n_base + 64 <= p.N && !(EPI == EPI_STORE && p.ksplit > 1 && !reduced);  // wave-uniform
     if (whole) {
       if constexpr (EPI == EPI_GELU || EPI == EPI_QGELU) {
         epilogue_tile64_pf_impl<EPI, OutT, false>(p, C, ep, lane, m_base, n_base);
@@ -790,7 +796,7 @@ __device__ __forceinline__ void epilogue_tile64_pf(const GemmArgs& p, OutT* __re
       return;
     }
   }
-  epilogue_tile64<EPI, OutT>(p, C, ep, lane, m_base, n_base);
+  epilogue_tile64<EPI, OutT>(p, C, ep, lane, m_base, n_base, reduced);
 }
 
 template <bool AK, bool BKc, int EPI, typename OutT, int BMv, int NS>
@@ -979,6 +985,82 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
 }
 
+// In-launch split-K reduction of one v3 tile (f32 STORE, ksplit = S > 1), replacing S x 256 KiB of f32 atomics per
+// tile: with every block of a weight-gradient launch reaching its epilogue together, the atomics ran as one burst at
+// the ~1.3 TB/s chip-wide atomic rate (MI355X_MICROARCH.md 'Global float atomics': ~52 us per InternViT fc pair).
+// Arrive-first protocol (cdna_hip_programming.md §5 'In-launch split-K reduction', Guideline 16): a block first
+// takes an arrival ticket; the first S - 1 arrivals store their partial as a slab (plain 16-B stores in register
+// order: one KiB per wave-instruction), then release (agent fence) and bump the tile's published counter; the LAST
+// arrival waits on that counter - only for blocks that have already arrived, so the wait cannot deadlock whatever
+// the residency - acquires (agent fence), adds the slabs to its own accumulators in split order (bit-identical
+// for any arrival order) and runs the ordinary epilogue once. It also resets both counters for the next launch.
+// Returns false for the blocks whose partial went to a slab (their tile is done).
+template <int S>
+__device__ __forceinline__ void v3_split_sum(const float* slabs, int y, f32x4 (&acc)[8][4], int wave, int lane) {
+  // total = ((part_0 + part_1) + part_2) + ... with this block's own partial (part_y) in its place; every slot is
+  // loaded (this block's own slot holds stale data and is never selected): no branch around a load
+  constexpr int CH = S == 2 ? 4 : 2;  // 16-B chunks in flight per slab (<= 32 VGPRs of loads: the accumulators are live)
+#pragma unroll
+  for (int c0 = 0; c0 < 32; c0 += CH) {
+    f32x4 sl[CH][S];
+#pragma unroll
+    for (int u = 0; u < CH; ++u)
+#pragma unroll
+      for (int yy = 0; yy < S; ++yy)
+        sl[u][yy] = *reinterpret_cast<const f32x4*>(slabs + (long)yy * 65536 + (((c0 + u) * 8 + wave) * 64 + lane) * 4);
+#pragma unroll
+    for (int u = 0; u < CH; ++u) {
+      f32x4& a = acc[(c0 + u) >> 2][(c0 + u) & 3];
+      f32x4 r = y == 0 ? a : sl[u][0];
+#pragma unroll
+      for (int yy = 1; yy < S; ++yy) r = r + (yy == y ? a : sl[u][yy]);
+      a = r;
+    }
+  }
+}
+
+__device__ __forceinline__ bool v3_split_reduce(const GemmArgs& p, int tile, f32x4 (&acc)[8][4], int* role_lds,
+                                                int wave, int lane) {
+  const int S = p.ksplit, y = blockIdx.y;
+  const int t = p.split_tile0 + tile;
+  int* arrive = p.split_cnt + 2 * t;
+  int* pub = arrive + 1;
+  float* slabs = p.split_ws + (long)t * S * 65536;
+  if (threadIdx.x == 0) *role_lds = __hip_atomic_fetch_add(arrive, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  const int role = *reinterpret_cast<volatile int*>(role_lds);
+  if (role < S - 1) {
+    float* slab = slabs + (long)y * 65536;
+#pragma unroll
+    for (int c = 0; c < 32; ++c)
+      *reinterpret_cast<f32x4*>(slab + ((c * 8 + wave) * 64 + lane) * 4) = acc[c >> 2][c & 3];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // keep: ROCm 7.2 can drop the fence's own wait
+      __hip_atomic_fetch_add(pub, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return false;
+  }
+  if (threadIdx.x == 0) {
+    // every other split has arrived (this block drew the last ticket); wait for their slabs, bounded
+    for (int spin = 0; spin < (1 << 22); ++spin) {
+      if (__hip_atomic_load(pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= S - 1) break;
+      __builtin_amdgcn_s_sleep(2);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(arrive, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(pub, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  if (S == 2) v3_split_sum<2>(slabs, y, acc, wave, lane);
+  else if (S == 3) v3_split_sum<3>(slabs, y, acc, wave, lane);
+  else v3_split_sum<4>(slabs, y, acc, wave, lane);
+  return true;
+}
+
 // One 256x256 output tile (tile index bid of p's grid after the XCD remap), K range of split blockIdx.y, batch z.
 template <bool AK, bool BKc, int EPI, typename OutT, bool SW>
 __device__ __forceinline__ void v3_tile(const GemmArgs& p, int bid, long z, char* smem) {
@@ -1080,6 +1162,14 @@ __device__ __forceinline__ void v3_tile(const GemmArgs& p, int bid, long z, char
   }
   if (wr == 0) v3_barrier();  // re-align the barrier counts of the two wave groups
 
+  bool reduced = false;
+  if constexpr (EPI == EPI_STORE) {
+    if (p.ksplit > 1 && p.split_ws) {
+      __syncthreads();  // every wave is done reading the ring (the role word sits past the epilogue region)
+      if (!v3_split_reduce(p, bid, acc, reinterpret_cast<int*>(smem + 8 * 64 * EP_LD * 4), wave, lane)) return;
+      reduced = true;
+    }
+  }
   // ---- epilogue: two 64x64 passes per wave through a wave-private LDS region
   __syncthreads();
   float* ep = reinterpret_cast<float*>(smem) + wave * (64 * EP_LD);
@@ -1100,8 +1190,8 @@ __device__ __forceinline__ void v3_tile(const GemmArgs& p, int bid, long z, char
           for (int r = 0; r < 4; ++r) ep[(i * 16 + (lane >> 4) * 4 + r) * EP_LD + j * 16 + (lane & 15)] = acc[4 * mh + i][j][r];
     }
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): wave-private region written
-    if constexpr (SW) epilogue_tile64_pf<EPI, OutT>(p, C, ep, lane, m0 + arow + 64 * mh, n0 + bcol);
-    else epilogue_tile64<EPI, OutT>(p, C, ep, lane, m0 + arow + 64 * mh, n0 + bcol);
+    if constexpr (SW) epilogue_tile64_pf<EPI, OutT>(p, C, ep, lane, m0 + arow + 64 * mh, n0 + bcol, reduced);
+    else epilogue_tile64<EPI, OutT>(p, C, ep, lane, m0 + arow + 64 * mh, n0 + bcol, reduced);
     __builtin_amdgcn_s_waitcnt(0xC07F);
   }
 }
@@ -1476,7 +1566,7 @@ static int launch_v4(GemmArgs a, int batch, hipStream_t st) {
 template <bool AK, bool BKc, int EPI, typename OutT, bool SW>
 static int launch_v3(GemmArgs a, int batch, hipStream_t st) {
   constexpr int LDS_RING = 2 * (V3_BM * BK * 2 + V3_BN * BK * 2);
-  constexpr int LDS_EP = 8 * 64 * EP_LD * 4;
+  constexpr int LDS_EP = 8 * 64 * EP_LD * 4 + 16;  // + the split-K role word
   constexpr int LDS = LDS_RING > LDS_EP ? LDS_RING : LDS_EP;
   static bool attr = false;
   if (!attr) {
@@ -1674,6 +1764,19 @@ static int colsum_reduce(const slx_gemm_desc* d, hipStream_t st) {
 }
 
 constexpr long kRemCntInts = 4096;  // arrival counters at the end of rem_ws (zeroed once by the caller)
+constexpr long kSplitCntInts = 16384;  // arrival / published counters at the end of split_ws (2 per tile)
+constexpr long kSlabFloats = 65536;    // one 256 x 256 f32 partial
+
+// The in-launch split-K reduction applies when the caller gave a workspace big enough for every tile's slabs, at
+// 2 splits: the InternViT fc2.w + fc1.w pair, 302 -> 295 us against f32 atomics; at 4 splits (proj.w + qkv.w) the
+// last arriver's serial read of three 256 KiB slabs made it slower than the atomics (178 vs 164 us,
+// tools/wgrad_group_bench.py SPLIT_AB=1, profiles/round3_split_ab.txt). SLX_SPLIT_REDUCE_MAX raises the cap (A/B).
+static bool split_ws_fits(const slx_gemm_desc* d, long tiles, int sp) {
+  static const int smax = [] { const char* e = getenv("SLX_SPLIT_REDUCE_MAX"); const int v = e ? atoi(e) : 2;
+                               return v >= 2 && v <= 4 ? v : 2; }();
+  return d->split_ws && sp > 1 && sp <= smax && 2 * tiles <= kSplitCntInts &&
+         tiles * sp * kSlabFloats <= d->split_ws_floats - kSplitCntInts;
+}
 // SLX_GEMM_FOLD_REM=0: the M remainder as its own split-K launch + epilogue launch (A/B)
 static bool fold_off() {
   static const bool off = [] { const char* e = getenv("SLX_GEMM_FOLD_REM"); return e && atoi(e) == 0; }();
@@ -1703,6 +1806,7 @@ static int gemm_launch(const slx_gemm_desc* d, int v, hipStream_t st, int mshift
   a.colsum_ws = d->colsum_ws;
   a.maskbits = d->maskbits; a.ldbits = d->ldbits;
   a.colsum_row0 = colsum_row0;
+  a.split_ws = nullptr; a.split_cnt = nullptr; a.split_tile0 = 0;
   a.mshift_last = 0;
   a.tilesM = (d->M + BM - 1) / BM;
   a.tilesN = (d->N + BN - 1) / BN;
@@ -1728,7 +1832,13 @@ static int gemm_launch(const slx_gemm_desc* d, int v, hipStream_t st, int mshift
     if (sp > 1) {
       a.ksplit = sp;
       a.kchunk = ((ksteps + sp - 1) / sp) * BK;
-      if (!d->accumulate && !split_stride) {
+      const long v3tiles = (long)((d->M + V3_BM - 1) / V3_BM) * ((d->N + V3_BN - 1) / V3_BN);
+      if ((v == 7 || v == 8) && batch == 1 && !split_stride && d->epilogue == SLX_EPI_STORE && d->out_f32 &&
+          split_ws_fits(d, v3tiles, sp)) {  // reduced inside the launch: plain stores, no pre-zeroed C
+        a.split_ws = d->split_ws;
+        a.split_cnt = reinterpret_cast<int*>(d->split_ws + d->split_ws_floats - kSplitCntInts);
+      }
+      if (!d->accumulate && !split_stride && !a.split_ws) {
         hipError_t e = hipMemset2DAsync(d->C, d->ldc * sizeof(float), 0, (size_t)d->N * sizeof(float), d->M, st);
         if (e != hipSuccess) { set_error("slx_gemm_bf16: memset2D failed: %s", hipGetErrorString(e)); return -1000 - (int)e; }
       }
@@ -1932,6 +2042,7 @@ extern "C" int slx_gemm_bf16(const slx_gemm_desc* d, slx_stream_t stream) {
 // each, qkv/proj: 48 + 16 tiles, K = 16400 tokens); together they split K over one full round of 256 blocks.
 static void pair_args(const slx_gemm_desc* d, GemmArgs& a) {
   memset(&a, 0, sizeof(a));
+  a.split_ws = nullptr; a.split_cnt = nullptr; a.split_tile0 = 0;
   a.A = (const bf16*)d->A; a.B = (const bf16*)d->B; a.C = d->C;
   a.lda = d->lda; a.ldb = d->ldb; a.ldc = d->ldc;
   a.M = d->M; a.N = d->N; a.K = d->K;
@@ -1945,7 +2056,7 @@ static void pair_args(const slx_gemm_desc* d, GemmArgs& a) {
 template <bool AK, bool BKc, bool SW>
 static int launch_pair(GemmArgs& a, GemmArgs& b, hipStream_t st) {
   constexpr int LDS_RING = 2 * (V3_BM * BK * 2 + V3_BN * BK * 2);
-  constexpr int LDS_EP = 8 * 64 * EP_LD * 4;
+  constexpr int LDS_EP = 8 * 64 * EP_LD * 4 + 16;  // + the split-K role word
   constexpr int LDS = LDS_RING > LDS_EP ? LDS_RING : LDS_EP;
   static bool attr = false;
   if (!attr) {
@@ -1981,10 +2092,17 @@ extern "C" int slx_gemm_bf16_pair(const slx_gemm_desc* d1, const slx_gemm_desc* 
   if (sp > ksteps / 4) sp = ksteps / 4;
   if (d1->ksplit_max > 0 && sp > d1->ksplit_max) sp = d1->ksplit_max;
   if (sp < 1) sp = 1;
+  // in-launch reduction (slabs in d1's split_ws) when split_ws_fits allows it, else f32 atomics
   const int per = ((ksteps + sp - 1) / sp) * BK;
   sp = (d1->K + per - 1) / per;
+  const bool red = split_ws_fits(d1, tiles, sp);
   a.ksplit = b.ksplit = sp;
   a.kchunk = b.kchunk = sp > 1 ? per : d1->K;
+  if (red && sp > 1) {
+    a.split_ws = b.split_ws = d1->split_ws;
+    a.split_cnt = b.split_cnt = reinterpret_cast<int*>(d1->split_ws + d1->split_ws_floats - kSplitCntInts);
+    b.split_tile0 = a.tilesM * a.tilesN;
+  }
   hipStream_t st = (hipStream_t)stream;
   static const bool sw_default = [] { const char* e = getenv("SLX_V3_KIND"); return e && atoi(e) == 8; }();
   const bool sw = d1->variant == 8 || (d1->variant == 0 && sw_default);

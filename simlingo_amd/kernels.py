@@ -40,7 +40,7 @@ class GemmDesc(ctypes.Structure):
         ("seed", c_u64), ("drop_p", c_float), ("ldmask", c_i64),
         ("ksplit_max", c_int), ("variant", c_int), ("drop_operand", c_int),
         ("colsum", c_vp), ("colsum_ws", c_vp), ("maskbits", c_vp), ("ldbits", c_i64), ("rem_ws", c_vp),
-        ("rem_ws_floats", c_i64), ("resid_bf16", c_int),
+        ("rem_ws_floats", c_i64), ("resid_bf16", c_int), ("split_ws", c_vp), ("split_ws_floats", c_i64),
     ]
 
 
@@ -117,6 +117,8 @@ def _require_cuda(*ts):
 _colsum_ws: dict = {}  # per-device partials workspace of the colsum epilogue (stream-ordered reuse)
 _rem_ws: dict = {}     # per-device split-K scratch of the M-remainder rows (stream-ordered reuse)
 REM_WS_FLOATS = 16 << 20  # 64 MB: 32 splits x 64 rows x 8192 columns
+_split_ws: dict = {}   # per-stream in-launch split-K slabs of the 256x256 kernel (weight gradients)
+SPLIT_WS_FLOATS = (32 << 20) + 16384  # 128 MB of slabs (e.g. 128 tiles x 4 splits) + 16384 counter words
 
 
 def gemm(A, B, C, M, N, K, layout, lda, ldb, ldc, **kw):
@@ -132,7 +134,7 @@ def gemm(A, B, C, M, N, K, layout, lda, ldb, ldc, **kw):
 def _gemm_desc(A, B, C, M, N, K, layout, lda, ldb, ldc, *, epi=EPI_STORE, alpha=1.0, bias=None, ls=None,
                aux=None, ldaux=0, aux_out=None, ldaux_out=0, resid=None, ldr=0, accumulate=False,
                seed=0, drop_p=0.0, ldmask=0, batch=1, sA=0, sB=0, sC=0, ksplit_max=0, variant=None, drop_operand=0,
-               colsum=None, maskbits=None):
+               colsum=None, maskbits=None, split_ws=True):
     _require_cuda(A, B, C)
     d = GemmDesc()
     d.layout, d.epilogue = layout, epi
@@ -165,6 +167,12 @@ def _gemm_desc(A, B, C, M, N, K, layout, lda, ldb, ldc, *, epi=EPI_STORE, alpha=
         # zeroed once: the last 4096 words are the folded-remainder arrival counters (reset by every GEMM that uses them)
         rw = _rem_ws[sk] = torch.zeros(REM_WS_FLOATS, dtype=torch.float32, device=C.device)
     d.rem_ws, d.rem_ws_floats = rw.data_ptr(), rw.numel()
+    if split_ws and d.out_f32 and d.epilogue == EPI_STORE:
+        sw = _split_ws.get(sk)
+        if sw is None:
+            # zeroed once: the last 16384 words are the in-launch split-K arrival counters (left zero by every call)
+            sw = _split_ws[sk] = torch.zeros(SPLIT_WS_FLOATS, dtype=torch.float32, device=C.device)
+        d.split_ws, d.split_ws_floats = sw.data_ptr(), sw.numel()
     if colsum is not None:
         need = (int(M) + 63) // 64 * int(N)
         ws = _colsum_ws.get(sk)

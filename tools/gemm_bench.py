@@ -26,6 +26,9 @@ SHAPES = {  # name: (M, N, K, layout)
     "llm_down": (6384, 896, 4864, K.GEMM_NT),
     "llm_gu_dgrad": (6384, 896, 9728, K.GEMM_NN),
     "sq8192": (8192, 8192, 8192, K.GEMM_NT),
+    "tn8192": (8192, 8192, 8192, K.GEMM_TN),   # both operands MN-contiguous (tr-reads), no split-K
+    "nn8192": (8192, 8192, 8192, K.GEMM_NN),
+    "tn4096x1024x8192": (4096, 1024, 8192, K.GEMM_TN),  # one split of the fc1.w gradient
     # weight gradients with a transposed (feature-major) copy of the forward activation X:
     # TT: dW = dY^T . Xt^T  (A = dY [tok][out] MN-contiguous, B = Xt [in][tok] K-contiguous)
     # NN: dW^T = Xt . dY     (A = Xt K-contiguous, B = dY [tok][out] MN-contiguous; output transposed)

@@ -1,0 +1,7 @@
+# Round-3 kernel-trace profile of the VLA step (steady-state per-step summary with launch-grid attribution)
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+O=gpurun_out/${R3TAG:-r3e}; mkdir -p $O
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 bench.py --steps 4 --warmup 2 --no-cpu-baseline --no-extras > $O/prof.log 2>&1 || { tail -20 $O/prof.log; exit 1; }
+python3 tools/prof_steps.py $O/prof --warmup 2 --top 60 > $O/steps.txt && python3 tools/prof_steps.py $O/prof --warmup 2 --top 80 --grid > $O/steps_grid.txt && head -45 $O/steps.txt

@@ -32,16 +32,27 @@ def run(M, N, batch=1, variant=0, split=0):
     return f
 
 
-def pair(s1, s2, split=0):
+def pair(s1, s2, split=0, ws=True, variant=None):
     o1 = [t[0] for t in operands(*s1)]
     o2 = [t[0] for t in operands(*s2)]
+    d = [K._gemm_desc(o[0], o[1], o[2], *K._mm_dims(o[0], o[1], o[2], True, False), o[0].stride(0), o[1].stride(0),
+                      o[2].stride(0), accumulate=True, ksplit_max=split, split_ws=ws, variant=variant) for o in (o1, o2)]
 
     def f():
-        K.mm_pair((o1[0], o1[1], o1[2]), (o2[0], o2[1], o2[2]), ksplit_max=split)
+        K.check(K.lib().slx_gemm_bf16_pair(K.ctypes.byref(d[0]), K.ctypes.byref(d[1]), K.stream_ptr()), "pair")
     return f
 
 
-cases = {
+if os.environ.get("SPLIT_AB"):  # in-launch split-K reduction vs f32 atomics (round 3)
+    cases = {
+        "fc2+fc1 pair atomics": pair((1024, 4096), (4096, 1024), ws=False),
+        "fc2+fc1 pair in-launch reduce": pair((1024, 4096), (4096, 1024), ws=True),
+        "proj+qkv pair atomics": pair((1024, 1024), (3072, 1024), ws=False),
+        "proj+qkv pair in-launch reduce": pair((1024, 1024), (3072, 1024), ws=True),
+        "fc2+fc1 pair reduce v8": pair((1024, 4096), (4096, 1024), ws=True, variant=8),
+    }
+else:
+  cases = {
     "fc2+fc1 pair (auto split)": pair((1024, 4096), (4096, 1024)),
     "proj+qkv pair (auto split)": pair((1024, 1024), (3072, 1024)),
     "proj+qkv pair split 3": pair((1024, 1024), (3072, 1024), 3),
@@ -54,7 +65,7 @@ cases = {
     "qkvproj_group_v3s4 (4096x1024)": run(4096, 1024, variant=7, split=4),
     "qkvproj_group_v3s3 (4096x1024)": run(4096, 1024, variant=7, split=3),
     "fc1_wgrad_v3s4": run(4096, 1024, variant=7, split=4),
-}
+  }
 for f in cases.values():
     f()
 torch.cuda.synchronize()
