@@ -639,6 +639,8 @@ template <typename OutT> struct EpiLd<EPI_RESID_LS, OutT> { static constexpr int
 template <typename OutT> struct EpiLd<EPI_GELU_BWD, OutT> { static constexpr int N = 1; };
 template <typename OutT> struct EpiLd<EPI_QGELU_BWD, OutT> { static constexpr int N = 1; };
 template <typename OutT> struct EpiLd<EPI_SWIGLU_BWD, OutT> { static constexpr int N = 2; };
+template <typename OutT> struct EpiLd<EPI_DROPMASK_SWIGLU, OutT> { static constexpr int N = 5; };    // resid f32 x2, g, u, bits
+template <typename OutT> struct EpiLd<EPI_DROPMASK_SWIGLU_B, OutT> { static constexpr int N = 4; };  // resid bf16, g, u, bits
 
 __device__ __forceinline__ void unpack_bf8(uint4 u, float (&f)[8]) {
   const bf16x8 x = __builtin_bit_cast(bf16x8, u);
@@ -665,6 +667,20 @@ __device__ __forceinline__ void epi_issue(const GemmArgs& p, const OutT* C, int 
   } else if constexpr (EPI == EPI_SWIGLU_BWD) {
     L[0] = *reinterpret_cast<const uint4*>(p.aux + (long)m * p.ldaux + n);
     L[1] = *reinterpret_cast<const uint4*>(p.aux + (long)m * p.ldaux + p.N + n);
+  } else if constexpr (EPI == EPI_DROPMASK_SWIGLU || EPI == EPI_DROPMASK_SWIGLU_B) {
+    constexpr int R = EPI == EPI_DROPMASK_SWIGLU ? 2 : 1;  // resid words
+    if constexpr (R == 2) {
+      const uint4* q = reinterpret_cast<const uint4*>(p.resid + (long)m * p.ldr + n);
+      L[0] = q[0];
+      L[1] = q[1];
+    } else {
+      L[0] = *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16*>(p.resid) + (long)m * p.ldr + n);
+    }
+    L[R] = *reinterpret_cast<const uint4*>(p.aux + (long)m * p.ldaux + n);
+    L[R + 1] = *reinterpret_cast<const uint4*>(p.aux + (long)m * p.ldaux + p.N + n);
+    // the keep-bit word (stored bits) - loaded unconditionally from a valid address, used only with maskbits
+    const uint32_t* bw = p.maskbits ? p.maskbits + (long)m * p.ldbits + (n >> 5) : reinterpret_cast<const uint32_t*>(p.aux);
+    L[R + 2].x = *bw;
   }
 }
 
@@ -720,6 +736,27 @@ __device__ __forceinline__ void epi_finish(const GemmArgs& p, OutT* __restrict__
 #pragma unroll
     for (int e = 0; e < 8; ++e) { o[e] = v[e] * u[e] * silu_grad(g[e]); u[e] = v[e] * silu(g[e]); }
     st8(C + ci, o);
+    st8(C + ci + p.N, u);
+  } else if constexpr (EPI == EPI_DROPMASK_SWIGLU || EPI == EPI_DROPMASK_SWIGLU_B) {
+    constexpr int R = EPI == EPI_DROPMASK_SWIGLU ? 2 : 1;
+    if (p.drop_p > 0.f) {
+      const uint32_t kb = p.maskbits ? (L[R + 2].x >> (n & 31)) & 0xFFu : epi_keep8(p, m, n);
+      const float sc = 1.0f / (1.0f - p.drop_p);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] *= (kb >> e) & 1u ? sc : 0.f;
+    }
+    float r[8], g[8], u[8];
+    if constexpr (R == 2) unpack_f8(L[0], L[1], r);
+    else unpack_bf8(L[0], r);
+    unpack_bf8(L[R], g);
+    unpack_bf8(L[R + 1], u);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float d = v[e] + r[e];
+      r[e] = d * u[e] * silu_grad(g[e]);
+      u[e] = d * silu(g[e]);
+    }
+    st8(C + ci, r);
     st8(C + ci + p.N, u);
   }
 }
@@ -781,7 +818,8 @@ template <int EPI, typename OutT>
 __device__ __forceinline__ void epilogue_tile64_pf(const GemmArgs& p, OutT* __restrict__ C, const float* ep, int lane,
                                                    int m_base, int n_base, bool reduced = false) {
   constexpr bool kPf = EPI == EPI_STORE || EPI == EPI_GELU || EPI == EPI_QGELU || EPI == EPI_RESID_LS ||
-                       EPI == EPI_GELU_BWD || EPI == EPI_QGELU_BWD || EPI == EPI_SWIGLU_BWD;
+                       EPI == EPI_GELU_BWD || EPI == EPI_QGELU_BWD || EPI == EPI_SWIGLU_BWD ||
+                       EPI == EPI_DROPMASK_SWIGLU || EPI == EPI_DROPMASK_SWIGLU_B;
   if constexpr (kPf) {
     const bool whole = p.vec_ok && n_base + 64 <= p.N && !(EPI == EPI_STORE && p.ksplit > 1 && !reduced);  // wave-uniform
     if (whole) {
@@ -903,7 +941,10 @@ __global__ __launch_bounds__(BMv * 2, 1) void gemm_bf16_dma_kernel(GemmArgs p) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) ep[(i * 16 + (lane >> 4) * 4 + r) * EP_LD + j * 16 + (lane & 15)] = acc[i][j][r];
   __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS writes done (wave-private region)
-  epilogue_tile64<EPI, OutT>(p, C, ep, lane, m0 + wm * 64, n0 + wn * 64);
+  if constexpr (EPI == EPI_DROPMASK_SWIGLU || EPI == EPI_DROPMASK_SWIGLU_B || EPI == EPI_SWIGLU_BWD)
+    epilogue_tile64_pf<EPI, OutT>(p, C, ep, lane, m0 + wm * 64, n0 + wn * 64);  // HBM-bound K = 64 SwiGLU' GEMMs
+  else
+    epilogue_tile64<EPI, OutT>(p, C, ep, lane, m0 + wm * 64, n0 + wn * 64);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1667,6 +1708,20 @@ static int dispatch_layout(int layout, GemmArgs& a, int batch, hipStream_t st, i
 // partially filled last rounds are priced in. For v3, a small M remainder (M % 256 <= 64, e.g. the 16
 // class tokens of 16 InternViT tiles: 16400 = 64*256 + 16) is peeled into a v2 launch so the main grid
 // is whole rounds.
+constexpr long kSplitCntInts = 16384;  // arrival / published counters at the end of split_ws (2 per tile)
+constexpr long kSlabFloats = 65536;    // one 256 x 256 f32 partial
+
+// The in-launch split-K reduction applies when the caller gave a workspace big enough for every tile's slabs, at
+// 2 splits: the InternViT fc2.w + fc1.w pair, 302 -> 295 us against f32 atomics; at 4 splits (proj.w + qkv.w) the
+// last arriver's serial read of three 256 KiB slabs made it slower than the atomics (178 vs 164 us,
+// tools/wgrad_group_bench.py SPLIT_AB=1, profiles/round3_split_ab.txt). SLX_SPLIT_REDUCE_MAX raises the cap (A/B).
+static bool split_ws_fits(const slx_gemm_desc* d, long tiles, int sp) {
+  static const int smax = [] { const char* e = getenv("SLX_SPLIT_REDUCE_MAX"); const int v = e ? atoi(e) : 2;
+                               return v >= 2 && v <= 4 ? v : 2; }();
+  return d->split_ws && sp > 1 && sp <= smax && 2 * tiles <= kSplitCntInts &&
+         tiles * sp * kSlabFloats <= d->split_ws_floats - kSplitCntInts;
+}
+
 static int v_tile_m(int v) { return v == 7 ? 256 : (v == 5 || v == 6) ? 256 : 128; }
 static int v_tile_n(int v) { return v == 7 ? 256 : 128; }
 static int v_slots(int v) { return v == 7 ? 256 : 512; }
@@ -1697,7 +1752,12 @@ static double v_cost(const slx_gemm_desc* d, int v, int M, int batch) {
   double block_rate = v == 7 ? 1.35e15 / 256 : 1.1e15 / 512;
   if (v != 7 && blocks <= 256) block_rate *= 1.4;
   double t = rounds * block_flop / block_rate;
-  if (sp > 1) t += (double)sp * M * d->N * 4.0 / 1.3e12;  // f32 atomics: ~1.3 TB/s chip-wide
+  if (sp > 1) {
+    if (v == 7 && batch == 1 && d->epilogue == SLX_EPI_STORE && d->out_f32 && split_ws_fits(d, (long)tiles, sp))
+      t += 5e-6;  // in-launch reduction: one 256 KiB slab per tile read by its last arriver
+    else
+      t += (double)sp * M * d->N * 4.0 / 1.3e12;  // f32 atomics: ~1.3 TB/s chip-wide
+  }
   if (v == 7 && blocks < 192) t *= 1.5;  // an under-filled 256x256 grid leaves whole CUs idle
   return t;
 }
@@ -1764,19 +1824,6 @@ static int colsum_reduce(const slx_gemm_desc* d, hipStream_t st) {
 }
 
 constexpr long kRemCntInts = 4096;  // arrival counters at the end of rem_ws (zeroed once by the caller)
-constexpr long kSplitCntInts = 16384;  // arrival / published counters at the end of split_ws (2 per tile)
-constexpr long kSlabFloats = 65536;    // one 256 x 256 f32 partial
-
-// The in-launch split-K reduction applies when the caller gave a workspace big enough for every tile's slabs, at
-// 2 splits: the InternViT fc2.w + fc1.w pair, 302 -> 295 us against f32 atomics; at 4 splits (proj.w + qkv.w) the
-// last arriver's serial read of three 256 KiB slabs made it slower than the atomics (178 vs 164 us,
-// tools/wgrad_group_bench.py SPLIT_AB=1, profiles/round3_split_ab.txt). SLX_SPLIT_REDUCE_MAX raises the cap (A/B).
-static bool split_ws_fits(const slx_gemm_desc* d, long tiles, int sp) {
-  static const int smax = [] { const char* e = getenv("SLX_SPLIT_REDUCE_MAX"); const int v = e ? atoi(e) : 2;
-                               return v >= 2 && v <= 4 ? v : 2; }();
-  return d->split_ws && sp > 1 && sp <= smax && 2 * tiles <= kSplitCntInts &&
-         tiles * sp * kSlabFloats <= d->split_ws_floats - kSplitCntInts;
-}
 // SLX_GEMM_FOLD_REM=0: the M remainder as its own split-K launch + epilogue launch (A/B)
 static bool fold_off() {
   static const bool off = [] { const char* e = getenv("SLX_GEMM_FOLD_REM"); return e && atoi(e) == 0; }();

@@ -119,6 +119,7 @@ _rem_ws: dict = {}     # per-device split-K scratch of the M-remainder rows (str
 REM_WS_FLOATS = 16 << 20  # 64 MB: 32 splits x 64 rows x 8192 columns
 _split_ws: dict = {}   # per-stream in-launch split-K slabs of the 256x256 kernel (weight gradients)
 SPLIT_WS_FLOATS = (32 << 20) + 16384  # 128 MB of slabs (e.g. 128 tiles x 4 splits) + 16384 counter words
+SPLIT_WS_ON = os.environ.get("SLX_SPLIT_WS", "1") != "0"  # A/B hook: 0 = split-K partials through f32 atomics
 
 
 def gemm(A, B, C, M, N, K, layout, lda, ldb, ldc, **kw):
@@ -167,7 +168,7 @@ def _gemm_desc(A, B, C, M, N, K, layout, lda, ldb, ldc, *, epi=EPI_STORE, alpha=
         # zeroed once: the last 4096 words are the folded-remainder arrival counters (reset by every GEMM that uses them)
         rw = _rem_ws[sk] = torch.zeros(REM_WS_FLOATS, dtype=torch.float32, device=C.device)
     d.rem_ws, d.rem_ws_floats = rw.data_ptr(), rw.numel()
-    if split_ws and d.out_f32 and d.epilogue == EPI_STORE:
+    if split_ws and SPLIT_WS_ON and d.out_f32 and d.epilogue == EPI_STORE:
         sw = _split_ws.get(sk)
         if sw is None:
             # zeroed once: the last 16384 words are the in-launch split-K arrival counters (left zero by every call)
