@@ -251,6 +251,17 @@ int slx_act_bwd(const float* dact, const float* pre, float* dpre, int64_t n, int
 int slx_ce_fwd(const float* logits, int64_t ld, const int* labels, int64_t R, int V, float* loss, float* lse, slx_stream_t s);
 int slx_ce_bwd(const float* logits, int64_t ld, const int* labels, const float* lse, int64_t R, int V, const float* gscale,
                void* dlogits, int64_t ldd, slx_stream_t s);
+/* Fused LM head + CE over the R gathered loss rows (the training step; replaces lm_head + slx_ce_fwd / slx_ce_bwd and
+ * their f32 [R, V] logits): feat [R][D] bf16 (ld ldf), W = lm_head [>=V][D] bf16 (ld ldw), labels [R] (-1 ignored).
+ * fwd: the LM-head GEMM's epilogue reduces each row's logits to (max, sum exp) per 64-column sub-tile and the label
+ * logit into ws (slx_lmhead_ce_ws_floats(R, V) floats); a combine pass writes loss[R] and lse[R].
+ * bwd: the GEMM recomputed with the softmax-gradient epilogue: dlogits [R][ldd] bf16 = (softmax - onehot) * gscale[0],
+ * zero past V (ldd >= V rounded up to 128), the operand of the dlogits x lm_head dgrad.                         */
+int slx_lmhead_ce_ws_floats(int64_t R, int V);
+int slx_lmhead_ce_fwd(const void* feat, int64_t ldf, const void* W, int64_t ldw, const int* labels, int64_t R, int V,
+                      int D, float* loss, float* lse, float* ws, int64_t ws_floats, slx_stream_t s);
+int slx_lmhead_ce_bwd(const void* feat, int64_t ldf, const void* W, int64_t ldw, const int* labels, const float* lse,
+                      int64_t R, int V, int D, const float* gscale, void* dlogits, int64_t ldd, slx_stream_t s);
 /* kind 0: smooth_l1(beta=1).sum(-1) per point (simlingo_training adaptors.py:205-213);
  * kind 1: mse.sum(-1) per point (simlingo_base_training adaptors.py:226)                       */
 int slx_wp_loss_fwd(const float* out, const float* label, int B, int n, int dims, int kind, float* pred, float* loss,

@@ -32,7 +32,9 @@ constexpr int BM = 128, BN = 128, BK = 64, NT = 256;
 
 enum { EPI_STORE = 0, EPI_GELU = 1, EPI_RESID_LS = 2, EPI_GELU_BWD = 3, EPI_SWIGLU_BWD = 4, EPI_DROPMASK = 5,
        EPI_DROPMASK_SWIGLU = 6, EPI_QGELU = 7, EPI_QGELU_BWD = 8,
-       EPI_DROPMASK_SWIGLU_B = 9 /* internal: DROPMASK_SWIGLU with a bf16 resid (slx_gemm_desc.resid_bf16) */ };
+       EPI_DROPMASK_SWIGLU_B = 9 /* internal: DROPMASK_SWIGLU with a bf16 resid (slx_gemm_desc.resid_bf16) */,
+       EPI_CE_PART = 10,  /* internal (slx_lmhead_ce_fwd): per-row (max, sum exp) over each 64-column sub-tile + label logit */
+       EPI_CE_GRAD = 11   /* internal (slx_lmhead_ce_bwd): bf16 (softmax - onehot) * gscale from recomputed logits */ };
 
 // CLIP quick_gelu x*sigmoid(1.702x) (transformers ACT2FN["quick_gelu"], the LLaVA-NeXT vision tower)
 __device__ __forceinline__ float qgelu(float x) { return x / (1.0f + __expf(-1.702f * x)); }
@@ -84,6 +86,13 @@ struct GemmArgs {
   float* split_ws;   // null = split-K partials go to C with f32 atomics
   int* split_cnt;    // [2 * tiles] arrival / published counters, zero on entry, reset by each tile's last arriver
   int split_tile0;   // tile-index offset of this GEMM in the shared workspace (slx_gemm_bf16_pair's second GEMM)
+  // fused LM head + cross entropy (EPI_CE_PART / EPI_CE_GRAD)
+  const int* ce_labels;  // [M] next-token label per row (-1 = ignored)
+  float* ce_part;        // [M][ce_ldpart] (max, sumexp) pairs, one per 64-column sub-tile
+  float* ce_lab;         // [M] the label's logit
+  const float* ce_lse;   // [M] log-sum-exp (backward)
+  const float* ce_gscale;  // d loss / d (per-row CE): one scalar (the LM loss weight / count)
+  int ce_ldpart;
 };
 
 // Dropout applied while loading an operand (LoRA dropout, regenerated bit-exactly in backward):
@@ -560,9 +569,67 @@ __device__ __forceinline__ void wait_vm() {
 }
 
 // LDS-staged epilogue of one 64x64 f32 sub-tile held in `ep` (row stride EP_LD), rows m_base.., cols n_base..
+// Fused LM head + CE epilogues on one 64 x 64 f32 sub-tile of logits (rows = loss rows, columns = vocabulary).
+// Lane: 8 columns (lane & 7) of row (lane >> 3) + 8 pass. CE_PART: the row's (max, sum exp(x - max)) over the
+// sub-tile's valid columns, combined over the 8 lanes of a row with xor shuffles, and the label logit where the
+// label falls; CE_GRAD: dlogits = (exp(x - lse) - [n == label]) * gscale in bf16, zero for ignored rows and for
+// the padded columns past V (the dgrad GEMM reads them).
+template <int EPI>
+__device__ __forceinline__ void ce_tile64(const GemmArgs& p, const float* ep, int lane, int m_base, int n_base) {
+  const int cc = (lane & 7) * 8, n = n_base + cc;
+  const float g = EPI == EPI_CE_GRAD ? *p.ce_gscale : 0.f;
+#pragma unroll 2
+  for (int pass = 0; pass < 8; ++pass) {
+    const int row = pass * 8 + (lane >> 3);
+    const int m = m_base + row;
+    const bool mok = m < p.M;
+    const int lab = mok ? p.ce_labels[m] : -1;
+    float v[8];
+    const float4 a0 = *reinterpret_cast<const float4*>(ep + row * EP_LD + cc);
+    const float4 a1 = *reinterpret_cast<const float4*>(ep + row * EP_LD + cc + 4);
+    v[0] = a0.x; v[1] = a0.y; v[2] = a0.z; v[3] = a0.w; v[4] = a1.x; v[5] = a1.y; v[6] = a1.z; v[7] = a1.w;
+    if constexpr (EPI == EPI_CE_PART) {
+      float mx = -INFINITY;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) mx = n + e < p.N ? fmaxf(mx, v[e]) : mx;
+      float sm = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) sm += n + e < p.N ? __expf(v[e] - mx) : 0.f;
+#pragma unroll
+      for (int o = 1; o < 8; o <<= 1) {
+        const float m2 = __shfl_xor(mx, o, 64), s2 = __shfl_xor(sm, o, 64);
+        const float mm = fmaxf(mx, m2);
+        sm = (mx == -INFINITY ? 0.f : sm * __expf(mx - mm)) + (m2 == -INFINITY ? 0.f : s2 * __expf(m2 - mm));
+        mx = mm;
+      }
+      if (mok && (lane & 7) == 0)
+        *reinterpret_cast<float2*>(p.ce_part + ((long)m * p.ce_ldpart + n_base / 64) * 2) = make_float2(mx, sm);
+      if (mok && lab >= n && lab < n + 8) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if (lab == n + e) p.ce_lab[m] = v[e];
+      }
+    } else {
+      if (!mok) continue;
+      const float lse = p.ce_lse[m];
+      bf16x8 o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float t = (lab >= 0 && n + e < p.N) ? (__expf(v[e] - lse) - (n + e == lab ? 1.f : 0.f)) * g : 0.f;
+        o[e] = (bf16)t;
+      }
+      *reinterpret_cast<bf16x8*>(reinterpret_cast<bf16*>(p.C) + (long)m * p.ldc + n) = o;
+    }
+  }
+}
+
 template <int EPI, typename OutT>
 __device__ __forceinline__ void epilogue_tile64(const GemmArgs& p, OutT* __restrict__ C, const float* ep, int lane,
                                                 int m_base, int n_base, bool reduced = false) {
+  if constexpr (EPI == EPI_CE_PART || EPI == EPI_CE_GRAD) {
+    ce_tile64<EPI>(p, ep, lane, m_base, n_base);
+    return;
+  }
   if constexpr (EPI == EPI_STORE) {
     if (p.ksplit > 1 && !reduced) {  // split-K partials: one 64-float row (256 contiguous bytes) per atomic wave-instruction
       const int n1 = n_base + lane;
@@ -2082,6 +2149,88 @@ extern "C" int slx_gemm_bf16(const slx_gemm_desc* d, slx_stream_t stream) {
   const int rc = gemm_launch(d, v == 7 ? v3k : v, st);
   if (rc) return rc;
   return d->colsum ? colsum_reduce(d, st) : 0;
+}
+
+// ---- fused LM head + cross entropy (LanguageAdaptor.compute_loss, adaptors.py:259-274, on the gathered loss rows) ----
+// Forward: the LM-head GEMM (NT, feat [R][D] x W [V][D]^T) keeps its logits in registers / LDS; its epilogue
+// writes one (max, sum exp) pair per row and 64-column sub-tile plus the label logit, and ce_combine_kernel folds
+// the pairs into lse and the loss. Backward: the same GEMM recomputed with the softmax-gradient epilogue writing
+// bf16 dlogits [R][ldd] (the operand of the dlogits x W dgrad). No f32 [R, V] logits buffer exists.
+__global__ __launch_bounds__(256) void ce_combine_kernel(const float* __restrict__ part, int ntile, const float* __restrict__ lab_logit,
+                                                         const int* __restrict__ labels, int V, float* loss, float* lse) {
+  __shared__ float sh[16];
+  const long r = blockIdx.x;
+  const float2* pr = reinterpret_cast<const float2*>(part) + r * ntile;
+  float mx = -INFINITY;
+  for (int i = threadIdx.x; i < ntile; i += blockDim.x) mx = fmaxf(mx, pr[i].x);
+  mx = warp_max(mx);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = mx;
+  __syncthreads();
+  mx = fmaxf(fmaxf(sh[0], sh[1]), fmaxf(sh[2], sh[3]));
+  float s = 0.f;
+  for (int i = threadIdx.x; i < ntile; i += blockDim.x) {
+    const float2 q = pr[i];
+    s += q.x == -INFINITY ? 0.f : q.y * __expf(q.x - mx);
+  }
+  __syncthreads();
+  s = block_sum(s, sh);
+  if (threadIdx.x == 0) {
+    const float l = mx + __logf(s);
+    lse[r] = l;
+    const int lab = labels[r];
+    loss[r] = (lab >= 0 && lab < V) ? l - lab_logit[r] : 0.f;  // ignore_index (-1): 0, as F.cross_entropy
+  }
+}
+
+static void ce_args(GemmArgs& a, const void* feat, int64_t ldf, const void* W, int64_t ldw, int64_t R, int V, int D) {
+  memset(&a, 0, sizeof(a));
+  a.A = (const bf16*)feat; a.lda = ldf;
+  a.B = (const bf16*)W; a.ldb = ldw;
+  a.M = (int)R; a.N = V; a.K = D;
+  a.alpha = 1.f;
+  a.ksplit = 1; a.kchunk = D;
+  a.tilesN = (V + BN - 1) / BN;
+}
+
+// one (max, sumexp) pair per row and 64-column sub-tile of the 128-column GEMM tiles, + the label logits
+static int ce_ntile(int V) { return 2 * ((V + BN - 1) / BN); }
+extern "C" int slx_lmhead_ce_ws_floats(int64_t R, int V) { return (int)(R * 2 * ce_ntile(V) + R); }
+
+extern "C" int slx_lmhead_ce_fwd(const void* feat, int64_t ldf, const void* W, int64_t ldw, const int* labels, int64_t R,
+                                 int V, int D, float* loss, float* lse, float* ws, int64_t ws_floats, slx_stream_t stream) {
+  if (R <= 0) return 0;
+  SLX_CHECK_ARG(feat && W && labels && loss && lse && ws, "slx_lmhead_ce_fwd: null pointer");
+  SLX_CHECK_ARG(D % BK == 0 && ldf % 8 == 0 && ldw % 8 == 0 && ((uintptr_t)feat & 15) == 0 && ((uintptr_t)W & 15) == 0,
+                "slx_lmhead_ce_fwd: D %% %d == 0, 16-B aligned operands, leading dims multiples of 8", BK);
+  const int nt = ce_ntile(V);
+  SLX_CHECK_ARG(ws_floats >= R * 2 * nt + R, "slx_lmhead_ce_fwd: workspace %lld < %lld floats", (long long)ws_floats,
+                (long long)(R * 2 * nt + R));
+  GemmArgs a;
+  ce_args(a, feat, ldf, W, ldw, R, V, D);
+  a.ce_labels = labels; a.ce_part = ws; a.ce_lab = ws + R * 2 * nt; a.ce_ldpart = nt;
+  hipStream_t st = (hipStream_t)stream;
+  const int rc = launch_v2<true, true, EPI_CE_PART, float, 128, 2>(a, 1, st);
+  if (rc) return rc;
+  hipLaunchKernelGGL(ce_combine_kernel, dim3((unsigned)R), dim3(256), 0, st, (const float*)ws, nt, (const float*)a.ce_lab,
+                     labels, V, loss, lse);
+  SLX_LAUNCH_CHECK("slx_lmhead_ce_fwd(combine)");
+  return 0;
+}
+
+extern "C" int slx_lmhead_ce_bwd(const void* feat, int64_t ldf, const void* W, int64_t ldw, const int* labels,
+                                 const float* lse, int64_t R, int V, int D, const float* gscale, void* dlogits, int64_t ldd,
+                                 slx_stream_t stream) {
+  if (R <= 0) return 0;
+  SLX_CHECK_ARG(feat && W && labels && lse && gscale && dlogits, "slx_lmhead_ce_bwd: null pointer");
+  SLX_CHECK_ARG(D % BK == 0 && ldf % 8 == 0 && ldw % 8 == 0 && ldd % 8 == 0 && ldd >= ((V + 127) / 128) * 128 &&
+                ((uintptr_t)feat & 15) == 0 && ((uintptr_t)W & 15) == 0 && ((uintptr_t)dlogits & 15) == 0,
+                "slx_lmhead_ce_bwd: D %% %d == 0, ldd >= V rounded up to 128, 16-B aligned operands", BK);
+  GemmArgs a;
+  ce_args(a, feat, ldf, W, ldw, R, V, D);
+  a.C = dlogits; a.ldc = ldd;
+  a.ce_labels = labels; a.ce_lse = lse; a.ce_gscale = gscale;
+  return launch_v2<true, true, EPI_CE_GRAD, float, 128, 2>(a, 1, (hipStream_t)stream);
 }
 
 // Two accumulating f32-output GEMMs of one layout and one K in a single v3 launch (gemm_bf16_v3_pair_kernel): the

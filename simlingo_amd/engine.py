@@ -268,12 +268,19 @@ class VLAEngine(EngineOps):
         if R:
             fl = self._e(R, d)
             self._gather_feat(feat, d, dplan["loss_pos"], R, d, fl)
-            logits = self._e(R, self.Vp, dtype=F32)
-            K.mm(fl, self.W["llm.lm_head"][: cfg.vocab], logits)
             lse_ce = self._e(R, dtype=F32)
-            K.call("slx_ce_fwd", K.P(logits), self.Vp, K.P(dplan["loss_labels"]), R, cfg.vocab, K.P(ce_loss),
-                   K.P(lse_ce), K.stream_ptr())
-            sv.update(fl=fl, logits=logits, lse_ce=lse_ce)
+            if self.precise:  # fp32 parity mode: materialised f32 logits + slx_ce_fwd
+                logits = self._e(R, self.Vp, dtype=F32)
+                K.mm(fl, self.W["llm.lm_head"][: cfg.vocab], logits)
+                K.call("slx_ce_fwd", K.P(logits), self.Vp, K.P(dplan["loss_labels"]), R, cfg.vocab, K.P(ce_loss),
+                       K.P(lse_ce), K.stream_ptr())
+                sv.update(logits=logits)
+            else:  # fused LM head + CE: no [R, V] logits buffer (slx_lmhead_ce_fwd)
+                nws = K.lib().slx_lmhead_ce_ws_floats(R, cfg.vocab)
+                ws = self._e(nws, dtype=F32)
+                K.call("slx_lmhead_ce_fwd", K.P(fl), d, K.P(self.W["llm.lm_head"]), d, K.P(dplan["loss_labels"]), R,
+                       cfg.vocab, d, K.P(ce_loss), K.P(lse_ce), K.P(ws), nws, K.stream_ptr())
+            sv.update(fl=fl, lse_ce=lse_ce)
         # ---------------- driving heads ----------------
         nr, ns = cfg.n_route, cfg.n_speed
         qpos = dplan["query_pos"].view(B, cfg.n_queries)
@@ -540,8 +547,12 @@ class VLAEngine(EngineOps):
         # ---------------- language loss ----------------
         if R:
             dlog = self._e(R, self.Vp)
-            K.call("slx_ce_bwd", K.P(sv["logits"]), self.Vp, K.P(dplan["loss_labels"]), K.P(sv["lse_ce"]), R,
-                   cfg.vocab, K.P(gs[0:1]), K.P(dlog), self.Vp, K.stream_ptr())
+            if "logits" in sv:
+                K.call("slx_ce_bwd", K.P(sv["logits"]), self.Vp, K.P(dplan["loss_labels"]), K.P(sv["lse_ce"]), R,
+                       cfg.vocab, K.P(gs[0:1]), K.P(dlog), self.Vp, K.stream_ptr())
+            else:  # the LM-head GEMM recomputed with the softmax-gradient epilogue (slx_lmhead_ce_bwd)
+                K.call("slx_lmhead_ce_bwd", K.P(sv["fl"]), d, K.P(self.W["llm.lm_head"]), d, K.P(dplan["loss_labels"]),
+                       K.P(sv["lse_ce"]), R, cfg.vocab, d, K.P(gs[0:1]), K.P(dlog), self.Vp, K.stream_ptr())
             dfl = self._e(R, d, dtype=F32)
             K.mm(dlog, self.W["llm.lm_head"], dfl, tb=False)  # [R,Vp] @ [Vp,d]
             K.call("slx_scatter_rows", K.P(dfl), d, K.P(dplan["loss_pos"]), R, d, K.P(dfeat), d, 1, K.stream_ptr())

@@ -302,6 +302,9 @@ for _n, _a in {
     "slx_act_bwd": [_vp, _vp, _vp, _I, _i, _vp],
     "slx_ce_fwd": [_vp, _I, _vp, _I, _i, _vp, _vp, _vp],
     "slx_ce_bwd": [_vp, _I, _vp, _vp, _I, _i, _vp, _vp, _I, _vp],
+    "slx_lmhead_ce_ws_floats": [_I, _i],
+    "slx_lmhead_ce_fwd": [_vp, _I, _vp, _I, _vp, _I, _i, _i, _vp, _vp, _vp, _I, _vp],
+    "slx_lmhead_ce_bwd": [_vp, _I, _vp, _I, _vp, _vp, _I, _i, _i, _vp, _vp, _I, _vp],
     "slx_wp_loss_fwd": [_vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp],
     "slx_wp_loss_bwd": [_vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp],
     "slx_affine": [_vp, _I, _f, _f, _vp, _vp],
