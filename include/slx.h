@@ -98,7 +98,11 @@ int slx_gemm_bf16_pair(const slx_gemm_desc* d1, const slx_gemm_desc* d2, slx_str
  * Replaces flash-attn 2.7.0.post2 (README.md:67-68) inside the InternVL2-1B remote code:
  * InternViT non-causal MHA (internvl2_model.py:114 -> extract_feature) and Qwen2 causal GQA with
  * key padding (driving.py:217-223, attention_mask = inputs_mask, valid-first layout).
- * q/k/v/o: token-major rows [B*S, ld], head h at columns h*64..h*64+63.                       */
+ * q/k/v/o: token-major rows [B*S, ld], head h at columns h*64..h*64+63.
+ * Deviation: the key-padding mask is a per-sequence valid-key COUNT (seqlens), i.e. keys [0, seqlens[b]) valid.
+ * That is the only layout AdaptorList.forward produces (adaptors.py: inputs are packed valid-first, padding
+ * after); an arbitrary [B, S] mask (holes, left padding of keys) is not expressible here, and the Python seam
+ * (vlm.py _valid_lengths) raises NotImplementedError for one instead of silently mis-masking.        */
 typedef struct slx_attn_desc {
   int B, S, Hq, Hkv, head_dim, causal;
   const void* q; int64_t ldq;

@@ -25,10 +25,6 @@ namespace slx {
 // Thread-local error string (the C-ABI's slx_last_error()).
 void set_error(const char* fmt, ...);
 
-// Fork/join onto a per-thread side stream (errors.hip): fork returns the side stream (nullptr on failure),
-// ordered after the work already queued on `main`; join orders `main` after the side stream's work.
-hipStream_t side_fork(hipStream_t main);
-int side_join(hipStream_t main);
 
 #define SLX_CHECK_ARG(cond, ...)            \
   do {                                      \

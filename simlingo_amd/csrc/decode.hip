@@ -426,10 +426,14 @@ __global__ __launch_bounds__(256) void dec_attn_kernel(DecAttnArgs a) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (t0) tr(a, 5);
-  if (tid == 0) last_s = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ns - 1;
+  if (tid == 0) {  // release (cumulative over the barrier) this split's partials, then arrive
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    last_s = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ns - 1;
+  }
   __syncthreads();
   if (t0) tr(a, 6);
   if (!last_s) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   if (a.trace) tr(a, 8);
   // the last arriver merges the ns partials of kv head g: lane = dim of heads wave, wave + 4; every (m, l, o)
   // of its splits is loaded at once (kMergeBatch splits per round trip), the weights computed per lane

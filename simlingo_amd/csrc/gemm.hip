@@ -1369,10 +1369,13 @@ __device__ __forceinline__ void v3_remainder(const GemmArgs& p, int u) {
       }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (tid == 0)
+  if (tid == 0) {  // release (cumulative over the barrier) the group's partials, then arrive
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     last_s = __hip_atomic_fetch_add(p.rem_cnt + cg, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == p.rem_nsplit - 1;
+  }
   __syncthreads();
   if (!last_s) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the last arriver sees every split's partials
   // last arriver: column n0 + (tid % CG), rows tid / CG, + 2, ...; four rows x up to 16 splits (64 agent-scope loads)
   // in flight per thread, so the group's epilogue costs a round trip or two, not one per split
   OutT* C = reinterpret_cast<OutT*>(p.C);

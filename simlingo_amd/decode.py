@@ -262,6 +262,11 @@ class GreedyDecoder:
                 break
         self._begin()  # records the last token (no-op after EOS)
         ev[2].record()
+        if FUSE_O and int(self.sync[:, 2].max().item()):
+            # a fused attention + O launch timed out waiting for its attention workgroups and skipped its O rows:
+            # the residual stream, hence every later token, is wrong (dec_attn_o_kernel, attention.hip)
+            self.sync[:, 2].zero_()
+            raise RuntimeError("slx_dec_attn_o: attention hand-off timed out; generated tokens are invalid")
         n = int(self.state[1].item())
         self.last_timing = {"prefill_ms": ev[0].elapsed_time(ev[1]), "decode_ms": ev[1].elapsed_time(ev[2]),
                             "decode_steps": done_steps}

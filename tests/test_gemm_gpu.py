@@ -244,7 +244,8 @@ def test_gemm_dropmask_swiglu_epilogue(dev, p, use_bits, resid_bf16):
                                    (K.EPI_STORE, 1000)])
 def test_gemm_colsum_bias_grad(dev, epi, M, variant):
     """colsum: the epilogue adds the column sums of its f32 output into a [N] vector (fc1.b's gradient from the
-    GELU_BWD dgrad), including the M % 256 remainder that runs on the side stream."""
+    GELU_BWD dgrad). M = 16400 (remainder 16) and 2308 (remainder 4) fold their M % 256 rows into the main launch's
+    last tiles; M = 1000 (remainder 232 > 64) runs them as a peeled 128-row-tile pass instead."""
     N, Kd = 512, 256
     g = torch.Generator(device=dev).manual_seed(M + epi)
     dy = torch.randn(M, Kd, device=dev, generator=g).bfloat16()
@@ -266,6 +267,53 @@ def test_gemm_colsum_bias_grad(dev, epi, M, variant):
         ref = pre
     torch.testing.assert_close(out.float(), ref, atol=3e-2 * Kd ** 0.5 / 16, rtol=2e-2)
     torch.testing.assert_close(cs, 0.5 + ref.sum(0), atol=2e-3 * M ** 0.5, rtol=1e-3)
+
+
+_FOLD_SCRIPT = r"""
+import sys, torch
+sys.path.insert(0, sys.argv[1])
+from simlingo_amd import kernels as K
+dev = torch.device("cuda")
+g = torch.Generator(device=dev).manual_seed(5)
+for M in (1088, 16400):
+    dy = torch.randn(M, 256, device=dev, generator=g).bfloat16()
+    w = torch.randn(256, 512, device=dev, generator=g).bfloat16() * 0.1
+    h = torch.randn(M, 512, device=dev, generator=g).bfloat16()
+    out = torch.empty(M, 512, device=dev, dtype=torch.bfloat16)
+    cs = torch.full((512,), 0.5, device=dev)
+    K.mm(dy, w, out, tb=False, epi=K.EPI_GELU_BWD, aux=h, ldaux=512, colsum=cs, variant=7)
+    acc = torch.full((M, 512), 0.25, device=dev)
+    K.mm(dy, w, acc, tb=False, accumulate=True, variant=7)
+    torch.cuda.synchronize()
+    torch.save({"out": out.float().cpu(), "cs": cs.cpu(), "acc": acc.cpu()}, sys.argv[2] + f"_{M}.pt")
+"""
+
+
+@pytest.mark.parametrize("fold", ["1", "0"])
+def test_gemm_fold_remainder_accumulate_and_unfolded_path(dev, fold, tmp_path):
+    """The folded M-remainder (M % 256 <= 64 rows summed into the main launch's last tiles through the arrival
+    hand-off) with a 64-row remainder (M = 1088) and with 16 rows (16400), in the GELU'+colsum epilogue and in an
+    accumulating f32 store; SLX_GEMM_FOLD_REM=0 runs the same remainder as its own split-K + rows-epilogue launches
+    (gemm_remainder + rows_epilogue with colsum). The env var is read once per process, so each form runs in a child
+    process (the GPU work is a few ms)."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, SLX_GEMM_FOLD_REM=fold)
+    subprocess.run([sys.executable, "-c", _FOLD_SCRIPT, root, str(tmp_path / "r")], env=env, check=True, timeout=240)
+    g = torch.Generator(device=dev).manual_seed(5)
+    for M in (1088, 16400):
+        dy = torch.randn(M, 256, device=dev, generator=g).bfloat16()
+        w = torch.randn(256, 512, device=dev, generator=g).bfloat16() * 0.1
+        h = torch.randn(M, 512, device=dev, generator=g).bfloat16()
+        r = torch.load(tmp_path / f"r_{M}.pt", weights_only=True)
+        pre = dy.float() @ w.float()
+        x = h.float()
+        ref = pre * (0.5 * (1 + torch.erf(x / 2 ** 0.5)) + x * torch.exp(-0.5 * x * x) / (2 * torch.pi) ** 0.5)
+        torch.testing.assert_close(r["out"].to(dev), ref, atol=3e-2, rtol=2e-2)
+        torch.testing.assert_close(r["cs"].to(dev), 0.5 + ref.sum(0), atol=2e-3 * M ** 0.5, rtol=1e-3)
+        torch.testing.assert_close(r["acc"].to(dev), 0.25 + pre, atol=2e-3, rtol=1e-3)
 
 
 def test_batched_splitk_accumulate_tn(dev):
