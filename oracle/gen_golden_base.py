@@ -1,7 +1,7 @@
-"""Generate tests/golden/base_tiny.npz (SimLingo-Base training step) from the REFERENCE code.
+"""Generate tests/golden/base_tiny.npz and base_full1.npz (SimLingo-Base training step) from the REFERENCE code.
 
 ORACLE TOOLING — test infrastructure only; runs in the build container where /root/reference exists:
-    python oracle/gen_golden_base.py
+    python oracle/gen_golden_base.py [tiny|full1]
 
 Runs the reference's own Python wherever it imports offline:
   * LingoLlavaNextModel.forward_image (simlingo_base_training/models/encoder/llavanext_model.py:45-178) on a
@@ -39,7 +39,7 @@ from simlingo_base_training.models.encoder.llavanext_model import LingoLlavaNext
 from simlingo_base_training.models.utils import summarise_losses  # noqa: E402
 from transformers import CLIPVisionConfig, LlamaConfig, LlamaModel, LlavaNextConfig  # noqa: E402
 
-from simlingo_amd.base_config import base_tiny_config  # noqa: E402
+from simlingo_amd.base_config import base_config, base_tiny_config  # noqa: E402
 from simlingo_amd.base_params import base_specs, init_base_params  # noqa: E402
 from simlingo_amd.base_types import make_base_batch  # noqa: E402
 
@@ -194,11 +194,25 @@ def grads_by_name(cfg, m):
     return G
 
 
-def generate(seed=5, B=2):
+# Full-width case: CLIP ViT-L/14-336 width (1024, 16 heads, FFN 4096, 577 tokens per 336 tile),
+# the 4096-wide LLaVA-NeXT projector, embed 512, Llama-tiny width 512, the 359 x 1024 frame's 2-tile anyres merge
+# (200 image tokens), depth cut to 1 used CLIP layer (+ the unused last one) and 1 Llama layer so the reference's CPU
+# forward/backward finishes in seconds.
+FULL1 = dict(vit_layers=2, llm_layers=1)
+CASES = {"tiny": (base_tiny_config, {}, 5, 2, 0.05, "base_tiny.npz"),
+         "full1": (base_config, FULL1, 9, 2, 0.02, "base_full1.npz")}
+
+
+def case_config(name):
+    mk, kw, seed, B, std, fname = CASES[name]
+    return mk(**kw), seed, B, std, fname
+
+
+def generate(name="tiny"):
     from oracle.gen_golden import grad_digest, param_checksum
-    cfg = base_tiny_config()
+    cfg, seed, B, std, fname = case_config(name)
     torch.manual_seed(seed)
-    P = init_base_params(cfg, seed=seed, std=0.05)
+    P = init_base_params(cfg, seed=seed, std=std)
     ex = make_base_batch(cfg, B=B, seed=seed + 1)
     m = build_reference(cfg, P)
     out, loss_dict, x = reference_forward_loss(m, ex)
@@ -207,7 +221,7 @@ def generate(seed=5, B=2):
     names = [s.name for s in base_specs(cfg)]
     assert sorted(G) == sorted(names), set(names) ^ set(G)
     di, dl = ex.driving_input, ex.driving_label
-    arrays = {"seed": np.asarray(seed), "B": np.asarray(B),
+    arrays = {"seed": np.asarray(seed), "B": np.asarray(B), "std": np.asarray(std),
               "out.loss": out.loss.detach().numpy(),
               "out.route_loss": out.loss_averages["route_loss"].detach().numpy(),
               "out.speed_wps_loss": out.loss_averages["speed_wps_loss"].detach().numpy(),
@@ -221,12 +235,12 @@ def generate(seed=5, B=2):
         for kk, vv in grad_digest(v.detach()).items():
             arrays[kk + "." + k] = vv
     os.makedirs(OUT, exist_ok=True)
-    path = os.path.join(OUT, "base_tiny.npz")
+    path = os.path.join(OUT, fname)
     np.savez_compressed(path, **arrays)
     print(f"wrote {path}: loss={out.loss.item():.6f} route={arrays['out.route_loss']:.6f} "
           f"speed={arrays['out.speed_wps_loss']:.6f} tokens={x.shape[1]}")
 
 
 if __name__ == "__main__":
-    torch.set_num_threads(4)
-    generate()
+    torch.set_num_threads(8)
+    generate(sys.argv[1] if len(sys.argv) > 1 else "tiny")

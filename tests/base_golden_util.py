@@ -1,21 +1,30 @@
-"""Rebuild the SimLingo-Base golden case (tests/golden/base_tiny.npz, made by oracle/gen_golden_base.py)."""
+"""Rebuild the SimLingo-Base golden cases (tests/golden/base_tiny.npz, base_full1.npz, made by
+oracle/gen_golden_base.py)."""
 import os
 
 import numpy as np
 import torch
 
-from simlingo_amd.base_config import base_tiny_config
+from simlingo_amd.base_config import base_config, base_tiny_config
 from simlingo_amd.base_params import init_base_params
 from simlingo_amd.base_types import make_base_batch
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 
-def load_base_case():
-    z = np.load(os.path.join(GOLDEN, "base_tiny.npz"), allow_pickle=False)
-    cfg = base_tiny_config()
+# the cases oracle/gen_golden_base.py writes: tiny widths, and full1 (CLIP-L / 4096 projector / Llama-tiny widths,
+# 1 used CLIP layer + 1 Llama layer)
+CASES = {"tiny": (base_tiny_config, {}, "base_tiny.npz"),
+         "full1": (base_config, dict(vit_layers=2, llm_layers=1), "base_full1.npz")}
+
+
+def load_base_case(name: str = "tiny"):
+    mk, kw, fname = CASES[name]
+    z = np.load(os.path.join(GOLDEN, fname), allow_pickle=False)
+    cfg = mk(**kw)
     seed, B = int(z["seed"]), int(z["B"])
-    P = init_base_params(cfg, seed=seed, std=0.05)
+    std = float(z["std"]) if "std" in z else 0.05
+    P = init_base_params(cfg, seed=seed, std=std)
     for k, v in P.items():
         t = v.double()
         got = np.asarray([t.sum().item(), t.abs().sum().item(), t.pow(2).sum().item()])
