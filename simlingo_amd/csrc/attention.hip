@@ -326,7 +326,11 @@ __device__ __forceinline__ void bwd_kv_chunk(const char* Ql, const char* Dl, con
   for (int qa = 0; qa < 2; ++qa) {
     f32x16 sp, dp;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) { sp[r] = 0.f; dp[r] = 0.f; }
+    for (int g = 0; g < 4; ++g) {  // dP^T starts from -delta of each register's query (row constants in LDS, negated)
+      const f32x4 D4 = *reinterpret_cast<const f32x4*>(del_l + qa * 32 + 8 * g + 4 * hl);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { sp[4 * g + e] = 0.f; dp[4 * g + e] = D4[e]; }
+    }
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) {
       sp = mfma32(row_frag(Ql, qa * 32, kk, lane), kf[kk], sp);
@@ -336,7 +340,6 @@ __device__ __forceinline__ void bwd_kv_chunk(const char* Ql, const char* Dl, con
     for (int g = 0; g < 4; ++g) {
       const int ql = qa * 32 + 8 * g + 4 * hl;  // local query of register 4g
       const f32x4 L4 = *reinterpret_cast<const f32x4*>(lse_l + ql);
-      const f32x4 D4 = *reinterpret_cast<const f32x4*>(del_l + ql);
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int r = 4 * g + e;
@@ -347,7 +350,7 @@ __device__ __forceinline__ void bwd_kv_chunk(const char* Ql, const char* Dl, con
           p = ok ? p : 0.f;
         }
         sp[r] = p;
-        dp[r] = p * (dp[r] - D4[e]);
+        dp[r] = p * dp[r];
       }
     }
 #pragma unroll
@@ -436,7 +439,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kv_kernel(AttnArgs a) {
     if (tid < 128) {
       const int qi = qc + (tid & 63);
       const long base = ((long)b * a.Hq + h) * S;
-      ld = qi < S ? (tid < 64 ? a.lse[base + qi] : a.delta[base + qi]) : 0.f;
+      ld = qi < S ? (tid < 64 ? a.lse[base + qi] : -a.delta[base + qi]) : 0.f;  // delta staged negated
     }
   };
   auto commit = [&](int buf, const uint4 (&rq)[2], const uint4 (&rd)[2], float ld) {
@@ -522,16 +525,18 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kv_kernel(AttnArgs a) {
 // (~1.3 TB/s chip-wide), which bounded the single-kernel backward.
 template <bool MASK>
 __device__ __forceinline__ void bwd_dq_tile(const char* Kl, const char* Vl, const bf16x8 (&qf)[4], const bf16x8 (&df)[4],
-                                            f32x16& dq0, f32x16& dq1, float c, float lse, float dlt, int key0,
+                                            f32x16& dq0, f32x16& dq1, float c, float lse, const f32x16& negd, int key0,
                                             int kvlen, int myq, bool causal, int lane) {
   const int hl = lane >> 5;
   f32x16 s[2], dp[2];
 #pragma unroll
   for (int kb = 0; kb < 2; ++kb) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) { s[kb][r] = 0.f; dp[kb][r] = 0.f; }
+    for (int r = 0; r < 16; ++r) s[kb][r] = 0.f;
+    s[kb] = mfma32(row_frag(Kl, kb * 32, 0, lane), qf[0], s[kb]);
+    dp[kb] = mfma32(row_frag(Vl, kb * 32, 0, lane), df[0], negd);  // dP^T - delta: the chain starts from -delta
 #pragma unroll
-    for (int kk = 0; kk < 4; ++kk) {
+    for (int kk = 1; kk < 4; ++kk) {
       s[kb] = mfma32(row_frag(Kl, kb * 32, kk, lane), qf[kk], s[kb]);
       dp[kb] = mfma32(row_frag(Vl, kb * 32, kk, lane), df[kk], dp[kb]);
     }
@@ -546,7 +551,7 @@ __device__ __forceinline__ void bwd_dq_tile(const char* Kl, const char* Vl, cons
         const bool ok = (key < kvlen) & (!causal | (key <= myq));
         p = ok ? p : 0.f;
       }
-      dp[kb][r] = p * (dp[kb][r] - dlt);
+      dp[kb][r] = p * dp[kb][r];
     }
 #pragma unroll
   for (int kb = 0; kb < 2; ++kb)
@@ -598,6 +603,9 @@ __global__ __launch_bounds__(256, ATTN_DQ_OCC) void attn_bwd_dq_kernel(AttnArgs 
     dlt += __shfl_xor(dlt, 32, 64);
     if (hl == 0 && active && myq < S) const_cast<float*>(a.delta)[li] = dlt;
   }
+  f32x16 negd;  // -delta of this lane's query, the dP^T chains' initial accumulator
+#pragma unroll
+  for (int r = 0; r < 16; ++r) negd[r] = -dlt;
   int kend = kvlen;
   if (a.causal) kend = min(kend, qb * 128 + 128);
   const int nt = (kend + 63) / 64;
@@ -620,8 +628,8 @@ __global__ __launch_bounds__(256, ATTN_DQ_OCC) void attn_bwd_dq_kernel(AttnArgs 
     }
     if (active) {
       const int kfull = a.causal ? min(kvlen, q0 + 1) : kvlen;
-      if ((t + 1) * 64 <= kfull) bwd_dq_tile<false>(Kl, Vl, qf, df, dq0, dq1, c, lse, dlt, t * 64, kvlen, myq, false, lane);
-      else bwd_dq_tile<true>(Kl, Vl, qf, df, dq0, dq1, c, lse, dlt, t * 64, kvlen, myq, a.causal, lane);
+      if ((t + 1) * 64 <= kfull) bwd_dq_tile<false>(Kl, Vl, qf, df, dq0, dq1, c, lse, negd, t * 64, kvlen, myq, false, lane);
+      else bwd_dq_tile<true>(Kl, Vl, qf, df, dq0, dq1, c, lse, negd, t * 64, kvlen, myq, a.causal, lane);
     }
     if (t + 1 < nt) {
       char* nx = smem + ((t + 1) & 1) * 16384;

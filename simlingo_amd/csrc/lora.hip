@@ -563,7 +563,9 @@ extern "C" int slx_lora_bwd(const slx_lora_bwd_desc* d, slx_stream_t stream) {
   a.dxb = (bf16*)d->dx_bf16; a.lddxb = d->lddx_bf16;
   a.sc = 1.0f / (1.0f - d->p);
   const int cb = d->Kin / 128;
-  int nch = (512 + cb - 1) / cb;  // ~2 blocks per CU
+  // M chunks: fewer chunks mean fewer f32 atomics into dA (nch x sites x 32 x Kin), more mean more blocks
+  static const int tgt = [] { const char* e = getenv("SLX_LORA_DA_BLOCKS"); return e ? atoi(e) : 512; }();
+  int nch = (tgt + cb - 1) / cb;
   int mchunk = (int)((d->M + nch - 1) / nch);
   mchunk = ((mchunk + 63) / 64) * 64;
   a.mchunk = mchunk < 64 ? 64 : mchunk;

@@ -25,8 +25,11 @@ def run(cfg, P, ex, dev):
     return eng, out4.cpu(), rp.cpu(), sp.cpu()
 
 
-def test_base_engine_vs_oracle(dev):
-    cfg, P, ex, _ = load_base_case()
+@pytest.mark.parametrize("case", ["tiny", "full1"])
+def test_base_engine_vs_oracle(dev, case):
+    """tiny widths, and full1: CLIP-L/14-336 width (1024 x 16 heads, 577-token tiles), the 4096-wide projector,
+    the 2-tile anyres merge of the 359 x 1024 frame, Llama-tiny width (1 used CLIP layer, 1 Llama layer)."""
+    cfg, P, ex, _ = load_base_case(case)
     ref, grads = O.loss_and_grads(P, cfg, ex)
     eng, out4, rp, sp = run(cfg, P, ex, dev)
     for got, k in ((out4[0], "loss"), (out4[2], "route_loss"), (out4[3], "speed_wps_loss")):

@@ -25,10 +25,15 @@ sys.path.insert(0, ROOT)
 SHAPES = {  # M = images x tokens, N = FFN, K = width (bench.py probe shapes)
     "vla": dict(M=16 * 1025, N=4096, K=1024, epi="GELU", tag="vla_b8"),
     "base": dict(M=64 * 577, N=4096, K=1024, epi="QGELU", tag="base_b32"),
+    # the VLA step's dominant kernel: the InternViT fc2.w + fc1.w weight-gradient pair (engine.py "vit.wgrad_fc"),
+    # one slx_gemm_bf16_pair launch of two accumulating TN GEMMs with K = tokens; recorded as the "_pair" record
+    "vla_pair": dict(M=16 * 1025, N=4096, K=1024, epi="PAIR", tag="vla_b8_pair"),
 }
 
 
 def algorithmic_bytes(s):
+    if s["epi"] == "PAIR":  # dY, GELU output, dH, LN2 output (bf16) read once; both f32 dW read + written
+        return s["M"] * 2 * (2 * s["K"] + 2 * s["N"]) + 2 * 2 * 4 * s["N"] * s["K"]
     # A [M,K] bf16 + W [N,K] bf16 + bias f32 read; activation [M,N] bf16 + pre-activation aux [M,N] bf16 written
     return 2 * s["M"] * s["K"] + 2 * s["N"] * s["K"] + 4 * s["N"] + 2 * 2 * s["M"] * s["N"]
 
@@ -39,6 +44,20 @@ def run(cfg, calls):
     s = SHAPES[cfg]
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev).manual_seed(0)
+    if s["epi"] == "PAIR":  # exactly engine.py's mm_pair call: (g, hact, dW_fc2), (dh, h2, dW_fc1), TN, accumulate
+        M, N, D = s["M"], s["N"], s["K"]
+        gy = (torch.randn(M, D, device=dev, generator=g) * 0.1).to(torch.bfloat16)
+        hact = (torch.randn(M, N, device=dev, generator=g) * 0.5).to(torch.bfloat16)
+        dh = (torch.randn(M, N, device=dev, generator=g) * 0.1).to(torch.bfloat16)
+        h2 = (torch.randn(M, D, device=dev, generator=g) * 0.5).to(torch.bfloat16)
+        dw2 = torch.zeros(D, N, device=dev)
+        dw1 = torch.zeros(N, D, device=dev)
+        torch.cuda.synchronize()
+        for _ in range(calls):
+            K.mm_pair((gy, hact, dw2), (dh, h2, dw1))
+        torch.cuda.synchronize()
+        print(json.dumps({"config": cfg, "calls": calls, **s}))
+        return
     x = (torch.randn(s["M"], s["K"], device=dev, generator=g) * 0.5).to(torch.bfloat16)
     w = (torch.randn(s["N"], s["K"], device=dev, generator=g) * 0.03).to(torch.bfloat16)
     b = torch.randn(s["N"], device=dev, generator=g) * 0.1
