@@ -1169,23 +1169,241 @@ __device__ __forceinline__ bool v3_split_reduce(const GemmArgs& p, int tile, f32
   return true;
 }
 
+// Tile origin of tile index bid (after the XCD remap): GROUP = 4 row tiles x all column tiles per group.
+// mshift_last: the partial last M tile is shifted up to end at M, so every tile is full; the rows it shares with
+// the previous tile are recomputed bit-identically (same K order) and stored twice with the same values.
+__device__ __forceinline__ void v3_origin(const GemmArgs& p, int bid, int& m0, int& n0) {
+  constexpr int GROUP = 4;
+  const int npg = GROUP * p.tilesN;
+  const int fm = (bid / npg) * GROUP;
+  const int gs = min(p.tilesM - fm, GROUP);
+  const int tm = fm + (bid % npg) % gs;
+  const int tn = (bid % npg) / gs;
+  m0 = (p.mshift_last && tm == p.tilesM - 1) ? p.M - V3_BM : tm * V3_BM;
+  n0 = tn * V3_BN;
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm_n() {
+  static_assert(N >= 0 && N <= 63, "vmcnt is 6 bits on gfx950");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// ---- FE: register-direct epilogue of the swapped-operand (SW) accumulator layout, with the next tile's first two
+// K-steps already in flight ----
+// The LDS-staged epilogue runs while the whole CU's matrix pipes idle, and every CU of a round stores its tile at the
+// same moment: in the K-sweep of tools/gemm_ksweep.py the fixed cost per 256 x 256 tile is 11-14 us with bf16 output
+// and 21 us with f32 output against ~1.4 us per 64-deep K-step - a third of an InternViT K = 1024 GEMM. Here the
+// epilogue needs no LDS, so the next tile's stages 0 and 1 (A and B) are issued by LDS-DMA before the first store:
+// the next tile's first wait then covers only its own loads (gfx950 counts stores in vmcnt, in issue order), and the
+// stores drain under the epilogue arithmetic and the first two K-steps instead of in front of them.
+// Lane l of a wave holds, in acc[a][b], rows 16a + (l & 15) and columns 16b + 4(l >> 4) + r (r = 0..3) of the wave's
+// 128 x 64 sub-tile. bf16 rows leave as 16-B stores after one v_permlane16_swap per packed dword pair (blocks b, b+1):
+// row-group g = l >> 4 then holds 8 consecutive columns, 16(b + (g & 1)) + 8(g >> 1) .. + 7.
+// Eligible (host side, fe_ok): ksplit 1, batch 1, whole tiles (M % 256 == 0, folded remainder or shifted last tile),
+// N % 256 == 0, 16-B aligned rows, no accumulation, K >= 192, epilogues STORE / GELU / QGELU / RESID_LS / GELU_BWD /
+// QGELU_BWD (colsum allowed).
+template <int EPI, typename OutT> struct FeStores { static constexpr int N = sizeof(OutT) == 2 ? 16 : 32; };
+template <typename OutT> struct FeStores<EPI_GELU, OutT> { static constexpr int N = 32; };
+template <typename OutT> struct FeStores<EPI_QGELU, OutT> { static constexpr int N = 32; };
+template <typename OutT> struct FeStores<EPI_RESID_LS, OutT> { static constexpr int N = 32; };  // (+ 16 with aux_out)
+
+__device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
+  bf16x2 v;
+  v[0] = (bf16)a;
+  v[1] = (bf16)b;
+  return __builtin_bit_cast(uint32_t, v);
+}
+// sum over the 16 lanes of a row group (every lane gets the sum): quad swaps, half-row mirror, row mirror
+__device__ __forceinline__ float row16_sum(float x) {
+  x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0xB1, 0xF, 0xF, false));
+  x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x4E, 0xF, 0xF, false));
+  x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x141, 0xF, 0xF, false));
+  x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x140, 0xF, 0xF, false));
+  return x;
+}
+// exchange with lane ^ 8 inside each 16-lane row group (DPP row_ror:8)
+__device__ __forceinline__ uint32_t xch8(uint32_t v) { return __builtin_amdgcn_update_dpp(0u, v, 0x128, 0xF, 0xF, false); }
+__device__ __forceinline__ uint4 xch8(uint4 v) { return make_uint4(xch8(v.x), xch8(v.y), xch8(v.z), xch8(v.w)); }
+__device__ __forceinline__ uint4 sel4(bool c, uint4 a, uint4 b) {
+  return make_uint4(c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z, c ? a.w : b.w);
+}
+
+// Stores of one 16-row block of the wave's sub-tile (y[b][r] in the register layout) as whole 128-B lines: each
+// store instruction covers 8 rows x 128 B (bf16: a row's 64 columns; f32: half of them), never half lines (16 rows x
+// 64 B per instruction measured slower than the LDS-staged epilogue on a single-round GEMM). bf16: one
+// v_permlane16_swap per packed dword pair of blocks (b, b + 1) gives lane (rr, g) 8 consecutive columns
+// P = 16(g & 1) + 8(g >> 1) .. + 7 of blocks 0/1 and Q = 32 + P of blocks 2/3; then lanes rr and rr ^ 8 swap Q for P
+// (DPP), so store 1 writes rows 0-7 (P from rr < 8, Q from rr >= 8) and store 2 rows 8-15. f32: per block pair the
+// same row-half swap of the two 16-B chunks.
+__device__ __forceinline__ void fe_st_bf16(bf16* base, long ld, int row0, int col0, int lane, const float (&y)[4][4]) {
+  const int rr = lane & 15, g = lane >> 4;
+  uint4 P, Q;
+  {
+    const auto s0 = __builtin_amdgcn_permlane16_swap(pk_bf16(y[0][0], y[0][1]), pk_bf16(y[1][0], y[1][1]), false, false);
+    const auto s1 = __builtin_amdgcn_permlane16_swap(pk_bf16(y[0][2], y[0][3]), pk_bf16(y[1][2], y[1][3]), false, false);
+    P = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+    const auto t0 = __builtin_amdgcn_permlane16_swap(pk_bf16(y[2][0], y[2][1]), pk_bf16(y[3][0], y[3][1]), false, false);
+    const auto t1 = __builtin_amdgcn_permlane16_swap(pk_bf16(y[2][2], y[2][3]), pk_bf16(y[3][2], y[3][3]), false, false);
+    Q = make_uint4(t0[0], t1[0], t0[1], t1[1]);
+  }
+  const bool lo = rr < 8;
+  const uint4 recv = xch8(lo ? Q : P);
+  bf16* p1 = base + (long)(row0 + (rr & 7)) * ld + col0 + 16 * (g & 1) + 8 * (g >> 1) + (lo ? 0 : 32);
+  *reinterpret_cast<uint4*>(p1) = lo ? P : recv;
+  *reinterpret_cast<uint4*>(p1 + 8 * ld) = lo ? recv : Q;
+}
+__device__ __forceinline__ void fe_st_f32(float* base, long ld, int row0, int col0, int lane, const float (&y)[4][4]) {
+  const int rr = lane & 15, g = lane >> 4;
+  const bool lo = rr < 8;
+  float* p1 = base + (long)(row0 + (rr & 7)) * ld + col0 + 4 * g + (lo ? 0 : 16);
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {  // block pairs (0, 1) and (2, 3)
+    const uint4 F0 = make_uint4(__float_as_uint(y[2 * h][0]), __float_as_uint(y[2 * h][1]), __float_as_uint(y[2 * h][2]),
+                                __float_as_uint(y[2 * h][3]));
+    const uint4 F1 = make_uint4(__float_as_uint(y[2 * h + 1][0]), __float_as_uint(y[2 * h + 1][1]),
+                                __float_as_uint(y[2 * h + 1][2]), __float_as_uint(y[2 * h + 1][3]));
+    const uint4 recv = xch8(lo ? F1 : F0);
+    *reinterpret_cast<uint4*>(p1 + 32 * h) = lo ? F0 : recv;
+    *reinterpret_cast<uint4*>(p1 + 32 * h + 8 * ld) = lo ? recv : F1;
+  }
+}
+
+template <int EPI, typename OutT, typename NextFn>
+__device__ __forceinline__ void fe_epilogue(const GemmArgs& p, OutT* __restrict__ C, const f32x4 (&acc)[8][4], int mw,
+                                            int nw, int lane, NextFn issue_next) {
+  const int rr = lane & 15, g = lane >> 4;
+  const int nc = nw + 4 * g;  // column of register 0 of block 0
+  constexpr bool kAux = EPI == EPI_GELU_BWD || EPI == EPI_QGELU_BWD;
+  constexpr bool kResid = EPI == EPI_RESID_LS;
+  constexpr bool kBias = EPI == EPI_STORE || EPI == EPI_GELU || EPI == EPI_QGELU || EPI == EPI_RESID_LS;
+  constexpr bool kCs = EPI == EPI_STORE || kAux;
+  // loads that must not wait behind the next tile's DMA are issued before it
+  f32x4 bias[4], lsv[4];
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    bias[b] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if constexpr (kBias) {
+      if (p.bias) bias[b] = *reinterpret_cast<const f32x4*>(p.bias + nc + 16 * b);
+    }
+    if constexpr (kResid) lsv[b] = *reinterpret_cast<const f32x4*>(p.ls + nc + 16 * b);
+  }
+  uint2 ax[4][4];  // bf16 pre-activations (GELU' epilogues), half the sub-tile at a time: 32 VGPRs
+  f32x4 rv[4][4];  // f32 residual rows, half the sub-tile at a time (RESID_LS): 64 VGPRs
+  if constexpr (kAux) {
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) ax[a][b] = *reinterpret_cast<const uint2*>(p.aux + (long)(mw + 16 * a + rr) * p.ldaux + nc + 16 * b);
+  }
+  if constexpr (kResid) {
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) rv[a][b] = *reinterpret_cast<const f32x4*>(p.resid + (long)(mw + 16 * a + rr) * p.ldr + nc + 16 * b);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  issue_next();
+  __builtin_amdgcn_sched_barrier(0);
+  float cs[4][4];
+#pragma unroll
+  for (int b = 0; b < 4; ++b)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) cs[b][r] = 0.f;
+#pragma unroll
+  for (int a = 0; a < 8; ++a) {
+    if (a == 4) {  // second half of the row inputs (waits behind the next tile's DMA, issued long before)
+      if constexpr (kResid) {
+#pragma unroll
+        for (int a2 = 0; a2 < 4; ++a2)
+#pragma unroll
+          for (int b = 0; b < 4; ++b)
+            rv[a2][b] = *reinterpret_cast<const f32x4*>(p.resid + (long)(mw + 16 * (4 + a2) + rr) * p.ldr + nc + 16 * b);
+      }
+      if constexpr (kAux) {
+#pragma unroll
+        for (int a2 = 0; a2 < 4; ++a2)
+#pragma unroll
+          for (int b = 0; b < 4; ++b)
+            ax[a2][b] = *reinterpret_cast<const uint2*>(p.aux + (long)(mw + 16 * (4 + a2) + rr) * p.ldaux + nc + 16 * b);
+      }
+    }
+    float y[4][4];
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) y[b][r] = acc[a][b][r] * p.alpha + bias[b][r];
+    if constexpr (EPI == EPI_STORE) {
+      if constexpr (sizeof(OutT) == 2) {
+        fe_st_bf16(reinterpret_cast<bf16*>(C), p.ldc, mw + 16 * a, nw, lane, y);
+      } else {
+        fe_st_f32(reinterpret_cast<float*>(C), p.ldc, mw + 16 * a, nw, lane, y);
+      }
+    } else if constexpr (EPI == EPI_GELU || EPI == EPI_QGELU) {
+      float h[4][4];
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) h[b][r] = (float)(bf16)y[b][r];
+      fe_st_bf16(p.aux_out, p.ldaux_out, mw + 16 * a, nw, lane, h);
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) h[b][r] = EPI == EPI_GELU ? gelu_erf(h[b][r]) : qgelu(h[b][r]);
+      fe_st_bf16(reinterpret_cast<bf16*>(C), p.ldc, mw + 16 * a, nw, lane, h);
+    } else if constexpr (EPI == EPI_RESID_LS) {
+      if (p.aux_out) fe_st_bf16(p.aux_out, p.ldaux_out, mw + 16 * a, nw, lane, y);
+      float o[4][4];
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[b][r] = rv[a & 3][b][r] + lsv[b][r] * y[b][r];
+      fe_st_f32(reinterpret_cast<float*>(C), p.ldc, mw + 16 * a, nw, lane, o);
+    } else if constexpr (kAux) {
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const bf16x4 hv = __builtin_bit_cast(bf16x4, ax[a & 3][b]);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) y[b][r] *= EPI == EPI_GELU_BWD ? gelu_erf_grad((float)hv[r]) : qgelu_grad((float)hv[r]);
+      }
+      fe_st_bf16(reinterpret_cast<bf16*>(C), p.ldc, mw + 16 * a, nw, lane, y);
+    }
+    if constexpr (kCs) {
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) cs[b][r] += y[b][r];
+    }
+  }
+  if constexpr (kCs) {
+    if (p.colsum) {  // the wave's 128 rows summed into the partial row of its first 64-row subtile, zeros in the second
+      float* w0 = p.colsum_ws + (long)(p.colsum_row0 + mw / 64) * p.N + nc;
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        f32x4 s;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) s[r] = row16_sum(cs[b][r]);
+        if (rr == 0) {
+          *reinterpret_cast<f32x4*>(w0 + 16 * b) = s;
+          *reinterpret_cast<f32x4*>(w0 + p.N + 16 * b) = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+      }
+    }
+  }
+}
+
 // One 256x256 output tile (tile index bid of p's grid after the XCD remap), K range of split blockIdx.y, batch z.
-template <bool AK, bool BKc, int EPI, typename OutT, bool SW>
-__device__ __forceinline__ void v3_tile(const GemmArgs& p, int bid, long z, char* smem) {
+// FE (with SW): register-direct epilogue; `pre` = this tile's stages 0 and 1 were issued by the previous tile's
+// epilogue; next_bid >= 0 = issue the next tile's stages 0 and 1 inside this tile's epilogue.
+template <bool AK, bool BKc, int EPI, typename OutT, bool SW, bool FE = false>
+__device__ __forceinline__ void v3_tile(const GemmArgs& p, int bid, long z, char* smem, bool pre = false,
+                                        int next_bid = -1) {
+  static_assert(!FE || SW, "the register-direct epilogue needs the swapped-operand accumulator layout");
   constexpr int NW = 8;
   constexpr int A_BYTES = V3_BM * BK * 2, B_BYTES = V3_BN * BK * 2;
   constexpr int STAGE = A_BYTES + B_BYTES;
-  const int tilesM = p.tilesM, tilesN = p.tilesN;
-  constexpr int GROUP = 4;
-  const int npg = GROUP * tilesN;
-  const int gid = bid / npg;
-  const int fm = gid * GROUP;
-  const int gs = min(tilesM - fm, GROUP);
-  const int tm = fm + (bid % npg) % gs;
-  const int tn = (bid % npg) / gs;
-  // mshift_last: the partial last M tile is shifted up to end at M, so every tile is full; the rows it shares with
-  // the previous tile are recomputed bit-identically (same K order) and stored twice with the same values.
-  const int m0 = (p.mshift_last && tm == tilesM - 1) ? p.M - V3_BM : tm * V3_BM, n0 = tn * V3_BN;
+  int m0, n0;
+  v3_origin(p, bid, m0, n0);
   const bf16* A = p.A + z * p.sA;
   const bf16* B = p.B + z * p.sB;
   OutT* __restrict__ C = reinterpret_cast<OutT*>(p.C) + z * p.sC;
@@ -1217,14 +1435,21 @@ __device__ __forceinline__ void v3_tile(const GemmArgs& p, int bid, long z, char
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // prologue: tile 0 (A and B) and tile 1's A pieces
-  dma_issue_range<AK, V3_BM, NW, 0, 4>(ra, smem, wave, kbeg, kend, p.lda, baseA, krA, okA);
-  dma_issue_range<BKc, V3_BN, NW, 0, 4>(rb, smem + A_BYTES, wave, kbeg, kend, p.ldb, baseB, krB, okB);
-  if (nk > 1) {
-    dma_issue_range<AK, V3_BM, NW, 0, 4>(ra, smem + STAGE, wave, kbeg + BK, kend, p.lda, baseA, krA, okA);
-    wait_vm<4>();
+  // FE: stores the previous tile's epilogue issued after this tile's stages 0 and 1 (a lower bound: waiting for
+  // fewer younger ops only waits longer)
+  constexpr int FES = FE ? FeStores<EPI, OutT>::N : 0;
+  if (FE && pre) {
+    wait_vm_n<8 + FES>();  // stage 0 landed; stage 1 (8 pieces) and the stores may still be in flight
   } else {
-    wait_vm<0>();
+    // prologue: tile 0 (A and B) and tile 1's A pieces
+    dma_issue_range<AK, V3_BM, NW, 0, 4>(ra, smem, wave, kbeg, kend, p.lda, baseA, krA, okA);
+    dma_issue_range<BKc, V3_BN, NW, 0, 4>(rb, smem + A_BYTES, wave, kbeg, kend, p.ldb, baseB, krB, okB);
+    if (nk > 1) {
+      dma_issue_range<AK, V3_BM, NW, 0, 4>(ra, smem + STAGE, wave, kbeg + BK, kend, p.lda, baseA, krA, okA);
+      wait_vm<4>();
+    } else {
+      wait_vm<0>();
+    }
   }
   v3_barrier();
   if (wr == 1) v3_barrier();  // the M-half-1 waves run one barrier behind
@@ -1236,7 +1461,8 @@ __device__ __forceinline__ void v3_tile(const GemmArgs& p, int bid, long z, char
     const char* Bs = As + A_BYTES;
     char* st1 = smem + ((t + 1) & 1) * STAGE;  // tile t+1
     char* st2 = smem + (t & 1) * STAGE;        // tile t+2 (this stage, free after q1)
-    const bool has1 = t + 1 < nk, has2 = t + 2 < nk;
+    const bool has2 = t + 2 < nk;
+    const bool has1 = t + 1 < nk && !(FE && pre && t == 0);  // (FE pre: stage 1's B came with the prefetch)
     const int k1 = kbeg + (t + 1) * BK, k2 = kbeg + (t + 2) * BK;
     // ---- q0
     v3_read<AK, BKc>(As, Bs, arow, bcol, lane, alo, blo);
@@ -1260,7 +1486,8 @@ __device__ __forceinline__ void v3_tile(const GemmArgs& p, int bid, long z, char
     // ---- q3
     if (has2) {
       dma_issue_range<AK, V3_BM, NW, 2, 2>(ra, st2, wave, k2, kend, p.lda, baseA, krA, okA);
-      wait_vm<4>();
+      if (FE && pre && t == 0) wait_vm_n<4 + FES>();  // stage 1 landed; the previous tile's stores may still drain
+      else wait_vm<4>();
     } else {
       wait_vm<0>();
     }
@@ -1270,6 +1497,24 @@ __device__ __forceinline__ void v3_tile(const GemmArgs& p, int bid, long z, char
   }
   if (wr == 0) v3_barrier();  // re-align the barrier counts of the two wave groups
 
+  if constexpr (FE) {
+    auto issue_next = [&]() {
+      if (next_bid < 0) return;
+      int mn, nn;
+      v3_origin(p, next_bid, mn, nn);
+      long bA[PA], bB[PB];
+      int kA[PA], kB[PB];
+      bool oA[PA], oB[PB];
+      dma_setup<AK, V3_BM, NW>(lane, wave, mn, p.M, p.lda, bA, kA, oA);
+      dma_setup<BKc, V3_BN, NW>(lane, wave, nn, p.N, p.ldb, bB, kB, oB);
+      dma_issue_range<AK, V3_BM, NW, 0, 4>(ra, smem, wave, kbeg, kend, p.lda, bA, kA, oA);
+      dma_issue_range<BKc, V3_BN, NW, 0, 4>(rb, smem + A_BYTES, wave, kbeg, kend, p.ldb, bB, kB, oB);
+      dma_issue_range<AK, V3_BM, NW, 0, 4>(ra, smem + STAGE, wave, kbeg + BK, kend, p.lda, bA, kA, oA);
+      dma_issue_range<BKc, V3_BN, NW, 0, 4>(rb, smem + STAGE + A_BYTES, wave, kbeg + BK, kend, p.ldb, bB, kB, oB);
+    };
+    fe_epilogue<EPI, OutT>(p, C, acc, m0 + arow, n0 + bcol, lane, issue_next);
+    return;
+  }
   bool reduced = false;
   if constexpr (EPI == EPI_STORE) {
     if (p.ksplit > 1 && p.split_ws) {
@@ -1432,6 +1677,26 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_v3_kernel(GemmArgs p) {
   for (int t = blockIdx.x; t < nwg; t += gridDim.x) {
     if (t != (int)blockIdx.x) __syncthreads();  // the previous tile's epilogue is done with the LDS
     v3_tile<AK, BKc, EPI, OutT, SW>(p, xcd_remap(t, nwg), blockIdx.z, smem);
+  }
+}
+
+// FE persistent kernel: each block walks its tiles with the next tile's first two K-steps issued inside the previous
+// tile's register-direct epilogue (no barrier between tiles: the epilogue uses no LDS).
+template <bool AK, bool BKc, int EPI, typename OutT>
+__global__ __launch_bounds__(512, 1) void gemm_bf16_v3fe_kernel(GemmArgs p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  if constexpr (AK) {
+    if (p.rem_r0 > 0 && (int)blockIdx.x < p.rem_nsplit * ((p.N + 255) / 256)) {
+      v3_remainder<BKc, EPI, OutT>(p, blockIdx.x);
+      __syncthreads();
+    }
+  }
+  const int nwg = p.tilesM * p.tilesN;
+  bool pre = false;
+  for (int t = blockIdx.x; t < nwg; t += gridDim.x) {
+    const int tn = t + (int)gridDim.x;
+    v3_tile<AK, BKc, EPI, OutT, true, true>(p, xcd_remap(t, nwg), 0, smem, pre, tn < nwg ? xcd_remap(tn, nwg) : -1);
+    pre = tn < nwg;
   }
 }
 
@@ -1674,14 +1939,17 @@ static int launch_v4(GemmArgs a, int batch, hipStream_t st) {
   return 0;
 }
 
-template <bool AK, bool BKc, int EPI, typename OutT, bool SW>
+template <bool AK, bool BKc, int EPI, typename OutT, bool SW, bool FE = false>
 static int launch_v3(GemmArgs a, int batch, hipStream_t st) {
   constexpr int LDS_RING = 2 * (V3_BM * BK * 2 + V3_BN * BK * 2);
-  constexpr int LDS_EP = 8 * 64 * EP_LD * 4 + 16;  // + the split-K role word
+  constexpr int LDS_EP = FE ? 0 : 8 * 64 * EP_LD * 4 + 16;  // + the split-K role word
   constexpr int LDS = LDS_RING > LDS_EP ? LDS_RING : LDS_EP;
+  const void* fn;
+  if constexpr (FE) fn = (const void*)gemm_bf16_v3fe_kernel<AK, BKc, EPI, OutT>;
+  else fn = (const void*)gemm_bf16_v3_kernel<AK, BKc, EPI, OutT, SW>;
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute((const void*)gemm_bf16_v3_kernel<AK, BKc, EPI, OutT, SW>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
     attr = true;
   }
   a.tilesM = a.rem_r0 > 0 ? a.rem_r0 / V3_BM : (a.M + V3_BM - 1) / V3_BM;  // folded remainder rows are not tiles
@@ -1704,9 +1972,24 @@ static int launch_v3(GemmArgs a, int batch, hipStream_t st) {
     if (a.rem_nsplit * ncg > gx) gx = a.rem_nsplit * ncg;
   }
   dim3 grid(gx, a.ksplit > 1 ? a.ksplit : 1, batch);
-  hipLaunchKernelGGL((gemm_bf16_v3_kernel<AK, BKc, EPI, OutT, SW>), grid, dim3(512), LDS, st, a);
+  if constexpr (FE) hipLaunchKernelGGL((gemm_bf16_v3fe_kernel<AK, BKc, EPI, OutT>), grid, dim3(512), LDS, st, a);
+  else hipLaunchKernelGGL((gemm_bf16_v3_kernel<AK, BKc, EPI, OutT, SW>), grid, dim3(512), LDS, st, a);
   SLX_LAUNCH_CHECK("slx_gemm_bf16(v3)");
   return 0;
+}
+
+// The FE member's eligibility (see fe_epilogue): whole 256 x 256 tiles, one K range, no accumulation, an epilogue it
+// implements. Anything else launches v3 with the swapped-operand LDS epilogue (variant 8).
+template <int EPI, typename OutT>
+static bool fe_ok(const GemmArgs& a, int batch) {
+  constexpr bool epi = EPI == EPI_STORE || EPI == EPI_GELU || EPI == EPI_QGELU || EPI == EPI_RESID_LS ||
+                       EPI == EPI_GELU_BWD || EPI == EPI_QGELU_BWD;
+  if (!epi || batch != 1 || a.ksplit > 1 || !a.vec_ok || a.accumulate || a.N % V3_BN != 0 || a.K % BK != 0 ||
+      a.K < 3 * BK)
+    return false;
+  if (EPI == EPI_STORE && a.split_stride) return false;
+  const int main_rows = a.rem_r0 > 0 ? a.rem_r0 : a.M;
+  return main_rows % V3_BM == 0 || (a.mshift_last && a.M >= V3_BM);
 }
 
 template <bool AK, bool BKc, int EPI, typename OutT>
@@ -1752,6 +2035,12 @@ static int launch_any(GemmArgs& a, int batch, hipStream_t st, int variant) {
     case 6: return launch_v2<AK, BKc, EPI, OutT, 256, 3>(a, batch, st);
     case 7: return launch_v3<AK, BKc, EPI, OutT, false>(a, batch, st);
     case 8: return launch_v3<AK, BKc, EPI, OutT, true>(a, batch, st);
+    case 11:
+      if constexpr (EPI == EPI_STORE || EPI == EPI_GELU || EPI == EPI_QGELU || EPI == EPI_RESID_LS ||
+                    EPI == EPI_GELU_BWD || EPI == EPI_QGELU_BWD) {
+        if (fe_ok<EPI, OutT>(a, batch)) return launch_v3<AK, BKc, EPI, OutT, true, true>(a, batch, st);
+      }
+      return launch_v3<AK, BKc, EPI, OutT, true>(a, batch, st);
     case 9: return launch_v4<AK, BKc, EPI, OutT, false>(a, batch, st);
     case 10: return launch_v4<AK, BKc, EPI, OutT, true>(a, batch, st);
     default: return launch<AK, BKc, EPI, OutT>(a, batch, st);
@@ -1936,11 +2225,11 @@ static int gemm_launch(const slx_gemm_desc* d, int v, hipStream_t st, int mshift
     a.vec_ok = ok ? 1 : 0;
   }
   const int batch = d->batch < 1 ? 1 : d->batch;
-  a.mshift_last = (v >= 7 && v <= 10) ? mshift_last : 0;
+  a.mshift_last = (v >= 7 && v <= 11) ? mshift_last : 0;
   a.ksplit = 1;
   a.kchunk = d->K;
   {  // split-K for under-filled grids (weight gradients): f32 atomics, >= 4 K-steps per split
-    int sp = rem_r0 ? 1 : force_split > 0 ? force_split : split_for(d, (v >= 7 && v <= 10) ? 7 : v, d->M, batch);  // (no split-K with a fold)
+    int sp = rem_r0 ? 1 : force_split > 0 ? force_split : split_for(d, (v >= 7 && v <= 11) ? 7 : v, d->M, batch);  // (no split-K with a fold)
     const int ksteps = (d->K + BK - 1) / BK;
     if (sp > 1) {
       const int per = ((ksteps + sp - 1) / sp) * BK;
@@ -1950,7 +2239,7 @@ static int gemm_launch(const slx_gemm_desc* d, int v, hipStream_t st, int mshift
       a.ksplit = sp;
       a.kchunk = ((ksteps + sp - 1) / sp) * BK;
       const long v3tiles = (long)((d->M + V3_BM - 1) / V3_BM) * ((d->N + V3_BN - 1) / V3_BN);
-      if ((v == 7 || v == 8) && batch == 1 && !split_stride && d->epilogue == SLX_EPI_STORE && d->out_f32 &&
+      if ((v == 7 || v == 8 || v == 11) && batch == 1 && !split_stride && d->epilogue == SLX_EPI_STORE && d->out_f32 &&
           split_ws_fits(d, v3tiles, sp)) {  // reduced inside the launch: plain stores, no pre-zeroed C
         a.split_ws = d->split_ws;
         a.split_cnt = reinterpret_cast<int*>(d->split_ws + d->split_ws_floats - kSplitCntInts);
@@ -2091,9 +2380,9 @@ extern "C" int slx_gemm_bf16(const slx_gemm_desc* d, slx_stream_t stream) {
   // swapped operands + batched-load epilogue, 9 / 10 = v4 (two workgroups per CU) without / with the swap.
   // SLX_V3_KIND picks the member the automatic choice launches (A/B hook).
   static const int kind_default = [] { const char* e = getenv("SLX_V3_KIND"); const int k = e ? atoi(e) : 7;
-                                       return k >= 7 && k <= 10 ? k : 7; }();
+                                       return k >= 7 && k <= 11 ? k : 7; }();
   int v3k = kind_default;
-  if (v >= 8 && v <= 10) { v3k = v; v = 7; }
+  if (v >= 8 && v <= 11) { v3k = v; v = 7; }
   else if (v == 7) v3k = 7;
   const int rem = d->M % V3_BM;
   const bool peel_ok = batch == 1 && d->epilogue != SLX_EPI_DROPMASK && d->epilogue != SLX_EPI_DROPMASK_SWIGLU &&

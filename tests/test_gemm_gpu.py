@@ -90,7 +90,7 @@ def test_gemm_split_k(dev, M, N, Kd, layout, accumulate):
     assert (C - ref).abs().max().item() < 2e-3 * Kd ** 0.5
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10])
+@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11])
 @pytest.mark.parametrize("layout", [K.GEMM_NT, K.GEMM_NN, K.GEMM_TN, K.GEMM_TT])
 def test_gemm_variants(dev, variant, layout):
     """Every main-loop variant (v1 register-staged, v2 LDS-DMA rings) on ragged M/N and K tails."""
@@ -108,7 +108,7 @@ def test_gemm_variants(dev, variant, layout):
         assert (C.float() - ref).abs().max().item() < tol
 
 
-@pytest.mark.parametrize("variant", [1, 2, 7, 8, 9, 10])
+@pytest.mark.parametrize("variant", [1, 2, 7, 8, 9, 10, 11])
 def test_gemm_unaligned_output_and_all_epilogues(dev, variant):
     """Scalar epilogue fallback (C rows not 16-B aligned) and every epilogue through the DMA kernel."""
     M, N, Kd = 200, 128, 256
@@ -133,7 +133,7 @@ def test_gemm_unaligned_output_and_all_epilogues(dev, variant):
     torch.testing.assert_close(dgu[:, N:].float(), uu.grad, atol=5e-2, rtol=2e-2)
 
 
-@pytest.mark.parametrize("variant", [7, 8, 9, 10])
+@pytest.mark.parametrize("variant", [7, 8, 9, 10, 11])
 @pytest.mark.parametrize("Kd", [64, 128, 192, 1024])
 @pytest.mark.parametrize("layout", [K.GEMM_NT, K.GEMM_NN, K.GEMM_TN])
 def test_gemm_v3_pipeline_depths(dev, Kd, layout, variant):
@@ -153,7 +153,7 @@ def test_gemm_v3_pipeline_depths(dev, Kd, layout, variant):
         assert (C - 3.0 - ref).abs().max().item() < 2e-3 * Kd ** 0.5
 
 
-@pytest.mark.parametrize("variant", [0, 7, 8, 9, 10])
+@pytest.mark.parametrize("variant", [0, 7, 8, 9, 10, 11])
 def test_gemm_v3_m_tail_peel_epilogues(dev, variant):
     """M = 2*256 + 16: v3 runs the first 512 rows and the 16-row remainder is peeled into a v2 launch with offset
     C/aux/aux_out/resid pointers (InternViT: 16400 = 64*256 + 16). Fused epilogues must agree across the seam."""
@@ -186,7 +186,7 @@ def test_gemm_v3_m_tail_peel_epilogues(dev, variant):
     torch.testing.assert_close(dx.float(), xx.grad, atol=5e-2, rtol=2e-2)
 
 
-@pytest.mark.parametrize("variant", [7, 8, 9, 10])
+@pytest.mark.parametrize("variant", [7, 8, 9, 10, 11])
 def test_gemm_v3_overlapped_last_tile(dev, variant):
     """Write-once epilogues run the partial last M tile of v3 shifted to end at M (rows shared with the previous
     tile are recomputed): the shared rows must be bit-identical to a launch without a remainder, the tail rows
@@ -239,7 +239,7 @@ def test_gemm_dropmask_swiglu_epilogue(dev, p, use_bits, resid_bf16):
     torch.testing.assert_close(dgu[:, F:].float(), uu.grad, atol=3e-2, rtol=2e-2)
 
 
-@pytest.mark.parametrize("variant", [0, 8, 9, 10])
+@pytest.mark.parametrize("variant", [0, 8, 9, 10, 11])
 @pytest.mark.parametrize("epi,M", [(K.EPI_GELU_BWD, 16400), (K.EPI_GELU_BWD, 1000), (K.EPI_QGELU_BWD, 2308),
                                    (K.EPI_STORE, 1000)])
 def test_gemm_colsum_bias_grad(dev, epi, M, variant):
@@ -267,6 +267,66 @@ def test_gemm_colsum_bias_grad(dev, epi, M, variant):
         ref = pre
     torch.testing.assert_close(out.float(), ref, atol=3e-2 * Kd ** 0.5 / 16, rtol=2e-2)
     torch.testing.assert_close(cs, 0.5 + ref.sum(0), atol=2e-3 * M ** 0.5, rtol=1e-3)
+
+
+@pytest.mark.parametrize("Kd", [192, 1024])
+@pytest.mark.parametrize("M", [8192, 8192 + 16])
+def test_gemm_fe_epilogues(dev, M, Kd):
+    """Variant 11 (v3 with the register-direct epilogue, FE): 288 or more 256 x 256 tiles, so blocks 0-31 walk two
+    tiles and the second one's first two K-steps are issued inside the first one's epilogue. Every FE epilogue
+    against torch, the output against the LDS-staged variant 8 of the same main loop (<= 1 bf16 ulp), and the
+    folded 16-row remainder (M = 8208) next to it."""
+    N = 2304
+    g = torch.Generator(device=dev).manual_seed(M + Kd)
+    x = torch.randn(M, Kd, device=dev, generator=g).bfloat16()
+    w = (torch.randn(N, Kd, device=dev, generator=g) * (2.0 / Kd ** 0.5)).bfloat16()
+    bias = torch.randn(N, device=dev, generator=g)
+    pre = x.float() @ w.float().t() + bias
+    outs = {}
+    for v in (8, 11):
+        h = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        hpre = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        K.gemm(x, w, h, M, N, Kd, K.GEMM_NT, Kd, Kd, N, epi=K.EPI_GELU, bias=bias, aux_out=hpre, ldaux_out=N, variant=v)
+        plain = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        K.gemm(x, w, plain, M, N, Kd, K.GEMM_NT, Kd, Kd, N, bias=bias, variant=v)
+        plain32 = torch.empty(M, N, device=dev)
+        K.gemm(x, w, plain32, M, N, Kd, K.GEMM_NT, Kd, Kd, N, variant=v, ksplit_max=-1)
+        resid = torch.randn(M, N, device=dev, generator=torch.Generator(device=dev).manual_seed(1))
+        ls = torch.rand(N, device=dev, generator=torch.Generator(device=dev).manual_seed(2))
+        out = torch.empty(M, N, device=dev)
+        y = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        K.gemm(x, w, out, M, N, Kd, K.GEMM_NT, Kd, Kd, N, epi=K.EPI_RESID_LS, bias=bias, resid=resid, ldr=N, ls=ls,
+               aux_out=y, ldaux_out=N, variant=v)
+        dy = torch.randn(M, Kd, device=dev, generator=torch.Generator(device=dev).manual_seed(3)).bfloat16()
+        dx = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        cs = torch.full((N,), 0.5, device=dev)
+        wt = w.t().contiguous()  # [Kd][N]: NN
+        K.gemm(dy, wt, dx, M, N, Kd, K.GEMM_NN, Kd, N, N, epi=K.EPI_GELU_BWD, aux=hpre, ldaux=N, colsum=cs, variant=v)
+        dq = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        K.gemm(dy, wt, dq, M, N, Kd, K.GEMM_NN, Kd, N, N, epi=K.EPI_QGELU_BWD, aux=hpre, ldaux=N, variant=v)
+        torch.cuda.synchronize()
+        outs[v] = dict(h=h, hpre=hpre, plain=plain, plain32=plain32, out=out, y=y, dx=dx, cs=cs, dq=dq)
+    o = outs[11]
+    torch.testing.assert_close(o["hpre"].float(), pre, atol=3e-2, rtol=1e-2)
+    torch.testing.assert_close(o["h"].float(), torch.nn.functional.gelu(o["hpre"].float()), atol=3e-2, rtol=1e-2)
+    torch.testing.assert_close(o["plain"].float(), pre, atol=3e-2, rtol=1e-2)
+    torch.testing.assert_close(o["plain32"], pre - bias, atol=2e-3, rtol=2e-3)
+    torch.testing.assert_close(o["out"], resid + ls * pre, atol=3e-3, rtol=3e-3)
+    torch.testing.assert_close(o["y"].float(), pre, atol=3e-2, rtol=1e-2)
+    hx = o["hpre"].float()
+    gd = 0.5 * (1 + torch.erf(hx / 2 ** 0.5)) + hx * torch.exp(-0.5 * hx * hx) / (2 * torch.pi) ** 0.5
+    ref = (dy.float() @ w.float().t()) * gd
+    torch.testing.assert_close(o["dx"].float(), ref, atol=3e-2, rtol=2e-2)
+    torch.testing.assert_close(o["cs"], 0.5 + ref.sum(0), atol=2e-3 * M ** 0.5, rtol=1e-3)
+    s = torch.sigmoid(1.702 * hx)
+    torch.testing.assert_close(o["dq"].float(), (dy.float() @ w.float().t()) * s * (1 + 1.702 * hx * (1 - s)), atol=3e-2,
+                               rtol=2e-2)
+    for k in o:  # same main loop as variant 8: equal up to the epilogue's rounding (column sums: summation order)
+        if k == "cs":
+            continue
+        a, b = o[k].float(), outs[8][k].float()
+        tol = 1e-5 if o[k].dtype == torch.float32 else 8e-3
+        assert ((a - b).abs() <= tol * (1 + b.abs())).all(), k
 
 
 _FOLD_SCRIPT = r"""
