@@ -1222,63 +1222,97 @@ __device__ __forceinline__ float row16_sum(float x) {
   x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x140, 0xF, 0xF, false));
   return x;
 }
-// exchange with lane ^ 8 inside each 16-lane row group (DPP row_ror:8)
-__device__ __forceinline__ uint32_t xch8(uint32_t v) { return __builtin_amdgcn_update_dpp(0u, v, 0x128, 0xF, 0xF, false); }
-__device__ __forceinline__ uint4 xch8(uint4 v) { return make_uint4(xch8(v.x), xch8(v.y), xch8(v.z), xch8(v.w)); }
-__device__ __forceinline__ uint4 sel4(bool c, uint4 a, uint4 b) {
-  return make_uint4(c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z, c ? a.w : b.w);
+typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
+
+// A 16-B buffer store whose data VGPRs the next instructions may overwrite. Measured on gfx950 / ROCm 7.2: when the
+// compiler reuses a dwordx4 store's data registers in the very next VALU instruction (v_pk_fma_f32 into v[22:23]
+// right after buffer_store_dwordx4 v[22:25]), lanes 12-15 of each 16-lane row stored the NEW value of dword 1
+// (tools/fe_dbg.py: rows 4-7 / 12-15, columns 2-3 of the second chunk wrong). Two wait states after the store, with
+// scheduling barriers so nothing is moved in between, keep the data read ahead of the overwrite.
+__device__ __forceinline__ void bst16(__amdgpu_buffer_rsrc_t r, uint4 d, int voff, int soff) {
+  __builtin_amdgcn_raw_buffer_store_b128(u32x4v{d.x, d.y, d.z, d.w}, r, voff, soff, 0);
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_nop 1" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
 }
 
-// Stores of one 16-row block of the wave's sub-tile (y[b][r] in the register layout) as whole 128-B lines: each
-// store instruction covers 8 rows x 128 B (bf16: a row's 64 columns; f32: half of them), never half lines (16 rows x
-// 64 B per instruction measured slower than the LDS-staged epilogue on a single-round GEMM). bf16: one
-// v_permlane16_swap per packed dword pair of blocks (b, b + 1) gives lane (rr, g) 8 consecutive columns
-// P = 16(g & 1) + 8(g >> 1) .. + 7 of blocks 0/1 and Q = 32 + P of blocks 2/3; then lanes rr and rr ^ 8 swap Q for P
-// (DPP), so store 1 writes rows 0-7 (P from rr < 8, Q from rr >= 8) and store 2 rows 8-15. f32: per block pair the
-// same row-half swap of the two 16-B chunks.
-__device__ __forceinline__ void fe_st_bf16(bf16* base, long ld, int row0, int col0, int lane, const float (&y)[4][4]) {
+// Stores of one 16-row block of the wave's sub-tile (y[b][r] in the register layout: row rr, columns 16b + 4g + r)
+// as 8-row x 128-B store instructions (whole lines; 16 rows x 64 B per instruction measured slower than the
+// LDS-staged epilogue). The block goes through the wave's private LDS scratch (rows of 16-B chunks XOR-swizzled by
+// the row: conflict-free 16-B writes and reads, 2-way for the bf16 8-B writes) and comes back one 16-B chunk per
+// lane in row order. LDS rather than cross-lane permutes: lgkmcnt, not vmcnt, so the stores in flight are never
+// waited for. Buffer stores: voffL = the lane's byte offset in the block's first row group, the block row and the
+// further row groups in soffset (wave-uniform); no 64-bit address arithmetic.
+__device__ __forceinline__ void fe_st_bf16(char* scr, __amdgpu_buffer_rsrc_t r, int voffL, int soff, int sgrp, int lane,
+                                           const float (&y)[4][4]) {
   const int rr = lane & 15, g = lane >> 4;
-  uint4 P, Q;
-  {
-    const auto s0 = __builtin_amdgcn_permlane16_swap(pk_bf16(y[0][0], y[0][1]), pk_bf16(y[1][0], y[1][1]), false, false);
-    const auto s1 = __builtin_amdgcn_permlane16_swap(pk_bf16(y[0][2], y[0][3]), pk_bf16(y[1][2], y[1][3]), false, false);
-    P = make_uint4(s0[0], s1[0], s0[1], s1[1]);
-    const auto t0 = __builtin_amdgcn_permlane16_swap(pk_bf16(y[2][0], y[2][1]), pk_bf16(y[3][0], y[3][1]), false, false);
-    const auto t1 = __builtin_amdgcn_permlane16_swap(pk_bf16(y[2][2], y[2][3]), pk_bf16(y[3][2], y[3][3]), false, false);
-    Q = make_uint4(t0[0], t1[0], t0[1], t1[1]);
-  }
-  const bool lo = rr < 8;
-  const uint4 recv = xch8(lo ? Q : P);
-  bf16* p1 = base + (long)(row0 + (rr & 7)) * ld + col0 + 16 * (g & 1) + 8 * (g >> 1) + (lo ? 0 : 32);
-  *reinterpret_cast<uint4*>(p1) = lo ? P : recv;
-  *reinterpret_cast<uint4*>(p1 + 8 * ld) = lo ? recv : Q;
-}
-__device__ __forceinline__ void fe_st_f32(float* base, long ld, int row0, int col0, int lane, const float (&y)[4][4]) {
-  const int rr = lane & 15, g = lane >> 4;
-  const bool lo = rr < 8;
-  float* p1 = base + (long)(row0 + (rr & 7)) * ld + col0 + 4 * g + (lo ? 0 : 16);
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {  // block pairs (0, 1) and (2, 3)
-    const uint4 F0 = make_uint4(__float_as_uint(y[2 * h][0]), __float_as_uint(y[2 * h][1]), __float_as_uint(y[2 * h][2]),
-                                __float_as_uint(y[2 * h][3]));
-    const uint4 F1 = make_uint4(__float_as_uint(y[2 * h + 1][0]), __float_as_uint(y[2 * h + 1][1]),
-                                __float_as_uint(y[2 * h + 1][2]), __float_as_uint(y[2 * h + 1][3]));
-    const uint4 recv = xch8(lo ? F1 : F0);
-    *reinterpret_cast<uint4*>(p1 + 32 * h) = lo ? F0 : recv;
-    *reinterpret_cast<uint4*>(p1 + 32 * h + 8 * ld) = lo ? recv : F1;
+  for (int b = 0; b < 4; ++b) {
+    bf16x4 v;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = (bf16)y[b][e];
+    const int c = 2 * b + (g >> 1);
+    *reinterpret_cast<bf16x4*>(scr + rr * 128 + ((c ^ (rr & 7)) << 4) + (g & 1) * 8) = v;
+  }
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {  // rows 8h .. 8h + 7
+    const int row = (lane >> 3) + 8 * h, c = lane & 7;
+    const uint4 d = *reinterpret_cast<const uint4*>(scr + row * 128 + ((c ^ (row & 7)) << 4));
+    bst16(r, d, voffL, soff + h * sgrp);
   }
 }
+__device__ __forceinline__ void fe_st_f32(char* scr, __amdgpu_buffer_rsrc_t r, int voffL, int soff, int sgrp, int lane,
+                                          const float (&y)[4][4]) {
+  const int rr = lane & 15, g = lane >> 4;
+#pragma unroll
+  for (int hb = 0; hb < 2; ++hb) {  // blocks 2hb, 2hb + 1: 16 rows x 128 B per pass (2 KiB of scratch)
+#pragma unroll
+    for (int bb = 0; bb < 2; ++bb) {
+      const int c = 4 * bb + g;
+      const float* v = y[2 * hb + bb];
+      *reinterpret_cast<f32x4*>(scr + rr * 128 + ((c ^ (rr & 7)) << 4)) = f32x4{v[0], v[1], v[2], v[3]};
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {  // rows 8h .. 8h + 7
+      const int row = (lane >> 3) + 8 * h, c = lane & 7;
+      const uint4 d = *reinterpret_cast<const uint4*>(scr + row * 128 + ((c ^ (row & 7)) << 4));
+      bst16(r, d, voffL + 128 * hb, soff + h * sgrp);
+    }
+  }
+}
+// the lane's byte offset in a block's first row group (8 rows x 8 16-B chunks: bf16 the whole 64 columns, f32 the
+// first 32) of a [rows][ld] matrix of sz-byte elements whose sub-tile starts at (mw, nw)
+__device__ __forceinline__ int fe_voff(int mw, int nw, long ld, int sz, int lane) {
+  return (int)(((long)(mw + (lane >> 3)) * ld + nw + (lane & 7) * (16 / sz)) * sz);
+}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t fe_rsrc(const void* base, long rows, long ld, int sz) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)(rows * ld * sz), 0x00020000);
+}
+constexpr int FE_SCR = 2048;  // LDS scratch per wave (16 rows x 128 B), past the ring
 
 template <int EPI, typename OutT, typename NextFn>
 __device__ __forceinline__ void fe_epilogue(const GemmArgs& p, OutT* __restrict__ C, const f32x4 (&acc)[8][4], int mw,
-                                            int nw, int lane, NextFn issue_next) {
+                                            int nw, int lane, char* scr, NextFn issue_next) {
   const int rr = lane & 15, g = lane >> 4;
   const int nc = nw + 4 * g;  // column of register 0 of block 0
   constexpr bool kAux = EPI == EPI_GELU_BWD || EPI == EPI_QGELU_BWD;
   constexpr bool kResid = EPI == EPI_RESID_LS;
   constexpr bool kBias = EPI == EPI_STORE || EPI == EPI_GELU || EPI == EPI_QGELU || EPI == EPI_RESID_LS;
-  constexpr bool kCs = EPI == EPI_STORE || kAux;
-  // loads that must not wait behind the next tile's DMA are issued before it
+  constexpr int csz = sizeof(OutT);
+  const __amdgpu_buffer_rsrc_t rc = fe_rsrc(C, p.M, p.ldc, csz);
+  const int vc = fe_voff(mw, nw, p.ldc, csz, lane);
+  const int sc = 16 * (int)p.ldc * csz;  // one 16-row block
+  __amdgpu_buffer_rsrc_t ra = rc;
+  int va = 0, sa = 0;
+  if constexpr (EPI == EPI_GELU || EPI == EPI_QGELU || EPI == EPI_RESID_LS) {
+    if (p.aux_out) {
+      ra = fe_rsrc(p.aux_out, p.M, p.ldaux_out, 2);
+      va = fe_voff(mw, nw, p.ldaux_out, 2, lane);
+      sa = 16 * (int)p.ldaux_out * 2;
+    }
+  }
+  // Every global load of the epilogue is issued before the next tile's DMA: a load issued after it (or after a
+  // store) could only be waited for behind them (vmcnt counts in issue order).
   f32x4 bias[4], lsv[4];
 #pragma unroll
   for (int b = 0; b < 4; ++b) {
@@ -1312,7 +1346,7 @@ __device__ __forceinline__ void fe_epilogue(const GemmArgs& p, OutT* __restrict_
     for (int r = 0; r < 4; ++r) cs[b][r] = 0.f;
 #pragma unroll
   for (int a = 0; a < 8; ++a) {
-    if (a == 4) {  // second half of the row inputs (waits behind the next tile's DMA, issued long before)
+    if (a == 4) {  // second half of the row inputs
       if constexpr (kResid) {
 #pragma unroll
         for (int a2 = 0; a2 < 4; ++a2)
@@ -1334,31 +1368,26 @@ __device__ __forceinline__ void fe_epilogue(const GemmArgs& p, OutT* __restrict_
 #pragma unroll
       for (int r = 0; r < 4; ++r) y[b][r] = acc[a][b][r] * p.alpha + bias[b][r];
     if constexpr (EPI == EPI_STORE) {
-      if constexpr (sizeof(OutT) == 2) {
-        fe_st_bf16(reinterpret_cast<bf16*>(C), p.ldc, mw + 16 * a, nw, lane, y);
-      } else {
-        fe_st_f32(reinterpret_cast<float*>(C), p.ldc, mw + 16 * a, nw, lane, y);
-      }
+      if constexpr (csz == 2) fe_st_bf16(scr, rc, vc, a * sc, sc / 2, lane, y);
+      else fe_st_f32(scr, rc, vc, a * sc, sc / 2, lane, y);
     } else if constexpr (EPI == EPI_GELU || EPI == EPI_QGELU) {
-      float h[4][4];
 #pragma unroll
       for (int b = 0; b < 4; ++b)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) h[b][r] = (float)(bf16)y[b][r];
-      fe_st_bf16(p.aux_out, p.ldaux_out, mw + 16 * a, nw, lane, h);
+        for (int r = 0; r < 4; ++r) y[b][r] = (float)(bf16)y[b][r];
+      fe_st_bf16(scr, ra, va, a * sa, sa / 2, lane, y);
 #pragma unroll
       for (int b = 0; b < 4; ++b)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) h[b][r] = EPI == EPI_GELU ? gelu_erf(h[b][r]) : qgelu(h[b][r]);
-      fe_st_bf16(reinterpret_cast<bf16*>(C), p.ldc, mw + 16 * a, nw, lane, h);
+        for (int r = 0; r < 4; ++r) y[b][r] = EPI == EPI_GELU ? gelu_erf(y[b][r]) : qgelu(y[b][r]);
+      fe_st_bf16(scr, rc, vc, a * sc, sc / 2, lane, y);
     } else if constexpr (EPI == EPI_RESID_LS) {
-      if (p.aux_out) fe_st_bf16(p.aux_out, p.ldaux_out, mw + 16 * a, nw, lane, y);
-      float o[4][4];
+      if (p.aux_out) fe_st_bf16(scr, ra, va, a * sa, sa / 2, lane, y);
 #pragma unroll
       for (int b = 0; b < 4; ++b)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) o[b][r] = rv[a & 3][b][r] + lsv[b][r] * y[b][r];
-      fe_st_f32(reinterpret_cast<float*>(C), p.ldc, mw + 16 * a, nw, lane, o);
+        for (int r = 0; r < 4; ++r) y[b][r] = rv[a & 3][b][r] + lsv[b][r] * y[b][r];
+      fe_st_f32(scr, rc, vc, a * sc, sc / 2, lane, y);
     } else if constexpr (kAux) {
 #pragma unroll
       for (int b = 0; b < 4; ++b) {
@@ -1366,25 +1395,23 @@ __device__ __forceinline__ void fe_epilogue(const GemmArgs& p, OutT* __restrict_
 #pragma unroll
         for (int r = 0; r < 4; ++r) y[b][r] *= EPI == EPI_GELU_BWD ? gelu_erf_grad((float)hv[r]) : qgelu_grad((float)hv[r]);
       }
-      fe_st_bf16(reinterpret_cast<bf16*>(C), p.ldc, mw + 16 * a, nw, lane, y);
-    }
-    if constexpr (kCs) {
+      fe_st_bf16(scr, rc, vc, a * sc, sc / 2, lane, y);
 #pragma unroll
       for (int b = 0; b < 4; ++b)
 #pragma unroll
         for (int r = 0; r < 4; ++r) cs[b][r] += y[b][r];
     }
   }
-  if constexpr (kCs) {
+  if constexpr (kAux) {
     if (p.colsum) {  // the wave's 128 rows summed into the partial row of its first 64-row subtile, zeros in the second
       float* w0 = p.colsum_ws + (long)(p.colsum_row0 + mw / 64) * p.N + nc;
 #pragma unroll
       for (int b = 0; b < 4; ++b) {
-        f32x4 s;
+        f32x4 t;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) s[r] = row16_sum(cs[b][r]);
+        for (int r = 0; r < 4; ++r) t[r] = row16_sum(cs[b][r]);
         if (rr == 0) {
-          *reinterpret_cast<f32x4*>(w0 + 16 * b) = s;
+          *reinterpret_cast<f32x4*>(w0 + 16 * b) = t;
           *reinterpret_cast<f32x4*>(w0 + p.N + 16 * b) = f32x4{0.f, 0.f, 0.f, 0.f};
         }
       }
@@ -1512,7 +1539,7 @@ __device__ __forceinline__ void v3_tile(const GemmArgs& p, int bid, long z, char
       dma_issue_range<AK, V3_BM, NW, 0, 4>(ra, smem + STAGE, wave, kbeg + BK, kend, p.lda, bA, kA, oA);
       dma_issue_range<BKc, V3_BN, NW, 0, 4>(rb, smem + STAGE + A_BYTES, wave, kbeg + BK, kend, p.ldb, bB, kB, oB);
     };
-    fe_epilogue<EPI, OutT>(p, C, acc, m0 + arow, n0 + bcol, lane, issue_next);
+    fe_epilogue<EPI, OutT>(p, C, acc, m0 + arow, n0 + bcol, lane, smem + 2 * STAGE + wave * FE_SCR, issue_next);
     return;
   }
   bool reduced = false;
@@ -1942,7 +1969,7 @@ static int launch_v4(GemmArgs a, int batch, hipStream_t st) {
 template <bool AK, bool BKc, int EPI, typename OutT, bool SW, bool FE = false>
 static int launch_v3(GemmArgs a, int batch, hipStream_t st) {
   constexpr int LDS_RING = 2 * (V3_BM * BK * 2 + V3_BN * BK * 2);
-  constexpr int LDS_EP = FE ? 0 : 8 * 64 * EP_LD * 4 + 16;  // + the split-K role word
+  constexpr int LDS_EP = FE ? LDS_RING + 8 * FE_SCR : 8 * 64 * EP_LD * 4 + 16;  // + the split-K role word
   constexpr int LDS = LDS_RING > LDS_EP ? LDS_RING : LDS_EP;
   const void* fn;
   if constexpr (FE) fn = (const void*)gemm_bf16_v3fe_kernel<AK, BKc, EPI, OutT>;
@@ -1979,7 +2006,7 @@ static int launch_v3(GemmArgs a, int batch, hipStream_t st) {
 }
 
 // The FE member's eligibility (see fe_epilogue): whole 256 x 256 tiles, one K range, no accumulation, an epilogue it
-// implements. Anything else launches v3 with the swapped-operand LDS epilogue (variant 8).
+// implements. Anything else launches plain v3 (variant 7).
 template <int EPI, typename OutT>
 static bool fe_ok(const GemmArgs& a, int batch) {
   constexpr bool epi = EPI == EPI_STORE || EPI == EPI_GELU || EPI == EPI_QGELU || EPI == EPI_RESID_LS ||
@@ -1987,7 +2014,7 @@ static bool fe_ok(const GemmArgs& a, int batch) {
   if (!epi || batch != 1 || a.ksplit > 1 || !a.vec_ok || a.accumulate || a.N % V3_BN != 0 || a.K % BK != 0 ||
       a.K < 3 * BK)
     return false;
-  if (EPI == EPI_STORE && a.split_stride) return false;
+  if (EPI == EPI_STORE && (a.split_stride || a.colsum)) return false;
   const int main_rows = a.rem_r0 > 0 ? a.rem_r0 : a.M;
   return main_rows % V3_BM == 0 || (a.mshift_last && a.M >= V3_BM);
 }
@@ -2040,7 +2067,7 @@ static int launch_any(GemmArgs& a, int batch, hipStream_t st, int variant) {
                     EPI == EPI_GELU_BWD || EPI == EPI_QGELU_BWD) {
         if (fe_ok<EPI, OutT>(a, batch)) return launch_v3<AK, BKc, EPI, OutT, true, true>(a, batch, st);
       }
-      return launch_v3<AK, BKc, EPI, OutT, true>(a, batch, st);
+      return launch_v3<AK, BKc, EPI, OutT, false>(a, batch, st);
     case 9: return launch_v4<AK, BKc, EPI, OutT, false>(a, batch, st);
     case 10: return launch_v4<AK, BKc, EPI, OutT, true>(a, batch, st);
     default: return launch<AK, BKc, EPI, OutT>(a, batch, st);
@@ -2239,7 +2266,7 @@ static int gemm_launch(const slx_gemm_desc* d, int v, hipStream_t st, int mshift
       a.ksplit = sp;
       a.kchunk = ((ksteps + sp - 1) / sp) * BK;
       const long v3tiles = (long)((d->M + V3_BM - 1) / V3_BM) * ((d->N + V3_BN - 1) / V3_BN);
-      if ((v == 7 || v == 8 || v == 11) && batch == 1 && !split_stride && d->epilogue == SLX_EPI_STORE && d->out_f32 &&
+      if ((v == 7 || v == 8 || v >= 11) && batch == 1 && !split_stride && d->epilogue == SLX_EPI_STORE && d->out_f32 &&
           split_ws_fits(d, v3tiles, sp)) {  // reduced inside the launch: plain stores, no pre-zeroed C
         a.split_ws = d->split_ws;
         a.split_cnt = reinterpret_cast<int*>(d->split_ws + d->split_ws_floats - kSplitCntInts);
@@ -2249,6 +2276,12 @@ static int gemm_launch(const slx_gemm_desc* d, int v, hipStream_t st, int mshift
         if (e != hipSuccess) { set_error("slx_gemm_bf16: memset2D failed: %s", hipGetErrorString(e)); return -1000 - (int)e; }
       }
     }
+  }
+  {  // more than one round of 256^2 tiles: the FE member (the next tile's loads overlap this tile's epilogue; on a
+     // single round there is no next tile and the LDS-staged epilogue is as fast or faster: gemm_epi_bench proj)
+    static const bool fe_on = [] { const char* e = getenv("SLX_GEMM_FE"); return !e || atoi(e) != 0; }();
+    const long t3 = (long)(((rem_r0 > 0 ? rem_r0 : d->M) + V3_BM - 1) / V3_BM) * ((d->N + V3_BN - 1) / V3_BN);
+    if (v == 7 && fe_on && batch == 1 && t3 > 256) v = 11;
   }
   SLX_CHECK_ARG(!d->colsum || (d->colsum_ws && a.vec_ok && a.ksplit == 1 && v != 1 && d->N % 8 == 0 &&
                                 (d->epilogue == SLX_EPI_STORE || d->epilogue == SLX_EPI_GELU_BWD ||
