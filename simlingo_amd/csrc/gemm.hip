@@ -1200,9 +1200,10 @@ __device__ __forceinline__ void wait_vm_n() {
 // Lane l of a wave holds, in acc[a][b], rows 16a + (l & 15) and columns 16b + 4(l >> 4) + r (r = 0..3) of the wave's
 // 128 x 64 sub-tile. bf16 rows leave as 16-B stores after one v_permlane16_swap per packed dword pair (blocks b, b+1):
 // row-group g = l >> 4 then holds 8 consecutive columns, 16(b + (g & 1)) + 8(g >> 1) .. + 7.
-// Eligible (host side, fe_ok): ksplit 1, batch 1, whole tiles (M % 256 == 0, folded remainder or shifted last tile),
-// N % 256 == 0, 16-B aligned rows, no accumulation, K >= 192, epilogues STORE / GELU / QGELU / RESID_LS / GELU_BWD /
-// QGELU_BWD (colsum allowed).
+// Eligible (host side, fe_ok): ksplit 1, batch 1, N % 256 == 0, 16-B aligned rows, no accumulation, K >= 192,
+// epilogues STORE / GELU / QGELU / RESID_LS / GELU_BWD / QGELU_BWD (colsum with the GELU' pair); whole tiles (M % 256
+// == 0, folded remainder or shifted last tile), or a partial last tile for STORE / GELU / QGELU (rows past M dropped
+// by the stores' range check).
 template <int EPI, typename OutT> struct FeStores { static constexpr int N = sizeof(OutT) == 2 ? 16 : 32; };
 template <typename OutT> struct FeStores<EPI_GELU, OutT> { static constexpr int N = 32; };
 template <typename OutT> struct FeStores<EPI_QGELU, OutT> { static constexpr int N = 32; };
@@ -2016,7 +2017,10 @@ static bool fe_ok(const GemmArgs& a, int batch) {
     return false;
   if (EPI == EPI_STORE && (a.split_stride || a.colsum)) return false;
   const int main_rows = a.rem_r0 > 0 ? a.rem_r0 : a.M;
-  return main_rows % V3_BM == 0 || (a.mshift_last && a.M >= V3_BM);
+  if (main_rows % V3_BM == 0 || (a.mshift_last && a.M >= V3_BM)) return true;
+  // a partial last M tile (Qwen2: 6384 = 24 * 256 + 240 rows): the buffer stores drop the rows past M (range check
+  // of the descriptor, num_records = M rows); only epilogues without per-row loads and without column sums
+  return a.rem_r0 == 0 && (EPI == EPI_STORE || EPI == EPI_GELU || EPI == EPI_QGELU);
 }
 
 template <bool AK, bool BKc, int EPI, typename OutT>

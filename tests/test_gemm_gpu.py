@@ -270,7 +270,7 @@ def test_gemm_colsum_bias_grad(dev, epi, M, variant):
 
 
 @pytest.mark.parametrize("Kd", [192, 1024])
-@pytest.mark.parametrize("M", [8192, 8192 + 16])
+@pytest.mark.parametrize("M", [8192, 8192 + 16, 8192 + 240])
 def test_gemm_fe_epilogues(dev, M, Kd):
     """Variant 11 (v3 with the register-direct epilogue, FE): 288 or more 256 x 256 tiles, so blocks 0-31 walk two
     tiles and the second one's first two K-steps are issued inside the first one's epilogue. Every FE epilogue
