@@ -69,30 +69,29 @@ __device__ __forceinline__ float block_sum(float v, float* sh) {
   return t;
 }
 
-// Normal CDF Phi(x) = 0.5 erfc(-x/sqrt2), branch-free: erfc(a), a >= 0, by the Chebyshev-fitted
-// t*exp(-a^2 + P(t)), t = 1/(1 + a/2) (Numerical Recipes erfcc, fractional error < 1.2e-7 everywhere).
-// One rcp, one exp and ~12 FMAs instead of the library erff's piecewise polynomial with its divergent
-// branch; the GEMM epilogues evaluate this on every element of InternViT's 16400 x 4096 fc1 output.
-__device__ __forceinline__ float normal_cdf(float x) {
+// GELU(erf) and its derivative, branch-free, from ONE exponential: with a = |x|/sqrt2, erfc(a) = P(t) e^{-a^2},
+// t = 1/(1 + p a) (Abramowitz & Stegun 7.1.26, |error of erf| <= 1.5e-7), and e^{-a^2} = e^{-x^2/2} is also the
+// normal density's exponential, so Phi(x) = 0.5 erfc(-x/sqrt2) and x phi(x) share it. One rcp + one exp2 + ~10 FMA
+// per element (the Numerical Recipes form used before: rcp + two exp2 + ~17): the GEMM epilogues evaluate these on
+// every element of InternViT's 16400 x 4096 fc1 output and fc2 input gradient, outside the MFMA main loop.
+struct GeluTerms { float cdf, e; };  // Phi(x), e^{-x^2/2}
+__device__ __forceinline__ GeluTerms gelu_terms(float x) {
   const float a = fabsf(x) * 0.70710678118654752f;
-  const float t = __builtin_amdgcn_rcpf(__builtin_fmaf(0.5f, a, 1.0f));
-  float p = 0.17087277f;
-  p = __builtin_fmaf(p, t, -0.82215223f);
-  p = __builtin_fmaf(p, t, 1.48851587f);
-  p = __builtin_fmaf(p, t, -1.13520398f);
-  p = __builtin_fmaf(p, t, 0.27886807f);
-  p = __builtin_fmaf(p, t, -0.18628806f);
-  p = __builtin_fmaf(p, t, 0.09678418f);
-  p = __builtin_fmaf(p, t, 0.37409196f);
-  p = __builtin_fmaf(p, t, 1.00002368f);
-  p = __builtin_fmaf(p, t, -1.26551223f);
-  const float half_erfc = 0.5f * t * __builtin_amdgcn_exp2f((p - a * a) * 1.4426950408889634f);
-  return x > 0.f ? 1.0f - half_erfc : half_erfc;
+  const float t = __builtin_amdgcn_rcpf(__builtin_fmaf(0.3275911f, a, 1.0f));
+  const float e = __builtin_amdgcn_exp2f(x * x * -0.72134752044448170f);  // e^{-x^2/2}
+  float q = 0.5f * 1.061405429f;  // 0.5 * (a1 t + ... + a5 t^5), Horner
+  q = __builtin_fmaf(q, t, 0.5f * -1.453152027f);
+  q = __builtin_fmaf(q, t, 0.5f * 1.421413741f);
+  q = __builtin_fmaf(q, t, 0.5f * -0.284496736f);
+  q = __builtin_fmaf(q, t, 0.5f * 0.254829592f);
+  const float half_erfc = q * t * e;
+  return GeluTerms{x > 0.f ? 1.0f - half_erfc : half_erfc, e};
 }
-__device__ __forceinline__ float gelu_erf(float x) { return x * normal_cdf(x); }
+__device__ __forceinline__ float normal_cdf(float x) { return gelu_terms(x).cdf; }
+__device__ __forceinline__ float gelu_erf(float x) { return x * gelu_terms(x).cdf; }
 __device__ __forceinline__ float gelu_erf_grad(float x) {
-  const float pdf = 0.39894228040143268f * __builtin_amdgcn_exp2f(-0.5f * 1.4426950408889634f * x * x);
-  return normal_cdf(x) + x * pdf;
+  const GeluTerms g = gelu_terms(x);
+  return __builtin_fmaf(x * 0.39894228040143268f, g.e, g.cdf);
 }
 __device__ __forceinline__ float silu(float x) { return x / (1.0f + __expf(-x)); }
 __device__ __forceinline__ float silu_grad(float x) {

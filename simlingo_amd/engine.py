@@ -37,6 +37,9 @@ PAIR_WGRAD = os.environ.get("SLX_PAIR_WGRAD", "1") != "0"
 # main loop of the K = 64 LoRA GEMM that carries the SwiGLU backward epilogue (an HBM-bound elementwise pass): v2 128^2
 # tiles, two blocks per CU, +0.1-0.15 % over the cost model's v3 (profiles/round2_s3_swiglu_bwd_ab.txt)
 SWIGLU_BWD_VARIANT = int(os.environ.get("SLX_SWIGLU_BWD_VARIANT", "2"))
+# LoRA B-gradient GEMMs (N = r = 32, K = the 6384 tokens): most K splits per launch (0 = the host cost model's choice).
+# A/B hook: these launches are bound by HBM and latency, not by the MFMA work the cost model prices.
+LORA_DB_SPLIT = int(os.environ.get("SLX_LORA_DB_SPLIT", "0"))
 ALIGN = 64  # elements; keeps every parameter view 256-B aligned
 
 
@@ -752,10 +755,12 @@ class VLAEngine(EngineOps):
                         and gn.shape == gb.shape and gn.data_ptr() > gb.data_ptr()):
                     sC = (gn.data_ptr() - gb.data_ptr()) // 4
                     K.gemm(dys[j], tx[:, r * j:], gb, out, r, dys[j].shape[0], K.GEMM_TN, dys[j].stride(0),
-                           tx.stride(0), r, alpha=s, accumulate=True, batch=2, sA=out, sB=r, sC=sC)
+                           tx.stride(0), r, alpha=s, accumulate=True, batch=2, sA=out, sB=r, sC=sC,
+                           ksplit_max=LORA_DB_SPLIT)
                     j += 2
                     continue
-            K.mm(dys[j], tx[:, r * j:r * (j + 1)], gb, ta=True, tb=False, alpha=s, accumulate=True)
+            K.mm(dys[j], tx[:, r * j:r * (j + 1)], gb, ta=True, tb=False, alpha=s, accumulate=True,
+                 ksplit_max=LORA_DB_SPLIT)
             j += 1
         # dA and the dx term in one launch. (Running the parameter-only part - dB GEMMs, dA - on a side stream was
         # measured 6 ms/step slower: per-call event/stream overhead on the host and slower main-stream GEMMs.)

@@ -12,7 +12,9 @@ from pathlib import Path
 
 import torch
 
-_LIB_PATH = Path(__file__).resolve().parent / "csrc" / "libslx_hip.so"
+# SLX_LIB_PATH: load another build of the library (A/B of two builds in alternating processes); the in-tree build
+# is the default and the only one the product path ships
+_LIB_PATH = Path(os.environ.get("SLX_LIB_PATH") or Path(__file__).resolve().parent / "csrc" / "libslx_hip.so")
 _lib = None
 
 c_int, c_i64, c_u64, c_float, c_vp = ctypes.c_int, ctypes.c_int64, ctypes.c_uint64, ctypes.c_float, ctypes.c_void_p
