@@ -86,6 +86,11 @@ typedef struct slx_gemm_desc {
                        the launch by each tile's last-arriving split (deterministic split order) instead of f32
                        atomics into C; its LAST 16384 words are arrival counters that must be zero before first use
                        (every call leaves them zero; one workspace per stream). NULL = atomics                     */
+  const float* rope_cos; const float* rope_sin; /* optional, STORE bf16 only: RoPE on the output columns < rope_ncols
+                       (64-wide heads, dims d / d + 32 rotated as a pair; position = row % rope_S, tables [rope_S][32]
+                       f32 as slx_rope takes them), applied to alpha*acc + bias before the bf16 rounding: the Qwen2
+                       q|k projection (modeling_qwen2 apply_rotary_pos_emb) fused into its GEMM                       */
+  int rope_S; int rope_ncols;
 } slx_gemm_desc;
 int slx_gemm_bf16(const slx_gemm_desc* d, slx_stream_t stream);
 /* Two independent accumulating f32 STORE GEMMs (same layout and K, no bias / colsum / batch) in one launch:

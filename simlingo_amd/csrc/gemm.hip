@@ -93,6 +93,10 @@ struct GemmArgs {
   const float* ce_lse;   // [M] log-sum-exp (backward)
   const float* ce_gscale;  // d loss / d (per-row CE): one scalar (the LM loss weight / count)
   int ce_ldpart;
+  // RoPE fused into a bf16 STORE epilogue (slx_gemm_desc.rope_*): columns < rope_ncols, position = row % rope_S
+  const float* rope_cos;
+  const float* rope_sin;
+  int rope_S, rope_ncols;
 };
 
 // Dropout applied while loading an operand (LoRA dropout, regenerated bit-exactly in backward):
@@ -653,6 +657,40 @@ __device__ __forceinline__ void epilogue_tile64(const GemmArgs& p, OutT* __restr
   const int cc = (lane & 7) * 8;
   const int n = n_base + cc;
   const bool vec_ok = p.vec_ok && n + 8 <= p.N;
+  if constexpr (EPI == EPI_STORE && sizeof(OutT) == 2) {
+    if (p.rope_cos && n_base < p.rope_ncols && p.vec_ok && n_base + 64 <= p.N) {  // wave-uniform: one 64-wide head
+      // y = alpha*acc + bias, then the head's dims d / d + 32 rotated as a pair: lane octet (lane & 7) holds 8
+      // consecutive columns, the partner half is lane ^ 4 of the same row (rope_pair of slx_rope, forward)
+      const int d32 = cc & 31;
+      const float sg = cc < 32 ? -1.f : 1.f;
+      float bv[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) bv[e] = p.bias ? p.bias[n + e] : 0.f;
+#pragma unroll 2
+      for (int pass = 0; pass < 8; ++pass) {
+        const int row = pass * 8 + (lane >> 3);
+        const int m = min(m_base + row, p.M - 1);  // (rows past M: computed, not stored - the shuffles need the lanes)
+        float v[8], w[8];
+        const float4 a0 = *reinterpret_cast<const float4*>(ep + row * EP_LD + cc);
+        const float4 a1 = *reinterpret_cast<const float4*>(ep + row * EP_LD + cc + 4);
+        v[0] = a0.x; v[1] = a0.y; v[2] = a0.z; v[3] = a0.w; v[4] = a1.x; v[5] = a1.y; v[6] = a1.z; v[7] = a1.w;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = v[e] * p.alpha + bv[e];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) w[e] = __shfl_xor(v[e], 4, 64);
+        const long tb = (long)(m % p.rope_S) * 32 + d32;
+        const float4 c0 = *reinterpret_cast<const float4*>(p.rope_cos + tb), c1 = *reinterpret_cast<const float4*>(p.rope_cos + tb + 4);
+        const float4 s0 = *reinterpret_cast<const float4*>(p.rope_sin + tb), s1 = *reinterpret_cast<const float4*>(p.rope_sin + tb + 4);
+        const float cv[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+        const float sv[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+        float o[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = v[e] * cv[e] + sg * w[e] * sv[e];
+        if (m_base + row < p.M) st8(C + (long)m * p.ldc + n, o);
+      }
+      return;
+    }
+  }
   float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll 2
   for (int pass = 0; pass < 8; ++pass) {
@@ -888,7 +926,8 @@ __device__ __forceinline__ void epilogue_tile64_pf(const GemmArgs& p, OutT* __re
                        EPI == EPI_GELU_BWD || EPI == EPI_QGELU_BWD || EPI == EPI_SWIGLU_BWD ||
                        EPI == EPI_DROPMASK_SWIGLU || EPI == EPI_DROPMASK_SWIGLU_B;
   if constexpr (kPf) {
-    const bool whole = p.vec_ok && n_base + 64 <= p.N && !(EPI == EPI_STORE && p.ksplit > 1 && !reduced);  // wave-uniform
+    const bool whole = p.vec_ok && n_base + 64 <= p.N && !(EPI == EPI_STORE && p.ksplit > 1 && !reduced) &&
+                       !(EPI == EPI_STORE && p.rope_cos);  // wave-uniform (RoPE: epilogue_tile64's row loop)
     if (whole) {
       if constexpr (EPI == EPI_GELU || EPI == EPI_QGELU) {
         epilogue_tile64_pf_impl<EPI, OutT, false>(p, C, ep, lane, m_base, n_base);
@@ -2015,7 +2054,7 @@ static bool fe_ok(const GemmArgs& a, int batch) {
   if (!epi || batch != 1 || a.ksplit > 1 || !a.vec_ok || a.accumulate || a.N % V3_BN != 0 || a.K % BK != 0 ||
       a.K < 3 * BK)
     return false;
-  if (EPI == EPI_STORE && (a.split_stride || a.colsum)) return false;
+  if (EPI == EPI_STORE && (a.split_stride || a.colsum || a.rope_cos)) return false;
   const int main_rows = a.rem_r0 > 0 ? a.rem_r0 : a.M;
   if (main_rows % V3_BM == 0 || (a.mshift_last && a.M >= V3_BM)) return true;
   // a partial last M tile (Qwen2: 6384 = 24 * 256 + 240 rows): the buffer stores drop the rows past M (range check
@@ -2244,6 +2283,7 @@ static int gemm_launch(const slx_gemm_desc* d, int v, hipStream_t st, int mshift
   a.maskbits = d->maskbits; a.ldbits = d->ldbits;
   a.colsum_row0 = colsum_row0;
   a.split_ws = nullptr; a.split_cnt = nullptr; a.split_tile0 = 0;
+  a.rope_cos = d->rope_cos; a.rope_sin = d->rope_sin; a.rope_S = d->rope_S; a.rope_ncols = d->rope_ncols;
   a.mshift_last = 0;
   a.tilesM = (d->M + BM - 1) / BM;
   a.tilesN = (d->N + BN - 1) / BN;
@@ -2260,7 +2300,7 @@ static int gemm_launch(const slx_gemm_desc* d, int v, hipStream_t st, int mshift
   a.ksplit = 1;
   a.kchunk = d->K;
   {  // split-K for under-filled grids (weight gradients): f32 atomics, >= 4 K-steps per split
-    int sp = rem_r0 ? 1 : force_split > 0 ? force_split : split_for(d, (v >= 7 && v <= 11) ? 7 : v, d->M, batch);  // (no split-K with a fold)
+    int sp = (rem_r0 || d->rope_cos) ? 1 : force_split > 0 ? force_split : split_for(d, (v >= 7 && v <= 11) ? 7 : v, d->M, batch);  // (no split-K with a fold)
     const int ksteps = (d->K + BK - 1) / BK;
     if (sp > 1) {
       const int per = ((ksteps + sp - 1) / sp) * BK;
@@ -2285,7 +2325,7 @@ static int gemm_launch(const slx_gemm_desc* d, int v, hipStream_t st, int mshift
      // single round there is no next tile and the LDS-staged epilogue is as fast or faster: gemm_epi_bench proj)
     static const bool fe_on = [] { const char* e = getenv("SLX_GEMM_FE"); return !e || atoi(e) != 0; }();
     const long t3 = (long)(((rem_r0 > 0 ? rem_r0 : d->M) + V3_BM - 1) / V3_BM) * ((d->N + V3_BN - 1) / V3_BN);
-    if (v == 7 && fe_on && batch == 1 && t3 > 256) v = 11;
+    if (v == 7 && fe_on && batch == 1 && t3 > 256 && !d->rope_cos) v = 11;
   }
   SLX_CHECK_ARG(!d->colsum || (d->colsum_ws && a.vec_ok && a.ksplit == 1 && v != 1 && d->N % 8 == 0 &&
                                 (d->epilogue == SLX_EPI_STORE || d->epilogue == SLX_EPI_GELU_BWD ||
@@ -2421,9 +2461,17 @@ extern "C" int slx_gemm_bf16(const slx_gemm_desc* d, slx_stream_t stream) {
   int v3k = kind_default;
   if (v >= 8 && v <= 11) { v3k = v; v = 7; }
   else if (v == 7) v3k = 7;
+  SLX_CHECK_ARG(!d->rope_cos || (d->rope_sin && d->epilogue == SLX_EPI_STORE && !d->out_f32 && !d->accumulate &&
+                                  batch == 1 && !d->colsum && d->rope_S > 0 && d->rope_ncols % 64 == 0 &&
+                                  d->K % BK == 0 && d->drop_operand == 0 && d->variant != 1 &&
+                                  d->rope_ncols <= d->N && d->ldc % 8 == 0 && ((uintptr_t)d->C & 15) == 0 &&
+                                  ((uintptr_t)d->rope_cos & 15) == 0 && ((uintptr_t)d->rope_sin & 15) == 0),
+                "slx_gemm_bf16: RoPE needs a bf16 STORE epilogue without accumulate / colsum / batch, K %% 64 == 0 (the "
+                "LDS-staged main loops), 16-B aligned C rows and tables, rope_S > 0 and rope_ncols a multiple of 64 not "
+                "past N");
   const int rem = d->M % V3_BM;
   const bool peel_ok = batch == 1 && d->epilogue != SLX_EPI_DROPMASK && d->epilogue != SLX_EPI_DROPMASK_SWIGLU &&
-                       d->M > V3_BM && rem > 0 && rem <= 64;
+                       d->M > V3_BM && rem > 0 && rem <= 64 && !d->rope_cos;  // (RoPE: partial last tile instead)
   if (v == 0) {
     v = dma_ok ? 2 : 1;
     if (dma_ok) {

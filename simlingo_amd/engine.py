@@ -40,6 +40,8 @@ SWIGLU_BWD_VARIANT = int(os.environ.get("SLX_SWIGLU_BWD_VARIANT", "2"))
 # LoRA B-gradient GEMMs (N = r = 32, K = the 6384 tokens): most K splits per launch (0 = the host cost model's choice).
 # A/B hook: these launches are bound by HBM and latency, not by the MFMA work the cost model prices.
 LORA_DB_SPLIT = int(os.environ.get("SLX_LORA_DB_SPLIT", "0"))
+# Qwen2 RoPE fused into the q|k|v GEMM epilogue (0: the separate slx_rope pass, A/B hook)
+FUSED_ROPE = os.environ.get("SLX_FUSED_ROPE", "1") != "0"
 ALIGN = 64  # elements; keeps every parameter view 256-B aligned
 
 
@@ -339,8 +341,11 @@ class VLAEngine(EngineOps):
             if lora:
                 L.update(self._lora_down(hx[:, :d], i, ("q", "k", "v"), hx[:, d:], sv))
             qkv = self._e(Ml, nqkv)
-            K.mm(hx, cat["qkv"] if lora else self.W[p + "qkv_w"], qkv, bias=self.P[p + "qkv_b"])
-            K.rope(qkv, Ml, S, Hq + Hk, cos, sin)  # q and k heads are the first Hq+Hk head slots
+            # q|k|v projection with RoPE on the q and k head slots (the first Hq+Hk) fused into its epilogue
+            K.mm(hx, cat["qkv"] if lora else self.W[p + "qkv_w"], qkv, bias=self.P[p + "qkv_b"],
+                 rope=(cos, sin, S, (Hq + Hk) * 64) if FUSED_ROPE else None)
+            if not FUSED_ROPE:
+                K.rope(qkv, Ml, S, Hq + Hk, cos, sin)
             ox = self._buf(("ox", i), Ml, qn + Po, zero=lora)
             o = ox[:, :qn]
             lse = self._e(B * Hq * S, dtype=F32)

@@ -43,6 +43,7 @@ class GemmDesc(ctypes.Structure):
         ("ksplit_max", c_int), ("variant", c_int), ("drop_operand", c_int),
         ("colsum", c_vp), ("colsum_ws", c_vp), ("maskbits", c_vp), ("ldbits", c_i64), ("rem_ws", c_vp),
         ("rem_ws_floats", c_i64), ("resid_bf16", c_int), ("split_ws", c_vp), ("split_ws_floats", c_i64),
+        ("rope_cos", c_vp), ("rope_sin", c_vp), ("rope_S", c_int), ("rope_ncols", c_int),
     ]
 
 
@@ -130,6 +131,10 @@ def gemm(A, B, C, M, N, K, layout, lda, ldb, ldc, **kw):
         if B.dtype != torch.float32 or C.dtype != torch.float32:
             raise RuntimeError("fp32 parity-mode GEMM needs f32 A, B and C")
         check(lib().slx_gemm_f32(ctypes.byref(d), stream_ptr()), "slx_gemm_f32")
+        rope = kw.get("rope")
+        if rope is not None:  # the f32 kernels have no fused RoPE epilogue: the separate rotation
+            cos, sin, rs, rn = rope
+            rope_rows(C, M, rs, rn // 64, cos, sin)
         return
     check(lib().slx_gemm_bf16(ctypes.byref(d), stream_ptr()), "slx_gemm_bf16")
 
@@ -137,7 +142,7 @@ def gemm(A, B, C, M, N, K, layout, lda, ldb, ldc, **kw):
 def _gemm_desc(A, B, C, M, N, K, layout, lda, ldb, ldc, *, epi=EPI_STORE, alpha=1.0, bias=None, ls=None,
                aux=None, ldaux=0, aux_out=None, ldaux_out=0, resid=None, ldr=0, accumulate=False,
                seed=0, drop_p=0.0, ldmask=0, batch=1, sA=0, sB=0, sC=0, ksplit_max=0, variant=None, drop_operand=0,
-               colsum=None, maskbits=None, split_ws=True):
+               colsum=None, maskbits=None, split_ws=True, rope=None):
     _require_cuda(A, B, C)
     d = GemmDesc()
     d.layout, d.epilogue = layout, epi
@@ -176,6 +181,10 @@ def _gemm_desc(A, B, C, M, N, K, layout, lda, ldb, ldc, *, epi=EPI_STORE, alpha=
             # zeroed once: the last 16384 words are the in-launch split-K arrival counters (left zero by every call)
             sw = _split_ws[sk] = torch.zeros(SPLIT_WS_FLOATS, dtype=torch.float32, device=C.device)
         d.split_ws, d.split_ws_floats = sw.data_ptr(), sw.numel()
+    if rope is not None:  # (cos, sin, S, ncols): RoPE fused into a bf16 STORE epilogue (the Qwen2 q|k columns)
+        cos, sin, rs, rn = rope
+        _require_cuda(cos, sin)
+        d.rope_cos, d.rope_sin, d.rope_S, d.rope_ncols = cos.data_ptr(), sin.data_ptr(), int(rs), int(rn)
     if colsum is not None:
         need = (int(M) + 63) // 64 * int(N)
         ws = _colsum_ws.get(sk)
@@ -388,6 +397,10 @@ def attn_ws(B, S, Hq, Hkv, device, rope=False):
         ws["dk_acc"] = torch.empty(B * S * Hq * 64, device=device)
         ws["dv_acc"] = torch.empty(B * S * Hq * 64, device=device)
     return ws
+
+
+def rope_rows(x, ntok, S, nheads, cos, sin):
+    rope(x, ntok, S, nheads, cos, sin)
 
 
 def rope(x, ntok, S, nheads, cos, sin, inverse=False):

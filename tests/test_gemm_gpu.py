@@ -329,6 +329,38 @@ def test_gemm_fe_epilogues(dev, M, Kd):
         assert ((a - b).abs() <= tol * (1 + b.abs())).all(), k
 
 
+@pytest.mark.parametrize("M,variant", [(6384, 0), (6384, 2), (6384, 7), (600, 0), (8432, 0)])
+def test_gemm_rope_epilogue(dev, M, variant):
+    """RoPE fused into the bf16 STORE epilogue (slx_gemm_desc.rope_*): the Qwen2 q|k|v projection with bias, rotation
+    on the q and k head slots (columns < 16 * 64), v untouched; position = row % S. Against torch (rotation of the f32
+    product, one rounding) and no further from it than the separate GEMM + slx_rope (two roundings)."""
+    from simlingo_amd import kernels as KK
+    S, N, Kd = 798, 1152, 1024
+    g = torch.Generator(device=dev).manual_seed(M + variant)
+    x = torch.randn(M, Kd, device=dev, generator=g).bfloat16()
+    w = (torch.randn(N, Kd, device=dev, generator=g) * 0.03).bfloat16()
+    bias = torch.randn(N, device=dev, generator=g)
+    cos, sin = KK.rope_tables(S, 1e6, dev)
+    fused = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    K.gemm(x, w, fused, M, N, Kd, K.GEMM_NT, Kd, Kd, N, bias=bias, rope=(cos, sin, S, 1024), variant=variant)
+    sep = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    K.gemm(x, w, sep, M, N, Kd, K.GEMM_NT, Kd, Kd, N, bias=bias, variant=variant)
+    K.rope(sep, M, S, 16, cos, sin)
+    y = x.float() @ w.float().t() + bias
+    pos = torch.arange(M, device=dev) % S
+    c, s_ = cos[pos].repeat(1, 1), sin[pos]
+    ref = y.clone()
+    for h in range(16):
+        a, b = y[:, 64 * h:64 * h + 32], y[:, 64 * h + 32:64 * h + 64]
+        ref[:, 64 * h:64 * h + 32] = a * c - b * s_
+        ref[:, 64 * h + 32:64 * h + 64] = b * c + a * s_
+    torch.testing.assert_close(fused.float(), ref, atol=2e-2, rtol=1e-2)
+    assert torch.equal(fused[:, 1024:], sep[:, 1024:])  # v columns: plain epilogue
+    # one rounding instead of two: never further from the f32 rotation than the separate pass
+    ef, es = (fused.float() - ref).abs().max().item(), (sep.float() - ref).abs().max().item()
+    assert ef <= es + 1e-6, (ef, es)
+
+
 _FOLD_SCRIPT = r"""
 import sys, torch
 sys.path.insert(0, sys.argv[1])
