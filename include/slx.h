@@ -310,9 +310,15 @@ int slx_llava_merge_bwd(const float* dout, int C, int64_t n_img, int npatch_h, i
                         int wu, int pool, void* dsrc, slx_stream_t s);
 /* table: n device-resident entries {src f32*, lds, dst*, ldd, rows, cols, float-bits scale, mode}:
  * dst = src * scale, mode 0 bf16, 1 f32 (the fp32 parity mode), 2 bf16 in slx_lora_pack_a's fragment order
- * (rows == 32), 3 bf16 in layout 1 of slx_lora_pack_a. Packs LoRA B (scaled by lora_alpha/r) into the fused
+ * (rows == 32), 3 bf16 in layout 1 of slx_lora_pack_a, 4 bf16 transposed (dst[c * ldd + r]).
+ * Packs LoRA B (scaled by lora_alpha/r) into the fused
  * [W | s*B] operands and LoRA A into the packed copies slx_lora_down / slx_lora_bwd read, once per optimizer step. */
 int slx_pack_scaled(const int64_t* table, int n, slx_stream_t s);
+/* table: n device-resident entries {src bf16*, lds, dst bf16*, ldd, rows, cols}: dst[c][r] = src[r][c].
+ * max_tiles >= the largest ceil(rows/64)*ceil(cols/64) of the entries. Refreshes the [in][out] copies of the
+ * weights whose data-gradient GEMM then runs in the NT layout (no reference counterpart: a layout choice of
+ * this implementation for torch.nn.Linear's backward, dX = dY W). */
+int slx_transpose_bf16(const int64_t* table, int n, int64_t max_tiles, slx_stream_t s);
 
 /* ---- KV-cached greedy decode (agent call, BASELINE configs[4]) -------------------------------------
  * Replaces the no-cache loop of LLM.greedy_sample (simlingo_training/models/language_model/llm.py:

@@ -2343,13 +2343,17 @@ static int gemm_launch(const slx_gemm_desc* d, int v, hipStream_t st, int mshift
       SLX_CHECK_ARG(d->out_f32 && d->layout == SLX_GEMM_NT && d->resid && d->ls, "slx_gemm_bf16: RESID_LS needs NT, f32 out, resid, ls");
       return launch_any<true, true, EPI_RESID_LS, float>(a, batch, st, v);
     case SLX_EPI_GELU_BWD:
-      SLX_CHECK_ARG(!d->out_f32 && d->layout == SLX_GEMM_NN && d->aux, "slx_gemm_bf16: GELU_BWD needs NN, bf16 out, aux");
+      SLX_CHECK_ARG(!d->out_f32 && (d->layout == SLX_GEMM_NN || d->layout == SLX_GEMM_NT) && d->aux,
+                    "slx_gemm_bf16: GELU_BWD needs NN or NT, bf16 out, aux");
+      if (d->layout == SLX_GEMM_NT) return launch_any<true, true, EPI_GELU_BWD, bf16>(a, batch, st, v);
       return launch_any<true, false, EPI_GELU_BWD, bf16>(a, batch, st, v);
     case SLX_EPI_QGELU:
       SLX_CHECK_ARG(!d->out_f32 && d->layout == SLX_GEMM_NT && d->aux_out, "slx_gemm_bf16: QGELU needs NT, bf16 out, aux_out");
       return launch_any<true, true, EPI_QGELU, bf16>(a, batch, st, v);
     case SLX_EPI_QGELU_BWD:
-      SLX_CHECK_ARG(!d->out_f32 && d->layout == SLX_GEMM_NN && d->aux, "slx_gemm_bf16: QGELU_BWD needs NN, bf16 out, aux");
+      SLX_CHECK_ARG(!d->out_f32 && (d->layout == SLX_GEMM_NN || d->layout == SLX_GEMM_NT) && d->aux,
+                    "slx_gemm_bf16: QGELU_BWD needs NN or NT, bf16 out, aux");
+      if (d->layout == SLX_GEMM_NT) return launch_any<true, true, EPI_QGELU_BWD, bf16>(a, batch, st, v);
       return launch_any<true, false, EPI_QGELU_BWD, bf16>(a, batch, st, v);
     case SLX_EPI_SWIGLU_BWD:
       SLX_CHECK_ARG(!d->out_f32 && d->layout == SLX_GEMM_NN && d->aux, "slx_gemm_bf16: SWIGLU_BWD needs NN, bf16 out, aux");

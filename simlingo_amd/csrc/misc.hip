@@ -468,7 +468,56 @@ __global__ void pack_scaled_kernel(const long long* tab, int n) {
     if (mode == 1) reinterpret_cast<float*>(t[2])[r * ldd + c] = v;
     else if (mode == 2) reinterpret_cast<bf16*>(t[2])[lora_frag_index((int)r, (int)c)] = (bf16)v;
     else if (mode == 3) reinterpret_cast<bf16*>(t[2])[lora_dxfrag_index((int)r, (int)c)] = (bf16)v;
+    else if (mode == 4) reinterpret_cast<bf16*>(t[2])[c * ldd + r] = (bf16)v;
     else reinterpret_cast<bf16*>(t[2])[r * ldd + c] = (bf16)v;
+  }
+}
+
+// Batched bf16 transpose dst[c][r] = src[r][c]: entry y of `tab` = {src, lds, dst, ldd, rows, cols}, block x = one
+// 64 x 64 tile (blocks past the entry's tile count exit). Whole, aligned tiles move as 16-B row pieces through a
+// padded LDS tile (one read and one write of every byte, coalesced on both sides); ragged edges go element-wise.
+// Keeps the [in][out] copies of the weights whose data-gradient GEMM dX = dY W would otherwise run NN (slower main
+// loop than NT on gfx950: tools/nn_vs_nt.py) in step with the optimizer.
+__global__ __launch_bounds__(256) void transpose_bf16_kernel(const long long* tab) {
+  const long long* t = tab + 6 * (long)blockIdx.y;
+  const unsigned short* src = reinterpret_cast<const unsigned short*>(t[0]);
+  const long lds = t[1];
+  unsigned short* dst = reinterpret_cast<unsigned short*>(t[2]);
+  const long ldd = t[3];
+  const long rows = t[4], cols = t[5];
+  const long tc = (cols + 63) / 64;
+  const long tile = blockIdx.x;
+  if (tile >= ((rows + 63) / 64) * tc) return;
+  const long r0 = (tile / tc) * 64, c0 = (tile % tc) * 64;
+  __shared__ __attribute__((aligned(16))) unsigned short s[64][72];
+  const int tid = threadIdx.x;
+  const bool vec = ((lds | ldd) & 7) == 0 && (((uintptr_t)src | (uintptr_t)dst) & 15) == 0 && r0 + 64 <= rows &&
+                   c0 + 64 <= cols;
+  if (vec) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int r = (tid >> 3) + 32 * h, c = (tid & 7) * 8;
+      *reinterpret_cast<uint4*>(&s[r][c]) = *reinterpret_cast<const uint4*>(src + (r0 + r) * lds + c0 + c);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int oc = (tid >> 3) + 32 * h, orr = (tid & 7) * 8;
+      unsigned short o[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = s[orr + j][oc];
+      *reinterpret_cast<uint4*>(dst + (c0 + oc) * ldd + r0 + orr) = *reinterpret_cast<const uint4*>(o);
+    }
+  } else {
+    for (int i = tid; i < 4096; i += 256) {
+      const long r = r0 + i / 64, c = c0 + i % 64;
+      if (r < rows && c < cols) s[i / 64][i % 64] = src[r * lds + c];
+    }
+    __syncthreads();
+    for (int i = tid; i < 4096; i += 256) {
+      const long c = c0 + i / 64, r = r0 + i % 64;
+      if (r < rows && c < cols) dst[c * ldd + r] = s[i % 64][i / 64];
+    }
   }
 }
 
@@ -783,6 +832,15 @@ int slx_pack_scaled(const int64_t* table, int n, slx_stream_t s) {
   if (n <= 0) return 0;
   hipLaunchKernelGGL(pack_scaled_kernel, dim3(n, 32), dim3(256), 0, (hipStream_t)s, (const long long*)table, n);
   SLX_LAUNCH_CHECK("slx_pack_scaled");
+  return 0;
+}
+
+int slx_transpose_bf16(const int64_t* table, int n, int64_t max_tiles, slx_stream_t s) {
+  SLX_CHECK_ARG(n >= 0 && n <= 65535 && max_tiles >= 0 && max_tiles <= 0x7fffffff, "slx_transpose_bf16: bad n / max_tiles");
+  if (n == 0 || max_tiles == 0) return 0;
+  hipLaunchKernelGGL(transpose_bf16_kernel, dim3((unsigned)max_tiles, n), dim3(256), 0, (hipStream_t)s,
+                     (const long long*)table);
+  SLX_LAUNCH_CHECK("slx_transpose_bf16");
   return 0;
 }
 

@@ -42,6 +42,9 @@ SWIGLU_BWD_VARIANT = int(os.environ.get("SLX_SWIGLU_BWD_VARIANT", "2"))
 LORA_DB_SPLIT = int(os.environ.get("SLX_LORA_DB_SPLIT", "0"))
 # Qwen2 RoPE fused into the q|k|v GEMM epilogue (0: the separate slx_rope pass, A/B hook)
 FUSED_ROPE = os.environ.get("SLX_FUSED_ROPE", "1") != "0"
+# Data-gradient GEMMs dX = dY W over [in][out] copies of the weights (NT main loop, 6-21% faster than NN on the step's
+# shapes: profiles/round3_nn_vs_nt.txt); 0 runs them NN over W itself (A/B hook)
+NT_DGRAD = os.environ.get("SLX_NT_DGRAD", "1") != "0"
 ALIGN = 64  # elements; keeps every parameter view 256-B aligned
 
 
@@ -131,6 +134,7 @@ class VLAEngine(EngineOps):
         self.saved = None
         self._cos_sin = {}
         self._build_lora_cat()
+        self._build_transposes()
         self.probe_site = None     # name of a call site to bracket with HIP events (bench roofline)
         self.probe_events = []
 
@@ -152,8 +156,9 @@ class VLAEngine(EngineOps):
                 else:
                     self.W[s.name].copy_(t.to(self.device, self.adt))
             self.wbf.copy_(self.master.to(BF16))
-            self._refresh_derived()
             self._build_lora_cat()
+            self._build_transposes()
+            self._refresh_derived()
         for name in ("m_state", "v_state"):
             if hasattr(self, name):
                 delattr(self, name)
@@ -178,6 +183,47 @@ class VLAEngine(EngineOps):
         self.wpatch[:, : cfg.patch_k].copy_(self.W["vit.patch.w"])
         if getattr(self, "_pack_tab", None) is not None:
             K.call("slx_pack_scaled", K.P(self._pack_tab), self._pack_n, K.stream_ptr())
+        if getattr(self, "_tr_tab", None) is not None:
+            K.call("slx_transpose_bf16", K.P(self._tr_tab), self._tr_tab.shape[0], self._tr_tiles, K.stream_ptr())
+
+    def _transpose_table(self, pairs):
+        """[(w [r][c], wt [c][r]), ...] -> (device table for slx_transpose_bf16, most 64 x 64 tiles of an entry)."""
+        rows = [[w.data_ptr(), w.stride(0), wt.data_ptr(), wt.stride(0), w.shape[0], w.shape[1]] for w, wt in pairs]
+        tiles = max(((w.shape[0] + 63) // 64) * ((w.shape[1] + 63) // 64) for w, _ in pairs)
+        return torch.tensor(rows, dtype=torch.int64, device=self.device), tiles
+
+    def _build_transposes(self):
+        """[in][out] copies W^T of the Linear weights whose data-gradient GEMM dX = dY W then runs NT (NT_DGRAD): the
+        mlp1 / InternViT (and, without LoRA, Qwen2) weights, re-transposed from their bf16 working copies after every
+        optimizer step by one batched launch (_refresh_derived). The LoRA-concatenated Qwen2 operands get theirs in
+        _build_lora_cat."""
+        self.WT = {}
+        self._tr_tab = None
+        if self.precise or not NT_DGRAD:
+            return
+        cfg = self.cfg
+        names = ["proj.fc1.w", "proj.fc2.w"]
+        if not cfg.vit_freeze:
+            names += [f"vit.{i}.{n}" for i in range(cfg.vit_layers) for n in ("qkv.w", "proj.w", "fc1.w", "fc2.w")]
+        if not cfg.lora:
+            names += [f"llm.{i}.{n}" for i in range(cfg.llm_layers) for n in ("qkv_w", "o_w", "gate_up_w", "down_w")]
+        for n in names:
+            w = self.W[n]
+            self.WT[n] = torch.empty(w.shape[1], w.shape[0], dtype=BF16, device=self.device)
+        self._tr_tab, self._tr_tiles = self._transpose_table([(self.W[n], self.WT[n]) for n in names])
+        K.call("slx_transpose_bf16", K.P(self._tr_tab), len(names), self._tr_tiles, K.stream_ptr())
+
+    def _dxw(self, cat, group, name):
+        """(w, w^T or None) of a Qwen2 data-gradient GEMM: the LoRA-concatenated operand of `group` or the weight."""
+        if cat is not None:
+            return cat[group], cat["T." + group]
+        return self.W[name], self.WT.get(name)
+
+    def _mm_dx(self, dy, w, wt, out, **kw):
+        """dX = dY W for a Linear weight w [out][in]: NT over its transposed copy wt [in][out] when there is one."""
+        if wt is not None:
+            return K.mm(dy, wt, out, tb=True, **kw)
+        return K.mm(dy, w, out, tb=False, **kw)
 
     # LoRA folded into the frozen GEMMs by K-concatenation: y = [x | t] . [W | s*B_blockdiag]^T with
     # t = drop(x) A^T written into the extra columns of the activation buffer. Per layer and group:
@@ -199,6 +245,8 @@ class VLAEngine(EngineOps):
         s = float(cfg.lora_scale)
         entries = []
         r = cfg.lora_r
+        nt = NT_DGRAD and not self.precise
+        once = []
         for i in range(cfg.llm_layers):
             p = f"llm.{i}."
             cats = {}
@@ -208,6 +256,10 @@ class VLAEngine(EngineOps):
                 N, Kin = base.shape
                 w = torch.zeros(N, Kin + pad, dtype=self.adt, device=self.device)
                 w[:, :Kin].copy_(base)
+                # [W | s*B]^T for the NT data-gradient GEMM: the frozen W^T once, the s*B^T rows with every pack
+                wt = torch.zeros(Kin + pad, N, dtype=self.adt, device=self.device) if nt else None
+                if nt:
+                    once.append((base, wt[:Kin]))
                 row = 0
                 for j, site in enumerate(sites):
                     out_s = lora_io(cfg, site)[1]
@@ -215,8 +267,13 @@ class VLAEngine(EngineOps):
                     dst = w[row:row + out_s, Kin + r * j: Kin + r * (j + 1)]
                     entries.append([b.data_ptr(), b.stride(0), dst.data_ptr(), dst.stride(0), out_s, r,
                                     int(np.float32(s).view(np.int32)), int(self.precise)])
+                    if nt:
+                        dt = wt[Kin + r * j: Kin + r * (j + 1), row:row + out_s]
+                        entries.append([b.data_ptr(), b.stride(0), dt.data_ptr(), dt.stride(0), out_s, r,
+                                        int(np.float32(s).view(np.int32)), 4])
                     row += out_s
                 cats[g] = w
+                cats["T." + g] = wt
             # A_s zero-padded to 64 rows: the dropout-masked dgrad dx += drop'(dT_s A_s) then runs as a K=64 GEMM
             # whose A operand is the 64-column window of the group's dT buffer starting at site s (the columns past
             # the site multiply the zero rows), which keeps it on the LDS-DMA path.
@@ -236,6 +293,10 @@ class VLAEngine(EngineOps):
         self._pack_tab = torch.tensor(entries, dtype=torch.int64, device=self.device)
         self._pack_n = len(entries)
         K.call("slx_pack_scaled", K.P(self._pack_tab), self._pack_n, K.stream_ptr())
+        if once:
+            tab, tiles = self._transpose_table(once)
+            K.call("slx_transpose_bf16", K.P(tab), len(once), tiles, K.stream_ptr())
+            torch.cuda.current_stream(self.device).synchronize()  # the one-time table dies here
 
     def rope_tables(self, S):
         if S not in self._cos_sin:
@@ -586,7 +647,7 @@ class VLAEngine(EngineOps):
             # bf16 with LoRA: the gradient of act that a bf16 Linear backward produces under autocast (read once by the
             # SwiGLU epilogue and, columns Fl.., as the dT operand); f32 for the plain slx_swiglu_bwd path
             dax = self._e(Ml, Fl + Pd, dtype=BF16 if lora else F32)
-            K.mm(dxb, cat["down"] if lora else self.W[p + "down_w"], dax, tb=False)
+            self._mm_dx(dxb, *self._dxw(cat, "down", p + "down_w"), dax)
             dgu = self._e(Ml, 2 * Fl)
             if lora:  # the down-site dropout dgrad and the SwiGLU backward share one GEMM epilogue
                 self._lora_bwd(i, ("down",), [dxb], ax[:, Fl:], ax[:, :Fl], dax[:, Fl:], dax[:, :Fl], sv,
@@ -596,7 +657,7 @@ class VLAEngine(EngineOps):
                        K.stream_ptr())
             del dax
             dh2x = self._e(Ml, d + Pg, dtype=F32)
-            K.mm(dgu, cat["gu"] if lora else self.W[p + "gate_up_w"], dh2x, tb=False)
+            self._mm_dx(dgu, *self._dxw(cat, "gu", p + "gate_up_w"), dh2x)
             if lora:
                 self._lora_bwd(i, ("gate", "up"), [dgu[:, :Fl], dgu[:, Fl:]], h2x[:, d:], h2x[:, :d], dh2x[:, d:],
                                dh2x[:, :d], sv)
@@ -604,7 +665,7 @@ class VLAEngine(EngineOps):
             K.norm_bwd(Ls["n2"], dh2x, dX, dx_accumulate=True, dx_bf16=dxb)
             # o projection
             dox = self._e(Ml, qn + Po, dtype=F32)
-            K.mm(dxb, cat["o"] if lora else self.W[p + "o_w"], dox, tb=False)
+            self._mm_dx(dxb, *self._dxw(cat, "o", p + "o_w"), dox)
             dob = self._e(Ml, qn)
             if lora:  # the LoRA dx term and the bf16 cast of dO in one pass
                 self._lora_bwd(i, ("o",), [dxb], ox[:, qn:], ox[:, :qn], dox[:, qn:], dox[:, :qn], sv, dx_bf16=dob)
@@ -617,7 +678,7 @@ class VLAEngine(EngineOps):
                        dqkv[:, :qn], dqkv[:, qn:qn + kn], dqkv[:, qn + kn:], ws, rope_cos=cos, rope_sin=sin,
                        B=B, S=S, Hq=Hq, Hkv=Hk, causal=True, seqlens=dplan["seqlens"])
             dhx = self._e(Ml, d + Pq, dtype=F32)
-            K.mm(dqkv, cat["qkv"] if lora else self.W[p + "qkv_w"], dhx, tb=False)
+            self._mm_dx(dqkv, *self._dxw(cat, "qkv", p + "qkv_w"), dhx)
             if lora:
                 self._lora_bwd(i, ("q", "k", "v"), [dqkv[:, :qn], dqkv[:, qn:qn + kn], dqkv[:, qn + kn:]], hx[:, d:],
                                hx[:, :d], dhx[:, d:], dhx[:, :d], sv)
@@ -646,11 +707,11 @@ class VLAEngine(EngineOps):
         K.mm(dimg, sv["a1"], self.G["proj.fc2.w"], ta=True, tb=False, accumulate=True)
         self._colsum(dimg, self.G["proj.fc2.b"], 0)
         da1 = self._e(Mi, d)
-        K.mm(dimg, self.W["proj.fc2.w"], da1, tb=False, epi=K.EPI_GELU_BWD, aux=sv["a1pre"], ldaux=d,
-             colsum=self.G["proj.fc1.b"])
+        self._mm_dx(dimg, self.W["proj.fc2.w"], self.WT.get("proj.fc2.w"), da1, epi=K.EPI_GELU_BWD, aux=sv["a1pre"],
+                    ldaux=d, colsum=self.G["proj.fc1.b"])
         K.mm(da1, sv["z"], self.G["proj.fc1.w"], ta=True, tb=False, accumulate=True)
         dz = self._e(Mi, 4 * D, dtype=F32)
-        K.mm(da1, self.W["proj.fc1.w"], dz, tb=False)
+        self._mm_dx(da1, self.W["proj.fc1.w"], self.WT.get("proj.fc1.w"), dz)
         T = cfg.vit_tokens
         dxv = self._z(Mv, D)
         ws_n = self._ws(K.norm_ws_floats(4 * D))
@@ -678,15 +739,15 @@ class VLAEngine(EngineOps):
             if not PAIR_WGRAD:
                 K.mm(g, Ls["hact"], self.G[p + "fc2.w"], ta=True, tb=False, accumulate=True)
             dh = self._e(Mv, F_)
-            K.mm(g, self.W[p + "fc2.w"], dh, tb=False, epi=K.EPI_GELU_BWD, aux=Ls["hpre"], ldaux=F_,
-                 colsum=self.G[p + "fc1.b"])  # fc1.b grad = column sums of dh, in the same epilogue
+            self._mm_dx(g, self.W[p + "fc2.w"], self.WT.get(p + "fc2.w"), dh, epi=K.EPI_GELU_BWD, aux=Ls["hpre"],
+                        ldaux=F_, colsum=self.G[p + "fc1.b"])  # fc1.b grad = column sums of dh, in the same epilogue
             if PAIR_WGRAD:  # fc2.w and fc1.w gradients as one launch (two under-filled grids fill the chip together)
                 with self._probe("vit.wgrad_fc"):
                     K.mm_pair((g, Ls["hact"], self.G[p + "fc2.w"]), (dh, Ls["h2"], self.G[p + "fc1.w"]))
             else:
                 K.mm(dh, Ls["h2"], self.G[p + "fc1.w"], ta=True, tb=False, accumulate=True)
             dh2 = self._e(Mv, D)  # bf16: the gradient a bf16 Linear backward hands the fp32 LayerNorm under autocast
-            K.mm(dh, self.W[p + "fc1.w"], dh2, tb=False)
+            self._mm_dx(dh, self.W[p + "fc1.w"], self.WT.get(p + "fc1.w"), dh2)
             del dh
             # x_mid = x_in + ls1 * proj(attn(ln1(x_in))): its branch backward (g = ls1 * dx_mid, dls1, proj.b grad)
             # fused into the LN2 backward that produces dx_mid
@@ -696,7 +757,7 @@ class VLAEngine(EngineOps):
             if not PAIR_WGRAD:
                 K.mm(g, Ls["o"], self.G[p + "proj.w"], ta=True, tb=False, accumulate=True)
             do = self._e(Mv, D)
-            K.mm(g, self.W[p + "proj.w"], do, tb=False)
+            self._mm_dx(g, self.W[p + "proj.w"], self.WT.get(p + "proj.w"), do)
             qkv = Ls["qkv"]
             dqkv = self._e(Mv, 3 * D)
             K.attn_bwd(qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], Ls["o"], Ls["lse"], do,
@@ -708,7 +769,7 @@ class VLAEngine(EngineOps):
                     K.mm_pair((g, Ls["o"], self.G[p + "proj.w"]), (dqkv, Ls["h1"], self.G[p + "qkv.w"]))
             else:
                 K.mm(dqkv, Ls["h1"], self.G[p + "qkv.w"], ta=True, tb=False, accumulate=True)
-            K.mm(dqkv, self.W[p + "qkv.w"], dh2, tb=False)
+            self._mm_dx(dqkv, self.W[p + "qkv.w"], self.WT.get(p + "qkv.w"), dh2)
             del dqkv
             nxt = None
             if i > 0:  # the next (lower) layer's ls2 branch backward, fused onto dx_in
