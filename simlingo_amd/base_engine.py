@@ -16,6 +16,7 @@ residual streams f32, GEMM operands and saved activations bf16, no activation re
 from __future__ import annotations
 
 import math
+import os
 
 import numpy as np
 import torch
@@ -29,6 +30,8 @@ from .plan import KIND_QUERY, KIND_WP
 
 BF16, F32 = torch.bfloat16, torch.float32
 ALIGN = 64
+# data-gradient GEMMs over [in][out] weight copies (engine.NT_DGRAD; 0: NN over the weights, A/B hook)
+NT_DGRAD = os.environ.get("SLX_NT_DGRAD", "1") != "0"
 
 
 class BaseEngine(EngineOps):
@@ -75,11 +78,18 @@ class BaseEngine(EngineOps):
         self._plans = {}
         self.probe_site = None
         self.probe_events = []
+        names = []
+        if NT_DGRAD and not self.precise:  # every weight is trainable: all copies refreshed after each optimizer step
+            names = ["enc.proj.w", "mm.fc1.w", "mm.fc2.w"]
+            names += [f"vit.{i}.{n}" for i in range(cfg.vit_used) for n in ("qkv.w", "proj.w", "fc1.w", "fc2.w")]
+            names += [f"llm.{i}.{n}" for i in range(cfg.llm_layers) for n in ("qkv_w", "o_w", "gate_up_w")]
+        self._transposed_copies(names)
         self._refresh_derived()
 
     def _refresh_derived(self):
         cfg = self.cfg
         self.wpatch[:, :cfg.patch_k].copy_(self.W["vit.patch.w"])
+        self._refresh_transposes()
 
     def rope_tables(self, S):
         if S not in self._cos_sin:
@@ -299,20 +309,20 @@ class BaseEngine(EngineOps):
                    aux=L["gu"], ldaux=2 * Fl)
             K.mm(dgu, L["h2"], self.G[p + "gate_up_w"], ta=True, tb=False, accumulate=True)
             dh2 = self._e(Ml, d, dtype=F32)
-            K.mm(dgu, self.W[p + "gate_up_w"], dh2, tb=False)
+            self._mm_dx(dgu, self.W[p + "gate_up_w"], self.WT.get(p + "gate_up_w"), dh2)
             del dgu
             K.norm_bwd(L["n2"], dh2, dX, dx_accumulate=True, dgamma=self.G[p + "ln2"], param_accumulate=True,
                        ws=self._ws(K.norm_ws_floats(d)), dx_bf16=dxb)
             K.mm(dxb, L["o"], self.G[p + "o_w"], ta=True, tb=False, accumulate=True)
             do = self._e(Ml, d)
-            K.mm(dxb, self.W[p + "o_w"], do, tb=False)
+            self._mm_dx(dxb, self.W[p + "o_w"], self.WT.get(p + "o_w"), do)
             qkv = L["qkv"]
             dqkv = self._e(Ml, 3 * d)
             K.attn_bwd(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], L["o"], L["lse"], do, dqkv[:, :d], dqkv[:, d:2 * d],
                        dqkv[:, 2 * d:], ws, rope_cos=cos, rope_sin=sin, B=B, S=S, Hq=Hh, Hkv=Hh, causal=True)
             K.mm(dqkv, L["h"], self.G[p + "qkv_w"], ta=True, tb=False, accumulate=True)
             dh = self._e(Ml, d, dtype=F32)
-            K.mm(dqkv, self.W[p + "qkv_w"], dh, tb=False)
+            self._mm_dx(dqkv, self.W[p + "qkv_w"], self.WT.get(p + "qkv_w"), dh)
             K.norm_bwd(L["n1"], dh, dX, dx_accumulate=True, dgamma=self.G[p + "ln1"], param_accumulate=True,
                        ws=self._ws(K.norm_ws_floats(d)), dx_bf16=dxb)
             del dqkv, dh, dh2, do
@@ -338,7 +348,7 @@ class BaseEngine(EngineOps):
         self.G["enc.camera"].copy_(self.G["enc.proj.b"])
         K.mm(dvisb, sv["merged"], self.G["enc.proj.w"], ta=True, tb=False, accumulate=True)
         dmerged = self._e(nv, Pd, dtype=F32)
-        K.mm(dvisb, self.W["enc.proj.w"], dmerged, tb=False)
+        self._mm_dx(dvisb, self.W["enc.proj.w"], self.WT.get("enc.proj.w"), dmerged)
         del dvis, dvisb, dpre
         # image_newline: the last column of every pooled row
         r0, hu, c0, wu = cfg.unpad()
@@ -353,12 +363,12 @@ class BaseEngine(EngineOps):
         K.mm(dp2, sv["p1"], self.G["mm.fc2.w"], ta=True, tb=False, accumulate=True)
         self._colsum(dp2, self.G["mm.fc2.b"], 0)
         dp1 = self._e(Mf, Pd)
-        K.mm(dp2, self.W["mm.fc2.w"], dp1, tb=False, epi=K.EPI_GELU_BWD, aux=sv["p1pre"], ldaux=Pd,
+        self._mm_dx(dp2, self.W["mm.fc2.w"], self.WT.get("mm.fc2.w"), dp1, epi=K.EPI_GELU_BWD, aux=sv["p1pre"], ldaux=Pd,
              colsum=self.G["mm.fc1.b"])
         del dp2
         K.mm(dp1, sv["feat"], self.G["mm.fc1.w"], ta=True, tb=False, accumulate=True)
         dfeatv = self._e(Mf, D, dtype=F32)
-        K.mm(dp1, self.W["mm.fc1.w"], dfeatv, tb=False)
+        self._mm_dx(dp1, self.W["mm.fc1.w"], self.WT.get("mm.fc1.w"), dfeatv)
         del dp1
         dxv = self._z(Mv, D)
         K.call("slx_scatter_rows", K.P(dfeatv), D, K.P(pl["nocls"]), Mf, D, K.P(dxv), D, 0, K.stream_ptr())
@@ -377,11 +387,11 @@ class BaseEngine(EngineOps):
                    K.P(self.G[p + "fc2.b"]), 1, K.P(None), K.stream_ptr())
             K.mm(gb, L["hact"], self.G[p + "fc2.w"], ta=True, tb=False, accumulate=True)
             dh = self._e(Mv, F_)
-            K.mm(gb, self.W[p + "fc2.w"], dh, tb=False, epi=K.EPI_QGELU_BWD, aux=L["hpre"], ldaux=F_,
+            self._mm_dx(gb, self.W[p + "fc2.w"], self.WT.get(p + "fc2.w"), dh, epi=K.EPI_QGELU_BWD, aux=L["hpre"], ldaux=F_,
                  colsum=self.G[p + "fc1.b"])
             K.mm(dh, L["h2"], self.G[p + "fc1.w"], ta=True, tb=False, accumulate=True)
             dh2 = self._e(Mv, D, dtype=F32)
-            K.mm(dh, self.W[p + "fc1.w"], dh2, tb=False)
+            self._mm_dx(dh, self.W[p + "fc1.w"], self.WT.get(p + "fc1.w"), dh2)
             del dh
             K.norm_bwd(L["n2"], dh2, dxv, dx_accumulate=True, dgamma=self.G[p + "ln2.w"], dbeta=self.G[p + "ln2.b"],
                        ws=nws, param_accumulate=True)
@@ -390,7 +400,7 @@ class BaseEngine(EngineOps):
                    K.P(self.G[p + "proj.b"]), 1, K.P(None), K.stream_ptr())
             K.mm(gb, L["o"], self.G[p + "proj.w"], ta=True, tb=False, accumulate=True)
             do = self._e(Mv, D)
-            K.mm(gb, self.W[p + "proj.w"], do, tb=False)
+            self._mm_dx(gb, self.W[p + "proj.w"], self.WT.get(p + "proj.w"), do)
             qkv = L["qkv"]
             dqkv = self._e(Mv, 3 * D)
             K.attn_bwd(qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:], L["o"], L["lse"], do, dqkv[:, :D],
@@ -398,7 +408,7 @@ class BaseEngine(EngineOps):
             del do
             K.mm(dqkv, L["h1"], self.G[p + "qkv.w"], ta=True, tb=False, accumulate=True)
             self._colsum(dqkv, self.G[p + "qkv.b"], 0)
-            K.mm(dqkv, self.W[p + "qkv.w"], dh2, tb=False)
+            self._mm_dx(dqkv, self.W[p + "qkv.w"], self.WT.get(p + "qkv.w"), dh2)
             del dqkv
             K.norm_bwd(L["n1"], dh2, dxv, dx_accumulate=True, dgamma=self.G[p + "ln1.w"], dbeta=self.G[p + "ln1.b"],
                        ws=nws, param_accumulate=True)

@@ -396,6 +396,37 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* p, const float* g, fl
   }
 }
 
+// The same update four parameters per lane (16-B loads and stores of p / g / m / v, 8-B bf16 stores): n4 quads from
+// 16-B aligned p / g / m / v and an 8-B aligned pbf; the launcher runs the scalar kernel on the tail.
+__global__ __launch_bounds__(256) void adamw4_kernel(float4* p, const float4* g, float4* m, float4* v, bf16x4* pbf,
+                                                     long n4, float lr, float b1, float b2, float eps, float wd, float bc1,
+                                                     float bc2s, const float* sumsq, float max_norm, float gscale) {
+  float coef = gscale;
+  if (sumsq && max_norm > 0.f) {
+    const float tn = sqrtf(*sumsq) * gscale;
+    coef = gscale * fminf(1.f, max_norm / (tn + 1e-6f));
+  }
+  const float step = lr / bc1;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
+    const float4 g4 = g[i], p4 = p[i], m4 = m[i], v4 = v[i];
+    float gi[4] = {g4.x, g4.y, g4.z, g4.w}, pi[4] = {p4.x, p4.y, p4.z, p4.w};
+    float mi[4] = {m4.x, m4.y, m4.z, m4.w}, vi[4] = {v4.x, v4.y, v4.z, v4.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float gj = gi[j] * coef;
+      pi[j] = pi[j] * (1.f - lr * wd);
+      mi[j] = mi[j] + (1.f - b1) * (gj - mi[j]);
+      vi[j] = vi[j] * b2 + (1.f - b2) * gj * gj;
+      const float den = sqrtf(vi[j]) / bc2s + eps;
+      pi[j] -= step * mi[j] / den;
+    }
+    p[i] = {pi[0], pi[1], pi[2], pi[3]};
+    m[i] = {mi[0], mi[1], mi[2], mi[3]};
+    v[i] = {vi[0], vi[1], vi[2], vi[3]};
+    if (pbf) pbf[i] = {(bf16)pi[0], (bf16)pi[1], (bf16)pi[2], (bf16)pi[3]};
+  }
+}
+
 // dst[idx[i], :] (+)= src[i, :]   (f32 rows; idx unique)
 __global__ void scatter_rows_kernel(const float* src, long lds, const int* idx, long n, int D, float* dst, long ldd, int accumulate) {
   const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -789,11 +820,33 @@ int slx_adamw(float* p, const float* g, float* m, float* v, void* p_bf16, int64_
   if (!n) return 0;
   const float bc1 = 1.f - powf(beta1, (float)step);
   const float bc2s = sqrtf(1.f - powf(beta2, (float)step));
-  long blocks = (n + 255) / 256;
-  if (blocks > 8192) blocks = 8192;
-  hipLaunchKernelGGL(adamw_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)s, p, g, m, v, (bf16*)p_bf16, n, lr,
-                     beta1, beta2, eps, weight_decay, bc1, bc2s, sumsq, max_norm, grad_scale);
-  SLX_LAUNCH_CHECK("slx_adamw");
+  const bool vec = ((((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) == 0) &&
+                   (((uintptr_t)p_bf16 & 7) == 0);
+  long done = 0;
+  if (vec && n >= 4) {
+    const long n4 = n / 4;
+    // one quad per lane, no grid-stride loop: 1730 us at 315M parameters vs 1.83-2.03 ms with the grid capped at
+    // 65536-1024 blocks and 1.94 ms for the scalar kernel (tools/adamw_bench.py, profiles/round3_adamw_grid.txt);
+    // SLX_ADAMW_BLOCKS caps it (A/B hook)
+    static const long cap = [] { const char* e = getenv("SLX_ADAMW_BLOCKS"); return e ? atol(e) : 0L; }();
+    long blocks = (n4 + 255) / 256;
+    if (cap > 0 && blocks > cap) blocks = cap;
+    if (blocks > 0x7fffffffL) blocks = 0x7fffffffL;
+    hipLaunchKernelGGL(adamw4_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)s, (float4*)p, (const float4*)g,
+                       (float4*)m, (float4*)v, (bf16x4*)p_bf16, n4, lr, beta1, beta2, eps, weight_decay, bc1, bc2s, sumsq,
+                       max_norm, grad_scale);
+    SLX_LAUNCH_CHECK("slx_adamw");
+    done = n4 * 4;
+  }
+  if (done < n) {
+    const long rest = n - done;
+    long blocks = (rest + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(adamw_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)s, p + done, g + done, m + done,
+                       v + done, p_bf16 ? (bf16*)p_bf16 + done : nullptr, rest, lr, beta1, beta2, eps, weight_decay, bc1,
+                       bc2s, sumsq, max_norm, grad_scale);
+    SLX_LAUNCH_CHECK("slx_adamw");
+  }
   return 0;
 }
 

@@ -183,23 +183,15 @@ class VLAEngine(EngineOps):
         self.wpatch[:, : cfg.patch_k].copy_(self.W["vit.patch.w"])
         if getattr(self, "_pack_tab", None) is not None:
             K.call("slx_pack_scaled", K.P(self._pack_tab), self._pack_n, K.stream_ptr())
-        if getattr(self, "_tr_tab", None) is not None:
-            K.call("slx_transpose_bf16", K.P(self._tr_tab), self._tr_tab.shape[0], self._tr_tiles, K.stream_ptr())
-
-    def _transpose_table(self, pairs):
-        """[(w [r][c], wt [c][r]), ...] -> (device table for slx_transpose_bf16, most 64 x 64 tiles of an entry)."""
-        rows = [[w.data_ptr(), w.stride(0), wt.data_ptr(), wt.stride(0), w.shape[0], w.shape[1]] for w, wt in pairs]
-        tiles = max(((w.shape[0] + 63) // 64) * ((w.shape[1] + 63) // 64) for w, _ in pairs)
-        return torch.tensor(rows, dtype=torch.int64, device=self.device), tiles
+        self._refresh_transposes()
 
     def _build_transposes(self):
         """[in][out] copies W^T of the Linear weights whose data-gradient GEMM dX = dY W then runs NT (NT_DGRAD): the
         mlp1 / InternViT (and, without LoRA, Qwen2) weights, re-transposed from their bf16 working copies after every
         optimizer step by one batched launch (_refresh_derived). The LoRA-concatenated Qwen2 operands get theirs in
         _build_lora_cat."""
-        self.WT = {}
-        self._tr_tab = None
         if self.precise or not NT_DGRAD:
+            self._transposed_copies([])
             return
         cfg = self.cfg
         names = ["proj.fc1.w", "proj.fc2.w"]
@@ -207,11 +199,7 @@ class VLAEngine(EngineOps):
             names += [f"vit.{i}.{n}" for i in range(cfg.vit_layers) for n in ("qkv.w", "proj.w", "fc1.w", "fc2.w")]
         if not cfg.lora:
             names += [f"llm.{i}.{n}" for i in range(cfg.llm_layers) for n in ("qkv_w", "o_w", "gate_up_w", "down_w")]
-        for n in names:
-            w = self.W[n]
-            self.WT[n] = torch.empty(w.shape[1], w.shape[0], dtype=BF16, device=self.device)
-        self._tr_tab, self._tr_tiles = self._transpose_table([(self.W[n], self.WT[n]) for n in names])
-        K.call("slx_transpose_bf16", K.P(self._tr_tab), len(names), self._tr_tiles, K.stream_ptr())
+        self._transposed_copies(names)
 
     def _dxw(self, cat, group, name):
         """(w, w^T or None) of a Qwen2 data-gradient GEMM: the LoRA-concatenated operand of `group` or the weight."""
@@ -219,11 +207,6 @@ class VLAEngine(EngineOps):
             return cat[group], cat["T." + group]
         return self.W[name], self.WT.get(name)
 
-    def _mm_dx(self, dy, w, wt, out, **kw):
-        """dX = dY W for a Linear weight w [out][in]: NT over its transposed copy wt [in][out] when there is one."""
-        if wt is not None:
-            return K.mm(dy, wt, out, tb=True, **kw)
-        return K.mm(dy, w, out, tb=False, **kw)
 
     # LoRA folded into the frozen GEMMs by K-concatenation: y = [x | t] . [W | s*B_blockdiag]^T with
     # t = drop(x) A^T written into the extra columns of the activation buffer. Per layer and group:

@@ -13,6 +13,35 @@ BF16, F32 = torch.bfloat16, torch.float32
 class EngineOps:
     """Mixin: expects self.device, self.bucketer (GradBucketer), self.world, self.P / self.G dicts."""
 
+    def _transpose_table(self, pairs):
+        """[(w [r][c], wt [c][r]), ...] -> (device table for slx_transpose_bf16, most 64 x 64 tiles of an entry)."""
+        rows = [[w.data_ptr(), w.stride(0), wt.data_ptr(), wt.stride(0), w.shape[0], w.shape[1]] for w, wt in pairs]
+        tiles = max(((w.shape[0] + 63) // 64) * ((w.shape[1] + 63) // 64) for w, _ in pairs)
+        return torch.tensor(rows, dtype=torch.int64, device=self.device), tiles
+
+    def _transposed_copies(self, names):
+        """W^T [in][out] for each named bf16 weight W [out][in] (self.WT), the refresh table (self._tr_tab, run by
+        _refresh_transposes after every optimizer step) and one refresh now."""
+        self.WT = {}
+        self._tr_tab = None
+        for n in names:
+            w = self.W[n]
+            self.WT[n] = torch.empty(w.shape[1], w.shape[0], dtype=BF16, device=self.device)
+        if names:
+            self._tr_tab, self._tr_tiles = self._transpose_table([(self.W[n], self.WT[n]) for n in names])
+            self._refresh_transposes()
+
+    def _refresh_transposes(self):
+        if getattr(self, "_tr_tab", None) is not None:
+            K.call("slx_transpose_bf16", K.P(self._tr_tab), self._tr_tab.shape[0], self._tr_tiles, K.stream_ptr())
+
+    def _mm_dx(self, dy, w, wt, out, **kw):
+        """dX = dY W for a Linear weight w [out][in]: NT over its transposed copy wt [in][out] when there is one
+        (the NT main loop is 6-21% faster than NN on the steps' shapes: profiles/round3_nn_vs_nt.txt)."""
+        if wt is not None:
+            return K.mm(dy, wt, out, tb=True, **kw)
+        return K.mm(dy, w, out, tb=False, **kw)
+
     def _probe(self, site):
         """Context manager: HIP events around one call site on the current stream (bench.py). `probe_site` is one
         site name or a set of them; events go to `probe_events` (a list for a single site, else {site: list})."""

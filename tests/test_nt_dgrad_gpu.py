@@ -102,3 +102,17 @@ def test_nt_dgrad_step_matches_nn(dev, monkeypatch, case):
     e_nt.adamw_step(1e-2, 1)
     torch.cuda.synchronize()
     _check_copies(e_nt)
+
+
+def test_base_engine_copies_follow_optimizer(dev):
+    """SimLingo-Base: every weight is trainable, so every transposed copy is refreshed after each AdamW step."""
+    from base_golden_util import load_base_case
+    from simlingo_amd.base_engine import BaseEngine
+    cfg, P, ex, _ = load_base_case("tiny")
+    eng = BaseEngine(cfg, dev, P)
+    assert eng.WT
+    eng.grad.normal_()
+    eng.adamw_step(1e-2, 1e-2, 1)
+    torch.cuda.synchronize()
+    for n, wt in eng.WT.items():
+        assert torch.equal(wt, eng.W[n].t()), n

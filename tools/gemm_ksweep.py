@@ -46,6 +46,8 @@ for N in [int(a) for a in sys.argv[1:]] or [4096, 1024]:
         rounds = tiles / 256
         pts.append((Kd, us))
         print(f"{LAYOUT} N={N} K={Kd}: {us:7.1f} us  {2.0 * M * N * Kd / us / 1e6:6.0f} TF  per-round {us / rounds:6.2f} us", flush=True)
+    if len(pts) < 2:
+        continue
     # least squares us = a + b * (K / 64)
     xs = [k / 64 for k, _ in pts]
     ys = [u for _, u in pts]
