@@ -398,7 +398,7 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* p, const float* g, fl
 
 // The same update four parameters per lane (16-B loads and stores of p / g / m / v, 8-B bf16 stores): n4 quads from
 // 16-B aligned p / g / m / v and an 8-B aligned pbf; the launcher runs the scalar kernel on the tail.
-__global__ __launch_bounds__(256) void adamw4_kernel(float4* p, const float4* g, float4* m, float4* v, bf16x4* pbf,
+__global__ __launch_bounds__(256) void adamw_kernel_x4(float4* p, const float4* g, float4* m, float4* v, bf16x4* pbf,
                                                      long n4, float lr, float b1, float b2, float eps, float wd, float bc1,
                                                      float bc2s, const float* sumsq, float max_norm, float gscale) {
   float coef = gscale;
@@ -832,7 +832,7 @@ int slx_adamw(float* p, const float* g, float* m, float* v, void* p_bf16, int64_
     long blocks = (n4 + 255) / 256;
     if (cap > 0 && blocks > cap) blocks = cap;
     if (blocks > 0x7fffffffL) blocks = 0x7fffffffL;
-    hipLaunchKernelGGL(adamw4_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)s, (float4*)p, (const float4*)g,
+    hipLaunchKernelGGL(adamw_kernel_x4, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)s, (float4*)p, (const float4*)g,
                        (float4*)m, (float4*)v, (bf16x4*)p_bf16, n4, lr, beta1, beta2, eps, weight_decay, bc1, bc2s, sumsq,
                        max_norm, grad_scale);
     SLX_LAUNCH_CHECK("slx_adamw");
