@@ -22,6 +22,9 @@ SHAPES = [  # name, M, N(=in), K(=out), epi
     ("llm.gate_up", R, 896, 9728, None),
     ("llm.down", R, 4864, 896, None),
 ]
+if os.environ.get("ONLY"):
+    SHAPES = [x for x in SHAPES if x[0] in os.environ["ONLY"].split(",")]
+SHAPES += [("llm.lm_head", int(os.environ.get("RLOSS", "128")), 896, 151680, None)] if os.environ.get("LMHEAD") else []
 
 
 def timeit(run, reps=10):
@@ -41,7 +44,7 @@ for name, M, N, Kd, epi in SHAPES:
     dy = torch.randn(M, Kd, device=dev).to(torch.bfloat16)
     W = (torch.randn(Kd, N, device=dev) * 0.03).to(torch.bfloat16)  # [out, in]: NN operand
     WT = W.t().contiguous()  # [in, out]: NT operand
-    out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    out = torch.empty(M, N, device=dev, dtype=torch.float32 if os.environ.get("OUTF32") else torch.bfloat16)
     kw = {}
     if epi == "gelu_bwd":
         aux = torch.randn(M, N, device=dev).to(torch.bfloat16)
