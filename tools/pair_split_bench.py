@@ -16,8 +16,9 @@ g, o, h1, hact, dh, h2 = r(T, 1024), r(T, 1024), r(T, 1024), r(T, 4096), r(T, 40
 dqkv = r(T, 3072)
 Gp, Gq = torch.zeros(1024, 1024, device=dev), torch.zeros(3072, 1024, device=dev)
 G2, G1 = torch.zeros(1024, 4096, device=dev), torch.zeros(4096, 1024, device=dev)
-pairs = {"fc2+fc1": lambda: K.mm_pair((g, hact, G2), (dh, h2, G1)),
-         "proj+qkv": lambda: K.mm_pair((g, o, Gp), (dqkv, h1, Gq))}
+KS = int(os.environ.get("KSMAX", "0"))  # cap on the pair's K splits (0 = the launcher's one-round choice)
+pairs = {"fc2+fc1": lambda: K.mm_pair((g, hact, G2), (dh, h2, G1), ksplit_max=KS),
+         "proj+qkv": lambda: K.mm_pair((g, o, Gp), (dqkv, h1, Gq), ksplit_max=KS)}
 for name, run in pairs.items():
     run()
     torch.cuda.synchronize()
@@ -30,4 +31,4 @@ for name, run in pairs.items():
         e1.record()
         torch.cuda.synchronize()
         ts.append(e0.elapsed_time(e1) / 10 * 1e3)
-    print(f"SLX_SPLIT_REDUCE_MAX={os.environ.get('SLX_SPLIT_REDUCE_MAX', '2')} {name}: {sorted(ts)[2]:.1f} us", flush=True)
+    print(f"SLX_SPLIT_REDUCE_MAX={os.environ.get('SLX_SPLIT_REDUCE_MAX', '2')} KSMAX={KS} {name}: {sorted(ts)[2]:.1f} us", flush=True)
