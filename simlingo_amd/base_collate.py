@@ -28,6 +28,7 @@ import torch
 
 from .base_config import BaseConfig
 from .base_types import CLIP_MEAN, CLIP_STD, DrivingExample, DrivingInput, DrivingLabel
+from .collate import camera_extrinsics, camera_intrinsics, encode_uint8
 
 
 def cut_bottom(frame: np.ndarray) -> np.ndarray:
@@ -83,25 +84,42 @@ def anyres_patches(frame: np.ndarray, pinpoints=((336, 672),), patch: int = 336,
     return np.stack([o.transpose(2, 0, 1) for o in out]).astype(np.float32)
 
 
+def waypoints_from_ego(full: np.ndarray) -> tuple[np.ndarray, np.ndarray]:
+    """dataset_base.py:368-385 (BaseDataset.load_waypoints, no augmentation): `full` = get_waypoints' ego-frame
+    positions [n, 2], current frame first. waypoints = full[1:-1]; waypoints_1d = the cumulative path length to each
+    of full[1..n-2] as (distance, 0) pairs (the 1-d speed target of speed_wps_mode '1d', adaptors.py:213)."""
+    full = np.asarray(full, dtype=np.float64)
+    arc = np.cumsum(np.linalg.norm(full[1:] - full[:-1], axis=1))
+    wp1d = np.stack([arc, np.zeros_like(arc)], 1)[:-1]
+    return full[1:-1], wp1d
+
+
 def base_collate(samples: list[dict], cfg: BaseConfig, cut: bool = True) -> DrivingExample:
     """datamodule.py:213-266 for the llavanext encoder. Each sample: 'rgb' uint8 [H, W, 3] (one view, one frame),
     'speed' float, 'target_point' [2], 'map_route' [n_tp, 2] (target points), 'waypoints' [11, 2],
-    'route_adjusted' [n_route, 2]."""
+    'waypoints_1d' [11, 2], 'route_adjusted' [n_route, 2], 'measurement_path' str.
+    camera_intrinsics / extrinsics are the fixed CARLA camera of :252-253 (get_camera_intrinsics(W, H, 110) of the
+    collated frame size, repeated [B, N=1, 3, 3] / [B, 1, 4, 4]); run_id = encode_uint8(measurement paths, 1000)
+    (:264)."""
     frames = [cut_bottom(s["rgb"]) if cut else s["rgb"] for s in samples]
     pix = np.stack([anyres_patches(f, pinpoints=((cfg.img_size * cfg.npatch_h, cfg.img_size * cfg.npatch_w),),
                                    patch=cfg.img_size) for f in frames])
     B = len(samples)
+    H, W = frames[0].shape[:2]
     sizes = torch.tensor([list(f.shape[:2]) for f in frames])
     wps = torch.tensor(np.stack([s["waypoints"] for s in samples])).float()
+    wp1d = torch.tensor(np.stack([s["waypoints_1d"] for s in samples])).float()
     di = DrivingInput(camera_images=torch.from_numpy(pix).view(B, 1, 1, *pix.shape[1:]), image_sizes=sizes,
-                      camera_intrinsics=torch.eye(3).repeat(B, 1, 1, 1), camera_extrinsics=torch.eye(4).repeat(B, 1, 1, 1),
+                      camera_intrinsics=camera_intrinsics(W, H, 110).expand(B, 1, 3, 3).contiguous(),
+                      camera_extrinsics=camera_extrinsics().expand(B, 1, 4, 4).contiguous(),
                       vehicle_speed=torch.tensor([[float(s["speed"])] for s in samples]),
                       map_route=torch.tensor(np.stack([s["map_route"] for s in samples])).float(),
                       target_point=torch.tensor(np.stack([s["target_point"] for s in samples])).float())
     dl = DrivingLabel(time_delta_sec=torch.tensor([0.2 * i for i in range(11)]).repeat(B, 1).float(), waypoints=wps,
-                      waypoints_1d=wps.clone(),
+                      waypoints_1d=wp1d,
                       route_adjusted=torch.tensor(np.stack([s["route_adjusted"] for s in samples])).float())
-    return DrivingExample(driving_input=di, driving_label=dl, run_id=[s.get("id", "") for s in samples],
+    return DrivingExample(driving_input=di, driving_label=dl,
+                          run_id=encode_uint8([s["measurement_path"] for s in samples], 1000),
                           timestamp=torch.zeros(B, dtype=torch.int64))
 
 
@@ -111,10 +129,12 @@ def synthetic_samples(cfg: BaseConfig, B: int, seed: int = 0, H: int = 512, W: i
     out = []
     for b in range(B):
         tp = rng.normal(0.0, 10.0, size=(cfg.n_tp, 2)).astype(np.float32)
+        ego = np.concatenate([np.zeros((1, 2)), np.cumsum(np.array([0.8, 0.0]) + 0.3 * rng.normal(size=(12, 2)), 0)])
+        wps, wp1d = waypoints_from_ego(ego)
         out.append({"rgb": rng.integers(0, 256, size=(H, W, 3), dtype=np.uint8), "speed": float(rng.uniform(0, 15)),
                     "target_point": tp[0], "map_route": tp,
-                    "waypoints": np.cumsum(np.array([0.8, 0.0]) + 0.3 * rng.normal(size=(11, 2)), 0).astype(np.float32),
+                    "waypoints": wps.astype(np.float32), "waypoints_1d": wp1d.astype(np.float32),
                     "route_adjusted": np.cumsum(np.array([1.0, 0.0]) + 0.1 * rng.normal(size=(cfg.n_route, 2)),
                                                 0).astype(np.float32),
-                    "id": f"synthetic-{seed}-{b}"})
+                    "measurement_path": f"synthetic/seed{seed}/Town00_route{b}/measurements"})
     return out

@@ -34,8 +34,15 @@ class DrivingLabel(NamedTuple):   # custom_types.py:88-103
 class DrivingExample(NamedTuple):  # custom_types.py:105-118
     driving_input: DrivingInput
     driving_label: DrivingLabel
-    run_id: list
+    run_id: Tensor                # [B, 1000] uint8 (encode_uint8 of the measurement paths, datamodule.py:264)
     timestamp: Tensor
+
+
+def _waypoints_1d(wps: Tensor) -> Tensor:
+    """dataset_base.py:381-385 on the ego-frame list [origin, wps...]: cumulative path length as (distance, 0)."""
+    full = torch.cat([torch.zeros(wps.shape[0], 1, 2), wps], 1)
+    arc = torch.cumsum((full[:, 1:] - full[:, :-1]).norm(dim=-1), 1)
+    return torch.stack([arc, torch.zeros_like(arc)], -1)
 
 
 def make_base_batch(cfg: BaseConfig, B: int, seed: int = 0) -> DrivingExample:
@@ -51,10 +58,13 @@ def make_base_batch(cfg: BaseConfig, B: int, seed: int = 0) -> DrivingExample:
     tp = torch.randn((B, cfg.n_tp, 2), generator=g) * 10.0
     route = torch.cumsum(torch.tensor([1.0, 0.0]) + 0.1 * torch.randn((B, cfg.n_route, 2), generator=g), 1)
     wps = torch.cumsum(torch.tensor([0.8, 0.0]) + 0.3 * torch.randn((B, 11, 2), generator=g), 1)
+    from .collate import camera_extrinsics, camera_intrinsics, encode_uint8
     di = DrivingInput(camera_images=pix, image_sizes=torch.tensor([[cfg.frame_h, cfg.frame_w]] * B),
-                      camera_intrinsics=torch.eye(3).repeat(B, 1, 1, 1), camera_extrinsics=torch.eye(4).repeat(B, 1, 1, 1),
+                      camera_intrinsics=camera_intrinsics(cfg.frame_w, cfg.frame_h, 110).expand(B, 1, 3, 3).contiguous(),
+                      camera_extrinsics=camera_extrinsics().expand(B, 1, 4, 4).contiguous(),
                       vehicle_speed=speed, map_route=tp, target_point=tp[:, 0].clone())
     dl = DrivingLabel(time_delta_sec=torch.linspace(0.2, 2.2, 11).repeat(B, 1), waypoints=wps,
-                      waypoints_1d=wps.clone(), route_adjusted=route)
-    return DrivingExample(driving_input=di, driving_label=dl, run_id=[f"synthetic-{seed}-{b}" for b in range(B)],
+                      waypoints_1d=_waypoints_1d(wps), route_adjusted=route)
+    return DrivingExample(driving_input=di, driving_label=dl,
+                          run_id=encode_uint8([f"synthetic-{seed}-{b}" for b in range(B)], 1000),
                           timestamp=torch.zeros(B))

@@ -213,7 +213,9 @@ def safe_load(path: str, max_standins: int = 64):
         except pickle.UnpicklingError as e:
             # a dict / list subclass (e.g. Lightning's AttributeDict) fills itself with SETITEM(S) / APPEND(S), which the
             # weights-only unpickler allows only on plain containers: stand in with the plain container instead
-            m = re.search(r"Can only (SETITEMS?|APPENDS?) for .* but got <class '[\w.]*\.(\w+)'>", str(e))
+            # (torch 2.10 wording: 'Can only SETITEMS for dicts...' / 'Can only append to lists' / 'Can only extend lists')
+            m = re.search(r"Can only (SETITEMS?|APPENDS?|append to lists|extend lists)[^<]*but got <class '[\w.]*\.(\w+)'>",
+                          str(e))
             if m:
                 i = next((j for j, (c, q) in enumerate(extra) if c.__name__ == m.group(2) and issubclass(c, _Inert)), None)
                 if i is None:

@@ -1191,11 +1191,10 @@ __device__ __forceinline__ bool v3_split_reduce(const GemmArgs& p, int tile, f32
     return false;
   }
   if (threadIdx.x == 0) {
-    // every other split has arrived (this block drew the last ticket); wait for their slabs, bounded
-    for (int spin = 0; spin < (1 << 22); ++spin) {
-      if (__hip_atomic_load(pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= S - 1) break;
-      __builtin_amdgcn_s_sleep(2);
-    }
+    // every other split has arrived (this block drew the last ticket), so each of them is resident and already past
+    // its ticket: all S - 1 publish unconditionally and this wait ends without a bound. A bounded wait that fell
+    // through would sum unwritten slabs and leave a nonzero counter for the next launch on this workspace.
+    while (__hip_atomic_load(pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < S - 1) __builtin_amdgcn_s_sleep(2);
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __hip_atomic_store(arrive, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2054,6 +2053,8 @@ static bool fe_ok(const GemmArgs& a, int batch) {
   if (!epi || batch != 1 || a.ksplit > 1 || !a.vec_ok || a.accumulate || a.N % V3_BN != 0 || a.K % BK != 0 ||
       a.K < 3 * BK)
     return false;
+  // the FE stores address the output through a buffer descriptor with 32-bit byte offsets and num_records
+  if ((long long)a.M * a.ldc * (long long)sizeof(OutT) >= (1LL << 31)) return false;
   if (EPI == EPI_STORE && (a.split_stride || a.colsum || a.rope_cos)) return false;
   const int main_rows = a.rem_r0 > 0 ? a.rem_r0 : a.M;
   if (main_rows % V3_BM == 0 || (a.mshift_last && a.M >= V3_BM)) return true;

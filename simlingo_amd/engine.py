@@ -105,9 +105,10 @@ class VLAEngine(EngineOps):
                 else:
                     self.W[s.name] = t.to(self.adt).contiguous()
         self.wbf.copy_(self.master.to(BF16))
-        # LM head padded to a multiple of 8 rows (its dgrad GEMM reads K = V rows as [K][N])
+        # LM head padded to a multiple of 128 rows: its dgrad GEMM reads K = V rows as [K][N], and the fused CE
+        # gradient epilogue (slx_lmhead_ce_bwd) writes whole 128-column tiles of dlog, so ldd >= round_up(V, 128)
         V, d = cfg.vocab, cfg.llm_dim
-        self.Vp = _pad64(V)
+        self.Vp = (V + 127) // 128 * 128
         if self.Vp != V:
             lm = torch.zeros(self.Vp, d, dtype=self.adt, device=dev)
             lm[:V].copy_(self.W["llm.lm_head"])

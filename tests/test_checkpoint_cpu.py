@@ -237,3 +237,32 @@ def test_safe_load_names_unknown_globals(tmp_path):
     cleanup()
     got = safe_load(str(tmp_path / "y.pt"))["ls"]
     assert type(got).__module__ == "simlingo_amd.checkpoint" and got._state == {"cur_scale": 32.0, "cur_iter": 0}
+
+
+@pytest.mark.parametrize("prefix", ["omegaconf.listconfig", "lightning.fabric.utilities.data"])
+def test_safe_load_list_subclass_becomes_plain_list(tmp_path, prefix):
+    """A list subclass under a stand-in prefix (OmegaConf's ListConfig, a Lightning container) fills itself with
+    APPEND / APPENDS; torch 2.10's weights-only unpickler words that error 'Can only append to lists' / 'Can only
+    extend lists'. safe_load replaces the subclass by a plain list instead of re-raising."""
+    import types
+    from simlingo_amd.checkpoint import safe_load
+    made = []
+    parts = prefix.split(".")
+    for i in range(1, len(parts) + 1):
+        n = ".".join(parts[:i])
+        if n not in sys.modules:
+            sys.modules[n] = types.ModuleType(n)
+            made.append(n)
+    m = sys.modules[prefix]
+
+    class ListConfig(list):
+        pass
+    ListConfig.__module__, ListConfig.__qualname__, m.ListConfig = prefix, "ListConfig", ListConfig
+    try:
+        torch.save({"hp": ListConfig([1, 2, 3]), "one": ListConfig([7]), "t": torch.ones(2)}, str(tmp_path / "l.pt"))
+    finally:
+        for n in made:
+            sys.modules.pop(n, None)
+    got = safe_load(str(tmp_path / "l.pt"))
+    assert type(got["hp"]) is list and got["hp"] == [1, 2, 3] and got["one"] == [7]
+    assert torch.equal(got["t"], torch.ones(2))

@@ -100,3 +100,26 @@ def test_precise_forward_north_star(dev, case):
     assert torch.allclose(out4, want, rtol=1e-4, atol=1e-5), msg
     with pytest.raises(RuntimeError):
         eng.backward(None)
+
+
+def test_engine_vocab_not_multiple_of_128(dev):
+    """the fused CE gradient epilogue writes whole 128-column tiles of dlogits, so the engine pads the LM
+    head and dlog to a multiple of 128 rows. V = 1030 (64-padding 1088 is not a multiple of 128): the training step
+    runs and matches the oracle at the bf16 gate of test_engine_vs_oracle (losses 1e-2 rel, waypoints 5e-2 m)."""
+    from simlingo_amd.config import tiny_config
+    from simlingo_amd.params import init_params
+    from simlingo_amd.synthetic import make_batch
+    cfg = tiny_config(vocab=1030, first_added_id=1030, target_point_id=1037)
+    P = init_params(cfg, seed=3, lora_b_std=0.02, std=0.05)
+    ex = make_batch(cfg, B=2, s_text=24, n_loss=6, seed=3, pad=[0, 3])
+    eng, out4, rp, sp = run_engine(cfg, P, ex, dev)
+    assert eng.Vp % 128 == 0 and eng.Vp >= cfg.vocab
+    ref, grads = O.loss_and_grads(engine_precision_params(eng, P), cfg, ex)
+    want = [ref["loss"].item(), ref["language_loss"].item(), ref["route_loss"].item(), ref["speed_wps_loss"].item()]
+    np.testing.assert_allclose(out4.numpy(), want, rtol=1e-2, atol=1e-4)
+    assert (rp - ref["route_pred"]).abs().max().item() <= 5e-2
+    assert (sp - ref["speed_pred"]).abs().max().item() <= 5e-2
+    for name in ("llm.0.lora.q.a", "vit.0.fc1.w", "route.0.w"):
+        if name in grads and grads[name].norm() > 1e-12:
+            e = eng.G[name].detach().float().cpu().reshape(-1)
+            assert torch.nn.functional.cosine_similarity(e, grads[name].reshape(-1), dim=0).item() >= 0.98, name

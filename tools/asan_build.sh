@@ -23,9 +23,9 @@ for src in "$ROOT"/simlingo_amd/csrc/*.hip; do
   fi
 done
 for p in "${pids[@]:-}"; do [ -n "$p" ] && wait "$p"; done
-"$CLANG" -fsanitize=address --hip-link --offload-arch=gfx950 -shared -fPIC "${objs[@]}" -L/opt/rocm/lib -lamdhip64 -Wl,-rpath,/opt/rocm/lib \
+"$CLANG" -fsanitize=address -fno-gpu-sanitize --hip-link --offload-arch=gfx950 -shared -fPIC "${objs[@]}" -L/opt/rocm/lib -lamdhip64 -Wl,-rpath,/opt/rocm/lib \
   -o "$OUT/libslx_hip_asan.so"
-/opt/rocm/llvm/bin/clang -fsanitize=address -fno-omit-frame-pointer -g -I"$ROOT/include" \
+/opt/rocm/llvm/bin/clang -fsanitize=address -fno-gpu-sanitize -fno-omit-frame-pointer -g -I"$ROOT/include" \
   "$ROOT/tests/asan/capi_errors.c" -L"$OUT" -lslx_hip_asan -Wl,-rpath,"$OUT" -Wl,-rpath,/opt/rocm/lib \
   -o "$OUT/capi_errors"
 echo "built $OUT/capi_errors"
