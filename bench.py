@@ -59,8 +59,8 @@ def parse():
                     help="gradient all-reduce wire dtype (bf16: half the xGMI bytes, f32 accumulation kept; "
                          "auto = bf16 at N > 1, SURVEY.md §8e)")
     ap.add_argument("--no-extras", action="store_true",
-                    help="skip the config-4 (S_text 512, 128 loss tokens) step and the config-5 agent latency that "
-                         "the N = 1 vla line carries as extra keys")
+                    help="skip the config-4 (S_text 512, 128 loss tokens) step, the config-5 agent latency and the "
+                         "config-2 SimLingo-Base step that the N = 1 vla line carries as extra keys")
     return ap.parse_args()
 
 
@@ -238,6 +238,47 @@ def config4_step(args, dev, steps=5, warmup=2):
             "loss_last": round(out4[0].item(), 5)}
 
 
+def base_line(args, dev, steps=5, warmup=2):
+    """BASELINE.json configs[1] on one GPU, carried as the `base` key of the N = 1 vla line: SimLingo-Base B = 32,
+    fwd + bwd + clip 1.0 + four-group AdamW, with its own roofline (the CLIP FC1 GEMM, HIP events on its stream over
+    the timed steps; traffic from the base PMC record)."""
+    import argparse as _ap
+    a = _ap.Namespace(**vars(args))
+    a.config, a.batch = "base", None
+    w = setup_base(a, dev, 1, 0)
+    eng, step, B = w["eng"], w["step"], w["B"]
+    for i in range(warmup):
+        step(i)
+    torch.cuda.synchronize()
+    pr = w["probe"]
+    eng.probe_site, eng.probe_events = "vit.fc1", []
+    t0 = time.perf_counter()
+    for i in range(steps):
+        out4 = step(warmup + i)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    eng.probe_site = None
+    v = B * steps / dt
+    res = {"workload": "config 2: SimLingo-Base (CLIP ViT-L/14-336 x2 tiles + projector + Llama 'tiny'), B=32, 1 GPU",
+           "value": round(v, 3), "unit": "samples/s", "ms_per_step": round(dt / steps * 1e3, 3), "steps": steps,
+           "warmup": warmup, "seq_len": w["metric_cfg"]["seq_len"], "gflop_per_sample": round(w["gflop"], 1),
+           "step_mfma_frac": round(v * w["gflop"] / 1e3 / PEAK_BF16_TFLOPS, 4), "loss_last": round(out4[0].item(), 5)}
+    if eng.probe_events:
+        ms = [e0.elapsed_time(e1) for e0, e1 in eng.probe_events]
+        avg_ms = sum(ms) / len(ms)
+        flop = 2.0 * pr["M"] * pr["N"] * pr["K"]
+        ach = flop / (avg_ms * 1e-3) / 1e12
+        rec, src = traffic_record(pr["tag"], pr["M"])
+        res["roofline"] = {"bound": "mfma", "kernel": pr["kernel"], "achieved": round(ach, 1), "peak": PEAK_BF16_TFLOPS,
+                           "unit": "TFLOP/s", "frac": round(ach / PEAK_BF16_TFLOPS, 4),
+                           "traffic": rec["traffic_bytes"] if rec else None, "flop_per_launch": flop,
+                           "avg_launch_ms": round(avg_ms, 4), "launches": len(ms),
+                           "algorithmic_bytes": rec.get("algorithmic_bytes") if rec else None,
+                           "traffic_source": src}
+    del eng, w
+    return res
+
+
 def agent_latency(dev, frames=5, new_tokens=100, s_text=64):
     """BASELINE.json configs[4]: team_code/agent_simlingo.py:797's DrivingModel.forward at bs = 1 (bench_infer.py's
     protocol: InternViT + assembly, prefill, KV-cached greedy decode of max_new_tokens, driving forward; median
@@ -365,6 +406,10 @@ def main():
             res["agent"] = agent_latency(dev)
         except Exception as e:
             res["agent"] = {"error": repr(e)[:200]}
+        try:
+            res["base"] = base_line(args, dev)
+        except Exception as e:
+            res["base"] = {"error": repr(e)[:200]}
     if rank == 0 and world == 1 and w["cpu"] and not args.no_cpu_baseline:
         try:
             res["cpu_baseline"] = w["cpu"]()
