@@ -112,6 +112,12 @@ __device__ __forceinline__ void store64(char* lds, const uint4 (&r)[2]) {
 }
 
 constexpr float LOG2E = 1.4426950408889634f;
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N <= 63, "vmcnt is 6 bits on gfx950");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
 constexpr float LAZY = 8.0f;  // forward lazy-rescale threshold (log2 units)
 constexpr float MASKED = -INFINITY;
 
@@ -439,7 +445,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kv_kernel(AttnArgs a) {
     if (tid < 128) {
       const int qi = qc + (tid & 63);
       const long base = ((long)b * a.Hq + h) * S;
-      ld = qi < S ? (tid < 64 ? a.lse[base + qi] : -a.delta[base + qi]) : 0.f;  // delta staged negated
+      ld = qi < S ? (tid < 64 ? a.lse[base + qi] : a.delta[base + qi]) : 0.f;  // delta is stored negated
     }
   };
   auto commit = [&](int buf, const uint4 (&rq)[2], const uint4 (&rd)[2], float ld) {
@@ -520,7 +526,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kv_kernel(AttnArgs a) {
 
 // ---- backward, dQ pass (the forward's structure): one workgroup = 4 waves = 128 queries of one (b, h);
 // K/V tiles of 64 keys double-buffered through LDS; per tile S^T = K Q^T and dP^T = V dO^T with the query on
-// the lane, dS^T = P^T (dP^T - delta) in registers, dQ^T += K^T dS^T (K read transposed). Plain stores, no
+// the lane, dS^T = P^T (dP^T - delta) in registers, dQ^T += K^T dS^T (K read transposed); it stores -delta for the dK/dV
+// pass (the initial accumulator of its dP chains, loaded as is by the LDS-DMA form). Plain stores, no
 // atomics: recomputing S and dP here costs less than summing dQ over key blocks with f32 atomics
 // (~1.3 TB/s chip-wide), which bounded the single-kernel backward.
 template <bool MASK>
@@ -601,7 +608,7 @@ __global__ __launch_bounds__(256, ATTN_DQ_OCC) void attn_bwd_dq_kernel(AttnArgs 
 #pragma unroll
       for (int j = 0; j < 8; ++j) dlt = __builtin_fmaf((float)df[kk][j], (float)of[kk][j], dlt);
     dlt += __shfl_xor(dlt, 32, 64);
-    if (hl == 0 && active && myq < S) const_cast<float*>(a.delta)[li] = dlt;
+    if (hl == 0 && active && myq < S) const_cast<float*>(a.delta)[li] = -dlt;  // stored negated (dP chains start there)
   }
   f32x16 negd;  // -delta of this lane's query, the dP^T chains' initial accumulator
 #pragma unroll
@@ -670,6 +677,375 @@ __global__ __launch_bounds__(256, ATTN_DQ_OCC) void attn_bwd_dq_kernel(AttnArgs 
   if (a.dbq) {
     __shared__ float red[256];
     block_colsum64(smem, red, c0, c1, a.dbq + h * 64, lane, w);
+  }
+}
+
+// ---- LDS-DMA staged forms (round 4) --------------------------------------------------------------------------------
+// The kernels above stage every K/V (or Q/dO) tile through registers: global loads issued one tile ahead, then
+// ds_write_b128 into the other half of a 2-slot LDS ring, one barrier per tile. PMC (profiles/round3_final_pmc.txt):
+// the ViT backward passes wait 31-37 % of their wave cycles (s_waitcnt / barrier) at MFMA busy 0.31; with the softmax
+// removed the forward structure alone ran at ~860 TF. Here tiles arrive by LDS-DMA (buffer_load_dwordx4 ... lds, the
+// v3 GEMM's staging): a ring of NSLOT slots, each tile issued NSLOT - 1 tiles ahead right after the barrier that frees
+// its slot, a counted vmcnt before that barrier (every wave issues the same number of pieces per tile; tiles past the
+// end are all-sentinel pieces that land zeros in a slot nobody reads), no staging registers, no ds_write. The compute
+// bodies (fwd_tile, bwd_dq_tile, bwd_kv_chunk) are the register-staged kernels' own, so the outputs are identical.
+constexpr unsigned kAttnSent = 0x7FFFFFF0u;  // past every descriptor: the DMA lands zeros
+
+__device__ __forceinline__ int sw_xor(int row) { return (((row >> 1) & 1) << 2) | ((row >> 2) & 3); }  // sw_off's swizzle
+
+// descriptor over rows [0, nrows) of a token-major bf16 slice (row stride ld elements, 64 columns)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t slice_rsrc(const void* base, long ld, int nrows, int esize) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0,
+                                           (int)(((long)(nrows > 0 ? nrows - 1 : 0) * ld + 64) * esize), 0x00020000);
+}
+
+// Wave w's two of the eight 1-KiB pieces of a 64-row x 64-column bf16 tile (rows row0 .. row0 + 63 of the slice)
+// into the sw_off image at lds: lane l of piece p carries row 8p + (l >> 3) into physical chunk l & 7, i.e. logical
+// (source) chunk (l & 7) ^ sw_xor(row) - the swizzle is applied on the source side. lane_off[i] = the lane's byte
+// offset within the tile for piece 2w + i (dma_lane_offsets); rows >= nrows land zeros.
+__device__ __forceinline__ void dma_lane_offsets(long ld, int w, int lane, int (&lane_off)[2], int (&lane_row)[2]) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int r = 16 * w + 8 * i + (lane >> 3);
+    lane_row[i] = r;
+    lane_off[i] = (int)(r * ld + 8 * ((lane & 7) ^ sw_xor(r))) * 2;
+  }
+}
+__device__ __forceinline__ void dma_tile64(__amdgpu_buffer_rsrc_t rs, char* lds, long ld, int row0, int nrows, int w,
+                                           const int (&lane_off)[2], const int (&lane_row)[2]) {
+  const int tile_off = (int)(row0 * ld * 2);  // < 2 GiB: slices are one sample's rows
+  const int lim = nrows - row0;               // rows of this tile that exist
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const unsigned off = lane_row[i] < lim ? (unsigned)(tile_off + lane_off[i]) : kAttnSent;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(lds + (2 * w + i) * 1024), 16,
+                                             off, 0, 0, 0);
+  }
+}
+
+// 64 consecutive f32 (elements i0 .. i0 + 63 of a row vector, valid below n) to lds[0..255] with one 4-B DMA
+__device__ __forceinline__ void dma_row64_f32(__amdgpu_buffer_rsrc_t rs, char* lds, int i0, int n, int lane) {
+  const int i = i0 + lane;
+  const unsigned off = i < n ? (unsigned)(i * 4) : kAttnSent;
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)lds, 4, off, 0, 0, 0);
+}
+
+#ifndef ATTN_NSLOT
+#define ATTN_NSLOT 3
+#endif
+
+// forward: attn_fwd_kernel with the K/V tiles of the (b, kv-head) streamed through an NSLOT ring (16 KiB per slot)
+__global__ __launch_bounds__(256, ATTN_FWD_OCC) void attn_fwd_dma_kernel(AttnArgs a) {
+  constexpr int NS = ATTN_NSLOT;
+  __shared__ __attribute__((aligned(1024))) char smem[NS * 16384];
+  const BlockCoord bc = attn_block((a.S + 127) / 128, a.Hq, a.Hkv, a.B, a.causal ? 1 : 0, a.tail_first);
+  const int qb = bc.blk, h = bc.h, b = bc.b;
+  const int hk = h / (a.Hq / a.Hkv);
+  const int S = a.S;
+  const int kvlen = a.seqlens ? min(a.seqlens[b], S) : S;
+  const int tid = threadIdx.x, lane = tid & 63, hl = lane >> 5;
+  const int w = tid >> 6;
+  const int wu = __builtin_amdgcn_readfirstlane(w);  // the DMA pieces' wave index (M0 must be uniform)
+  const int q0 = qb * 128 + w * 32;
+  const int myq = q0 + (lane & 31);
+  const bool active = q0 < S;
+  const float c = a.scale * LOG2E;
+  const bf16* kbase = a.k + (long)b * S * a.ldk + hk * 64;
+  const bf16* vbase = a.v + (long)b * S * a.ldv + hk * 64;
+  const __amdgpu_buffer_rsrc_t rk = slice_rsrc(kbase, a.ldk, S, 2), rv = slice_rsrc(vbase, a.ldv, S, 2);
+
+  bf16x8 qf[4];
+  {
+    const bf16* qrow = a.q + ((long)b * S + min(myq, S - 1)) * a.ldq + h * 64;
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      bf16x8 z;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) z[j] = (bf16)0.f;
+      qf[kk] = myq < S ? *reinterpret_cast<const bf16x8*>(qrow + 16 * kk + 8 * hl) : z;
+    }
+  }
+  int kend = kvlen;
+  if (a.causal) kend = min(kend, qb * 128 + 128);
+  const int nt = (kend + 63) / 64;
+  int ko[2], kr_[2], vo[2], vr_[2];
+  dma_lane_offsets(a.ldk, wu, lane, ko, kr_);
+  dma_lane_offsets(a.ldv, wu, lane, vo, vr_);
+  auto issue = [&](int t) {  // 4 pieces per wave per tile; t >= nt: sentinel pieces only
+    char* slot = smem + (t % NS) * 16384;
+    const int r0 = t < nt ? t * 64 : S;
+    dma_tile64(rk, slot, a.ldk, r0, S, wu, ko, kr_);
+    dma_tile64(rv, slot + 8192, a.ldv, r0, S, wu, vo, vr_);
+  };
+
+
+  f32x16 o0, o1, lacc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) { o0[r] = 0.f; o1[r] = 0.f; lacc[r] = 0.f; }
+  float m = -1e30f;
+#pragma unroll
+  for (int j = 0; j < NS - 1; ++j) issue(j);
+  for (int t = 0; t < nt; ++t) {
+    wait_vmcnt<4 * (NS - 2)>();  // this wave's pieces of tile t landed (tiles t+1 .. t+NS-2 may still fly)
+    __syncthreads();             // every wave's pieces landed; every wave is done with tile t-1 (its slot is free)
+    issue(t + NS - 1);
+    const char* Kl = smem + (t % NS) * 16384;
+    const char* Vl = Kl + 8192;
+    if (active && !(a.causal && t * 64 > q0 + 31)) {  // causal: tiles wholly above this wave's diagonal skipped
+      const int kfull = a.causal ? min(kvlen, q0 + 1) : kvlen;
+      if ((t + 1) * 64 <= kfull) fwd_tile<false>(Kl, Vl, qf, o0, o1, lacc, m, c, t * 64, kvlen, myq, false, lane);
+      else fwd_tile<true>(Kl, Vl, qf, o0, o1, lacc, m, c, t * 64, kvlen, myq, a.causal, lane);
+    }
+  }
+  wait_vmcnt<0>();  // the trailing sentinel pieces have landed before the workgroup's LDS is released
+  if (!active || myq >= S) return;
+  const float lt = lacc[0];
+  const float inv = 1.0f / lt;
+  bf16* orow = a.o + ((long)b * S + myq) * a.ldo + h * 64;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const int d = 8 * g + 4 * hl;
+    bf16x4 v0, v1;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      v0[e] = (bf16)(o0[4 * g + e] * inv);
+      v1[e] = (bf16)(o1[4 * g + e] * inv);
+    }
+    *reinterpret_cast<bf16x4*>(orow + d) = v0;
+    *reinterpret_cast<bf16x4*>(orow + 32 + d) = v1;
+  }
+  if (hl == 0 && a.lse) a.lse[((long)b * a.Hq + h) * S + myq] = m + __log2f(lt);
+}
+
+// dQ pass: attn_bwd_dq_kernel with the K/V tiles through the NSLOT ring
+__global__ __launch_bounds__(256, ATTN_DQ_OCC) void attn_bwd_dq_dma_kernel(AttnArgs a) {
+  constexpr int NS = ATTN_NSLOT;
+  __shared__ __attribute__((aligned(1024))) char smem[NS * 16384];
+  const BlockCoord bc = attn_block((a.S + 127) / 128, a.Hq, a.Hkv, a.B, a.causal ? 1 : 0, a.tail_first);
+  const int qb = bc.blk, h = bc.h, b = bc.b;
+  const int hk = h / (a.Hq / a.Hkv);
+  const int S = a.S;
+  const int kvlen = a.seqlens ? min(a.seqlens[b], S) : S;
+  const int tid = threadIdx.x, lane = tid & 63, hl = lane >> 5;
+  const int w = tid >> 6;
+  const int wu = __builtin_amdgcn_readfirstlane(w);  // the DMA pieces' wave index (M0 must be uniform)
+  const int q0 = qb * 128 + w * 32;
+  const int myq = q0 + (lane & 31);
+  const bool active = q0 < S;
+  const float c = a.scale * LOG2E;
+  const bf16* kbase = a.k + (long)b * S * a.ldk + hk * 64;
+  const bf16* vbase = a.v + (long)b * S * a.ldv + hk * 64;
+  const __amdgpu_buffer_rsrc_t rk = slice_rsrc(kbase, a.ldk, S, 2), rv = slice_rsrc(vbase, a.ldv, S, 2);
+
+  bf16x8 qf[4], df[4];
+  float lse = 0.f, dlt = 0.f;
+  {
+    const int qr = min(myq, S - 1);
+    const bf16* qrow = a.q + ((long)b * S + qr) * a.ldq + h * 64;
+    const bf16* drow = a.dout + ((long)b * S + qr) * a.lddo + h * 64;
+    const bf16* orow = a.o + ((long)b * S + qr) * a.ldo + h * 64;
+    bf16x8 of[4];
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      qf[kk] = *reinterpret_cast<const bf16x8*>(qrow + 16 * kk + 8 * hl);
+      df[kk] = *reinterpret_cast<const bf16x8*>(drow + 16 * kk + 8 * hl);
+      of[kk] = *reinterpret_cast<const bf16x8*>(orow + 16 * kk + 8 * hl);
+    }
+    const long li = ((long)b * a.Hq + h) * S + qr;
+    lse = a.lse[li];
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dlt = __builtin_fmaf((float)df[kk][j], (float)of[kk][j], dlt);
+    dlt += __shfl_xor(dlt, 32, 64);
+    if (hl == 0 && active && myq < S) const_cast<float*>(a.delta)[li] = -dlt;
+  }
+  f32x16 negd;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) negd[r] = -dlt;
+  int kend = kvlen;
+  if (a.causal) kend = min(kend, qb * 128 + 128);
+  const int nt = (kend + 63) / 64;
+  int ko[2], kr_[2], vo[2], vr_[2];
+  dma_lane_offsets(a.ldk, wu, lane, ko, kr_);
+  dma_lane_offsets(a.ldv, wu, lane, vo, vr_);
+  auto issue = [&](int t) {  // 4 pieces per wave per tile; t >= nt: sentinel pieces only
+    char* slot = smem + (t % NS) * 16384;
+    const int r0 = t < nt ? t * 64 : S;
+    dma_tile64(rk, slot, a.ldk, r0, S, wu, ko, kr_);
+    dma_tile64(rv, slot + 8192, a.ldv, r0, S, wu, vo, vr_);
+  };
+
+  f32x16 dq0, dq1;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) { dq0[r] = 0.f; dq1[r] = 0.f; }
+#pragma unroll
+  for (int j = 0; j < NS - 1; ++j) issue(j);
+  for (int t = 0; t < nt; ++t) {
+    wait_vmcnt<4 * (NS - 2)>();
+    __syncthreads();
+    issue(t + NS - 1);
+    const char* Kl = smem + (t % NS) * 16384;
+    const char* Vl = Kl + 8192;
+    if (active && !(a.causal && t * 64 > q0 + 31)) {
+      const int kfull = a.causal ? min(kvlen, q0 + 1) : kvlen;
+      if ((t + 1) * 64 <= kfull) bwd_dq_tile<false>(Kl, Vl, qf, df, dq0, dq1, c, lse, negd, t * 64, kvlen, myq, false, lane);
+      else bwd_dq_tile<true>(Kl, Vl, qf, df, dq0, dq1, c, lse, negd, t * 64, kvlen, myq, a.causal, lane);
+    }
+  }
+  wait_vmcnt<0>();
+  __syncthreads();  // the ring is free for the bias column sums' LDS tiles
+  const bool qvalid = active && myq < S;
+  float c0[16], c1[16];
+  const long qi = qvalid ? myq : 0;
+  bf16* qrow = a.dq + ((long)b * S + qi) * a.lddq + h * 64;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const int d = 8 * g + 4 * hl;
+    bf16x4 v0, v1;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float x0 = dq0[4 * g + e] * a.scale, x1 = dq1[4 * g + e] * a.scale;
+      if (a.rcos) {
+        const float cs = a.rcos[qi * 32 + d + e], sn = a.rsin[qi * 32 + d + e];
+        const float y0 = x0 * cs + x1 * sn, y1 = x1 * cs - x0 * sn;
+        x0 = y0;
+        x1 = y1;
+      }
+      v0[e] = (bf16)x0;
+      v1[e] = (bf16)x1;
+      c0[4 * g + e] = qvalid ? (float)v0[e] : 0.f;
+      c1[4 * g + e] = qvalid ? (float)v1[e] : 0.f;
+    }
+    if (qvalid) {
+      *reinterpret_cast<bf16x4*>(qrow + d) = v0;
+      *reinterpret_cast<bf16x4*>(qrow + 32 + d) = v1;
+    }
+  }
+  if (a.dbq) {
+    __shared__ float red[256];
+    block_colsum64(smem, red, c0, c1, a.dbq + h * 64, lane, w);
+  }
+}
+
+// dK/dV pass: attn_bwd_kv_kernel with each (q-head, 64-query chunk) stage - Q tile, dO tile, lse[64], -delta[64] -
+// through the NSLOT ring (16.5 KiB per slot). Per wave and stage 5 DMA instructions: Q and dO pieces (2 + 2) and one
+// 4-B row piece (wave 0: lse, wave 1: -delta, waves 2-3: a sentinel piece into the slot's scratch row).
+constexpr int KV_SLOT = 16384 + 4 * 256;
+__global__ __launch_bounds__(256, 2) void attn_bwd_kv_dma_kernel(AttnArgs a) {
+  constexpr int NS = ATTN_NSLOT;
+  __shared__ __attribute__((aligned(1024))) char smem[NS * KV_SLOT];
+  const BlockCoord bc = attn_block((a.S + 127) / 128, a.Hkv * a.nsplit, a.Hkv * a.nsplit, a.B, a.causal ? 2 : 0, a.tail_first);
+  const int kblk = bc.blk, hk = bc.h / a.nsplit, sp = bc.h % a.nsplit, b = bc.b;
+  const int G = a.Hq / a.Hkv;
+  const int hg0 = sp * a.hsplit;
+  const int ng = min(G, hg0 + a.hsplit) - hg0;
+  const int S = a.S;
+  const int kvlen = a.seqlens ? min(a.seqlens[b], S) : S;
+  const int tid = threadIdx.x, lane = tid & 63, hl = lane >> 5;
+  const int w = tid >> 6;
+  const int wu = __builtin_amdgcn_readfirstlane(w);  // the DMA pieces' wave index (M0 must be uniform)
+  const int k0 = kblk * 128;
+  const int kw0 = k0 + 32 * w;
+  const int mykey = kw0 + (lane & 31);
+  const float c = a.scale * LOG2E;
+
+  bf16x8 kf[4], vf[4];
+  {
+    const int kr = min(mykey, S - 1);
+    const bf16* kp = a.k + ((long)b * S + kr) * a.ldk + hk * 64;
+    const bf16* vp = a.v + ((long)b * S + kr) * a.ldv + hk * 64;
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      kf[kk] = *reinterpret_cast<const bf16x8*>(kp + 16 * kk + 8 * hl);
+      vf[kk] = *reinterpret_cast<const bf16x8*>(vp + 16 * kk + 8 * hl);
+    }
+  }
+  f32x16 dk0, dk1, dv0, dv1;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) { dk0[r] = dk1[r] = dv0[r] = dv1[r] = 0.f; }
+
+  const int qstart = a.causal ? (k0 / 64) * 64 : 0;
+  const int nch = qstart < S ? (S - qstart + 63) / 64 : 0;
+  const int nit = nch * ng;
+  int qo[2], qr_[2], doo[2], dr_[2];
+  dma_lane_offsets(a.ldq, wu, lane, qo, qr_);
+  dma_lane_offsets(a.lddo, wu, lane, doo, dr_);
+  auto issue = [&](int it) {
+    char* slot = smem + (it % NS) * KV_SLOT;
+    const bool real = it < nit;
+    const int h = hk * G + hg0 + (real ? it / nch : 0), qc = real ? qstart + (it % nch) * 64 : S;
+    const bf16* qb_ = a.q + (long)b * S * a.ldq + h * 64;
+    const bf16* db_ = a.dout + (long)b * S * a.lddo + h * 64;
+    dma_tile64(slice_rsrc(qb_, a.ldq, S, 2), slot, a.ldq, qc, S, wu, qo, qr_);
+    dma_tile64(slice_rsrc(db_, a.lddo, S, 2), slot + 8192, a.lddo, qc, S, wu, doo, dr_);
+    const long base = ((long)b * a.Hq + h) * S;
+    const float* src = wu == 0 ? a.lse + base : a.delta + base;
+    dma_row64_f32(__builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(src), (short)0, S * 4, 0x00020000),
+                  slot + 16384 + 256 * wu, qc, wu < 2 ? S : 0, lane);
+  };
+
+
+#pragma unroll
+  for (int j = 0; j < NS - 1; ++j) issue(j);
+  for (int it = 0; it < nit; ++it) {
+    wait_vmcnt<5 * (NS - 2)>();
+    __syncthreads();
+    const int qc = qstart + (it % nch) * 64;
+    const char* slot = smem + (it % NS) * KV_SLOT;
+    const char* Ql = slot;
+    const char* Dl = slot + 8192;
+    const float* lse_l = reinterpret_cast<const float*>(slot + 16384);
+    const bool full = (qc + 64 <= S) && (kw0 + 32 <= kvlen) && (!a.causal || kw0 + 31 <= qc);
+    if (kw0 >= kvlen || (a.causal && kw0 > qc + 63)) {  // padding keys, or every key of the wave above the chunk
+    } else if (full) bwd_kv_chunk<false>(Ql, Dl, lse_l, lse_l + 64, kf, vf, dk0, dk1, dv0, dv1, c, qc, S, mykey, kvlen, false, lane);
+    else bwd_kv_chunk<true>(Ql, Dl, lse_l, lse_l + 64, kf, vf, dk0, dk1, dv0, dv1, c, qc, S, mykey, kvlen, a.causal, lane);
+    issue(it + NS - 1);  // into slot (it - 1) % NS: every wave finished stage it - 1 before this iteration's barrier
+  }
+  wait_vmcnt<0>();
+  __syncthreads();  // ring free for the bias column sums' LDS tiles
+
+  const bool kvalid = mykey < S;
+  float ck0[16], ck1[16], cv0[16], cv1[16];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const int d = 8 * g + 4 * hl;
+    if (!kvalid) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) ck0[4 * g + e] = ck1[4 * g + e] = cv0[4 * g + e] = cv1[4 * g + e] = 0.f;
+    } else if (a.dk_acc) {
+      const long off = (long)sp * a.B * S * (a.Hkv * 64) + ((long)b * S + mykey) * (a.Hkv * 64) + hk * 64;
+      float* kp = a.dk_acc + off;
+      float* vp = a.dv_acc + off;
+      *reinterpret_cast<float4*>(kp + d) = make_float4(dk0[4 * g] * a.scale, dk0[4 * g + 1] * a.scale, dk0[4 * g + 2] * a.scale, dk0[4 * g + 3] * a.scale);
+      *reinterpret_cast<float4*>(kp + 32 + d) = make_float4(dk1[4 * g] * a.scale, dk1[4 * g + 1] * a.scale, dk1[4 * g + 2] * a.scale, dk1[4 * g + 3] * a.scale);
+      *reinterpret_cast<float4*>(vp + d) = make_float4(dv0[4 * g], dv0[4 * g + 1], dv0[4 * g + 2], dv0[4 * g + 3]);
+      *reinterpret_cast<float4*>(vp + 32 + d) = make_float4(dv1[4 * g], dv1[4 * g + 1], dv1[4 * g + 2], dv1[4 * g + 3]);
+    } else {
+      bf16* kp = a.dk + ((long)b * S + mykey) * a.lddk + hk * 64;
+      bf16* vp = a.dv + ((long)b * S + mykey) * a.lddv + hk * 64;
+      bf16x4 k0v, k1v, v0v, v1v;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        k0v[e] = (bf16)(dk0[4 * g + e] * a.scale);
+        k1v[e] = (bf16)(dk1[4 * g + e] * a.scale);
+        v0v[e] = (bf16)dv0[4 * g + e];
+        v1v[e] = (bf16)dv1[4 * g + e];
+        ck0[4 * g + e] = (float)k0v[e];
+        ck1[4 * g + e] = (float)k1v[e];
+        cv0[4 * g + e] = (float)v0v[e];
+        cv1[4 * g + e] = (float)v1v[e];
+      }
+      *reinterpret_cast<bf16x4*>(kp + d) = k0v;
+      *reinterpret_cast<bf16x4*>(kp + 32 + d) = k1v;
+      *reinterpret_cast<bf16x4*>(vp + d) = v0v;
+      *reinterpret_cast<bf16x4*>(vp + 32 + d) = v1v;
+    }
+  }
+  if (a.dbk) {
+    __shared__ float red[256];
+    block_colsum64(smem, red, ck0, ck1, a.dbk + hk * 64, lane, w);
+    block_colsum64(smem, red, cv0, cv1, a.dbv + hk * 64, lane, w);
   }
 }
 
@@ -1063,13 +1439,20 @@ static int fill_common(AttnArgs& a, const slx_attn_desc* d) {
   return 0;
 }
 
+// SLX_ATTN_DMA: 1 (default) = the LDS-DMA staged kernels, 0 = the register-staged ones (A/B; identical outputs)
+static bool attn_dma() {
+  static const bool on = [] { const char* e = getenv("SLX_ATTN_DMA"); return e ? atoi(e) != 0 : true; }();
+  return on;
+}
+
 extern "C" int slx_attn_fwd(const slx_attn_desc* d, slx_stream_t stream) {
   AttnArgs a;
   int rc = fill_common(a, d);
   if (rc) return rc;
   if (a.B == 0 || a.S == 0) return 0;
   dim3 grid(((a.S + 127) / 128) * a.Hq * a.B);
-  hipLaunchKernelGGL(attn_fwd_kernel, grid, dim3(256), 0, (hipStream_t)stream, a);
+  if (attn_dma()) hipLaunchKernelGGL(attn_fwd_dma_kernel, grid, dim3(256), 0, (hipStream_t)stream, a);
+  else hipLaunchKernelGGL(attn_fwd_kernel, grid, dim3(256), 0, (hipStream_t)stream, a);
   SLX_LAUNCH_CHECK("slx_attn_fwd");
   return 0;
 }
@@ -1098,7 +1481,8 @@ extern "C" int slx_attn_bwd(const slx_attn_desc* d, const slx_attn_bwd_desc* g, 
   const long ntok = (long)a.B * a.S;
   const int nblk = (a.S + 127) / 128;
   // dQ pass first: it computes delta = rowsum(dO * O) per query in its prologue and stores it for the dK/dV pass
-  hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3(nblk * a.Hq * a.B), dim3(256), 0, st, a);
+  if (attn_dma()) hipLaunchKernelGGL(attn_bwd_dq_dma_kernel, dim3(nblk * a.Hq * a.B), dim3(256), 0, st, a);
+  else hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3(nblk * a.Hq * a.B), dim3(256), 0, st, a);
   SLX_LAUNCH_CHECK("slx_attn_bwd(dq)");
   {  // split a GQA group's q-heads over workgroups: one q-head per workgroup (Qwen2: 7 x 112 = 784 workgroups; with the
      // heaviest-first order +0.25 % on the step over the 4-way split that just fills the chip,
@@ -1111,7 +1495,8 @@ extern "C" int slx_attn_bwd(const slx_attn_desc* d, const slx_attn_bwd_desc* g, 
     a.hsplit = (G + ns - 1) / ns;
     a.nsplit = (G + a.hsplit - 1) / a.hsplit;
   }
-  hipLaunchKernelGGL(attn_bwd_kv_kernel, dim3(nblk * a.Hkv * a.nsplit * a.B), dim3(256), 0, st, a);
+  if (attn_dma()) hipLaunchKernelGGL(attn_bwd_kv_dma_kernel, dim3(nblk * a.Hkv * a.nsplit * a.B), dim3(256), 0, st, a);
+  else hipLaunchKernelGGL(attn_bwd_kv_kernel, dim3(nblk * a.Hkv * a.nsplit * a.B), dim3(256), 0, st, a);
   SLX_LAUNCH_CHECK("slx_attn_bwd(dk/dv)");
   // finalize: f32 -> bf16, summing head-split partials and applying the RoPE transpose where asked
   auto conv = [&](const float* src, int heads, bf16* dst, long ld, bool rope, int nsplit) -> int {

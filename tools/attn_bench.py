@@ -27,9 +27,17 @@ def timeit(fn, n=10):
     return sorted(ts)[2]
 
 
-for name in sys.argv[1:] or list(SHAPES):
+save = None
+args = sys.argv[1:]
+if "--save" in args:
+    i = args.index("--save")
+    save = args[i + 1]
+    args = args[:i] + args[i + 2:]
+outs = {}
+for name in args or list(SHAPES):
     c = SHAPES[name]
     B, S, Hq, Hkv = c["B"], c["S"], c["Hq"], c["Hkv"]
+    torch.manual_seed(0)
     qkv = (torch.randn(B * S, (Hq + 2 * Hkv) * 64, device=dev) * 0.5).bfloat16()
     q, k, v = qkv[:, :Hq * 64], qkv[:, Hq * 64:(Hq + Hkv) * 64], qkv[:, (Hq + Hkv) * 64:]
     o = torch.empty(B * S, Hq * 64, device=dev, dtype=torch.bfloat16)
@@ -45,5 +53,9 @@ for name in sys.argv[1:] or list(SHAPES):
     ws = K.attn_ws(B, S, Hq, Hkv, dev)
     tb = timeit(lambda: K.attn_bwd(q, k, v, o, lse, dout, dqkv[:, :Hq * 64], dqkv[:, Hq * 64:(Hq + Hkv) * 64],
                                    dqkv[:, (Hq + Hkv) * 64:], ws, **kw))
-    print(f"{name}: fwd {tf * 1e3:7.1f} us {fl / tf / 1e9:6.0f} TF | bwd {tb * 1e3:7.1f} us {2.5 * fl / tb / 1e9:6.0f} TF",
-          flush=True)
+    print(f"{name}: fwd {tf * 1e3:7.1f} us {fl / tf / 1e9:6.0f} TF | bwd {tb * 1e3:7.1f} us {2.5 * fl / tb / 1e9:6.0f} TF"
+          f" [SLX_ATTN_DMA={os.environ.get('SLX_ATTN_DMA', '1')}]", flush=True)
+    if save:
+        outs[name] = {"o": o.cpu(), "lse": lse.cpu(), "dqkv": dqkv.cpu()}
+if save:
+    torch.save(outs, save)
