@@ -31,6 +31,9 @@
 #ifndef ATTN_DQ_OCC
 #define ATTN_DQ_OCC 2
 #endif
+#ifndef ATTN_KV_SB
+#define ATTN_KV_SB 0
+#endif
 
 namespace slx {
 
@@ -368,6 +371,9 @@ __device__ __forceinline__ void bwd_kv_chunk(const char* Ql, const char* Dl, con
       dk0 = mfma32(tr_frag(Ql, qa * 32 + 16 * st, 0, lane), sb, dk0);
       dk1 = mfma32(tr_frag(Ql, qa * 32 + 16 * st, 32, lane), sb, dk1);
     }
+#if ATTN_KV_SB
+    __builtin_amdgcn_sched_barrier(0);  // A/B: keep the two 32-query halves' live ranges apart
+#endif
   }
 }
 
@@ -932,7 +938,10 @@ __global__ __launch_bounds__(256, ATTN_DQ_OCC) void attn_bwd_dq_dma_kernel(AttnA
 // through the NSLOT ring (16.5 KiB per slot). Per wave and stage 5 DMA instructions: Q and dO pieces (2 + 2) and one
 // 4-B row piece (wave 0: lse, wave 1: -delta, waves 2-3: a sentinel piece into the slot's scratch row).
 constexpr int KV_SLOT = 16384 + 4 * 256;
-__global__ __launch_bounds__(256, 2) void attn_bwd_kv_dma_kernel(AttnArgs a) {
+#ifndef ATTN_KV_OCC
+#define ATTN_KV_OCC 2
+#endif
+__global__ __launch_bounds__(256, ATTN_KV_OCC) void attn_bwd_kv_dma_kernel(AttnArgs a) {
   constexpr int NS = ATTN_NSLOT;
   __shared__ __attribute__((aligned(1024))) char smem[NS * KV_SLOT];
   const BlockCoord bc = attn_block((a.S + 127) / 128, a.Hkv * a.nsplit, a.Hkv * a.nsplit, a.B, a.causal ? 2 : 0, a.tail_first);
@@ -1440,8 +1449,11 @@ static int fill_common(AttnArgs& a, const slx_attn_desc* d) {
 }
 
 // SLX_ATTN_DMA: 1 (default) = the LDS-DMA staged kernels, 0 = the register-staged ones (A/B; identical outputs)
+#ifndef ATTN_DMA_DEFAULT
+#define ATTN_DMA_DEFAULT 1
+#endif
 static bool attn_dma() {
-  static const bool on = [] { const char* e = getenv("SLX_ATTN_DMA"); return e ? atoi(e) != 0 : true; }();
+  static const bool on = [] { const char* e = getenv("SLX_ATTN_DMA"); return e ? atoi(e) != 0 : ATTN_DMA_DEFAULT != 0; }();
   return on;
 }
 

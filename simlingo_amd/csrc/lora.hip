@@ -448,15 +448,17 @@ __global__ __launch_bounds__(512) void lora_dx_kernel(LoraBwdArgs a) {
       }
     }
   };
+  // the block's column tiles: wave w takes w + 8 y, then every 8 * gridDim.y-th (gridDim.y column groups per row tile)
+  const int c0 = w + 8 * blockIdx.y, cs = 8 * gridDim.y;
   DxRegs<NS> R0, R1;
-  if (w < nct) load(w, R0);
-  for (int ct = w; ct < nct; ct += 16) {
-    const bool more = ct + 8 < nct;
-    if (more) load(ct + 8, R1);
+  if (c0 < nct) load(c0, R0);
+  for (int ct = c0; ct < nct; ct += 2 * cs) {
+    const bool more = ct + cs < nct;
+    if (more) load(ct + cs, R1);
     process(ct, R0);
     if (!more) break;
-    if (ct + 16 < nct) load(ct + 16, R0);
-    process(ct + 8, R1);
+    if (ct + 2 * cs < nct) load(ct + 2 * cs, R0);
+    process(ct + cs, R1);
   }
 }
 
@@ -528,7 +530,12 @@ extern "C" int slx_dropout_bits(const slx_dropout_bits_desc* d, slx_stream_t str
 template <int NS, bool DTB>
 static void launch_bwd_t(const LoraBwdArgs& a, dim3 grid, hipStream_t st) {
   if (a.dA[0]) hipLaunchKernelGGL((lora_da_kernel<NS, DTB>), grid, dim3(256), 0, st, a);
-  if (a.dx) hipLaunchKernelGGL((lora_dx_kernel<NS, DTB>), dim3((unsigned)((a.M + 31) / 32)), dim3(512), 0, st, a);
+  // column groups per 32-row tile: 200 row tiles alone (Qwen2, M = 6384) under-fill the 256 CUs
+  static const int dxg = [] { const char* e = getenv("SLX_LORA_DX_GROUPS"); return e ? atoi(e) : 2; }();
+  const int nct = a.Kin / 32;
+  int g = dxg < 1 ? 1 : dxg;
+  while (g > 1 && 8 * g > nct) --g;
+  if (a.dx) hipLaunchKernelGGL((lora_dx_kernel<NS, DTB>), dim3((unsigned)((a.M + 31) / 32), (unsigned)g), dim3(512), 0, st, a);
 }
 template <int NS>
 static void launch_bwd(const LoraBwdArgs& a, dim3 grid, hipStream_t st) {

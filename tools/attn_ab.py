@@ -13,7 +13,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 sys.path.insert(0, ROOT)
-OUT = os.path.join(HERE, "_ab")
+OUT = os.environ.get("AB_DIR", os.path.join(HERE, "_ab"))  # AB_DIR=ab_builds: builds that travel to the GPU box
 CSRC = os.path.join(ROOT, "simlingo_amd", "csrc")
 
 
