@@ -934,6 +934,238 @@ __global__ __launch_bounds__(256, ATTN_DQ_OCC) void attn_bwd_dq_dma_kernel(AttnA
   }
 }
 
+// ---- ping-pong dQ pass (round 4) --------------------------------------------------------------------------------
+// 8 waves per workgroup: group A (waves 0-3) and group B (waves 4-7) hold the SAME 128 queries (32 per wave, wave
+// w & 3) and split the key tiles by parity (A: even, B: odd). Each wave alternates an MFMA phase (S = K Q^T and
+// dP = V dO^T - delta of its current tile, 16 MFMAs, plus dQ^T += K^T dS^T of its previous tile, 8 MFMAs) and a VALU
+// phase (p = exp2(S c - lse), dS = p dP, the bf16 dS^T fragments), and the two groups run one phase apart, so every
+// SIMD holds one wave in its matrix phase beside one in its VALU phase (MI355X_MICROARCH.md 'Two waves per SIMD': the
+// matrix pipe and the VALU issue of a SIMD run two waves' complementary segments concurrently). One s_barrier per
+// phase for the 8 waves; K/V tiles arrive by LDS-DMA into a PP_NSL-slot ring, tile ph + PP_D issued at the start of
+// phase ph (tile t is read in phases t and t + 2). At the end group B hands its partial dQ to group A through LDS.
+// Same arithmetic per (query, key) as attn_bwd_dq_kernel; the dQ sum is split in two halves (even / odd key tiles)
+// added once, so the output differs from the single-chain kernels by f32 rounding only.
+#ifndef PP_NSL
+#define PP_NSL 5
+#endif
+constexpr int PP_D = PP_NSL - 3;  // DMA distance in tiles (the slot of tile ph + D held tile ph + D - NSL <= ph - 3)
+
+template <bool MASK>
+__device__ __forceinline__ void pp_sdp(const char* Kl, const char* Vl, const bf16x8 (&qf)[4], const bf16x8 (&df)[4],
+                                       const f32x16& negd, f32x16 (&s)[2], f32x16 (&dp)[2], int lane) {
+#pragma unroll
+  for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s[kb][r] = 0.f;
+    s[kb] = mfma32(row_frag(Kl, kb * 32, 0, lane), qf[0], s[kb]);
+    dp[kb] = mfma32(row_frag(Vl, kb * 32, 0, lane), df[0], negd);
+#pragma unroll
+    for (int kk = 1; kk < 4; ++kk) {
+      s[kb] = mfma32(row_frag(Kl, kb * 32, kk, lane), qf[kk], s[kb]);
+      dp[kb] = mfma32(row_frag(Vl, kb * 32, kk, lane), df[kk], dp[kb]);
+    }
+  }
+}
+
+template <bool MASK>
+__device__ __forceinline__ void pp_ds(const f32x16 (&s)[2], const f32x16 (&dp)[2], bf16x8 (&dsb)[2][2], float c,
+                                      float lse, int key0, int kvlen, int myq, bool causal, int lane) {
+  const int hl = lane >> 5;
+#pragma unroll
+  for (int kb = 0; kb < 2; ++kb) {
+    f32x16 ds;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[kb][r], c, -lse));
+      if constexpr (MASK) {
+        const int key = key0 + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
+        const bool ok = (key < kvlen) & (!causal | (key <= myq));
+        p = ok ? p : 0.f;
+      }
+      ds[r] = p * dp[kb][r];
+    }
+    dsb[kb][0] = acc_frag(ds, 0);
+    dsb[kb][1] = acc_frag(ds, 1);
+  }
+}
+
+__device__ __forceinline__ void pp_dq(const char* Kl, const bf16x8 (&dsb)[2][2], f32x16& dq0, f32x16& dq1, int lane) {
+#pragma unroll
+  for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      dq0 = mfma32(tr_frag(Kl, kb * 32 + 16 * st, 0, lane), dsb[kb][st], dq0);
+      dq1 = mfma32(tr_frag(Kl, kb * 32 + 16 * st, 32, lane), dsb[kb][st], dq1);
+    }
+}
+
+__global__ __launch_bounds__(512, 1) void attn_bwd_dq_pp_kernel(AttnArgs a) {
+  constexpr int NS = PP_NSL, D = PP_D;
+  __shared__ __attribute__((aligned(1024))) char smem[NS * 16384];
+  const BlockCoord bc = attn_block((a.S + 127) / 128, a.Hq, a.Hkv, a.B, a.causal ? 1 : 0, a.tail_first);
+  const int qb = bc.blk, h = bc.h, b = bc.b;
+  const int hk = h / (a.Hq / a.Hkv);
+  const int S = a.S;
+  const int kvlen = a.seqlens ? min(a.seqlens[b], S) : S;
+  const int tid = threadIdx.x, lane = tid & 63, hl = lane >> 5;
+  const int w = tid >> 6;
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  const int grp = wu >> 2;  // 0 = A (even key tiles), 1 = B (odd key tiles)
+  const int q0 = qb * 128 + (w & 3) * 32;
+  const int myq = q0 + (lane & 31);
+  const bool active = q0 < S;
+  const float c = a.scale * LOG2E;
+  const bf16* kbase = a.k + (long)b * S * a.ldk + hk * 64;
+  const bf16* vbase = a.v + (long)b * S * a.ldv + hk * 64;
+  const __amdgpu_buffer_rsrc_t rk = slice_rsrc(kbase, a.ldk, S, 2), rv = slice_rsrc(vbase, a.ldv, S, 2);
+
+  bf16x8 qf[4], df[4];
+  float lse = 0.f, dlt = 0.f;
+  {
+    const int qr = min(myq, S - 1);
+    const bf16* qrow = a.q + ((long)b * S + qr) * a.ldq + h * 64;
+    const bf16* drow = a.dout + ((long)b * S + qr) * a.lddo + h * 64;
+    const bf16* orow = a.o + ((long)b * S + qr) * a.ldo + h * 64;
+    bf16x8 of[4];
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      qf[kk] = *reinterpret_cast<const bf16x8*>(qrow + 16 * kk + 8 * hl);
+      df[kk] = *reinterpret_cast<const bf16x8*>(drow + 16 * kk + 8 * hl);
+      of[kk] = *reinterpret_cast<const bf16x8*>(orow + 16 * kk + 8 * hl);
+    }
+    const long li = ((long)b * a.Hq + h) * S + qr;
+    lse = a.lse[li];
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dlt = __builtin_fmaf((float)df[kk][j], (float)of[kk][j], dlt);
+    dlt += __shfl_xor(dlt, 32, 64);
+    if (grp == 0 && hl == 0 && active && myq < S) const_cast<float*>(a.delta)[li] = -dlt;
+  }
+  f32x16 negd;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) negd[r] = -dlt;
+  int kend = kvlen;
+  if (a.causal) kend = min(kend, qb * 128 + 128);
+  const int nt = (kend + 63) / 64;
+  const int ng = grp == 0 ? (nt + 1) / 2 : nt / 2;  // this group's tiles: grp, grp + 2, ...
+  // per-phase DMA: 16 pieces per tile, two per wave (waves 0-3: K pieces 0-7, waves 4-7: V pieces 0-7)
+  int lo[2], lr[2];
+  dma_lane_offsets(grp ? a.ldv : a.ldk, wu & 3, lane, lo, lr);
+  auto issue = [&](int t) {
+    char* slot = smem + (t % NS) * 16384 + grp * 8192;
+    const int r0 = t < nt ? t * 64 : S;
+    dma_tile64(grp ? rv : rk, slot, grp ? a.ldv : a.ldk, r0, S, wu & 3, lo, lr);
+  };
+  f32x16 dq0, dq1, s[2], dp[2];
+  bf16x8 dsb[2][2];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) { dq0[r] = 0.f; dq1[r] = 0.f; }
+#pragma unroll
+  for (int j = 0; j < D; ++j) issue(j);
+  // phases: group g's tile j (key tile 2j + g) has its MFMA phase at ph = 2j + g + 2j... (local phase 2j), its VALU
+  // phase one later, and its dQ MFMAs in the next MFMA phase (local 2j + 2); B runs one phase behind A
+  const int nph = max(2 * ((nt + 1) / 2) + 1, 2 * (nt / 2) + 2);
+  for (int ph = 0; ph < nph; ++ph) {
+    wait_vmcnt<2 * (D - 1)>();  // this wave's pieces of tile ph landed (tiles ph+1 .. ph+D-1 may still fly)
+    __syncthreads();             // every wave's pieces landed; phase ph - 1 finished everywhere (frees tile ph-3's slot)
+    issue(ph + D);
+    const int loc = ph - grp;
+    if (loc < 0 || !active) continue;
+    const int j = loc >> 1;
+    if ((loc & 1) == 0) {  // MFMA phase: dQ of the previous tile, then S / dP of tile j
+      if (j >= 1) {
+        const int tp = 2 * (j - 1) + grp;
+        if (!(a.causal && tp * 64 > q0 + 31)) pp_dq(smem + (tp % NS) * 16384, dsb, dq0, dq1, lane);
+      }
+      if (j < ng) {
+        const int t = 2 * j + grp;
+        if (!(a.causal && t * 64 > q0 + 31)) {
+          const char* Kl = smem + (t % NS) * 16384;
+          pp_sdp<false>(Kl, Kl + 8192, qf, df, negd, s, dp, lane);
+        }
+      }
+    } else if (j < ng) {  // VALU phase of tile j
+      const int t = 2 * j + grp;
+      if (!(a.causal && t * 64 > q0 + 31)) {
+        const int kfull = a.causal ? min(kvlen, q0 + 1) : kvlen;
+        if ((t + 1) * 64 <= kfull) pp_ds<false>(s, dp, dsb, c, lse, t * 64, kvlen, myq, false, lane);
+        else pp_ds<true>(s, dp, dsb, c, lse, t * 64, kvlen, myq, a.causal, lane);
+      }
+    }
+  }
+  wait_vmcnt<0>();
+  __syncthreads();
+  // group B's partial dQ -> group A through LDS ([4 waves][2][16 regs][64 lanes] f32 = 32 KiB)
+  float* xch = reinterpret_cast<float*>(smem);
+  if (grp == 1) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      xch[(((w & 3) * 2 + 0) * 16 + r) * 64 + lane] = dq0[r];
+      xch[(((w & 3) * 2 + 1) * 16 + r) * 64 + lane] = dq1[r];
+    }
+  }
+  __syncthreads();
+  const bool qvalid = grp == 0 && active && myq < S;
+  float c0[16], c1[16];
+  if (grp == 0) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      dq0[r] += xch[(((w & 3) * 2 + 0) * 16 + r) * 64 + lane];
+      dq1[r] += xch[(((w & 3) * 2 + 1) * 16 + r) * 64 + lane];
+    }
+    const long qi = qvalid ? myq : 0;
+    bf16* qrow = a.dq + ((long)b * S + qi) * a.lddq + h * 64;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int d = 8 * g + 4 * hl;
+      bf16x4 v0, v1;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float x0 = dq0[4 * g + e] * a.scale, x1 = dq1[4 * g + e] * a.scale;
+        if (a.rcos) {
+          const float cs = a.rcos[qi * 32 + d + e], sn = a.rsin[qi * 32 + d + e];
+          const float y0 = x0 * cs + x1 * sn, y1 = x1 * cs - x0 * sn;
+          x0 = y0;
+          x1 = y1;
+        }
+        v0[e] = (bf16)x0;
+        v1[e] = (bf16)x1;
+        c0[4 * g + e] = qvalid ? (float)v0[e] : 0.f;
+        c1[4 * g + e] = qvalid ? (float)v1[e] : 0.f;
+      }
+      if (qvalid) {
+        *reinterpret_cast<bf16x4*>(qrow + d) = v0;
+        *reinterpret_cast<bf16x4*>(qrow + 32 + d) = v1;
+      }
+    }
+  }
+  if (a.dbq) {  // bias column sums over group A's 128 rows (block_colsum64's scheme; group B only joins the barriers)
+    __shared__ float red[256];
+    __syncthreads();  // the exchange area is read
+    float* tl = reinterpret_cast<float*>(smem) + (w & 3) * 2048;
+    const int q = lane & 31;
+    if (grp == 0) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int c4 = 2 * g + hl;
+        *reinterpret_cast<float4*>(tl + q * 64 + ((c4 ^ (q & 15)) << 2)) =
+            make_float4(c0[4 * g], c0[4 * g + 1], c0[4 * g + 2], c0[4 * g + 3]);
+        *reinterpret_cast<float4*>(tl + q * 64 + (((8 + c4) ^ (q & 15)) << 2)) =
+            make_float4(c1[4 * g], c1[4 * g + 1], c1[4 * g + 2], c1[4 * g + 3]);
+      }
+      __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      float sum = 0.f;
+      const int c4 = lane >> 2, e = lane & 3;
+#pragma unroll
+      for (int r = 0; r < 32; ++r) sum += tl[r * 64 + ((c4 ^ (r & 15)) << 2) + e];
+      red[w * 64 + lane] = sum;
+    }
+    __syncthreads();
+    if (w == 0) atomicAdd(a.dbq + h * 64 + lane, red[lane] + red[64 + lane] + red[128 + lane] + red[192 + lane]);
+  }
+}
+
 // dK/dV pass: attn_bwd_kv_kernel with each (q-head, 64-query chunk) stage - Q tile, dO tile, lse[64], -delta[64] -
 // through the NSLOT ring (16.5 KiB per slot). Per wave and stage 5 DMA instructions: Q and dO pieces (2 + 2) and one
 // 4-B row piece (wave 0: lse, wave 1: -delta, waves 2-3: a sentinel piece into the slot's scratch row).
@@ -1452,6 +1684,14 @@ static int fill_common(AttnArgs& a, const slx_attn_desc* d) {
 #ifndef ATTN_DMA_DEFAULT
 #define ATTN_DMA_DEFAULT 1
 #endif
+// SLX_ATTN_PP: 1 = the ping-pong (8-wave, MFMA / VALU phase-alternating) dQ pass
+#ifndef ATTN_PP_DEFAULT
+#define ATTN_PP_DEFAULT 0
+#endif
+static bool attn_pp() {
+  static const bool on = [] { const char* e = getenv("SLX_ATTN_PP"); return e ? atoi(e) != 0 : ATTN_PP_DEFAULT != 0; }();
+  return on;
+}
 static bool attn_dma() {
   static const bool on = [] { const char* e = getenv("SLX_ATTN_DMA"); return e ? atoi(e) != 0 : ATTN_DMA_DEFAULT != 0; }();
   return on;
@@ -1493,7 +1733,8 @@ extern "C" int slx_attn_bwd(const slx_attn_desc* d, const slx_attn_bwd_desc* g, 
   const long ntok = (long)a.B * a.S;
   const int nblk = (a.S + 127) / 128;
   // dQ pass first: it computes delta = rowsum(dO * O) per query in its prologue and stores it for the dK/dV pass
-  if (attn_dma()) hipLaunchKernelGGL(attn_bwd_dq_dma_kernel, dim3(nblk * a.Hq * a.B), dim3(256), 0, st, a);
+  if (attn_pp()) hipLaunchKernelGGL(attn_bwd_dq_pp_kernel, dim3(nblk * a.Hq * a.B), dim3(512), 0, st, a);
+  else if (attn_dma()) hipLaunchKernelGGL(attn_bwd_dq_dma_kernel, dim3(nblk * a.Hq * a.B), dim3(256), 0, st, a);
   else hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3(nblk * a.Hq * a.B), dim3(256), 0, st, a);
   SLX_LAUNCH_CHECK("slx_attn_bwd(dq)");
   {  // split a GQA group's q-heads over workgroups: one q-head per workgroup (Qwen2: 7 x 112 = 784 workgroups; with the

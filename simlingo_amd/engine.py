@@ -45,6 +45,10 @@ FUSED_ROPE = os.environ.get("SLX_FUSED_ROPE", "1") != "0"
 # Data-gradient GEMMs dX = dY W over [in][out] copies of the weights (NT main loop, 6-21% faster than NN on the step's
 # shapes: profiles/round3_nn_vs_nt.txt); 0 runs them NN over W itself (A/B hook)
 NT_DGRAD = os.environ.get("SLX_NT_DGRAD", "1") != "0"
+# The Qwen2 gate/up data-gradient GEMM is one round of 200 v3 blocks (100 tiles x 2 K splits; 56 CUs idle for ~150
+# us). SLX_LORA_DB_SIDE=1 runs the gate/up LoRA B-gradient GEMM (it reads the same dgu, nothing reads its output before
+# the optimizer) on a side stream launched right after the dgrad, so its blocks take the idle CUs.
+LORA_DB_SIDE = os.environ.get("SLX_LORA_DB_SIDE", "0") == "1"
 ALIGN = 64  # elements; keeps every parameter view 256-B aligned
 
 
@@ -136,6 +140,8 @@ class VLAEngine(EngineOps):
         self._cos_sin = {}
         self._build_lora_cat()
         self._build_transposes()
+        self._side = None          # side stream of the LORA_DB_SIDE overlap, and its pending completion events
+        self._side_pending = []
         self.probe_site = None     # name of a call site to bracket with HIP events (bench roofline)
         self.probe_events = []
 
@@ -641,10 +647,25 @@ class VLAEngine(EngineOps):
                        K.stream_ptr())
             del dax
             dh2x = self._e(Ml, d + Pg, dtype=F32)
+            side = lora and LORA_DB_SIDE and not self.precise
+            if side:
+                ev_dgu = torch.cuda.Event()
+                ev_dgu.record()
             self._mm_dx(dgu, *self._dxw(cat, "gu", p + "gate_up_w"), dh2x)
+            if side:  # the gate/up B gradients beside the dgrad's single round (see LORA_DB_SIDE)
+                if self._side is None:
+                    self._side = torch.cuda.Stream(device=self.device)
+                self._side.wait_event(ev_dgu)
+                with torch.cuda.stream(self._side):
+                    self._lora_db(i, ("gate", "up"), [dgu[:, :Fl], dgu[:, Fl:]], h2x[:, d:])
+                    ev_db = torch.cuda.Event()
+                    ev_db.record()
+                dgu.record_stream(self._side)
+                h2x.record_stream(self._side)
+                self._side_pending.append(ev_db)
             if lora:
                 self._lora_bwd(i, ("gate", "up"), [dgu[:, :Fl], dgu[:, Fl:]], h2x[:, d:], h2x[:, :d], dh2x[:, d:],
-                               dh2x[:, :d], sv)
+                               dh2x[:, :d], sv, skip_db=side)
             del dgu
             K.norm_bwd(Ls["n2"], dh2x, dX, dx_accumulate=True, dx_bf16=dxb)
             # o projection
@@ -669,6 +690,7 @@ class VLAEngine(EngineOps):
             K.norm_bwd(Ls["n1"], dhx, dX, dx_accumulate=True, dx_bf16=dxb)
             del dqkv, dhx, dh2x
             if lora:
+                self._join_side()  # the layer's gradients are complete before its bucket can be exchanged
                 self._group_done(f"llm{i}")
         # ---------------- token assembly backward ----------------
         qg = self.G["drv.query_route"]  # [20, d] followed by [10, d] (adjacent)
@@ -776,25 +798,19 @@ class VLAEngine(EngineOps):
         self.bucketer.mark("backward_end")
         self.saved = None
 
-    def _lora_bwd(self, i, sites, dys, tx, x, dtx, dx, sv, swiglu=None, dx_bf16=None):
-        """LoRA sites of one group sharing the input x. dys[j] bf16 [M, out_j] (views of the output grad),
-        tx bf16 [M, P] (forward down-projections t_j in columns 32j..), x bf16 [M, in] (undropped input),
-        dtx f32 [M, P] (columns 32j.. hold dt_j = s dy_j B_j, produced by the fused dgrad GEMM; padding columns
-        are exactly 0 because W_cat's are), dx f32 [M, in] (the base input gradient):
-        dB_j = s dy_j^T t_j (GEMMs) ; dA_j = dt_j^T drop_j(x) and dx += drop_j'(dt_j A_j) in one slx_lora_bwd launch
-        (dx_bf16: write bf16(dx + ...) there instead of updating dx).
-        swiglu=(gu, dgu) (down projection only): the dx term and the SwiGLU backward run in one GEMM epilogue instead:
-        dgu = swiglu'(gu) applied to dx + drop'(dt A)."""
-        cfg = self.cfg
-        s = cfg.lora_scale
-        r = cfg.lora_r
-        drop = sv["drop"]
-        keep = sv["llm"][i]["lora"]
-        bits = [keep[site] for site in sites]
-        As = [self.cat[i]["axfrag." + site] for site in sites]
-        # dB_j = s dy_j^T t_j. Sites of equal width whose dy columns are adjacent (k|v, gate|up) and whose B-gradient
-        # slices sit a fixed stride apart in the flat buffer (a, b interleaved per site) run as one batched split-K
-        # launch instead of one each.
+    def _join_side(self):
+        """The compute stream waits for the side-stream LoRA B-gradient GEMMs issued so far."""
+        cur = torch.cuda.current_stream(self.device)
+        for ev in self._side_pending:
+            cur.wait_event(ev)
+        self._side_pending = []
+
+    def _lora_db(self, i, sites, dys, tx):
+        """dB_j = s dy_j^T t_j. Sites of equal width whose dy columns are adjacent (k|v, gate|up) and whose B-gradient
+        slices sit a fixed stride apart in the flat buffer (a, b interleaved per site) run as one batched split-K
+        launch instead of one each."""
+        s = self.cfg.lora_scale
+        r = self.cfg.lora_r
         j = 0
         while j < len(sites):
             gb = self.G[f"llm.{i}.lora.{sites[j]}.b"]
@@ -812,6 +828,23 @@ class VLAEngine(EngineOps):
             K.mm(dys[j], tx[:, r * j:r * (j + 1)], gb, ta=True, tb=False, alpha=s, accumulate=True,
                  ksplit_max=LORA_DB_SPLIT)
             j += 1
+
+    def _lora_bwd(self, i, sites, dys, tx, x, dtx, dx, sv, swiglu=None, dx_bf16=None, skip_db=False):
+        """LoRA sites of one group sharing the input x. dys[j] bf16 [M, out_j] (views of the output grad),
+        tx bf16 [M, P] (forward down-projections t_j in columns 32j..), x bf16 [M, in] (undropped input),
+        dtx f32 [M, P] (columns 32j.. hold dt_j = s dy_j B_j, produced by the fused dgrad GEMM; padding columns
+        are exactly 0 because W_cat's are), dx f32 [M, in] (the base input gradient):
+        dB_j = s dy_j^T t_j (GEMMs) ; dA_j = dt_j^T drop_j(x) and dx += drop_j'(dt_j A_j) in one slx_lora_bwd launch
+        (dx_bf16: write bf16(dx + ...) there instead of updating dx).
+        swiglu=(gu, dgu) (down projection only): the dx term and the SwiGLU backward run in one GEMM epilogue instead:
+        dgu = swiglu'(gu) applied to dx + drop'(dt A)."""
+        cfg = self.cfg
+        drop = sv["drop"]
+        keep = sv["llm"][i]["lora"]
+        bits = [keep[site] for site in sites]
+        As = [self.cat[i]["axfrag." + site] for site in sites]
+        if not skip_db:
+            self._lora_db(i, sites, dys, tx)
         # dA and the dx term in one launch. (Running the parameter-only part - dB GEMMs, dA - on a side stream was
         # measured 6 ms/step slower: per-call event/stream overhead on the host and slower main-stream GEMMs.)
         K.lora_bwd(x, dtx, As, bits, [self.G[f"llm.{i}.lora.{site}.a"] for site in sites],

@@ -1,0 +1,44 @@
+"""SLX_LORA_DB_SIDE (engine.LORA_DB_SIDE): the gate/up LoRA B-gradient GEMM on a side stream beside the gate/up
+data-gradient GEMM. Same kernels, other stream: the step's gradients must match the single-stream step (to the
+f32 atomic-order rounding of the split-K B-gradient GEMM) at the full Qwen2 widths with LoRA dropout on, and the
+side stream must be joined before the layer's gradient group is marked done."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _step(dev, side, monkeypatch):
+    import simlingo_amd.engine as E
+    from simlingo_amd.config import full_config
+    from simlingo_amd.params import init_params
+    from simlingo_amd.plan import plan_from_example
+    from simlingo_amd.synthetic import make_batch
+    monkeypatch.setattr(E, "LORA_DB_SIDE", side)
+    cfg = full_config(vit_layers=1, llm_layers=2, lora_dropout=0.1)
+    eng = E.VLAEngine(cfg, dev, init_params(cfg, seed=3, lora_b_std=0.02))
+    eng.step_seed = 9
+    ex = make_batch(cfg, B=2, s_text=128, n_loss=8, seed=4)
+    plan = plan_from_example(cfg, ex)
+    lab = ex.driving_label
+    marks = []
+    orig = eng._group_done
+    eng._group_done = lambda g: (marks.append((g, len(eng._side_pending))), orig(g))
+    out4, _, _ = eng.forward(ex.driving_input.camera_images.to(dev), plan, plan.to_device(dev), lab.path.to(dev),
+                             lab.waypoints.to(dev), training=True)
+    eng.backward(None)
+    torch.cuda.synchronize()
+    return out4.cpu(), {k: v.detach().float().cpu().clone() for k, v in eng.G.items()}, marks
+
+
+def test_lora_db_side_stream_matches(dev, monkeypatch):
+    o0, g0, _ = _step(dev, False, monkeypatch)
+    o1, g1, marks = _step(dev, True, monkeypatch)
+    assert torch.equal(o0, o1)
+    assert all(n == 0 for g, n in marks if g.startswith("llm")), marks  # joined before each layer's group is done
+    for k in g0:
+        a, b = g0[k].reshape(-1), g1[k].reshape(-1)
+        if a.norm() == 0:
+            assert b.norm() == 0, k
+            continue
+        assert ((a - b).norm() / a.norm()).item() < 1e-5, k
