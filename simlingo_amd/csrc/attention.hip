@@ -1290,6 +1290,267 @@ __global__ __launch_bounds__(256, ATTN_KV_OCC) void attn_bwd_kv_dma_kernel(AttnA
   }
 }
 
+// ---- ping-pong dK/dV pass (round 4) ------------------------------------------------------------------------------
+// attn_bwd_kv_dma_kernel's work in 8 waves: groups A (waves 0-3) and B (4-7) hold the SAME 128 keys (32 per wave,
+// w & 3) and split the (q-head, 64-query chunk) stages by parity (A even, B odd). Per stage a wave runs an MFMA phase
+// (dV^T += dO^T P and dK^T += Q^T dS of its previous stage, 16 MFMAs, then S^T = Q K^T and dP^T = dO V^T - delta of
+// the current stage, 16 MFMAs) and a VALU phase (p, dS and their bf16 fragments), the groups one phase apart (see
+// attn_bwd_dq_pp_kernel). A stage's slot is read in phases it (S / dP), it + 1 (lse, delta) and it + 2 (dV / dK);
+// stage it + PP_D is issued at the start of phase it. Group B's partial dK / dV reach group A through LDS at the end.
+// bf16 fragments packed into the low 8 dwords of the f32 accumulator they were computed from (no separate fragment
+// registers: P and dS of a stage live in the registers of its S and dP accumulators until the next MFMA phase)
+__device__ __forceinline__ void pack_frags(f32x16& x, const bf16x8& f0, const bf16x8& f1) {
+  const uint4 u0 = __builtin_bit_cast(uint4, f0), u1 = __builtin_bit_cast(uint4, f1);
+  x[0] = __uint_as_float(u0.x); x[1] = __uint_as_float(u0.y); x[2] = __uint_as_float(u0.z); x[3] = __uint_as_float(u0.w);
+  x[4] = __uint_as_float(u1.x); x[5] = __uint_as_float(u1.y); x[6] = __uint_as_float(u1.z); x[7] = __uint_as_float(u1.w);
+}
+__device__ __forceinline__ bf16x8 packed_frag(const f32x16& x, int st) {
+  const uint4 u = make_uint4(__float_as_uint(x[4 * st]), __float_as_uint(x[4 * st + 1]), __float_as_uint(x[4 * st + 2]),
+                             __float_as_uint(x[4 * st + 3]));
+  return __builtin_bit_cast(bf16x8, u);
+}
+
+template <bool MASK>
+__device__ __forceinline__ void ppkv_valu(const float* lse_l, f32x16 (&sp)[2], f32x16 (&dp)[2], float c, int qc, int S,
+                                          int mykey, int kvlen, bool causal, int lane) {
+  const int hl = lane >> 5;
+#pragma unroll
+  for (int qa = 0; qa < 2; ++qa) {
+    f32x16 p16, d16;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int ql = qa * 32 + 8 * g + 4 * hl;
+      const f32x4 L4 = *reinterpret_cast<const f32x4*>(lse_l + ql);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int r = 4 * g + e;
+        float p = __builtin_amdgcn_exp2f(__builtin_fmaf(sp[qa][r], c, -L4[e]));
+        if constexpr (MASK) {
+          const int q = qc + ql + e;
+          const bool ok = (q < S) & (mykey < kvlen) & (!causal | (mykey <= q));
+          p = ok ? p : 0.f;
+        }
+        p16[r] = p;
+        d16[r] = p * dp[qa][r];
+      }
+    }
+    pack_frags(sp[qa], acc_frag(p16, 0), acc_frag(p16, 1));
+    pack_frags(dp[qa], acc_frag(d16, 0), acc_frag(d16, 1));
+  }
+}
+
+__global__ __launch_bounds__(512, 1) void attn_bwd_kv_pp_kernel(AttnArgs a) {
+  constexpr int NS = PP_NSL, D = PP_D;
+  __shared__ __attribute__((aligned(1024))) char smem[NS * KV_SLOT > 65536 ? NS * KV_SLOT : 65536];
+  const BlockCoord bc = attn_block((a.S + 127) / 128, a.Hkv * a.nsplit, a.Hkv * a.nsplit, a.B, a.causal ? 2 : 0, a.tail_first);
+  const int kblk = bc.blk, hk = bc.h / a.nsplit, sp_ = bc.h % a.nsplit, b = bc.b;
+  const int G = a.Hq / a.Hkv;
+  const int hg0 = sp_ * a.hsplit;
+  const int ng = min(G, hg0 + a.hsplit) - hg0;
+  const int S = a.S;
+  const int kvlen = a.seqlens ? min(a.seqlens[b], S) : S;
+  const int tid = threadIdx.x, lane = tid & 63, hl = lane >> 5;
+  const int w = tid >> 6;
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  const int grp = wu >> 2;
+  const int k0 = kblk * 128;
+  const int kw0 = k0 + 32 * (w & 3);
+  const int mykey = kw0 + (lane & 31);
+  const float c = a.scale * LOG2E;
+
+  bf16x8 kf[4], vf[4];
+  {
+    const int kr = min(mykey, S - 1);
+    const bf16* kp = a.k + ((long)b * S + kr) * a.ldk + hk * 64;
+    const bf16* vp = a.v + ((long)b * S + kr) * a.ldv + hk * 64;
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      kf[kk] = *reinterpret_cast<const bf16x8*>(kp + 16 * kk + 8 * hl);
+      vf[kk] = *reinterpret_cast<const bf16x8*>(vp + 16 * kk + 8 * hl);
+    }
+  }
+  f32x16 dk0, dk1, dv0, dv1;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) { dk0[r] = dk1[r] = dv0[r] = dv1[r] = 0.f; }
+
+  const int qstart = a.causal ? (k0 / 64) * 64 : 0;
+  const int nch = qstart < S ? (S - qstart + 63) / 64 : 0;
+  const int nit = nch * ng;
+  // per stage 16 + 16 + 1 DMA pieces: waves 0-3 the Q tile (2 each), waves 4-7 the dO tile (2 each); the lse row by
+  // wave 0 and the -delta row by wave 4 (the other waves issue a sentinel row piece into the slot's scratch rows, so
+  // every wave issues 3 pieces per stage)
+  int lo[2], lr[2];
+  dma_lane_offsets(grp ? a.lddo : a.ldq, wu & 3, lane, lo, lr);
+  auto issue = [&](int it) {
+    char* slot = smem + (it % NS) * KV_SLOT;
+    const bool real = it < nit;
+    const int h = hk * G + hg0 + (real ? it / nch : 0), qc = real ? qstart + (it % nch) * 64 : S;
+    const bf16* src = grp ? a.dout + (long)b * S * a.lddo + h * 64 : a.q + (long)b * S * a.ldq + h * 64;
+    const long ld = grp ? a.lddo : a.ldq;
+    dma_tile64(slice_rsrc(src, ld, S, 2), slot + grp * 8192, ld, qc, S, wu & 3, lo, lr);
+    const long base = ((long)b * a.Hq + h) * S;
+    const int rowp = (wu & 3) == 0 ? grp : 2 + (wu & 1);  // waves 0 / 4: the lse / delta rows; others: scratch rows
+    const float* fsrc = grp ? a.delta + base : a.lse + base;
+    dma_row64_f32(__builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(fsrc), (short)0, S * 4, 0x00020000),
+                  slot + 16384 + 256 * rowp, qc, (wu & 3) == 0 ? S : 0, lane);
+  };
+
+  f32x16 spa[2], dpa[2];
+  int prev_qc = 0;
+  bool prev_on = false;
+#pragma unroll
+  for (int j = 0; j < D; ++j) issue(j);
+  const int nph = max(2 * ((nit + 1) / 2) + 1, 2 * (nit / 2) + 2);
+  for (int ph = 0; ph < nph; ++ph) {
+    wait_vmcnt<3 * (D - 1)>();
+    __syncthreads();
+    issue(ph + D);
+    const int loc = ph - grp;
+    if (loc < 0 || kw0 >= kvlen) continue;
+    const int j = loc >> 1;
+    const int my_n = grp == 0 ? (nit + 1) / 2 : nit / 2;
+    if ((loc & 1) == 0) {  // MFMA phase: dV / dK of the previous stage, S / dP of this one
+      if (j >= 1 && prev_on) {
+        const int itp = 2 * (j - 1) + grp;
+        const char* slot = smem + (itp % NS) * KV_SLOT;
+#pragma unroll
+        for (int qa = 0; qa < 2; ++qa)
+#pragma unroll
+          for (int st = 0; st < 2; ++st) {
+            const bf16x8 pbf = packed_frag(spa[qa], st), sbf = packed_frag(dpa[qa], st);
+            dv0 = mfma32(tr_frag(slot + 8192, qa * 32 + 16 * st, 0, lane), pbf, dv0);
+            dv1 = mfma32(tr_frag(slot + 8192, qa * 32 + 16 * st, 32, lane), pbf, dv1);
+            dk0 = mfma32(tr_frag(slot, qa * 32 + 16 * st, 0, lane), sbf, dk0);
+            dk1 = mfma32(tr_frag(slot, qa * 32 + 16 * st, 32, lane), sbf, dk1);
+          }
+      }
+      prev_on = false;
+      if (j < my_n) {
+        const int it = 2 * j + grp;
+        const int qc = qstart + (it % nch) * 64;
+        if (!(a.causal && kw0 > qc + 63)) {
+          const char* slot = smem + (it % NS) * KV_SLOT;
+          const float* ld_ = reinterpret_cast<const float*>(slot + 16384);
+#pragma unroll
+          for (int qa = 0; qa < 2; ++qa) {
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {  // dP^T starts from -delta (stored negated) of each register's query
+              const f32x4 D4 = *reinterpret_cast<const f32x4*>(ld_ + 64 + qa * 32 + 8 * g + 4 * hl);
+#pragma unroll
+              for (int e = 0; e < 4; ++e) { spa[qa][4 * g + e] = 0.f; dpa[qa][4 * g + e] = D4[e]; }
+            }
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk) {
+              spa[qa] = mfma32(row_frag(slot, qa * 32, kk, lane), kf[kk], spa[qa]);
+              dpa[qa] = mfma32(row_frag(slot + 8192, qa * 32, kk, lane), vf[kk], dpa[qa]);
+            }
+          }
+          prev_on = true;
+          prev_qc = qc;
+        }
+      }
+    } else if (j < my_n && prev_on) {  // VALU phase of stage j (prev_on: its S / dP ran)
+      const int it = 2 * j + grp;
+      const char* slot = smem + (it % NS) * KV_SLOT;
+      const float* lse_l = reinterpret_cast<const float*>(slot + 16384);
+      const int qc = prev_qc;
+      const bool full = (qc + 64 <= S) && (kw0 + 32 <= kvlen) && (!a.causal || kw0 + 31 <= qc);
+      if (full) ppkv_valu<false>(lse_l, spa, dpa, c, qc, S, mykey, kvlen, false, lane);
+      else ppkv_valu<true>(lse_l, spa, dpa, c, qc, S, mykey, kvlen, a.causal, lane);
+    }
+  }
+  wait_vmcnt<0>();
+  __syncthreads();
+  // group B's partial dK / dV -> group A: [4 waves][4 accumulators][16][64] f32 = 64 KiB
+  float* xch = reinterpret_cast<float*>(smem);
+  if (grp == 1) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      float* xw = xch + ((w & 3) * 4) * 1024 + r * 64 + lane;
+      xw[0] = dk0[r];
+      xw[1024] = dk1[r];
+      xw[2048] = dv0[r];
+      xw[3072] = dv1[r];
+    }
+  }
+  __syncthreads();
+  const bool kvalid = grp == 0 && mykey < S;
+  float ck0[16], ck1[16], cv0[16], cv1[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) ck0[r] = ck1[r] = cv0[r] = cv1[r] = 0.f;
+  if (grp == 0) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float* xw = xch + ((w & 3) * 4) * 1024 + r * 64 + lane;
+      dk0[r] += xw[0];
+      dk1[r] += xw[1024];
+      dv0[r] += xw[2048];
+      dv1[r] += xw[3072];
+    }
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int d = 8 * g + 4 * hl;
+      if (!kvalid) {
+      } else if (a.dk_acc) {
+        const long off = (long)sp_ * a.B * S * (a.Hkv * 64) + ((long)b * S + mykey) * (a.Hkv * 64) + hk * 64;
+        float* kp = a.dk_acc + off;
+        float* vp = a.dv_acc + off;
+        *reinterpret_cast<float4*>(kp + d) = make_float4(dk0[4 * g] * a.scale, dk0[4 * g + 1] * a.scale, dk0[4 * g + 2] * a.scale, dk0[4 * g + 3] * a.scale);
+        *reinterpret_cast<float4*>(kp + 32 + d) = make_float4(dk1[4 * g] * a.scale, dk1[4 * g + 1] * a.scale, dk1[4 * g + 2] * a.scale, dk1[4 * g + 3] * a.scale);
+        *reinterpret_cast<float4*>(vp + d) = make_float4(dv0[4 * g], dv0[4 * g + 1], dv0[4 * g + 2], dv0[4 * g + 3]);
+        *reinterpret_cast<float4*>(vp + 32 + d) = make_float4(dv1[4 * g], dv1[4 * g + 1], dv1[4 * g + 2], dv1[4 * g + 3]);
+      } else {
+        bf16* kp = a.dk + ((long)b * S + mykey) * a.lddk + hk * 64;
+        bf16* vp = a.dv + ((long)b * S + mykey) * a.lddv + hk * 64;
+        bf16x4 k0v, k1v, v0v, v1v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          k0v[e] = (bf16)(dk0[4 * g + e] * a.scale);
+          k1v[e] = (bf16)(dk1[4 * g + e] * a.scale);
+          v0v[e] = (bf16)dv0[4 * g + e];
+          v1v[e] = (bf16)dv1[4 * g + e];
+          ck0[4 * g + e] = (float)k0v[e];
+          ck1[4 * g + e] = (float)k1v[e];
+          cv0[4 * g + e] = (float)v0v[e];
+          cv1[4 * g + e] = (float)v1v[e];
+        }
+        *reinterpret_cast<bf16x4*>(kp + d) = k0v;
+        *reinterpret_cast<bf16x4*>(kp + 32 + d) = k1v;
+        *reinterpret_cast<bf16x4*>(vp + d) = v0v;
+        *reinterpret_cast<bf16x4*>(vp + 32 + d) = v1v;
+      }
+    }
+  }
+  if (a.dbk) {  // bias column sums over group A's 128 keys; group B joins the barriers only
+    __shared__ float red[256];
+    for (int pass = 0; pass < 2; ++pass) {
+      const float (&v0)[16] = pass ? cv0 : ck0;
+      const float (&v1)[16] = pass ? cv1 : ck1;
+      __syncthreads();
+      float* tl = reinterpret_cast<float*>(smem) + (w & 3) * 2048;
+      const int q = lane & 31;
+      if (grp == 0) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int c4 = 2 * g + hl;
+          *reinterpret_cast<float4*>(tl + q * 64 + ((c4 ^ (q & 15)) << 2)) =
+              make_float4(v0[4 * g], v0[4 * g + 1], v0[4 * g + 2], v0[4 * g + 3]);
+          *reinterpret_cast<float4*>(tl + q * 64 + (((8 + c4) ^ (q & 15)) << 2)) =
+              make_float4(v1[4 * g], v1[4 * g + 1], v1[4 * g + 2], v1[4 * g + 3]);
+        }
+        __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        float sum = 0.f;
+        const int c4 = lane >> 2, e = lane & 3;
+#pragma unroll
+        for (int r = 0; r < 32; ++r) sum += tl[r * 64 + ((c4 ^ (r & 15)) << 2) + e];
+        red[w * 64 + lane] = sum;
+      }
+      __syncthreads();
+      if (w == 0) atomicAdd((pass ? a.dbv : a.dbk) + hk * 64 + lane, red[lane] + red[64 + lane] + red[128 + lane] + red[192 + lane]);
+    }
+  }
+}
+
 __device__ __forceinline__ void rope_pair(float& x0, float& x1, float cs, float sn, bool inverse) {
   const float a = x0, b = x1;
   if (!inverse) { x0 = a * cs - b * sn; x1 = b * cs + a * sn; }
@@ -1748,7 +2009,8 @@ extern "C" int slx_attn_bwd(const slx_attn_desc* d, const slx_attn_bwd_desc* g, 
     a.hsplit = (G + ns - 1) / ns;
     a.nsplit = (G + a.hsplit - 1) / a.hsplit;
   }
-  if (attn_dma()) hipLaunchKernelGGL(attn_bwd_kv_dma_kernel, dim3(nblk * a.Hkv * a.nsplit * a.B), dim3(256), 0, st, a);
+  if (attn_pp()) hipLaunchKernelGGL(attn_bwd_kv_pp_kernel, dim3(nblk * a.Hkv * a.nsplit * a.B), dim3(512), 0, st, a);
+  else if (attn_dma()) hipLaunchKernelGGL(attn_bwd_kv_dma_kernel, dim3(nblk * a.Hkv * a.nsplit * a.B), dim3(256), 0, st, a);
   else hipLaunchKernelGGL(attn_bwd_kv_kernel, dim3(nblk * a.Hkv * a.nsplit * a.B), dim3(256), 0, st, a);
   SLX_LAUNCH_CHECK("slx_attn_bwd(dk/dv)");
   // finalize: f32 -> bf16, summing head-split partials and applying the RoPE transpose where asked
