@@ -1290,13 +1290,6 @@ __global__ __launch_bounds__(256, ATTN_KV_OCC) void attn_bwd_kv_dma_kernel(AttnA
   }
 }
 
-// ---- ping-pong dK/dV pass (round 4) ------------------------------------------------------------------------------
-// attn_bwd_kv_dma_kernel's work in 8 waves: groups A (waves 0-3) and B (4-7) hold the SAME 128 keys (32 per wave,
-// w & 3) and split the (q-head, 64-query chunk) stages by parity (A even, B odd). Per stage a wave runs an MFMA phase
-// (dV^T += dO^T P and dK^T += Q^T dS of its previous stage, 16 MFMAs, then S^T = Q K^T and dP^T = dO V^T - delta of
-// the current stage, 16 MFMAs) and a VALU phase (p, dS and their bf16 fragments), the groups one phase apart (see
-// attn_bwd_dq_pp_kernel). A stage's slot is read in phases it (S / dP), it + 1 (lse, delta) and it + 2 (dV / dK);
-// stage it + PP_D is issued at the start of phase it. Group B's partial dK / dV reach group A through LDS at the end.
 // bf16 fragments packed into the low 8 dwords of the f32 accumulator they were computed from (no separate fragment
 // registers: P and dS of a stage live in the registers of its S and dP accumulators until the next MFMA phase)
 __device__ __forceinline__ void pack_frags(f32x16& x, const bf16x8& f0, const bf16x8& f1) {
@@ -1310,6 +1303,180 @@ __device__ __forceinline__ bf16x8 packed_frag(const f32x16& x, int st) {
   return __builtin_bit_cast(bf16x8, u);
 }
 
+// ---- ping-pong forward (round 4) ------------------------------------------------------------------------------
+// attn_fwd_kernel's work in 8 waves: groups A / B hold the same 128 queries and split the key tiles by parity. MFMA
+// phase: O^T += V^T P^T (and the row sums) of the previous tile, then S^T = K Q^T of the current one; VALU phase: the
+// max, the lazy rescale of O / l, p = exp2(s c - m) packed to bf16 in S's registers. Each group keeps its own (m, l,
+// O); group B's are merged into A's through LDS at the end (O = O_A 2^(m_A - m) + O_B 2^(m_B - m), same for l).
+__global__ __launch_bounds__(512, 1) void attn_fwd_pp_kernel(AttnArgs a) {
+  constexpr int NS = PP_NSL, D = PP_D;
+  __shared__ __attribute__((aligned(1024))) char smem[NS * 16384];
+  const BlockCoord bc = attn_block((a.S + 127) / 128, a.Hq, a.Hkv, a.B, a.causal ? 1 : 0, a.tail_first);
+  const int qb = bc.blk, h = bc.h, b = bc.b;
+  const int hk = h / (a.Hq / a.Hkv);
+  const int S = a.S;
+  const int kvlen = a.seqlens ? min(a.seqlens[b], S) : S;
+  const int tid = threadIdx.x, lane = tid & 63, hl = lane >> 5;
+  const int w = tid >> 6;
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  const int grp = wu >> 2;
+  const int q0 = qb * 128 + (w & 3) * 32;
+  const int myq = q0 + (lane & 31);
+  const bool active = q0 < S;
+  const float c = a.scale * LOG2E;
+  const bf16* kbase = a.k + (long)b * S * a.ldk + hk * 64;
+  const bf16* vbase = a.v + (long)b * S * a.ldv + hk * 64;
+  const __amdgpu_buffer_rsrc_t rk = slice_rsrc(kbase, a.ldk, S, 2), rv = slice_rsrc(vbase, a.ldv, S, 2);
+  bf16x8 qf[4];
+  {
+    const bf16* qrow = a.q + ((long)b * S + min(myq, S - 1)) * a.ldq + h * 64;
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      bf16x8 z;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) z[j] = (bf16)0.f;
+      qf[kk] = myq < S ? *reinterpret_cast<const bf16x8*>(qrow + 16 * kk + 8 * hl) : z;
+    }
+  }
+  int kend = kvlen;
+  if (a.causal) kend = min(kend, qb * 128 + 128);
+  const int nt = (kend + 63) / 64;
+  const int ng = grp == 0 ? (nt + 1) / 2 : nt / 2;
+  int lo[2], lr[2];
+  dma_lane_offsets(grp ? a.ldv : a.ldk, wu & 3, lane, lo, lr);
+  auto issue = [&](int t) {
+    char* slot = smem + (t % NS) * 16384 + grp * 8192;
+    const int r0 = t < nt ? t * 64 : S;
+    dma_tile64(grp ? rv : rk, slot, grp ? a.ldv : a.ldk, r0, S, wu & 3, lo, lr);
+  };
+  f32x16 o0, o1, lacc, s2[2];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) { o0[r] = 0.f; o1[r] = 0.f; lacc[r] = 0.f; }
+  float m = -1e30f;
+  bf16x8 ones;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ones[j] = (bf16)1.0f;
+  bool prev_on = false;
+  int prev_t = 0;
+#pragma unroll
+  for (int j = 0; j < D; ++j) issue(j);
+  const int nph = max(2 * ((nt + 1) / 2) + 1, 2 * (nt / 2) + 2);
+  for (int ph = 0; ph < nph; ++ph) {
+    wait_vmcnt<2 * (D - 1)>();
+    __syncthreads();
+    issue(ph + D);
+    const int loc = ph - grp;
+    if (loc < 0 || !active) continue;
+    const int j = loc >> 1;
+    if ((loc & 1) == 0) {  // MFMA phase: P V (and row sums) of the previous tile, S of this one
+      if (j >= 1 && prev_on) {
+        const char* Vl = smem + (prev_t % NS) * 16384 + 8192;
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+          for (int st = 0; st < 2; ++st) {
+            const bf16x8 pb = packed_frag(s2[kb], st);
+            o0 = mfma32(tr_frag(Vl, kb * 32 + 16 * st, 0, lane), pb, o0);
+            o1 = mfma32(tr_frag(Vl, kb * 32 + 16 * st, 32, lane), pb, o1);
+            lacc = mfma32(ones, pb, lacc);
+          }
+      }
+      prev_on = false;
+      if (j < ng) {
+        const int t = 2 * j + grp;
+        if (!(a.causal && t * 64 > q0 + 31)) {
+          const char* Kl = smem + (t % NS) * 16384;
+#pragma unroll
+          for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) s2[kb][r] = 0.f;
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk) s2[kb] = mfma32(row_frag(Kl, kb * 32, kk, lane), qf[kk], s2[kb]);
+          }
+          prev_on = true;
+          prev_t = t;
+        }
+      }
+    } else if (j < ng && prev_on) {  // VALU phase: softmax of tile j
+      const int t = prev_t, key0 = t * 64;
+      const int kfull = a.causal ? min(kvlen, q0 + 1) : kvlen;
+      if ((t + 1) * 64 > kfull) {
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int key = key0 + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
+            const bool ok = (key < kvlen) & (!a.causal | (key <= myq));
+            s2[kb][r] = ok ? s2[kb][r] : MASKED;
+          }
+      }
+      float mx = s2[0][0];
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s2[kb][r]);
+      mx = half_swap_max(mx) * c;
+      if (__builtin_amdgcn_ballot_w64(mx > m + LAZY)) {
+        const float mnew = fmaxf(m, mx);
+        const float alpha = __builtin_amdgcn_exp2f(m - mnew);
+        m = mnew;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) { o0[r] *= alpha; o1[r] *= alpha; lacc[r] *= alpha; }
+      }
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) {
+        f32x16 p;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) p[r] = __builtin_amdgcn_exp2f(__builtin_fmaf(s2[kb][r], c, -m));
+        pack_frags(s2[kb], acc_frag(p, 0), acc_frag(p, 1));
+      }
+    }
+  }
+  wait_vmcnt<0>();
+  __syncthreads();
+  // merge group B's (m, l, O) into group A's: [4 waves][o0 16 | o1 16 | l 16 | m][64] f32
+  float* xch = reinterpret_cast<float*>(smem);
+  float* xw = xch + (w & 3) * 49 * 64 + lane;
+  if (grp == 1) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { xw[r * 64] = o0[r]; xw[(16 + r) * 64] = o1[r]; xw[(32 + r) * 64] = lacc[r]; }
+    xw[48 * 64] = m;
+  }
+  __syncthreads();
+  if (grp == 1 || !active || myq >= S) return;
+  const float mb = xw[48 * 64];
+  const float mm = fmaxf(m, mb);
+  const float fa = __builtin_amdgcn_exp2f(m - mm), fb = __builtin_amdgcn_exp2f(mb - mm);
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    o0[r] = o0[r] * fa + xw[r * 64] * fb;
+    o1[r] = o1[r] * fa + xw[(16 + r) * 64] * fb;
+  }
+  const float lt = lacc[0] * fa + xw[32 * 64] * fb;
+  const float inv = 1.0f / lt;
+  bf16* orow = a.o + ((long)b * S + myq) * a.ldo + h * 64;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const int d = 8 * g + 4 * hl;
+    bf16x4 v0, v1;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      v0[e] = (bf16)(o0[4 * g + e] * inv);
+      v1[e] = (bf16)(o1[4 * g + e] * inv);
+    }
+    *reinterpret_cast<bf16x4*>(orow + d) = v0;
+    *reinterpret_cast<bf16x4*>(orow + 32 + d) = v1;
+  }
+  if (hl == 0 && a.lse) a.lse[((long)b * a.Hq + h) * S + myq] = mm + __log2f(lt);
+}
+
+// ---- ping-pong dK/dV pass (round 4) ------------------------------------------------------------------------------
+// attn_bwd_kv_dma_kernel's work in 8 waves: groups A (waves 0-3) and B (4-7) hold the SAME 128 keys (32 per wave,
+// w & 3) and split the (q-head, 64-query chunk) stages by parity (A even, B odd). Per stage a wave runs an MFMA phase
+// (dV^T += dO^T P and dK^T += Q^T dS of its previous stage, 16 MFMAs, then S^T = Q K^T and dP^T = dO V^T - delta of
+// the current stage, 16 MFMAs) and a VALU phase (p, dS and their bf16 fragments), the groups one phase apart (see
+// attn_bwd_dq_pp_kernel). A stage's slot is read in phases it (S / dP), it + 1 (lse, delta) and it + 2 (dV / dK);
+// stage it + PP_D is issued at the start of phase it. Group B's partial dK / dV reach group A through LDS at the end.
 template <bool MASK>
 __device__ __forceinline__ void ppkv_valu(const float* lse_l, f32x16 (&sp)[2], f32x16 (&dp)[2], float c, int qc, int S,
                                           int mykey, int kvlen, bool causal, int lane) {
@@ -1964,7 +2131,8 @@ extern "C" int slx_attn_fwd(const slx_attn_desc* d, slx_stream_t stream) {
   if (rc) return rc;
   if (a.B == 0 || a.S == 0) return 0;
   dim3 grid(((a.S + 127) / 128) * a.Hq * a.B);
-  if (attn_dma()) hipLaunchKernelGGL(attn_fwd_dma_kernel, grid, dim3(256), 0, (hipStream_t)stream, a);
+  if (attn_pp()) hipLaunchKernelGGL(attn_fwd_pp_kernel, grid, dim3(512), 0, (hipStream_t)stream, a);
+  else if (attn_dma()) hipLaunchKernelGGL(attn_fwd_dma_kernel, grid, dim3(256), 0, (hipStream_t)stream, a);
   else hipLaunchKernelGGL(attn_fwd_kernel, grid, dim3(256), 0, (hipStream_t)stream, a);
   SLX_LAUNCH_CHECK("slx_attn_fwd");
   return 0;
