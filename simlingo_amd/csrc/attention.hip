@@ -737,7 +737,7 @@ __device__ __forceinline__ void dma_row64_f32(__amdgpu_buffer_rsrc_t rs, char* l
 }
 
 #ifndef ATTN_NSLOT
-#define ATTN_NSLOT 3
+#define ATTN_NSLOT 2  // one tile ahead: fastest of 2 / 3 / 4 slots on both shapes (profiles/round4_attn_dma_ab.txt)
 #endif
 
 // forward: attn_fwd_kernel with the K/V tiles of the (b, kv-head) streamed through an NSLOT ring (16 KiB per slot)

@@ -50,8 +50,7 @@ def test_twenty_step_drift(dev):
         eng.backward(None)
         eng.adamw_step(LR, i + 1, betas=cfg.betas, eps=cfg.eps, weight_decay=cfg.weight_decay, max_norm=cfg.grad_clip)
         torch.cuda.synchronize()
-        with torch.no_grad():
-            r, grads = O.loss_and_grads({k: v.detach() for k, v in ref.items()}, cfg, ex)
+        r, grads = O.loss_and_grads({k: v.detach() for k, v in ref.items()}, cfg, ex)
         for k in names:
             ref[k].grad = grads[k].clone()
         torch.nn.utils.clip_grad_norm_([ref[k] for k in names], cfg.grad_clip)
@@ -70,8 +69,7 @@ def test_twenty_step_drift(dev):
     _, rp, sp = eng.forward(ex.driving_input.camera_images.to(dev), plan, plan.to_device(dev), lab.path.to(dev),
                             lab.waypoints.to(dev), training=False)
     torch.cuda.synchronize()
-    with torch.no_grad():
-        r, _ = O.loss_and_grads({k: v.detach() for k, v in ref.items()}, cfg, ex)
+    r, _ = O.loss_and_grads({k: v.detach() for k, v in ref.items()}, cfg, ex)
     d_route = (rp.cpu() - r["route_pred"]).abs().max().item()
     d_speed = (sp.cpu() - r["speed_pred"]).abs().max().item()
     print(f"final: route max {d_route:.4g} m, speed max {d_speed:.4g} m, worst step loss rel {worst:.3g}")
