@@ -86,6 +86,7 @@ struct GemmArgs {
   float* split_ws;   // null = split-K partials go to C with f32 atomics
   int* split_cnt;    // [2 * tiles] arrival / published counters, zero on entry, reset by each tile's last arriver
   int split_tile0;   // tile-index offset of this GEMM in the shared workspace (slx_gemm_bf16_pair's second GEMM)
+  int xcd_split;     // slx_gemm_bf16_pair: 1-D grid of 256, XCD x takes K split x % ksplit (gemm_bf16_v3_pair_kernel)
   // fused LM head + cross entropy (EPI_CE_PART / EPI_CE_GRAD)
   const int* ce_labels;  // [M] next-token label per row (-1 = ignored)
   float* ce_part;        // [M][ce_ldpart] (max, sumexp) pairs, one per 64-column sub-tile
@@ -1167,8 +1168,8 @@ __device__ __forceinline__ void v3_split_sum(const float* slabs, int y, f32x4 (&
 }
 
 __device__ __forceinline__ bool v3_split_reduce(const GemmArgs& p, int tile, f32x4 (&acc)[8][4], int* role_lds,
-                                                int wave, int lane) {
-  const int S = p.ksplit, y = blockIdx.y;
+                                                int wave, int lane, int y) {
+  const int S = p.ksplit;
   const int t = p.split_tile0 + tile;
   int* arrive = p.split_cnt + 2 * t;
   int* pub = arrive + 1;
@@ -1463,7 +1464,8 @@ __device__ __forceinline__ void fe_epilogue(const GemmArgs& p, OutT* __restrict_
 // epilogue; next_bid >= 0 = issue the next tile's stages 0 and 1 inside this tile's epilogue.
 template <bool AK, bool BKc, int EPI, typename OutT, bool SW, bool FE = false>
 __device__ __forceinline__ void v3_tile(const GemmArgs& p, int bid, long z, char* smem, bool pre = false,
-                                        int next_bid = -1) {
+                                        int next_bid = -1, int ysplit = -1) {
+  const int ys = ysplit >= 0 ? ysplit : (int)blockIdx.y;  // this block's K split
   static_assert(!FE || SW, "the register-direct epilogue needs the swapped-operand accumulator layout");
   constexpr int NW = 8;
   constexpr int A_BYTES = V3_BM * BK * 2, B_BYTES = V3_BN * BK * 2;
@@ -1479,7 +1481,7 @@ __device__ __forceinline__ void v3_tile(const GemmArgs& p, int bid, long z, char
 
   int kbeg = 0, kend = p.K;
   if (p.ksplit > 1) {
-    kbeg = blockIdx.y * p.kchunk;
+    kbeg = ys * p.kchunk;
     kend = min(p.K, kbeg + p.kchunk);
   }
   const int nk = (kend - kbeg + BK - 1) / BK;
@@ -1585,7 +1587,7 @@ __device__ __forceinline__ void v3_tile(const GemmArgs& p, int bid, long z, char
   if constexpr (EPI == EPI_STORE) {
     if (p.ksplit > 1 && p.split_ws) {
       __syncthreads();  // every wave is done reading the ring (the role word sits past the epilogue region)
-      if (!v3_split_reduce(p, bid, acc, reinterpret_cast<int*>(smem + 8 * 64 * EP_LD * 4), wave, lane)) return;
+      if (!v3_split_reduce(p, bid, acc, reinterpret_cast<int*>(smem + 8 * 64 * EP_LD * 4), wave, lane, ys)) return;
       reduced = true;
     }
   }
@@ -1773,7 +1775,19 @@ template <bool AK, bool BKc, bool SW>
 __global__ __launch_bounds__(512, 1) void gemm_bf16_v3_pair_kernel(GemmArgs p, GemmArgs q) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int n1 = p.tilesM * p.tilesN;
-  const int bid = xcd_remap(blockIdx.x, n1 + q.tilesM * q.tilesN);
+  const int nt = n1 + q.tilesM * q.tilesN;
+  if (p.xcd_split) {
+    // one round of 8 x 32 blocks (tiles x splits = 256): blocks dealt round-robin over the XCDs, so XCD x = L & 7 takes
+    // K split x % S of the tile range [region * nt / R, +nt / R), R = 8 / S regions: every XCD streams ONE K range of
+    // a contiguous run of tiles (the 4 x 8 / 8 x 4 regions of v3_origin's tile order) instead of both splits of a 4 x 4
+    // region, which cuts the operand panels each XCD's L2 fills (placement only decides speed, never correctness)
+    const int L = blockIdx.x, x = L & 7, S = p.ksplit, R = 8 / S;
+    const int tile = (x / S) * (nt / R) + (L >> 3);
+    if (tile < n1) v3_tile<AK, BKc, EPI_STORE, float, SW>(p, tile, 0, smem, false, -1, x % S);
+    else v3_tile<AK, BKc, EPI_STORE, float, SW>(q, tile - n1, 0, smem, false, -1, x % S);
+    return;
+  }
+  const int bid = xcd_remap(blockIdx.x, nt);
   if (bid < n1) v3_tile<AK, BKc, EPI_STORE, float, SW>(p, bid, 0, smem);
   else v3_tile<AK, BKc, EPI_STORE, float, SW>(q, bid - n1, 0, smem);
 }
@@ -2641,7 +2655,11 @@ static int launch_pair(GemmArgs& a, GemmArgs& b, hipStream_t st) {
     hipFuncSetAttribute((const void*)gemm_bf16_v3_pair_kernel<AK, BKc, SW>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
     attr = true;
   }
-  dim3 grid(a.tilesM * a.tilesN + b.tilesM * b.tilesN, a.ksplit);
+  const int nt = a.tilesM * a.tilesN + b.tilesM * b.tilesN, sp = a.ksplit;
+  static const bool xs_env = [] { const char* e = getenv("SLX_PAIR_XCD_SPLIT"); return e ? atoi(e) != 0 : true; }();
+  const bool xs = xs_env && nt * sp == 256 && (sp == 1 || sp == 2 || sp == 4 || sp == 8) && nt % (8 / sp) == 0;
+  a.xcd_split = b.xcd_split = xs ? 1 : 0;
+  dim3 grid = xs ? dim3(256) : dim3(nt, sp);
   hipLaunchKernelGGL((gemm_bf16_v3_pair_kernel<AK, BKc, SW>), grid, dim3(512), LDS, st, a, b);
   SLX_LAUNCH_CHECK("slx_gemm_bf16_pair");
   return 0;

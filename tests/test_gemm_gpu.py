@@ -493,3 +493,26 @@ def test_gemm_splitk_in_launch_reduction(dev, split, variant):
     assert torch.equal(p1[0], p1[1]) and torch.equal(p2[0], p2[1])
     assert (p1[0] - ref).abs().max().item() < 2e-3 * T ** 0.5
     assert (p2[0] - dy2.float().t() @ x2.float()).abs().max().item() < 2e-3 * T ** 0.5
+
+
+@pytest.mark.parametrize("shapes", [((1024, 4096), (4096, 1024)),   # InternViT fc2.w + fc1.w: 128 tiles x 2 splits
+                                    ((3072, 1024), (1024, 1024))])  # qkv.w + proj.w: 64 tiles x 4 splits
+def test_gemm_pair_xcd_split_full_shape(dev, shapes):
+    """The InternViT weight-gradient pairs at their real shapes (K = 16 x 1025 tokens): tiles x splits = 256, so the
+    pair launches as one 1-D round with XCD x taking K split x % S of a contiguous tile range (SLX_PAIR_XCD_SPLIT);
+    each gradient vs torch fp32 on the same bf16 operands, accumulating into a nonzero C, twice (counters reset)."""
+    T = 16400
+    g = torch.Generator(device=dev).manual_seed(sum(a * b for a, b in shapes))
+    ops, refs = [], []
+    for (N, Kd) in shapes:
+        dy = torch.randn(T, N, device=dev, generator=g).bfloat16()
+        x = torch.randn(T, Kd, device=dev, generator=g).bfloat16()
+        C = torch.randn(N, Kd, device=dev, generator=g)
+        refs.append(C + 2 * (dy.float().t() @ x.float()))
+        ops.append((dy, x, C))
+    for _ in range(2):
+        K.mm_pair(ops[0], ops[1])
+    torch.cuda.synchronize()
+    for (_, _, C), ref in zip(ops, refs):
+        err = (C - ref).abs().max().item()
+        assert err < 4e-3 * T ** 0.5, err
