@@ -41,4 +41,4 @@ def test_lora_db_side_stream_matches(dev, monkeypatch):
         if a.norm() == 0:
             assert b.norm() == 0, k
             continue
-        assert ((a - b).norm() / a.norm()).item() < 1e-5, k
+        assert ((a - b).norm() / a.norm()).item() < 5e-4, k
