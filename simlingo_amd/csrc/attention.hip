@@ -576,6 +576,47 @@ __device__ __forceinline__ void bwd_dq_tile(const char* Kl, const char* Vl, cons
     }
 }
 
+// The dQ tile one 32-key half at a time (S, dP, dS and the dQ MFMAs of half kb before half kb + 1), with dP started
+// from a splat of -delta instead of a held vector: half the live S / dP registers, so the DMA-staged dQ pass fits
+// 168 VGPRs and three workgroups per CU (ATTN_DQ_SER, A/B).
+template <bool MASK>
+__device__ __forceinline__ void bwd_dq_tile_ser(const char* Kl, const char* Vl, const bf16x8 (&qf)[4], const bf16x8 (&df)[4],
+                                                f32x16& dq0, f32x16& dq1, float c, float lse, float negdelta, int key0,
+                                                int kvlen, int myq, bool causal, int lane) {
+  const int hl = lane >> 5;
+#pragma unroll
+  for (int kb = 0; kb < 2; ++kb) {
+    f32x16 sv, dp;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { sv[r] = 0.f; dp[r] = negdelta; }
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      sv = mfma32(row_frag(Kl, kb * 32, kk, lane), qf[kk], sv);
+      dp = mfma32(row_frag(Vl, kb * 32, kk, lane), df[kk], dp);
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      float pv = __builtin_amdgcn_exp2f(__builtin_fmaf(sv[r], c, -lse));
+      if constexpr (MASK) {
+        const int key = key0 + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
+        const bool ok = (key < kvlen) & (!causal | (key <= myq));
+        pv = ok ? pv : 0.f;
+      }
+      dp[r] = pv * dp[r];
+    }
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      const bf16x8 sb = acc_frag(dp, st);
+      dq0 = mfma32(tr_frag(Kl, kb * 32 + 16 * st, 0, lane), sb, dq0);
+      dq1 = mfma32(tr_frag(Kl, kb * 32 + 16 * st, 32, lane), sb, dq1);
+    }
+  }
+}
+
+#ifndef ATTN_DQ_SER
+#define ATTN_DQ_SER 0
+#endif
+
 __global__ __launch_bounds__(256, ATTN_DQ_OCC) void attn_bwd_dq_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) char smem[2 * 2 * 8192];
   const BlockCoord bc = attn_block((a.S + 127) / 128, a.Hq, a.Hkv, a.B, a.causal ? 1 : 0, a.tail_first);
@@ -895,8 +936,13 @@ __global__ __launch_bounds__(256, ATTN_DQ_OCC) void attn_bwd_dq_dma_kernel(AttnA
     const char* Vl = Kl + 8192;
     if (active && !(a.causal && t * 64 > q0 + 31)) {
       const int kfull = a.causal ? min(kvlen, q0 + 1) : kvlen;
+#if ATTN_DQ_SER
+      if ((t + 1) * 64 <= kfull) bwd_dq_tile_ser<false>(Kl, Vl, qf, df, dq0, dq1, c, lse, -dlt, t * 64, kvlen, myq, false, lane);
+      else bwd_dq_tile_ser<true>(Kl, Vl, qf, df, dq0, dq1, c, lse, -dlt, t * 64, kvlen, myq, a.causal, lane);
+#else
       if ((t + 1) * 64 <= kfull) bwd_dq_tile<false>(Kl, Vl, qf, df, dq0, dq1, c, lse, negd, t * 64, kvlen, myq, false, lane);
       else bwd_dq_tile<true>(Kl, Vl, qf, df, dq0, dq1, c, lse, negd, t * 64, kvlen, myq, a.causal, lane);
+#endif
     }
   }
   wait_vmcnt<0>();

@@ -4,5 +4,5 @@ set -e
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-AB_DIR=ab_builds timeout -k 10 240 python3 tools/attn_ab.py run reg dma3 dma2 dma4 dma3sb pp5 pp4 pp6
+AB_DIR=ab_builds timeout -k 10 240 python3 tools/attn_ab.py run reg dma2 dq3s dqs pp5
 timeout -k 10 300 python3 -u -m pytest tests/test_attention_gpu.py tests/test_attention_variants_gpu.py tests/test_lora_dropout_gpu.py -x -q --timeout 120 --timeout-method thread 2>&1 | tail -3
