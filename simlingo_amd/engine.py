@@ -49,6 +49,10 @@ NT_DGRAD = os.environ.get("SLX_NT_DGRAD", "1") != "0"
 # us). SLX_LORA_DB_SIDE=1 runs the gate/up LoRA B-gradient GEMM (it reads the same dgu, nothing reads its output before
 # the optimizer) on a side stream launched right after the dgrad, so its blocks take the idle CUs.
 LORA_DB_SIDE = os.environ.get("SLX_LORA_DB_SIDE", "0") == "1"
+# SLX_PAIR_SIDE=1: each InternViT weight-gradient pair runs on the side stream beside its independent data-gradient GEMM
+# (fc2.w + fc1.w beside the fc1 dgrad, proj.w + qkv.w beside the qkv dgrad); the compute stream waits for it before
+# the next LayerNorm backward, which rewrites the g buffer the pair reads.
+PAIR_SIDE = os.environ.get("SLX_PAIR_SIDE", "0") == "1"
 ALIGN = 64  # elements; keeps every parameter view 256-B aligned
 
 
@@ -747,13 +751,21 @@ class VLAEngine(EngineOps):
             dh = self._e(Mv, F_)
             self._mm_dx(g, self.W[p + "fc2.w"], self.WT.get(p + "fc2.w"), dh, epi=K.EPI_GELU_BWD, aux=Ls["hpre"],
                         ldaux=F_, colsum=self.G[p + "fc1.b"])  # fc1.b grad = column sums of dh, in the same epilogue
-            if PAIR_WGRAD:  # fc2.w and fc1.w gradients as one launch (two under-filled grids fill the chip together)
+            side = PAIR_WGRAD and PAIR_SIDE and not self.precise
+            if side:
+                ev_side = self._side_fork()
+            elif PAIR_WGRAD:  # fc2.w and fc1.w gradients as one launch (two under-filled grids fill the chip together)
                 with self._probe("vit.wgrad_fc"):
                     K.mm_pair((g, Ls["hact"], self.G[p + "fc2.w"]), (dh, Ls["h2"], self.G[p + "fc1.w"]))
             else:
                 K.mm(dh, Ls["h2"], self.G[p + "fc1.w"], ta=True, tb=False, accumulate=True)
             dh2 = self._e(Mv, D)  # bf16: the gradient a bf16 Linear backward hands the fp32 LayerNorm under autocast
             self._mm_dx(dh, self.W[p + "fc1.w"], self.WT.get(p + "fc1.w"), dh2)
+            if side:  # the pair beside the fc1 dgrad (issued after it, so the dgrad's blocks are dispatched first)
+                with torch.cuda.stream(self._side):
+                    self._side.wait_event(ev_side)
+                    K.mm_pair((g, Ls["hact"], self.G[p + "fc2.w"]), (dh, Ls["h2"], self.G[p + "fc1.w"]))
+                self._side_join_now([g, dh, Ls["hact"], Ls["h2"]])
             del dh
             # x_mid = x_in + ls1 * proj(attn(ln1(x_in))): its branch backward (g = ls1 * dx_mid, dls1, proj.b grad)
             # fused into the LN2 backward that produces dx_mid
@@ -770,12 +782,19 @@ class VLAEngine(EngineOps):
                        dqkv[:, :D], dqkv[:, D:2 * D], dqkv[:, 2 * D:], vws, B=N, S=T, Hq=H, Hkv=H, causal=False,
                        dbias=self.G[p + "qkv.b"])  # qkv.b grad = column sums of dq | dk | dv, in the same kernels
             del do
-            if PAIR_WGRAD:  # proj.w (g still holds ls1 * dx_mid) and qkv.w gradients as one launch
+            if side:
+                ev_side = self._side_fork()
+            elif PAIR_WGRAD:  # proj.w (g still holds ls1 * dx_mid) and qkv.w gradients as one launch
                 with self._probe("vit.wgrad_attn"):
                     K.mm_pair((g, Ls["o"], self.G[p + "proj.w"]), (dqkv, Ls["h1"], self.G[p + "qkv.w"]))
             else:
                 K.mm(dqkv, Ls["h1"], self.G[p + "qkv.w"], ta=True, tb=False, accumulate=True)
             self._mm_dx(dqkv, self.W[p + "qkv.w"], self.WT.get(p + "qkv.w"), dh2)
+            if side:
+                with torch.cuda.stream(self._side):
+                    self._side.wait_event(ev_side)
+                    K.mm_pair((g, Ls["o"], self.G[p + "proj.w"]), (dqkv, Ls["h1"], self.G[p + "qkv.w"]))
+                self._side_join_now([g, dqkv, Ls["o"], Ls["h1"]])
             del dqkv
             nxt = None
             if i > 0:  # the next (lower) layer's ls2 branch backward, fused onto dx_in
@@ -797,6 +816,22 @@ class VLAEngine(EngineOps):
         self._group_done("vit_embed")
         self.bucketer.mark("backward_end")
         self.saved = None
+
+    def _side_fork(self):
+        """An event on the compute stream that side-stream work issued next waits for."""
+        if self._side is None:
+            self._side = torch.cuda.Stream(device=self.device)
+        ev = torch.cuda.Event()
+        ev.record()
+        return ev
+
+    def _side_join_now(self, tensors):
+        """The compute stream waits here for everything issued on the side stream so far."""
+        ev = torch.cuda.Event()
+        ev.record(self._side)
+        torch.cuda.current_stream(self.device).wait_event(ev)
+        for t in tensors:
+            t.record_stream(self._side)
 
     def _join_side(self):
         """The compute stream waits for the side-stream LoRA B-gradient GEMMs issued so far."""

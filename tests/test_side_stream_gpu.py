@@ -8,8 +8,9 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def _step(dev, side, monkeypatch):
+def _step(dev, side, monkeypatch, pair_side=False):
     import simlingo_amd.engine as E
+    monkeypatch.setattr(E, "PAIR_SIDE", pair_side)
     from simlingo_amd.config import full_config
     from simlingo_amd.params import init_params
     from simlingo_amd.plan import plan_from_example
@@ -36,6 +37,20 @@ def test_lora_db_side_stream_matches(dev, monkeypatch):
     o1, g1, marks = _step(dev, True, monkeypatch)
     assert torch.equal(o0, o1)
     assert all(n == 0 for g, n in marks if g.startswith("llm")), marks  # joined before each layer's group is done
+    for k in g0:
+        a, b = g0[k].reshape(-1), g1[k].reshape(-1)
+        if a.norm() == 0:
+            assert b.norm() == 0, k
+            continue
+        assert ((a - b).norm() / a.norm()).item() < 5e-4, k
+
+
+def test_pair_side_stream_matches(dev, monkeypatch):
+    """SLX_PAIR_SIDE: the InternViT weight-gradient pairs on the side stream beside their data-gradient GEMMs give the
+    single-stream gradients (5e-4 relative: the qkv.w + proj.w pair's split-K atomics are order-dependent)."""
+    o0, g0, _ = _step(dev, False, monkeypatch)
+    o1, g1, _ = _step(dev, False, monkeypatch, pair_side=True)
+    assert torch.equal(o0, o1)
     for k in g0:
         a, b = g0[k].reshape(-1), g1[k].reshape(-1)
         if a.norm() == 0:
