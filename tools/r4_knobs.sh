@@ -2,7 +2,5 @@
 set -e
 cd $GRAFT_REPO_ROOT
 bash tools/r4_step_ab.sh "SLX_PAIR_XCD_SPLIT=0" "SLX_PAIR_XCD_SPLIT=1" 2
-bash tools/r4_step_ab.sh "SLX_LORA_DB_SIDE=0" "SLX_LORA_DB_SIDE=1" 2
-bash tools/r4_step_ab.sh "SLX_LORA_DX_GROUPS=1" "SLX_LORA_DX_GROUPS=2" 2
-bash tools/r4_step_ab.sh "SLX_ATTN_DMA=0" "SLX_ATTN_DMA=1" 1
 bash tools/r4_step_ab.sh "SLX_PAIR_SIDE=0" "SLX_PAIR_SIDE=1" 2
+bash tools/r4_step_ab.sh "SLX_LORA_DB_SIDE=0" "SLX_LORA_DB_SIDE=1" 2
