@@ -238,6 +238,11 @@ typedef struct {
   int dt_bf16;                        /* 1: dt points to bf16 rows (lddt % 8 == 0), e.g. the bf16 dgrad GEMM output */
 } slx_lora_bwd_desc;
 int slx_lora_bwd(const slx_lora_bwd_desc* d, slx_stream_t stream);
+/* The same with dA summed without atomics: each (column block, row chunk) block stores its f32 partial into ws and a
+ * second launch adds the row chunks' partials into dA_j in chunk order (deterministic). ws_floats must be at least
+ * slx_lora_bwd_ws_floats(M, Kin, nsites); a smaller ws falls back to slx_lora_bwd's atomics. */
+int64_t slx_lora_bwd_ws_floats(int64_t M, int Kin, int nsites);
+int slx_lora_bwd_ws(const slx_lora_bwd_desc* d, float* ws, int64_t ws_floats, slx_stream_t stream);
 
 /* small strided f32 GEMM (driving heads adaptors.py:113-132, WaypointInputAdaptor :80)        */
 enum { SLX_ACT_NONE = 0, SLX_ACT_RELU = 1, SLX_ACT_SILU = 2 };

@@ -221,6 +221,7 @@ struct LoraBwdArgs {
   float sc;       // 1 / (1 - p)
   int mchunk;
   int dt_bf16;    // dt holds bf16 rows
+  float* dA_part; // non-null: per-row-chunk partials [nchunk][nsites][32][Kin] (plain stores) instead of atomics
 };
 
 __device__ __forceinline__ int la_sw(int row, int chunk) {
@@ -354,6 +355,17 @@ __global__ __launch_bounds__(256, 2) void lora_da_kernel(LoraBwdArgs a) {
       __syncthreads();
     }
   }
+  if (a.dA_part) {  // this row chunk's partial, summed in chunk order by lora_da_reduce_kernel
+    float* part = a.dA_part + (long)blockIdx.y * NS * 32 * a.Kin;
+#pragma unroll
+    for (int j = 0; j < NS; ++j)
+#pragma unroll
+      for (int g = 0; g < 16; ++g) {
+        const int rr = (g & 3) + 8 * (g >> 2) + 4 * h;
+        part[((long)j * 32 + rr) * a.Kin + mycol] = acc[j][g];
+      }
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < NS; ++j)
 #pragma unroll
@@ -361,6 +373,23 @@ __global__ __launch_bounds__(256, 2) void lora_da_kernel(LoraBwdArgs a) {
       const int rr = (g & 3) + 8 * (g >> 2) + 4 * h;
       atomicAdd(a.dA[j] + (long)rr * a.Kin + mycol, acc[j][g]);
     }
+}
+
+// dA_j[r][k] += sum over the row chunks c (in order) of part[c][j][r][k]: one thread per 4 consecutive k
+__global__ __launch_bounds__(256) void lora_da_reduce_kernel(LoraBwdArgs a, int nchunk) {
+  const long per = (long)a.nsites * 32 * a.Kin;
+  const long i4 = ((long)blockIdx.x * 256 + threadIdx.x) * 4;
+  if (i4 >= per) return;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int c = 0; c < nchunk; ++c) {
+    const float4 v = *reinterpret_cast<const float4*>(a.dA_part + c * per + i4);
+    s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+  }
+  const int j = (int)(i4 / (32L * a.Kin));
+  float* d = a.dA[j] + (i4 - (long)j * 32 * a.Kin);
+  float4 o = *reinterpret_cast<float4*>(d);
+  o.x += s.x; o.y += s.y; o.z += s.z; o.w += s.w;
+  *reinterpret_cast<float4*>(d) = o;
 }
 
 // dx += sum_j keep_j / (1-p) * (dT_j A_j) (f32 in place, or bf16(dx + ...) to dxb): block = one 32-row tile, 8 waves
@@ -529,7 +558,13 @@ extern "C" int slx_dropout_bits(const slx_dropout_bits_desc* d, slx_stream_t str
 
 template <int NS, bool DTB>
 static void launch_bwd_t(const LoraBwdArgs& a, dim3 grid, hipStream_t st) {
-  if (a.dA[0]) hipLaunchKernelGGL((lora_da_kernel<NS, DTB>), grid, dim3(256), 0, st, a);
+  if (a.dA[0]) {
+    hipLaunchKernelGGL((lora_da_kernel<NS, DTB>), grid, dim3(256), 0, st, a);
+    if (a.dA_part) {
+      const long per4 = (long)NS * 32 * a.Kin / 4;
+      hipLaunchKernelGGL(lora_da_reduce_kernel, dim3((unsigned)((per4 + 255) / 256)), dim3(256), 0, st, a, (int)grid.y);
+    }
+  }
   // column groups per 32-row tile: 200 row tiles alone (Qwen2, M = 6384) under-fill the 256 CUs
   static const int dxg = [] { const char* e = getenv("SLX_LORA_DX_GROUPS"); return e ? atoi(e) : 2; }();
   const int nct = a.Kin / 32;
@@ -543,7 +578,35 @@ static void launch_bwd(const LoraBwdArgs& a, dim3 grid, hipStream_t st) {
   else launch_bwd_t<NS, false>(a, grid, st);
 }
 
+// row chunks of the dA pass (shared by the launch and the workspace size): fewer chunks mean fewer dA partials, more
+// mean more blocks
+static int lora_da_mchunk(long M, int Kin) {
+  static const int tgt = [] { const char* e = getenv("SLX_LORA_DA_BLOCKS"); return e ? atoi(e) : 512; }();
+  const int cb = Kin / 128;
+  const int nch = (tgt + cb - 1) / cb;
+  int mchunk = (int)((M + nch - 1) / nch);
+  mchunk = ((mchunk + 63) / 64) * 64;
+  return mchunk < 64 ? 64 : mchunk;
+}
+
+extern "C" int64_t slx_lora_bwd_ws_floats(int64_t M, int Kin, int nsites) {
+  if (M <= 0 || Kin <= 0 || Kin % 128 != 0 || nsites < 1) return 0;
+  const int mchunk = lora_da_mchunk(M, Kin);
+  const long nch = (M + mchunk - 1) / mchunk;
+  return nch * nsites * 32L * Kin;
+}
+
+static int lora_bwd_impl(const slx_lora_bwd_desc* d, float* ws, int64_t ws_floats, slx_stream_t stream);
+
 extern "C" int slx_lora_bwd(const slx_lora_bwd_desc* d, slx_stream_t stream) {
+  return lora_bwd_impl(d, nullptr, 0, stream);
+}
+
+extern "C" int slx_lora_bwd_ws(const slx_lora_bwd_desc* d, float* ws, int64_t ws_floats, slx_stream_t stream) {
+  return lora_bwd_impl(d, ws, ws_floats, stream);
+}
+
+static int lora_bwd_impl(const slx_lora_bwd_desc* d, float* ws, int64_t ws_floats, slx_stream_t stream) {
   SLX_CHECK_ARG(d->nsites >= 1 && d->nsites <= 4 && d->r == 32, "slx_lora_bwd: 1..4 sites of rank 32");
   SLX_CHECK_ARG(d->Kin % 128 == 0 && d->ldx % 8 == 0 && d->lddt % 4 == 0, "slx_lora_bwd: Kin %% 128, ldx %% 8, lddt %% 4");
   SLX_CHECK_ARG(!d->dx || (d->lddx % 4 == 0 && (!d->dx_bf16 || d->lddx_bf16 % 4 == 0)),
@@ -570,13 +633,12 @@ extern "C" int slx_lora_bwd(const slx_lora_bwd_desc* d, slx_stream_t stream) {
   a.dxb = (bf16*)d->dx_bf16; a.lddxb = d->lddx_bf16;
   a.sc = 1.0f / (1.0f - d->p);
   const int cb = d->Kin / 128;
-  // M chunks: fewer chunks mean fewer f32 atomics into dA (nch x sites x 32 x Kin), more mean more blocks
-  static const int tgt = [] { const char* e = getenv("SLX_LORA_DA_BLOCKS"); return e ? atoi(e) : 512; }();
-  int nch = (tgt + cb - 1) / cb;
-  int mchunk = (int)((d->M + nch - 1) / nch);
-  mchunk = ((mchunk + 63) / 64) * 64;
-  a.mchunk = mchunk < 64 ? 64 : mchunk;
+  a.mchunk = lora_da_mchunk(d->M, d->Kin);
   dim3 grid((unsigned)cb, (unsigned)((d->M + a.mchunk - 1) / a.mchunk));
+  SLX_CHECK_ARG(!ws || !d->dA[0] || ws_floats >= slx_lora_bwd_ws_floats(d->M, d->Kin, d->nsites),
+                "slx_lora_bwd_ws: workspace holds %lld floats, slx_lora_bwd_ws_floats asks for %lld", (long long)ws_floats,
+                (long long)slx_lora_bwd_ws_floats(d->M, d->Kin, d->nsites));
+  a.dA_part = (ws && d->dA[0]) ? ws : nullptr;
   hipStream_t st = (hipStream_t)stream;
   switch (d->nsites) {
     case 1: launch_bwd<1>(a, grid, st); break;

@@ -291,6 +291,8 @@ for _n, _a in {
     "slx_lora_down": [ctypes.POINTER(LoraDownDesc), _vp],
     "slx_lora_pack_a": [_vp, ctypes.c_int64, ctypes.c_int, ctypes.c_int, _vp, _vp],
     "slx_lora_bwd": [ctypes.POINTER(LoraBwdDesc), _vp],
+    "slx_lora_bwd_ws": [ctypes.POINTER(LoraBwdDesc), _vp, _I, _vp],
+    "slx_lora_bwd_ws_floats": [_I, _i, _i],  # int64 result, < 2^31 at every shape used (restype int)
     "slx_dropout_bits": [ctypes.POINTER(DropoutBitsDesc), _vp],
     "slx_attn_bwd": [ctypes.POINTER(AttnDesc), ctypes.POINTER(AttnBwdDesc), _vp],
     "slx_rope": [_vp, _I, _I, _i, _i, _vp, _vp, _i, _vp],
@@ -530,6 +532,12 @@ def lora_down(x, As, t, seeds, p=0.0, ldmask=None, bits=None, packed=False):
     check(lib().slx_lora_down(ctypes.byref(d), stream_ptr()), "slx_lora_down")
 
 
+_lora_ws: dict = {}  # per-stream dA partials of slx_lora_bwd_ws
+# SLX_LORA_DA_SLAB=1: the LoRA A gradients through per-row-chunk partials + an in-order sum (slx_lora_bwd_ws) instead of
+# the dA kernel's f32 atomics
+LORA_DA_SLAB = os.environ.get("SLX_LORA_DA_SLAB", "0") == "1"
+
+
 def lora_bwd(x, dt, As, bits, dAs, dx=None, dx_bf16=None, p=0.0, packed=False):
     """peft LoRA backward of the sites sharing x (one launch): dAs[j] (f32 [32, kin]) += dT_j^T drop_j(x) (dAs=None:
     skipped) and, if dx (f32 [M, kin]) is given, dx += sum_j drop_j'(dT_j As[j]) in place - or written as
@@ -566,6 +574,14 @@ def lora_bwd(x, dt, As, bits, dAs, dx=None, dx_bf16=None, p=0.0, packed=False):
         assert dx_bf16.dtype == torch.bfloat16 and dx_bf16.shape[0] == M
         d.dx_bf16, d.lddx_bf16 = dx_bf16.data_ptr(), dx_bf16.stride(0)
     d.p = float(p)
+    if LORA_DA_SLAB and dAs is not None:  # dA summed through per-row-chunk partials (no f32 atomics, deterministic)
+        need = lib().slx_lora_bwd_ws_floats(M, kin, len(As))
+        sk = (x.device, torch.cuda.current_stream(x.device).cuda_stream)
+        ws = _lora_ws.get(sk)
+        if ws is None or ws.numel() < need:
+            ws = _lora_ws[sk] = torch.empty(need, dtype=torch.float32, device=x.device)
+        check(lib().slx_lora_bwd_ws(ctypes.byref(d), P(ws), ws.numel(), stream_ptr()), "slx_lora_bwd_ws")
+        return
     check(lib().slx_lora_bwd(ctypes.byref(d), stream_ptr()), "slx_lora_bwd")
 
 

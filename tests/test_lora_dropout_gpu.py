@@ -88,11 +88,13 @@ def test_dropmask_dgrad_padded_k64(dev):
                                                  (6384, 4864, 1, 0.1, "none"), (798, 128, 3, 0.0, "f32"),
                                                  (798, 896, 2, 0.0, "bf16")])
 @pytest.mark.parametrize("dt_bf16", [False, True])
-def test_lora_bwd_grouped(dev, M, kin, nsites, p, mode, dt_bf16):
+@pytest.mark.parametrize("slab", [False, True])
+def test_lora_bwd_grouped(dev, M, kin, nsites, p, mode, dt_bf16, slab, monkeypatch):
     """slx_lora_bwd: dA_j += dT_j^T drop_j(x) and dx += sum_j drop_j'(dT_j A_j) (f32 in place / bf16 out / none),
     masks read from the keep bits of slx_lora_down, dT read as f32 from a strided view (the dgrad GEMM's extra
-    columns)."""
+    columns). slab: dA through slx_lora_bwd_ws's per-row-chunk partials and in-order sum instead of f32 atomics."""
     from simlingo_amd.dropmask import keep_bits
+    monkeypatch.setattr(K, "LORA_DA_SLAB", slab)
     g = torch.Generator(device=dev).manual_seed(13)
     x = torch.randn(M, kin, device=dev, generator=g).bfloat16()
     dtfull = torch.randn(M, 32 * nsites + 64, device=dev, generator=g)
@@ -124,3 +126,25 @@ def test_lora_bwd_grouped(dev, M, kin, nsites, p, mode, dt_bf16):
         assert torch.equal(dx, dx0)  # the f32 base gradient is only read
     else:
         assert torch.equal(dx, dx0)
+
+
+@pytest.mark.parametrize("M,kin,nsites", [(6384, 896, 3), (16400, 1024, 1)])
+def test_lora_da_slab_deterministic(dev, M, kin, nsites, monkeypatch):
+    """SLX_LORA_DA_SLAB: the slab-reduced dA is bit-identical run to run (fixed chunking and summation order) and
+    agrees with the atomics path to f32 summation-order rounding."""
+    monkeypatch.setattr(K, "LORA_DA_SLAB", True)
+    g = torch.Generator(device=dev).manual_seed(5)
+    x = torch.randn(M, kin, device=dev, generator=g).bfloat16()
+    dt = torch.randn(M, 32 * nsites, device=dev, generator=g)
+    As = [(torch.randn(32, kin, device=dev, generator=g) * 0.1).bfloat16() for _ in range(nsites)]
+    outs = []
+    for _ in range(2):
+        dAs = [torch.zeros(32, kin, device=dev) for _ in range(nsites)]
+        K.lora_bwd(x, dt, As, [None] * nsites, dAs)
+        outs.append(dAs)
+    monkeypatch.setattr(K, "LORA_DA_SLAB", False)
+    dAt = [torch.zeros(32, kin, device=dev) for _ in range(nsites)]
+    K.lora_bwd(x, dt, As, [None] * nsites, dAt)
+    for a, b, c in zip(*outs, dAt):
+        assert torch.equal(a, b)
+        assert ((a - c).norm() / c.norm()).item() < 1e-5
