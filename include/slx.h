@@ -377,6 +377,14 @@ int slx_dec_sync_ints(void);
 int slx_dec_attn_o(void* cache, int64_t ld, int Hq, int Hkv, const float* cos_tab, const float* sin_tab, int lmax,
                    float* ws, void* out, const slx_dec_state* st, const void* Wo, int64_t ldwo, int N, int K, float* X,
                    int* sync, slx_stream_t s);
+/* the attention split over keys WITHOUT an in-launch merge (SLX_DEC_SPLIT_NS workgroups per kv head, default 8, each
+ * at most 8 key blocks of 32: lmax <= 256 * ns; partials in ws, sized by slx_dec_attn_ws_floats), then the O GEMV +
+ * residual X[n] += W_o[n, :] . out, whose prologue merges the partials (two launches, no counters). out (optional, bf16
+ * [Hq*64]) receives the merged attention output. Replaces slx_dec_attn + the O GEMV (the o_proj call of
+ * Qwen2Attention inside llm.py:178-250's greedy loop).                                                          */
+int slx_dec_attn_o_split(void* cache, int64_t ld, int Hq, int Hkv, const float* cos_tab, const float* sin_tab,
+                         int lmax, float* ws, void* out, const slx_dec_state* st, const void* Wo, int64_t ldwo, int N,
+                         int K, float* X, slx_stream_t s);
 int slx_dec_attn_ws_floats(int Hq, int Hkv, int lmax);
 int slx_dec_attn(void* cache, int64_t ld, int Hq, int Hkv, const float* cos_tab, const float* sin_tab, int lmax,
                  float* ws, void* out, const slx_dec_state* st, slx_stream_t s);

@@ -2120,6 +2120,191 @@ int dec_attn_o_launch(void* cache, long ld, int Hq, int Hkv, const float* cos_ta
   return 0;
 }
 
+// ---- decode attention split over keys, merged by the O GEMV (slx_dec_attn_o_split) ----------------------------------
+// Grid (Hkv, ns), 4 waves: workgroup (g, sp) takes the 32-key blocks [sp*bpw, (sp+1)*bpw) of kv head g (bpw =
+// ceil(nb/ns) <= 8; wave w owns blocks w and w + 4) with the operand forms of dec_attn_mfma_body, and stores its
+// partial softmax state per query head, unnormalised: m (max of the log2-domain scores), l (sum of the bf16 P) and
+// o[64] = sum P v, at ws + (g*ns + sp) * G*66 (m[G], l[G], o[G][64]). No counter and no merge in this launch: the O
+// GEMV that follows reads every split's partial (the kernel boundary makes them visible) and merges them while its
+// weight rows are in flight, so the attention costs one short launch on Hkv*ns CUs instead of one CU per kv head
+// loading the whole cache.
+__global__ __launch_bounds__(256) void dec_attn_mfma_split_kernel(DecMfmaArgs a, float* ws) {
+  __shared__ __attribute__((aligned(16))) char Vl[256 * 128];  // this split's V rows, swizzled; then O^T partials
+  __shared__ __attribute__((aligned(16))) char Ql[32 * 128];
+  __shared__ float kpos[64];
+  __shared__ float red[4 * 32];
+  __shared__ float Mh[32], Lh[32];
+  if (a.st[2]) return;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hl = lane >> 5;
+  const int g = blockIdx.x, sp = blockIdx.y, ns = gridDim.y;
+  const int pos = a.st[0], L = pos + 1;
+  const int G = a.Hq / a.Hkv;
+  const int qn = a.Hq * 64, kn = a.Hkv * 64;
+  const int nb = (L + 31) >> 5;
+  const int bpw = (nb + ns - 1) / ns;
+  const int b0 = sp * bpw, b1 = min(nb, b0 + bpw);
+  float* part = ws + ((long)g * ns + sp) * (G * 66);
+  if (b0 >= b1) {  // empty split: neutral partial (m = -inf, l = 0, o = 0)
+    for (int i = tid; i < G * 66; i += 256) part[i] = i < G ? -INFINITY : 0.f;
+    return;
+  }
+  const int r0 = b0 * 32, nrow = min(L, b1 * 32) - r0;  // this split's cache rows [r0, r0 + nrow)
+  const bf16* kcol = a.cache + qn + g * 64;
+  const bf16* vcol = a.cache + qn + kn + g * 64;
+  bf16x8 kf[2][4];
+#pragma unroll
+  for (int bb = 0; bb < 2; ++bb) {
+    const int blk = b0 + w + 4 * bb;
+    const int key = min(blk * 32 + (lane & 31), L - 1);
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk)
+      kf[bb][kk] = blk < b1 ? *reinterpret_cast<const bf16x8*>(kcol + (long)key * a.ld + 16 * kk + 8 * hl) : bf16x8{};
+  }
+  uint4 vr[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int c = tid + 256 * i, row = c >> 3;
+    vr[i] = row < nrow ? *reinterpret_cast<const uint4*>(vcol + (long)(r0 + row) * a.ld + 8 * (c & 7))
+                       : make_uint4(0u, 0u, 0u, 0u);
+  }
+  bf16* prow = a.cache + (long)pos * a.ld;
+  const float* cs = a.cos + (long)pos * 32;
+  const float* sn = a.sin + (long)pos * 32;
+  for (int e = tid; e < 32 * 32; e += 256) {  // rotate_half RoPE of the G q heads into Ql (rows >= G: zeros)
+    const int h = e >> 5, j = e & 31;
+    float q0r = 0.f, q1r = 0.f;
+    if (h < G) {
+      const bf16* q = prow + (g * G + h) * 64;
+      const float q0 = (float)q[j], q1 = (float)q[j + 32];
+      q0r = q0 * cs[j] - q1 * sn[j];
+      q1r = q1 * cs[j] + q0 * sn[j];
+    }
+    *reinterpret_cast<bf16*>(Ql + sw_elem(h, j)) = (bf16)q0r;
+    *reinterpret_cast<bf16*>(Ql + sw_elem(h, j + 32)) = (bf16)q1r;
+  }
+  const bool has_pos = (pos >> 5) < b1;  // the last split with keys holds row pos
+  if (has_pos && w == 0 && lane < 32) {  // k of this token: rotated, written back once
+    const int j = lane;
+    bf16* k = prow + qn + g * 64;
+    const float k0 = (float)k[j], k1 = (float)k[j + 32];
+    const bf16 kr0 = (bf16)(k0 * cs[j] - k1 * sn[j]), kr1 = (bf16)(k1 * cs[j] + k0 * sn[j]);
+    k[j] = kr0;
+    k[j + 32] = kr1;
+    kpos[j] = (float)kr0;
+    kpos[j + 32] = (float)kr1;
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int c = tid + 256 * i, row = c >> 3;
+    if (row < (b1 - b0) * 32) *reinterpret_cast<uint4*>(Vl + sw_off(row, c & 7)) = vr[i];
+  }
+  __syncthreads();
+  if (has_pos) {
+#pragma unroll
+    for (int bb = 0; bb < 2; ++bb)
+      if (b0 + w + 4 * bb == (pos >> 5) && (lane & 31) == (pos & 31)) {
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) kf[bb][kk][j] = (bf16)kpos[16 * kk + 8 * hl + j];
+      }
+  }
+  bf16x8 qf[4];
+#pragma unroll
+  for (int kk = 0; kk < 4; ++kk) qf[kk] = row_frag(Ql, 0, kk, lane);
+  const float c = a.scale * LOG2E;
+  f32x16 s[2];
+  float mx = -INFINITY;
+#pragma unroll
+  for (int bb = 0; bb < 2; ++bb) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s[bb][r] = 0.f;
+    const int blk = b0 + w + 4 * bb;
+    if (blk < b1) {
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) s[bb] = mfma32(kf[bb][kk], qf[kk], s[bb]);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = blk * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
+        s[bb][r] = key < L ? s[bb][r] * c : -INFINITY;
+        mx = fmaxf(mx, s[bb][r]);
+      }
+    }
+  }
+  mx = half_swap_max(mx);
+  if (lane < 32) red[w * 32 + lane] = mx;
+  __syncthreads();
+  if (tid < 32) {
+    float m = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) m = fmaxf(m, red[i * 32 + tid]);
+    Mh[tid] = m;
+  }
+  __syncthreads();
+  const float M = Mh[lane & 31];
+  float ls = 0.f;
+  f32x16 o0, o1;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) { o0[r] = 0.f; o1[r] = 0.f; }
+#pragma unroll
+  for (int bb = 0; bb < 2; ++bb) {
+    const int blk = b0 + w + 4 * bb;
+    if (blk < b1) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        s[bb][r] = __builtin_amdgcn_exp2f(s[bb][r] - M);
+        ls += (float)(bf16)s[bb][r];  // the bf16 P the MFMA sums
+      }
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+        const bf16x8 pb = acc_frag(s[bb], st);
+        const int lrow = (blk - b0) * 32 + 16 * st;
+        o0 = mfma32(tr_frag(Vl, lrow, 0, lane), pb, o0);
+        o1 = mfma32(tr_frag(Vl, lrow, 32, lane), pb, o1);
+      }
+    }
+  }
+  {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(ls), __float_as_uint(ls), false, false);
+    ls = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  }
+  __syncthreads();  // every wave is done with Vl: reuse it for the O^T partials [4][G][64]
+  float* op = reinterpret_cast<float*>(Vl);
+  if (lane < 32) red[w * 32 + lane] = ls;
+  const int h = lane & 31;
+  if (h < G) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int d = 8 * (r >> 2) + 4 * hl + (r & 3);
+      op[(w * G + h) * 64 + d] = o0[r];
+      op[(w * G + h) * 64 + 32 + d] = o1[r];
+    }
+  }
+  __syncthreads();
+  if (tid < G) {
+    float l = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) l += red[i * 32 + tid];
+    part[tid] = Mh[tid];
+    part[G + tid] = l;
+  }
+  for (int e = tid; e < G * 64; e += 256) {
+    const int hh = e >> 6, d = e & 63;
+    float acc = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc += op[(i * G + hh) * 64 + d];
+    part[2 * G + e] = acc;
+  }
+}
+
+int dec_attn_split_launch(void* cache, long ld, int Hq, int Hkv, const float* cos_tab, const float* sin_tab,
+                          float* ws, int ns, const void* st, hipStream_t s) {
+  DecMfmaArgs a{(bf16*)cache, ld, Hq, Hkv, cos_tab, sin_tab, nullptr, (const int*)st, 0.125f};
+  hipLaunchKernelGGL(dec_attn_mfma_split_kernel, dim3(Hkv, ns), dim3(256), 0, s, a, ws);
+  SLX_LAUNCH_CHECK("slx_dec_attn_o_split(attention)");
+  return 0;
+}
+
 int dec_attn_mfma_launch(void* cache, long ld, int Hq, int Hkv, const float* cos_tab, const float* sin_tab, void* out,
                          const void* st, hipStream_t s) {
   constexpr int LDS = kDecKeys * 128 + 32 * 128 + (64 + 16 * 32 + 32 + 32) * 4;

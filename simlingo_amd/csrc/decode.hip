@@ -21,7 +21,10 @@
 namespace slx {
 
 constexpr int kKeyShards = 64;
-// attention.hip: the single-workgroup-per-kv-head MFMA form for caches of <= 1024 rows
+// attention.hip: the split MFMA form whose partials the O GEMV merges (slx_dec_attn_o_split), and the
+// single-workgroup-per-kv-head MFMA form for caches of <= 1024 rows
+int dec_attn_split_launch(void* cache, long ld, int Hq, int Hkv, const float* cos_tab, const float* sin_tab,
+                          float* ws, int ns, const void* st, hipStream_t s);
 int dec_attn_mfma_launch(void* cache, long ld, int Hq, int Hkv, const float* cos_tab, const float* sin_tab, void* out,
                          const void* st, hipStream_t s);
 int dec_attn_o_launch(void* cache, long ld, int Hq, int Hkv, const float* cos_tab, const float* sin_tab, void* out,
@@ -96,7 +99,11 @@ struct GemvArgs {
   int F;                                           // SWIGLU: up rows start at F (= N)
   const slx_dec_state* st;                         // may be null (prefill)
   long long* trace;                                // tools only (slx_dec_attn_set_trace): workgroup 0's phases
+  // MG (slx_dec_attn_o_split): x = the attention output merged from the split partials of dec_attn_mfma_split_kernel,
+  // part + (g*pns + s) * pG*66 = m[pG], l[pG], o[pG][64] of kv head g's split s; pout (optional) receives x (block 0)
+  const float* part; int pns; int pG; bf16* pout;
 };
+constexpr int kMergeMaxNs = 8;
 
 // One wave owns R output rows (SWIGLU: R gate + R up rows) of a row group; lane l holds 16-B chunks
 // l, l+64, ... (CPL per row) of each row. Load order is the latency schedule of a batch-1 layer: the
@@ -104,7 +111,7 @@ struct GemvArgs {
 // group's weight stream, and only then the scalar done-flag check, so the norm waits for x alone
 // (in-order vmcnt) and the flag / x / weight round trips all overlap.
 constexpr int kGemvXPer = 8;  // x elements per thread held in registers (K <= 2048 with X, K <= 8192 with xb)
-template <int MODE, int R, int CPL>
+template <int MODE, int R, int CPL, bool MG = false>
 __global__ __launch_bounds__(256) void dec_gemv_kernel(GemvArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   bf16* xs = reinterpret_cast<bf16*>(smem_raw);
@@ -113,7 +120,23 @@ __global__ __launch_bounds__(256) void dec_gemv_kernel(GemvArgs a) {
   const int K = a.K, nch = K >> 3;
   float xv[kGemvXPer], gv[kGemvXPer];
   uint4 xq[kGemvXPer / 2];
-  if (a.X) {
+  float pm[MG ? 4 : 1][kMergeMaxNs], pl[MG ? 4 : 1][kMergeMaxNs], po[MG ? 4 : 1][kMergeMaxNs];
+  if constexpr (MG) {  // every split's (m, l, o) of this thread's 4 elements e = tid + 256 i (head e / 64), loaded at once
+    const int stride = a.pG * 66;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int e = tid + 256 * i, h = e >> 6, d = e & 63;
+      const int g = h / a.pG, hh = h - g * a.pG;
+      const float* base = a.part + (long)g * a.pns * stride;
+#pragma unroll
+      for (int sp = 0; sp < kMergeMaxNs; ++sp) {
+        const bool ok = e < K && sp < a.pns;
+        pm[i][sp] = ok ? base[sp * stride + hh] : -INFINITY;
+        pl[i][sp] = ok ? base[sp * stride + a.pG + hh] : 0.f;
+        po[i][sp] = ok ? base[sp * stride + 2 * a.pG + hh * 64 + d] : 0.f;
+      }
+    }
+  } else if (a.X) {
 #pragma unroll
     for (int i = 0; i < kGemvXPer; ++i) {
       const int j = tid + 256 * i;
@@ -153,7 +176,27 @@ __global__ __launch_bounds__(256) void dec_gemv_kernel(GemvArgs a) {
   if (rg < nrg) issue(rg);
   if (t0) a.trace[32] = (long long)wall_clock64();
   if (a.st && a.st->done) return;
-  if (a.X) {
+  if constexpr (MG) {  // flash-decoding merge in the log2 domain of the split kernel's scores
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int e = tid + 256 * i;
+      float M = -INFINITY;
+#pragma unroll
+      for (int sp = 0; sp < kMergeMaxNs; ++sp) M = fmaxf(M, pm[i][sp]);
+      float den = 0.f, num = 0.f;
+#pragma unroll
+      for (int sp = 0; sp < kMergeMaxNs; ++sp) {
+        const float wgt = __builtin_amdgcn_exp2f(pm[i][sp] - M);
+        den = __builtin_fmaf(wgt, pl[i][sp], den);
+        num = __builtin_fmaf(wgt, po[i][sp], num);
+      }
+      if (e < K) {
+        const bf16 x = (bf16)(num / den);
+        xs[e] = x;
+        if (a.pout && blockIdx.x == 0) a.pout[e] = x;
+      }
+    }
+  } else if (a.X) {
     float ss = 0.f;
 #pragma unroll
     for (int i = 0; i < kGemvXPer; ++i) ss += xv[i] * xv[i];
@@ -580,6 +623,34 @@ int slx_dec_attn(void* cache, int64_t ld, int Hq, int Hkv, const float* cos_tab,
   SLX_CHECK_ARG(((uintptr_t)ws & 3) == 0, "slx_dec_attn: ws must be 4-B aligned (and zeroed once: it holds the counters)");
   hipLaunchKernelGGL(dec_attn_kernel, dim3(Hkv, ns), dim3(256), 0, (hipStream_t)s, a);
   SLX_LAUNCH_CHECK("slx_dec_attn");
+  return 0;
+}
+
+// split attention + O projection: dec_attn_mfma_split_kernel (Hkv x ns workgroups, partials in ws), then the O GEMV
+// (+ residual) merging the partials in its prologue (dec_gemv_kernel MG); ns = SLX_DEC_SPLIT_NS (default 8)
+int slx_dec_attn_o_split(void* cache, int64_t ld, int Hq, int Hkv, const float* cos_tab, const float* sin_tab,
+                         int lmax, float* ws, void* out, const slx_dec_state* st, const void* Wo, int64_t ldwo, int N,
+                         int K, float* X, slx_stream_t s) {
+  static const int ns_env = [] { const char* e = getenv("SLX_DEC_SPLIT_NS"); return e ? atoi(e) : 8; }();
+  const int ns = ns_env;
+  SLX_CHECK_ARG(cache && cos_tab && sin_tab && ws && st && Wo && X, "slx_dec_attn_o_split: null argument");
+  SLX_CHECK_ARG(ns >= 1 && ns <= kMergeMaxNs && lmax > 0 && lmax <= 256 * ns && ns <= slx_dec_attn_nsplit(lmax),
+                "slx_dec_attn_o_split: 1 <= ns <= %d splits of at most 8 key blocks (lmax %d, ns %d)", kMergeMaxNs,
+                lmax, ns);
+  SLX_CHECK_ARG(Hkv > 0 && Hq % Hkv == 0 && Hq / Hkv <= 32 && K == Hq * 64 && K <= 1024 && K % 8 == 0,
+                "slx_dec_attn_o_split: K == Hq * 64 <= 1024, Hq/Hkv <= 32");
+  SLX_CHECK_ARG(ld % 8 == 0 && ((uintptr_t)cache & 15) == 0 && ldwo % 8 == 0 && ((uintptr_t)Wo & 15) == 0 &&
+                ((uintptr_t)ws & 3) == 0, "slx_dec_attn_o_split: 16-B aligned cache and W_o rows");
+  int rc = dec_attn_split_launch(cache, ld, Hq, Hkv, cos_tab, sin_tab, ws, ns, st, (hipStream_t)s);
+  if (rc) return rc;
+  GemvArgs a;
+  memset(&a, 0, sizeof(a));
+  a.W = (const bf16*)Wo; a.ldw = ldwo; a.N = N; a.K = K; a.resid = X; a.st = st; a.F = N;
+  a.part = ws; a.pns = ns; a.pG = Hq / Hkv; a.pout = (bf16*)out;
+  const int groups = (N + 3) / 4;
+  hipLaunchKernelGGL((dec_gemv_kernel<GV_RESID, 1, 2, true>), dim3(groups < 2048 ? groups : 2048), dim3(256),
+                     (size_t)K * 2, (hipStream_t)s, a);
+  SLX_LAUNCH_CHECK("slx_dec_attn_o_split(O GEMV)");
   return 0;
 }
 

@@ -37,6 +37,9 @@ BF16, F32 = torch.bfloat16, torch.float32
 # attention + O projection as one launch (slx_dec_attn_o) instead of slx_dec_attn + the O GEMV: off by default, it
 # measured 35 us per token SLOWER (tools/fuse_o_ab.sh, profiles/round2_s3_fuse_o_ab.txt); SLX_DEC_FUSE_O=1 turns it on
 FUSE_O = os.environ.get("SLX_DEC_FUSE_O", "0") == "1"
+# the attention split over keys (Hkv x 8 workgroups) with its partials merged by the O GEMV's prologue
+# (slx_dec_attn_o_split) instead of one MFMA workgroup per kv head + the O GEMV; SLX_DEC_SPLIT_O=1 turns it on
+SPLIT_O = os.environ.get("SLX_DEC_SPLIT_O", "0") == "1"
 DEC_STORE_ROW, DEC_RESID, DEC_SWIGLU, DEC_ARGMAX = 0, 1, 2, 3
 
 
@@ -57,6 +60,8 @@ K.register("slx_dec_attn", [K.c_vp, K.c_i64, K.c_int, K.c_int, K.c_vp, K.c_vp, K
 K.register("slx_dec_sync_ints", [])
 K.register("slx_dec_attn_o", [K.c_vp, K.c_i64, K.c_int, K.c_int, K.c_vp, K.c_vp, K.c_int, K.c_vp, K.c_vp, K.c_vp, K.c_vp,
                               K.c_i64, K.c_int, K.c_int, K.c_vp, K.c_vp, K.c_vp])
+K.register("slx_dec_attn_o_split", [K.c_vp, K.c_i64, K.c_int, K.c_int, K.c_vp, K.c_vp, K.c_int, K.c_vp, K.c_vp, K.c_vp,
+                                    K.c_vp, K.c_i64, K.c_int, K.c_int, K.c_vp, K.c_vp])
 
 
 def _gemv_desc(mode, W, N, Kd, *, X=None, gamma=None, eps=0.0, xb=None, bias=None, out=None, out_ld=0, resid=None,
@@ -168,7 +173,13 @@ class GreedyDecoder:
         lib = K.lib()
         for i, (qkv, cache, o, gu, down) in enumerate(self._steps):
             K.check(lib.slx_dec_gemv(ctypes.byref(qkv), s), "slx_dec_gemv")
-            if FUSE_O:  # attention + O projection (+ residual): one launch for caches of <= 1024 rows
+            if SPLIT_O and self.max_len <= 2048:  # split attention, merged by the O GEMV (+ residual)
+                wo = self.Wm[i]["o_w"]
+                K.check(lib.slx_dec_attn_o_split(K.P(cache), cache.stride(0), cfg.llm_heads, cfg.llm_kv_heads,
+                                                 K.P(self.cos), K.P(self.sin), self.max_len, K.P(self.attn_ws), None,
+                                                 K.P(self.state), K.P(wo), wo.stride(0), cfg.llm_dim, self.qn,
+                                                 K.P(self.X), s), "slx_dec_attn_o_split")
+            elif FUSE_O:  # attention + O projection (+ residual): one launch for caches of <= 1024 rows
                 wo = self.Wm[i]["o_w"]
                 K.check(lib.slx_dec_attn_o(K.P(cache), cache.stride(0), cfg.llm_heads, cfg.llm_kv_heads, K.P(self.cos),
                                            K.P(self.sin), self.max_len, K.P(self.attn_ws), K.P(self.obuf),

@@ -1,7 +1,12 @@
 """SLX_LORA_DB_SIDE (engine.LORA_DB_SIDE): the gate/up LoRA B-gradient GEMM on a side stream beside the gate/up
 data-gradient GEMM. Same kernels, other stream: the step's gradients must match the single-stream step (to the
 f32 atomic-order rounding of the split-K B-gradient GEMM) at the full Qwen2 widths with LoRA dropout on, and the
-side stream must be joined before the layer's gradient group is marked done."""
+side stream must be joined before the layer's gradient group is marked done.
+
+The gate: per tensor, the side-stream step's difference from the single-stream step within 3x the run-to-run
+difference of two single-stream steps, or 2e-3 relative (f32 atomics in the split-K B-gradient GEMMs and the LoRA dA
+kernel sum in arrival order; through the bf16 backward that reaches ~1e-3 on layer 0's LoRA A). A missing join shows
+as O(1) differences."""
 import pytest
 import torch
 
@@ -32,28 +37,32 @@ def _step(dev, side, monkeypatch, pair_side=False):
     return out4.cpu(), {k: v.detach().float().cpu().clone() for k, v in eng.G.items()}, marks
 
 
+def _rel(a, b):
+    a, b = a.reshape(-1), b.reshape(-1)
+    return ((a - b).norm() / a.norm()).item() if a.norm() > 0 else float(b.norm() > 0)
+
+
+def _check(g0, g0b, g1):
+    worst = max(((_rel(g0[k], g1[k]), _rel(g0[k], g0b[k]), k) for k in g0))
+    print("worst (side vs single, single vs single, tensor):", worst)
+    for k in g0:
+        assert _rel(g0[k], g1[k]) <= max(3 * _rel(g0[k], g0b[k]), 2e-3), (k, _rel(g0[k], g1[k]), _rel(g0[k], g0b[k]))
+
+
 def test_lora_db_side_stream_matches(dev, monkeypatch):
     o0, g0, _ = _step(dev, False, monkeypatch)
+    _, g0b, _ = _step(dev, False, monkeypatch)
     o1, g1, marks = _step(dev, True, monkeypatch)
     assert torch.equal(o0, o1)
     assert all(n == 0 for g, n in marks if g.startswith("llm")), marks  # joined before each layer's group is done
-    for k in g0:
-        a, b = g0[k].reshape(-1), g1[k].reshape(-1)
-        if a.norm() == 0:
-            assert b.norm() == 0, k
-            continue
-        assert ((a - b).norm() / a.norm()).item() < 5e-4, k
+    _check(g0, g0b, g1)
 
 
 def test_pair_side_stream_matches(dev, monkeypatch):
     """SLX_PAIR_SIDE: the InternViT weight-gradient pairs on the side stream beside their data-gradient GEMMs give the
-    single-stream gradients (5e-4 relative: the qkv.w + proj.w pair's split-K atomics are order-dependent)."""
+    single-stream gradients (the gate of _check)."""
     o0, g0, _ = _step(dev, False, monkeypatch)
+    _, g0b, _ = _step(dev, False, monkeypatch)
     o1, g1, _ = _step(dev, False, monkeypatch, pair_side=True)
     assert torch.equal(o0, o1)
-    for k in g0:
-        a, b = g0[k].reshape(-1), g1[k].reshape(-1)
-        if a.norm() == 0:
-            assert b.norm() == 0, k
-            continue
-        assert ((a - b).norm() / a.norm()).item() < 5e-4, k
+    _check(g0, g0b, g1)
