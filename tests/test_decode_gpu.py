@@ -115,6 +115,18 @@ def test_driving_model_forward_surface(dev):
     assert lang1 == [] and sp1.shape == sp.shape
 
 
+def _check_rotated_k(krow, want, orig):
+    """The k row written back is rotate_half(k) rounded to bf16: equal to the torch rotation except where the kernel's
+    fused multiply-add (x0 c - x1 s in one rounding) lands on the other side of a bf16 rounding boundary, i.e. at most
+    one bf16 ulp on a couple of elements (seen on cancelling terms: 2.1839e-4 vs 2.1744e-4)."""
+    bad = (krow != want).nonzero().flatten()
+    assert bad.numel() <= 2, bad.tolist()
+    assert ((krow - want).abs() <= want.abs().clamp_min(krow.abs()) * 2.0 ** -7).all(), \
+        (bad.tolist(), krow[bad].tolist(), want[bad].tolist())
+    if not torch.equal(want, orig):
+        assert not torch.equal(krow, orig)  # rotated, not left as written by the q|k|v GEMV
+
+
 @pytest.mark.parametrize("pos", [0, 31, 300, 1000])
 def test_dec_attn_forms_vs_torch(dev, pos):
     """slx_dec_attn at the agent geometry (14 q / 2 kv heads): the single-workgroup MFMA form (caches <= 1024 rows) and
@@ -161,7 +173,8 @@ def test_dec_attn_forms_vs_torch(dev, pos):
         assert err <= 2e-2 * ref.abs().max().item() + 1e-3, (split, err)
         for g in range(Hkv):
             krow = cache[pos, Hq * 64 + 64 * g: Hq * 64 + 64 * (g + 1)].float()
-            assert torch.equal(krow, rope(c0[pos:pos + 1, Hq * 64 + 64 * g: Hq * 64 + 64 * (g + 1)])[0]), split
+            orig = c0[pos, Hq * 64 + 64 * g: Hq * 64 + 64 * (g + 1)]
+            _check_rotated_k(krow, rope(orig[None])[0], orig)
 
 
 @pytest.mark.parametrize("pos,split", [(300, 0), (1000, 0), (300, 1)])
@@ -250,7 +263,9 @@ def test_dec_attn_o_split_vs_torch(dev, pos):
         assert (X - Xref).abs().max().item() <= 1e-4 * Xref.abs().max().item() + 1e-5
         for g in range(Hkv):
             krow = cache[pos, Hq * 64 + 64 * g: Hq * 64 + 64 * (g + 1)].float()
-            assert torch.equal(krow, rope(c0[pos:pos + 1, Hq * 64 + 64 * g: Hq * 64 + 64 * (g + 1)])[0])
+            orig = c0[pos, Hq * 64 + 64 * g: Hq * 64 + 64 * (g + 1)]
+            want = rope(orig[None])[0]
+            _check_rotated_k(krow, want, orig)
     # against the single-workgroup form + the O GEMV (different summation order: bf16-level agreement)
     c1, X1, o1 = cache0.clone(), X0.clone(), torch.empty(Hq * 64, dtype=torch.bfloat16, device=dev)
     K.check(lib.slx_dec_attn(K.P(c1), ld, Hq, Hkv, K.P(cos), K.P(sin), lmax, K.P(ws), K.P(o1), K.P(st),
