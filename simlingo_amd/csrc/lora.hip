@@ -375,16 +375,30 @@ __global__ __launch_bounds__(256, 2) void lora_da_kernel(LoraBwdArgs a) {
     }
 }
 
-// dA_j[r][k] += sum over the row chunks c (in order) of part[c][j][r][k]: one thread per 4 consecutive k
+// dA_j[r][k] += sum over the row chunks c of part[c][j][r][k]: 16 lanes per 4 consecutive k, lane t loading chunks
+// t, t + 16, ... (at most kDaRedPer, all issued before the first add) and summing them in chunk order, then a fixed
+// xor-butterfly over the 16 lanes (a + b == b + a, so every lane ends with the same total): deterministic, and one load
+// round trip instead of nchunk dependent ones
+constexpr int kDaRedLanes = 16, kDaRedPer = 12;
 __global__ __launch_bounds__(256) void lora_da_reduce_kernel(LoraBwdArgs a, int nchunk) {
   const long per = (long)a.nsites * 32 * a.Kin;
-  const long i4 = ((long)blockIdx.x * 256 + threadIdx.x) * 4;
-  if (i4 >= per) return;
-  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-  for (int c = 0; c < nchunk; ++c) {
-    const float4 v = *reinterpret_cast<const float4*>(a.dA_part + c * per + i4);
-    s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+  const long i4 = ((long)blockIdx.x * (256 / kDaRedLanes) + (threadIdx.x / kDaRedLanes)) * 4;
+  const int t = threadIdx.x % kDaRedLanes;
+  const bool ok = i4 < per;
+  float4 v[kDaRedPer];
+#pragma unroll
+  for (int k = 0; k < kDaRedPer; ++k) {
+    const int c = t + kDaRedLanes * k;
+    v[k] = (ok && c < nchunk) ? *reinterpret_cast<const float4*>(a.dA_part + c * per + i4) : make_float4(0.f, 0.f, 0.f, 0.f);
   }
+  float4 s = v[0];
+#pragma unroll
+  for (int k = 1; k < kDaRedPer; ++k) { s.x += v[k].x; s.y += v[k].y; s.z += v[k].z; s.w += v[k].w; }
+#pragma unroll
+  for (int m = 1; m < kDaRedLanes; m <<= 1) {
+    s.x += __shfl_xor(s.x, m); s.y += __shfl_xor(s.y, m); s.z += __shfl_xor(s.z, m); s.w += __shfl_xor(s.w, m);
+  }
+  if (!ok || t != 0) return;
   const int j = (int)(i4 / (32L * a.Kin));
   float* d = a.dA[j] + (i4 - (long)j * 32 * a.Kin);
   float4 o = *reinterpret_cast<float4*>(d);
@@ -561,8 +575,9 @@ static void launch_bwd_t(const LoraBwdArgs& a, dim3 grid, hipStream_t st) {
   if (a.dA[0]) {
     hipLaunchKernelGGL((lora_da_kernel<NS, DTB>), grid, dim3(256), 0, st, a);
     if (a.dA_part) {
-      const long per4 = (long)NS * 32 * a.Kin / 4;
-      hipLaunchKernelGGL(lora_da_reduce_kernel, dim3((unsigned)((per4 + 255) / 256)), dim3(256), 0, st, a, (int)grid.y);
+      const long per4 = (long)NS * 32 * a.Kin / 4, per_block = 256 / kDaRedLanes;
+      hipLaunchKernelGGL(lora_da_reduce_kernel, dim3((unsigned)((per4 + per_block - 1) / per_block)), dim3(256), 0, st, a,
+                         (int)grid.y);
     }
   }
   // column groups per 32-row tile: 200 row tiles alone (Qwen2, M = 6384) under-fill the 256 CUs
@@ -639,6 +654,9 @@ static int lora_bwd_impl(const slx_lora_bwd_desc* d, float* ws, int64_t ws_float
                 "slx_lora_bwd_ws: workspace holds %lld floats, slx_lora_bwd_ws_floats asks for %lld", (long long)ws_floats,
                 (long long)slx_lora_bwd_ws_floats(d->M, d->Kin, d->nsites));
   a.dA_part = (ws && d->dA[0]) ? ws : nullptr;
+  SLX_CHECK_ARG(!a.dA_part || (long)grid.y <= (long)kDaRedLanes * kDaRedPer,
+                "slx_lora_bwd_ws: %u row chunks, at most %d (SLX_LORA_DA_BLOCKS too high for M)", grid.y,
+                kDaRedLanes * kDaRedPer);
   hipStream_t st = (hipStream_t)stream;
   switch (d->nsites) {
     case 1: launch_bwd<1>(a, grid, st); break;
