@@ -236,13 +236,31 @@ typedef struct {
   void* dx_bf16; int64_t lddx_bf16;   /* optional bf16 [M, Kin] output instead of updating dx in place */
   float p;
   int dt_bf16;                        /* 1: dt points to bf16 rows (lddt % 8 == 0), e.g. the bf16 dgrad GEMM output */
+  void* dt_bf16_out; int64_t ld_dt_bf16_out;  /* optional bf16 [M, 32*nsites]: the dx term also writes dT as bf16 here
+                                                 (the operand slx_lora_grad takes) */
 } slx_lora_bwd_desc;
 int slx_lora_bwd(const slx_lora_bwd_desc* d, slx_stream_t stream);
 /* The same with dA summed without atomics: each (column block, row chunk) block stores its f32 partial into ws and a
- * second launch adds the row chunks' partials into dA_j in chunk order (deterministic). ws_floats must be at least
- * slx_lora_bwd_ws_floats(M, Kin, nsites); a smaller ws falls back to slx_lora_bwd's atomics. */
+ * second launch adds the row chunks' partials into dA_j in a fixed order (deterministic). ws_floats must be at least
+ * slx_lora_bwd_ws_floats(M, Kin, nsites) (a smaller ws is an argument error). */
 int64_t slx_lora_bwd_ws_floats(int64_t M, int Kin, int nsites);
 int slx_lora_bwd_ws(const slx_lora_bwd_desc* d, float* ws, int64_t ws_floats, slx_stream_t stream);
+/* The LoRA parameter gradients of one layer group in ONE launch: per job, out_j += alpha * t_j^T . x_j' over the M rows,
+ * where x_j' = x (B gradients: x = the site's output gradient dy [M][n], t = its forward down-projection t_j, alpha = s,
+ * out_nr = 1: out is the [n][32] B gradient) or x_j' = bf16(x / (1-p)) & keep_j (A gradients: x = the site input,
+ * t = dT_j, alpha = 1, out_nr = 0: out is the [32][n] A gradient; up to 3 sites share one x). Replaces the dB
+ * split-K GEMMs and the dA part of slx_lora_bwd (peft lora_B / lora_A weight gradients, llm.py:106-119).
+ * n % 128 == 0, ldx % 8, x 16-B aligned; t bf16 [M][32*nsites], 16-B aligned, ldt % 8 (t_bf16 must be 1: a dT
+ * that lives in f32 comes as bf16 from slx_lora_bwd's dt_bf16_out); at most 12 jobs.                              */
+typedef struct slx_lora_grad_job {
+  const void* x; int64_t ldx; int n;
+  const void* t; int64_t ldt; int t_bf16;
+  int nsites;
+  const uint32_t* bits[3]; int64_t ldbits; float p;
+  float alpha;
+  float* out[3]; int out_nr;
+} slx_lora_grad_job;
+int slx_lora_grad(const slx_lora_grad_job* jobs, int njobs, int64_t M, slx_stream_t s);
 
 /* small strided f32 GEMM (driving heads adaptors.py:113-132, WaypointInputAdaptor :80)        */
 enum { SLX_ACT_NONE = 0, SLX_ACT_RELU = 1, SLX_ACT_SILU = 2 };

@@ -222,6 +222,7 @@ struct LoraBwdArgs {
   int mchunk;
   int dt_bf16;    // dt holds bf16 rows
   float* dA_part; // non-null: per-row-chunk partials [nchunk][nsites][32][Kin] (plain stores) instead of atomics
+  bf16* dtb; long lddtb;  // non-null: the dx kernel also writes the bf16 dT rows it converts (slx_lora_grad's operand)
 };
 
 __device__ __forceinline__ int la_sw(int row, int chunk) {
@@ -445,6 +446,13 @@ __global__ __launch_bounds__(512) void lora_dx_kernel(LoraBwdArgs a) {
         tb[j][kb][4] = (bf16)f1.x; tb[j][kb][5] = (bf16)f1.y; tb[j][kb][6] = (bf16)f1.z; tb[j][kb][7] = (bf16)f1.w;
       }
     }
+  if (a.dtb && w == 0 && rok && blockIdx.y == 0) {  // bf16 dT for slx_lora_grad: one wave of the row tile writes it
+#pragma unroll
+    for (int j = 0; j < NS; ++j)
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+        *reinterpret_cast<bf16x8*>(a.dtb + (long)row * a.lddtb + 32 * j + 16 * kb + 8 * h) = tb[j][kb];
+  }
   auto load = [&](int ct, DxRegs<NS>& R) {
 #pragma unroll
     for (int j = 0; j < NS; ++j) {
@@ -502,6 +510,179 @@ __global__ __launch_bounds__(512) void lora_dx_kernel(LoraBwdArgs a) {
     if (!more) break;
     if (ct + 2 * cs < nct) load(ct + 2 * cs, R0);
     process(ct + cs, R1);
+  }
+}
+
+// ---- LoRA parameter gradients of a layer in one launch (slx_lora_grad) -------------------------------------------
+// out_j (+)= alpha * T_j^T . X_j' for a list of jobs, X_j' = X (dB: X = dy, T = t) or bf16(X / (1-p)) & keep_j (dA: X = the
+// site input, T = dT): the skinny [32 x N] = [32 x M] . [M x N] products whose standalone launches (split-K GEMMs for
+// dB, lora_da_kernel for dA) stream their big operand at ~1-2 TB/s because every block's row range is only one or two
+// 64-row sub-chunks deep, so each block waits one full memory latency per sub-chunk. Here all the products of a layer
+// group are work items (job, 128-column block, row chunk) of one persistent launch sized to one item per block slot;
+// each item walks its row chunk with two 64-row sub-chunks in flight (register sets R0 / R1) behind the one being
+// multiplied, and ends with one set of f32 atomics (the [n][32] B-gradient layout through an LDS transpose, so the
+// atomics stay coalesced). Operand staging, masks and MFMA forms are lora_da_kernel's.
+constexpr int kLgMaxJobs = 12;
+struct LgJob {
+  const bf16* X; long ldx; int N;
+  const bf16* T; long ldt;
+  int ns;
+  const uint32_t* bits[3]; long ldbits;
+  float sc;      // 1 / (1 - p) (dropout scale of X, applied with the mask)
+  float alpha;   // scale of the f32 product
+  float* out[3]; int nr;
+  int ncb, kch, item0;
+};
+struct LgArgs { int M, njobs, nitems; LgJob j[kLgMaxJobs]; };
+
+__device__ __forceinline__ LgJob lg_job(const LgArgs& a, int jb) {
+  switch (jb) {  // static indices only: a dynamic index into the kernel-argument array would copy it to scratch
+    case 0: return a.j[0];
+    case 1: return a.j[1];
+    case 2: return a.j[2];
+    case 3: return a.j[3];
+    case 4: return a.j[4];
+    case 5: return a.j[5];
+    case 6: return a.j[6];
+    case 7: return a.j[7];
+    case 8: return a.j[8];
+    case 9: return a.j[9];
+    case 10: return a.j[10];
+    default: return a.j[11];
+  }
+}
+
+struct LgRegs {
+  uint4 rx[4];
+  uint4 rt[4];
+  uint32_t rm[3];
+};
+
+__global__ __launch_bounds__(256, 2) void lora_grad_kernel(LgArgs a) {
+  __shared__ __attribute__((aligned(16))) char smem[8 * 8192];  // X: 3 sites x 2 panels | T: 2 panels
+  char* ts = smem + 6 * 8192;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
+  const int srow = tid >> 2;
+  for (int item = blockIdx.x; item < a.nitems; item += gridDim.x) {
+    int jb = 0;
+#pragma unroll
+    for (int q = 1; q < kLgMaxJobs; ++q) jb += (q < a.njobs && item >= lg_job(a, q).item0) ? 1 : 0;
+    const LgJob J = lg_job(a, jb);
+    const int li = item - J.item0, cb = li % J.ncb, kc = li / J.ncb;
+    const int c0 = cb * 128, mb = kc * J.kch, me = min(a.M, mb + J.kch);
+    const int mycol = c0 + 32 * w + (lane & 31);
+    const bool drop = J.bits[0] != nullptr;
+    const int ns = J.ns;
+    f32x16 acc[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[j][i] = 0.f;
+    auto load = [&](int mm, LgRegs& R) {
+      const int gm = mm + srow;
+      const bool ok = gm < me;
+#pragma unroll
+      for (int c4 = 0; c4 < 4; ++c4) {
+        const int c = (tid & 3) * 4 + c4;
+        R.rx[c4] = ok ? *reinterpret_cast<const uint4*>(J.X + (long)gm * J.ldx + c0 + 8 * c) : make_uint4(0u, 0u, 0u, 0u);
+        if (8 * c < 32 * ns)
+          R.rt[c4] = ok ? *reinterpret_cast<const uint4*>(J.T + (long)gm * J.ldt + 8 * c) : make_uint4(0u, 0u, 0u, 0u);
+      }
+#pragma unroll
+      for (int j = 0; j < 3; ++j)
+        R.rm[j] = (drop && j < ns) ? (ok ? J.bits[j][(long)gm * J.ldbits + (c0 >> 5) + (tid & 3)] : 0u) : 0xFFFFFFFFu;
+    };
+    auto commit = [&](const LgRegs& R) {
+#pragma unroll
+      for (int c4 = 0; c4 < 4; ++c4) {
+        const int c = (tid & 3) * 4 + c4;
+        uint4 v = R.rx[c4];
+        uint32_t* u = reinterpret_cast<uint32_t*>(&v);
+        if (drop) {  // bf16(x / (1-p)), the rounding of peft's dropout output
+#pragma unroll
+          for (int d = 0; d < 4; ++d) {
+            bf16x2 o;
+            o[0] = (bf16)(__uint_as_float(u[d] << 16) * J.sc);
+            o[1] = (bf16)(__uint_as_float(u[d] & 0xFFFF0000u) * J.sc);
+            u[d] = __builtin_bit_cast(uint32_t, o);
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          if (j < ns) {
+            uint4 m = v;
+            if (drop) {
+              uint32_t* mu = reinterpret_cast<uint32_t*>(&m);
+#pragma unroll
+              for (int d = 0; d < 4; ++d) {
+                const uint32_t lo = (uint32_t)__builtin_amdgcn_sbfe((int)R.rm[j], 8 * c4 + 2 * d, 1);
+                const uint32_t hi = (uint32_t)__builtin_amdgcn_sbfe((int)R.rm[j], 8 * c4 + 2 * d + 1, 1);
+                mu[d] &= (lo & 0xFFFFu) | (hi & 0xFFFF0000u);
+              }
+            }
+            *reinterpret_cast<uint4*>(smem + (2 * j + (c >> 3)) * 8192 + la_sw(srow, c & 7)) = m;
+          }
+        }
+        if (8 * c < 32 * ns) *reinterpret_cast<uint4*>(ts + (c >> 3) * 8192 + la_sw(srow, c & 7)) = R.rt[c4];
+      }
+    };
+    auto mma = [&]() {
+#pragma unroll
+      for (int ms = 0; ms < 4; ++ms)
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+          if (j < ns) {
+            const bf16x8 xm = la_tr(smem + (2 * j + (w >> 1)) * 8192, 16 * ms, 32 * (w & 1), lane);
+            const bf16x8 ta = la_tr(ts + ((32 * j) >> 6) * 8192, 16 * ms, (32 * j) & 63, lane);
+            acc[j] = mfma32x32(ta, xm, acc[j]);
+          }
+    };
+    const int nsub = (me - mb + 63) / 64;
+    LgRegs R0, R1;
+    if (nsub > 0) load(mb, R0);
+    if (nsub > 1) load(mb + 64, R1);
+    for (int sb = 0; sb < nsub; sb += 2) {
+      commit(R0);
+      __syncthreads();
+      if (sb + 2 < nsub) load(mb + 64 * (sb + 2), R0);
+      mma();
+      __syncthreads();
+      if (sb + 1 >= nsub) break;
+      commit(R1);
+      __syncthreads();
+      if (sb + 3 < nsub) load(mb + 64 * (sb + 3), R1);
+      mma();
+      __syncthreads();
+    }
+    if (!J.nr) {
+#pragma unroll
+      for (int j = 0; j < 3; ++j)
+        if (j < ns) {
+#pragma unroll
+          for (int g = 0; g < 16; ++g) {
+            const int rr = (g & 3) + 8 * (g >> 2) + 4 * h;
+            atomicAdd(J.out[j] + (long)rr * J.N + mycol, J.alpha * acc[j][g]);
+          }
+        }
+    } else {  // out[n][32]: transpose through LDS ([32][129] f32), then 32 consecutive r per 32 lanes
+      float* red = reinterpret_cast<float*>(smem);
+#pragma unroll
+      for (int j = 0; j < 3; ++j)
+        if (j < ns) {
+#pragma unroll
+          for (int g = 0; g < 16; ++g) {
+            const int rr = (g & 3) + 8 * (g >> 2) + 4 * h;
+            red[rr * 129 + 32 * w + (lane & 31)] = acc[j][g];
+          }
+          __syncthreads();
+          for (int e = tid; e < 32 * 128; e += 256) {
+            const int col = e >> 5, r = e & 31;
+            atomicAdd(J.out[j] + (long)(c0 + col) * 32 + r, J.alpha * red[r * 129 + col]);
+          }
+          __syncthreads();
+        }
+    }
+    __syncthreads();  // the next item overwrites the panels
   }
 }
 
@@ -646,6 +827,9 @@ static int lora_bwd_impl(const slx_lora_bwd_desc* d, float* ws, int64_t ws_float
   a.ldbits = d->ldbits;
   a.dx = d->dx; a.lddx = d->lddx;
   a.dxb = (bf16*)d->dx_bf16; a.lddxb = d->lddx_bf16;
+  a.dtb = (bf16*)d->dt_bf16_out; a.lddtb = d->ld_dt_bf16_out;
+  SLX_CHECK_ARG(!a.dtb || (d->dx && a.lddtb % 8 == 0 && ((uintptr_t)a.dtb & 15) == 0),
+                "slx_lora_bwd: dt_bf16_out needs the dx term (its kernel converts dT), 16-B aligned rows");
   a.sc = 1.0f / (1.0f - d->p);
   const int cb = d->Kin / 128;
   a.mchunk = lora_da_mchunk(d->M, d->Kin);
@@ -665,5 +849,58 @@ static int lora_bwd_impl(const slx_lora_bwd_desc* d, float* ws, int64_t ws_float
     default: launch_bwd<4>(a, grid, st); break;
   }
   SLX_LAUNCH_CHECK("slx_lora_bwd");
+  return 0;
+}
+
+extern "C" int slx_lora_grad(const slx_lora_grad_job* jobs, int njobs, int64_t M, slx_stream_t stream) {
+  SLX_CHECK_ARG(jobs && njobs >= 1 && njobs <= kLgMaxJobs, "slx_lora_grad: 1..%d jobs", kLgMaxJobs);
+  SLX_CHECK_ARG(M >= 0 && M < (1LL << 31), "slx_lora_grad: M out of range");
+  if (M == 0) return 0;
+  LgArgs a;
+  memset(&a, 0, sizeof(a));
+  a.M = (int)M; a.njobs = njobs;
+  long ncb_sum = 0;
+  for (int i = 0; i < njobs; ++i) {
+    const slx_lora_grad_job& d = jobs[i];
+    SLX_CHECK_ARG(d.x && d.t && d.nsites >= 1 && d.nsites <= 3 && d.n > 0 && d.n % 128 == 0 && d.ldx % 8 == 0 &&
+                  ((uintptr_t)d.x & 15) == 0, "slx_lora_grad: job %d needs x (16-B aligned, ldx %% 8), n %% 128, 1..3 sites", i);
+    SLX_CHECK_ARG(d.t_bf16 == 1 && d.ldt % 8 == 0 && ((uintptr_t)d.t & 15) == 0,
+                  "slx_lora_grad: job %d: t bf16 (t_bf16 = 1), 16-B aligned, ldt %% 8", i);
+    SLX_CHECK_ARG(d.p >= 0.f && d.p < 1.f && (d.p == 0.f || (d.bits[0] && d.ldbits >= d.n / 32)),
+                  "slx_lora_grad: job %d: 0 <= p < 1, p > 0 needs keep bits", i);
+    LgJob& J = a.j[i];
+    J.X = (const bf16*)d.x; J.ldx = d.ldx; J.N = d.n;
+    J.T = (const bf16*)d.t; J.ldt = d.ldt;
+    J.ns = d.nsites;
+    for (int j = 0; j < 3; ++j) {
+      SLX_CHECK_ARG(j >= d.nsites || d.out[j], "slx_lora_grad: job %d site %d has no output", i, j);
+      SLX_CHECK_ARG(j >= d.nsites || d.p == 0.f || d.bits[j], "slx_lora_grad: job %d site %d has no keep bits", i, j);
+      J.out[j] = j < d.nsites ? d.out[j] : nullptr;
+      J.bits[j] = (d.p > 0.f && j < d.nsites) ? d.bits[j] : nullptr;
+    }
+    J.ldbits = d.ldbits;
+    J.sc = 1.0f / (1.0f - d.p);
+    J.alpha = d.alpha;
+    J.nr = d.out_nr;
+    J.ncb = d.n / 128;
+    ncb_sum += J.ncb;
+  }
+  // row chunks: about one item per block slot (2 per CU), each chunk a whole number of 64-row sub-chunks
+  static const int slots = [] { const char* e = getenv("SLX_LORA_GRAD_ITEMS"); return e ? atoi(e) : 512; }();
+  const long nsub = (M + 63) / 64;
+  long nkc = (slots + ncb_sum - 1) / ncb_sum;
+  nkc = nkc < 1 ? 1 : (nkc > nsub ? nsub : nkc);
+  const int kch = (int)(((nsub + nkc - 1) / nkc) * 64);
+  nkc = (M + kch - 1) / kch;
+  int items = 0;
+  for (int i = 0; i < njobs; ++i) {
+    a.j[i].kch = kch;
+    a.j[i].item0 = items;
+    items += a.j[i].ncb * (int)nkc;
+  }
+  a.nitems = items;
+  const int grid = items < 512 ? items : 512;
+  hipLaunchKernelGGL(lora_grad_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, a);
+  SLX_LAUNCH_CHECK("slx_lora_grad");
   return 0;
 }

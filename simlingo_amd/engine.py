@@ -53,6 +53,10 @@ LORA_DB_SIDE = os.environ.get("SLX_LORA_DB_SIDE", "0") == "1"
 # (fc2.w + fc1.w beside the fc1 dgrad, proj.w + qkv.w beside the qkv dgrad); the compute stream waits for it before
 # the next LayerNorm backward, which rewrites the g buffer the pair reads.
 PAIR_SIDE = os.environ.get("SLX_PAIR_SIDE", "0") == "1"
+# SLX_LORA_GRAD_GROUP=1: every LoRA parameter gradient (dB_j = s dy_j^T t_j, dA_j = dT_j^T drop_j(x)) of a layer half
+# (the MLP sites, then the attention sites) is deferred to ONE slx_lora_grad launch issued before the norm backward that
+# overwrites their shared operand, instead of a split-K GEMM per B gradient and a dA pass per site group
+LORA_GRAD_GROUP = os.environ.get("SLX_LORA_GRAD_GROUP", "0") == "1"
 ALIGN = 64  # elements; keeps every parameter view 256-B aligned
 
 
@@ -146,6 +150,7 @@ class VLAEngine(EngineOps):
         self._build_transposes()
         self._side = None          # side stream of the LORA_DB_SIDE overlap, and its pending completion events
         self._side_pending = []
+        self._lg_jobs = []         # deferred slx_lora_grad jobs of the current layer half (LORA_GRAD_GROUP)
         self.probe_site = None     # name of a call site to bracket with HIP events (bench roofline)
         self.probe_events = []
 
@@ -651,7 +656,7 @@ class VLAEngine(EngineOps):
                        K.stream_ptr())
             del dax
             dh2x = self._e(Ml, d + Pg, dtype=F32)
-            side = lora and LORA_DB_SIDE and not self.precise
+            side = lora and LORA_DB_SIDE and not self.precise and not LORA_GRAD_GROUP
             if side:
                 ev_dgu = torch.cuda.Event()
                 ev_dgu.record()
@@ -671,6 +676,7 @@ class VLAEngine(EngineOps):
                 self._lora_bwd(i, ("gate", "up"), [dgu[:, :Fl], dgu[:, Fl:]], h2x[:, d:], h2x[:, :d], dh2x[:, d:],
                                dh2x[:, :d], sv, skip_db=side)
             del dgu
+            self._lg_flush(Ml)  # before dxb (the down site's dy) is overwritten
             K.norm_bwd(Ls["n2"], dh2x, dX, dx_accumulate=True, dx_bf16=dxb)
             # o projection
             dox = self._e(Ml, qn + Po, dtype=F32)
@@ -691,6 +697,7 @@ class VLAEngine(EngineOps):
             if lora:
                 self._lora_bwd(i, ("q", "k", "v"), [dqkv[:, :qn], dqkv[:, qn:qn + kn], dqkv[:, qn + kn:]], hx[:, d:],
                                hx[:, :d], dhx[:, d:], dhx[:, :d], sv)
+            self._lg_flush(Ml)  # before dxb (the o site's dy) is overwritten
             K.norm_bwd(Ls["n1"], dhx, dX, dx_accumulate=True, dx_bf16=dxb)
             del dqkv, dhx, dh2x
             if lora:
@@ -878,6 +885,9 @@ class VLAEngine(EngineOps):
         keep = sv["llm"][i]["lora"]
         bits = [keep[site] for site in sites]
         As = [self.cat[i]["axfrag." + site] for site in sites]
+        if LORA_GRAD_GROUP and not self.precise:
+            self._lora_bwd_grouped(i, sites, dys, tx, x, dtx, dx, swiglu, dx_bf16, drop, bits, As, sv["step_seed"])
+            return
         if not skip_db:
             self._lora_db(i, sites, dys, tx)
         # dA and the dx term in one launch. (Running the parameter-only part - dB GEMMs, dA - on a side stream was
@@ -899,6 +909,39 @@ class VLAEngine(EngineOps):
                    seed=lora_site_seed(sv["step_seed"], i, LORA_SITES.index("down")), drop_p=drop,
                    ldmask=x.shape[1], maskbits=bits[0], variant=SWIGLU_BWD_VARIANT)
 
+
+    def _lora_bwd_grouped(self, i, sites, dys, tx, x, dtx, dx, swiglu, dx_bf16, drop, bits, As, step_seed):
+        """LORA_GRAD_GROUP: the dx term (or the down site's SwiGLU epilogue) now; dB_j and dA_j as slx_lora_grad jobs
+        deferred to the layer half's _lg_flush. A dT that lives in f32 (the fused dgrad GEMM's extra columns) is
+        written as bf16 by the dx kernel, the rounding the dA pass applied to it."""
+        cfg = self.cfg
+        r = cfg.lora_r
+        M = x.shape[0]
+        for j, site in enumerate(sites):
+            self._lg_jobs.append(dict(x=dys[j], t=tx[:, r * j:r * (j + 1)], outs=[self.G[f"llm.{i}.lora.{site}.b"]],
+                                      out_nr=True, alpha=float(cfg.lora_scale)))
+        if dtx.dtype == torch.bfloat16:
+            dTb = dtx
+        else:
+            dTb = self._buf(("lg_dT",) + tuple(sites), M, r * len(sites), dtype=torch.bfloat16)
+        self._lg_jobs.append(dict(x=x, t=dTb, outs=[self.G[f"llm.{i}.lora.{site}.a"] for site in sites], out_nr=False,
+                                  alpha=1.0, p=drop, bits=bits))
+        if swiglu is None:
+            K.lora_bwd(x, dtx, As, bits, None, dx=dx, dx_bf16=dx_bf16, p=drop, packed=True,
+                       dt_out=None if dTb is dtx else dTb)
+            return
+        assert dTb is dtx, "the SwiGLU path takes dT from the bf16 dgrad output"
+        gu, dgu = swiglu
+        F = gu.shape[1] // 2
+        K.gemm(dtx, self.cat[i]["apad.down"], dgu, M, F, 64, K.GEMM_NN, dtx.stride(0), x.shape[1], dgu.stride(0),
+               epi=K.EPI_DROPMASK_SWIGLU, resid=dx, ldr=dx.stride(0), aux=gu, ldaux=gu.stride(0),
+               seed=lora_site_seed(step_seed, i, LORA_SITES.index("down")), drop_p=drop,
+               ldmask=x.shape[1], maskbits=bits[0], variant=SWIGLU_BWD_VARIANT)
+
+    def _lg_flush(self, M):
+        if self._lg_jobs:
+            K.lora_grad(self._lg_jobs, M)
+            self._lg_jobs = []
 
     # ==========================================================================================
     # optimizer

@@ -282,6 +282,14 @@ class LoraBwdDesc(ctypes.Structure):
         ("x", c_vp), ("ldx", c_i64), ("M", c_i64), ("Kin", c_int), ("r", c_int), ("nsites", c_int),
         ("dt", c_vp), ("lddt", c_i64), ("A", c_vp * 4), ("bits", c_vp * 4), ("ldbits", c_i64), ("dA", c_vp * 4),
         ("dx", c_vp), ("lddx", c_i64), ("dx_bf16", c_vp), ("lddx_bf16", c_i64), ("p", c_float), ("dt_bf16", c_int),
+        ("dt_bf16_out", c_vp), ("ld_dt_bf16_out", c_i64),
+    ]
+
+
+class LoraGradJob(ctypes.Structure):
+    _fields_ = [
+        ("x", c_vp), ("ldx", c_i64), ("n", c_int), ("t", c_vp), ("ldt", c_i64), ("t_bf16", c_int), ("nsites", c_int),
+        ("bits", c_vp * 3), ("ldbits", c_i64), ("p", c_float), ("alpha", c_float), ("out", c_vp * 3), ("out_nr", c_int),
     ]
 
 
@@ -293,6 +301,7 @@ for _n, _a in {
     "slx_lora_bwd": [ctypes.POINTER(LoraBwdDesc), _vp],
     "slx_lora_bwd_ws": [ctypes.POINTER(LoraBwdDesc), _vp, _I, _vp],
     "slx_lora_bwd_ws_floats": [_I, _i, _i],  # int64 result, < 2^31 at every shape used (restype int)
+    "slx_lora_grad": [ctypes.POINTER(LoraGradJob), _i, _I, _vp],
     "slx_dropout_bits": [ctypes.POINTER(DropoutBitsDesc), _vp],
     "slx_attn_bwd": [ctypes.POINTER(AttnDesc), ctypes.POINTER(AttnBwdDesc), _vp],
     "slx_rope": [_vp, _I, _I, _i, _i, _vp, _vp, _i, _vp],
@@ -538,7 +547,7 @@ _lora_ws: dict = {}  # per-stream dA partials of slx_lora_bwd_ws
 LORA_DA_SLAB = os.environ.get("SLX_LORA_DA_SLAB", "0") == "1"
 
 
-def lora_bwd(x, dt, As, bits, dAs, dx=None, dx_bf16=None, p=0.0, packed=False):
+def lora_bwd(x, dt, As, bits, dAs, dx=None, dx_bf16=None, p=0.0, packed=False, dt_out=None):
     """peft LoRA backward of the sites sharing x (one launch): dAs[j] (f32 [32, kin]) += dT_j^T drop_j(x) (dAs=None:
     skipped) and, if dx (f32 [M, kin]) is given, dx += sum_j drop_j'(dT_j As[j]) in place - or written as
     bf16(dx + ...) to dx_bf16.
@@ -573,6 +582,10 @@ def lora_bwd(x, dt, As, bits, dAs, dx=None, dx_bf16=None, p=0.0, packed=False):
     if dx_bf16 is not None:
         assert dx_bf16.dtype == torch.bfloat16 and dx_bf16.shape[0] == M
         d.dx_bf16, d.lddx_bf16 = dx_bf16.data_ptr(), dx_bf16.stride(0)
+    if dt_out is not None:  # the dx kernel also writes the bf16 dT (slx_lora_grad's operand)
+        assert dx is not None and dt_out.dtype == torch.bfloat16 and dt_out.shape[0] == M and dt_out.stride(1) == 1
+        assert dt_out.shape[1] >= 32 * len(As)
+        d.dt_bf16_out, d.ld_dt_bf16_out = dt_out.data_ptr(), dt_out.stride(0)
     d.p = float(p)
     if LORA_DA_SLAB and dAs is not None:  # dA summed through per-row-chunk partials (no f32 atomics, deterministic)
         need = lib().slx_lora_bwd_ws_floats(M, kin, len(As))
@@ -583,6 +596,35 @@ def lora_bwd(x, dt, As, bits, dAs, dx=None, dx_bf16=None, p=0.0, packed=False):
         check(lib().slx_lora_bwd_ws(ctypes.byref(d), P(ws), ws.numel(), stream_ptr()), "slx_lora_bwd_ws")
         return
     check(lib().slx_lora_bwd(ctypes.byref(d), stream_ptr()), "slx_lora_bwd")
+
+
+def lora_grad(jobs, M):
+    """The LoRA parameter gradients of one layer group in one launch (slx_lora_grad). jobs: dicts with
+    x (bf16 [M, n] view, n % 128 == 0), t (bf16 [M, >= 32 * nsites] view), outs (list of f32 gradients, 1..3 sites),
+    out_nr (True: outs are [n, 32] B gradients; False: [32, n] A gradients), alpha, and for A gradients with dropout
+    p > 0 the keep bits (list, one int32 [M, >= n/32] per site)."""
+    assert 1 <= len(jobs) <= 12
+    arr = (LoraGradJob * len(jobs))()
+    for i, jb in enumerate(jobs):
+        x, t, outs = jb["x"], jb["t"], jb["outs"]
+        n = x.shape[1]
+        assert x.dtype == torch.bfloat16 and x.shape[0] == M and x.stride(1) == 1 and n % 128 == 0
+        assert t.dtype == torch.bfloat16 and t.shape[0] == M and t.stride(1) == 1 and t.shape[1] >= 32 * len(outs)
+        d = arr[i]
+        d.x, d.ldx, d.n = x.data_ptr(), x.stride(0), n
+        d.t, d.ldt, d.t_bf16, d.nsites = t.data_ptr(), t.stride(0), 1, len(outs)
+        for j, o in enumerate(outs):
+            assert o.dtype == torch.float32 and o.is_contiguous()
+            assert o.shape == ((n, 32) if jb["out_nr"] else (32, n)), (o.shape, n)
+            d.out[j] = o.data_ptr()
+        p = float(jb.get("p", 0.0))
+        if p > 0:
+            for j, b in enumerate(jb["bits"]):
+                assert b.dtype == torch.int32 and b.shape[0] == M and b.shape[1] * 32 >= n
+                d.bits[j] = b.data_ptr()
+            d.ldbits = jb["bits"][0].stride(0)
+        d.p, d.alpha, d.out_nr = p, float(jb.get("alpha", 1.0)), int(bool(jb["out_nr"]))
+    check(lib().slx_lora_grad(arr, len(jobs), M, stream_ptr()), "slx_lora_grad")
 
 
 def _mm_dims(A, B, C, ta, tb):

@@ -58,6 +58,7 @@ def test_struct_layouts_match_header(tmp_path):
                "slx_lora_down_desc": K.LoraDownDesc,
                "slx_lora_bwd_desc": K.LoraBwdDesc, "slx_dropout_bits_desc": K.DropoutBitsDesc,
                "slx_dropout_bits_job": K.DropoutBitsJob, "slx_dec_gemv_desc": DecGemvDesc,
+               "slx_lora_grad_job": K.LoraGradJob,
                "slx_frame_desc": FrameDesc}
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "slx.h"', "int main(void){"]
     for cname, cls in structs.items():

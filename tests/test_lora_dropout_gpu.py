@@ -148,3 +148,31 @@ def test_lora_da_slab_deterministic(dev, M, kin, nsites, monkeypatch):
     for a, b, c in zip(*outs, dAt):
         assert torch.equal(a, b)
         assert ((a - c).norm() / c.norm()).item() < 1e-5
+
+
+@pytest.mark.parametrize("M,p", [(6384, 0.1), (1000, 0.0), (77, 0.1)])
+def test_lora_grad_jobs(dev, M, p):
+    """slx_lora_grad: a B-gradient job (out [n][32] += s dy^T t) and an A-gradient job of 3 sites sharing x with keep
+    bits (out_j [32][n] += dT_j^T bf16(x/(1-p)) & keep_j), against torch fp32 on the same bf16 operands."""
+    from simlingo_amd.dropmask import keep_bits
+    g = torch.Generator(device=dev).manual_seed(21)
+    s = 2.0
+    dy = torch.randn(M, 4864, device=dev, generator=g).bfloat16()
+    t = torch.randn(M, 96, device=dev, generator=g).bfloat16()
+    x = torch.randn(M, 896, device=dev, generator=g).bfloat16()
+    dT = torch.randn(M, 96, device=dev, generator=g).bfloat16()
+    seeds = [5, 6, 7]
+    bits = [torch.from_numpy(keep_bits(sd, M, 896, 896, p).view("int32")).to(dev) for sd in seeds] if p > 0 else None
+    dB = torch.full((4864, 32), 0.25, device=dev)
+    dA = [torch.full((32, 896), -0.5, device=dev) for _ in range(3)]
+    jobs = [dict(x=dy, t=t[:, 32:64], outs=[dB], out_nr=True, alpha=s),
+            dict(x=x, t=dT, outs=dA, out_nr=False, alpha=1.0, p=p, bits=bits)]
+    K.lora_grad(jobs, M)
+    torch.cuda.synchronize()
+    refB = 0.25 + s * dy.float().t() @ t[:, 32:64].float()
+    torch.testing.assert_close(dB, refB, atol=2e-3 * refB.abs().max().item(), rtol=1e-4)
+    for j in range(3):
+        mask = torch.from_numpy(keep_scale(seeds[j], M, 896, 896, p)).to(dev) if p > 0 else 1.0
+        xd = (x.float() * mask).bfloat16().float()
+        refA = -0.5 + dT[:, 32 * j:32 * (j + 1)].float().t() @ xd
+        torch.testing.assert_close(dA[j], refA, atol=2e-3 * refA.abs().max().item(), rtol=1e-4)

@@ -66,3 +66,16 @@ def test_pair_side_stream_matches(dev, monkeypatch):
     o1, g1, _ = _step(dev, False, monkeypatch, pair_side=True)
     assert torch.equal(o0, o1)
     _check(g0, g0b, g1)
+
+
+def test_lora_grad_group_matches(dev, monkeypatch):
+    """SLX_LORA_GRAD_GROUP: every LoRA parameter gradient of a layer half deferred to one slx_lora_grad launch gives the
+    per-site path's gradients (the gate of _check; the B gradients are summed in another order than the split-K
+    GEMM's)."""
+    import simlingo_amd.engine as E
+    o0, g0, _ = _step(dev, False, monkeypatch)
+    _, g0b, _ = _step(dev, False, monkeypatch)
+    monkeypatch.setattr(E, "LORA_GRAD_GROUP", True)
+    o1, g1, _ = _step(dev, False, monkeypatch)
+    assert torch.equal(o0, o1)
+    _check(g0, g0b, g1)
