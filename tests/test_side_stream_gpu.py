@@ -13,9 +13,10 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def _step(dev, side, monkeypatch, pair_side=False):
+def _step(dev, side, monkeypatch, pair_side=False, group=False):
     import simlingo_amd.engine as E
     monkeypatch.setattr(E, "PAIR_SIDE", pair_side)
+    monkeypatch.setattr(E, "LORA_GRAD_GROUP", group)  # the side-stream knobs act on the per-site LoRA path
     from simlingo_amd.config import full_config
     from simlingo_amd.params import init_params
     from simlingo_amd.plan import plan_from_example
@@ -72,10 +73,8 @@ def test_lora_grad_group_matches(dev, monkeypatch):
     """SLX_LORA_GRAD_GROUP: every LoRA parameter gradient of a layer half deferred to one slx_lora_grad launch gives the
     per-site path's gradients (the gate of _check; the B gradients are summed in another order than the split-K
     GEMM's)."""
-    import simlingo_amd.engine as E
     o0, g0, _ = _step(dev, False, monkeypatch)
     _, g0b, _ = _step(dev, False, monkeypatch)
-    monkeypatch.setattr(E, "LORA_GRAD_GROUP", True)
-    o1, g1, _ = _step(dev, False, monkeypatch)
+    o1, g1, _ = _step(dev, False, monkeypatch, group=True)
     assert torch.equal(o0, o1)
     _check(g0, g0b, g1)

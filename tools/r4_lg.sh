@@ -6,3 +6,4 @@ timeout -k 10 300 python3 -u -m pytest tests/test_lora_dropout_gpu.py tests/test
 grep -h "worst (side" gpurun_out/r4_lg_tests.log || true
 tail -1 gpurun_out/r4_lg_tests.log
 bash tools/r4_step_ab.sh "SLX_LORA_GRAD_GROUP=0" "SLX_LORA_GRAD_GROUP=1" 2
+bash tools/r4_step_ab.sh "SLX_LORA_GRAD_GROUP=1 SLX_LORA_GRAD_ITEMS=256" "SLX_LORA_GRAD_GROUP=1 SLX_LORA_GRAD_ITEMS=1024" 1
