@@ -886,7 +886,7 @@ class VLAEngine(EngineOps):
         keep = sv["llm"][i]["lora"]
         bits = [keep[site] for site in sites]
         As = [self.cat[i]["axfrag." + site] for site in sites]
-        if LORA_GRAD_GROUP and not self.precise:
+        if LORA_GRAD_GROUP and not self.precise and self._lg_shapes_ok():
             self._lora_bwd_grouped(i, sites, dys, tx, x, dtx, dx, swiglu, dx_bf16, drop, bits, As, sv["step_seed"])
             return
         if not skip_db:
@@ -938,6 +938,13 @@ class VLAEngine(EngineOps):
                epi=K.EPI_DROPMASK_SWIGLU, resid=dx, ldr=dx.stride(0), aux=gu, ldaux=gu.stride(0),
                seed=lora_site_seed(step_seed, i, LORA_SITES.index("down")), drop_p=drop,
                ldmask=x.shape[1], maskbits=bits[0], variant=SWIGLU_BWD_VARIANT)
+
+    def _lg_shapes_ok(self):
+        """slx_lora_grad takes 128-column blocks: every LoRA site's input and output width a multiple of 128 (the
+        InternVL2-1B widths are; the tiny test geometries run the per-site path)."""
+        cfg = self.cfg
+        widths = (cfg.llm_dim, cfg.llm_heads * 64, cfg.llm_kv_heads * 64, cfg.llm_ffn)
+        return all(w % 128 == 0 for w in widths)
 
     def _lg_flush(self, M):
         if self._lg_jobs:
