@@ -552,137 +552,160 @@ __device__ __forceinline__ LgJob lg_job(const LgArgs& a, int jb) {
   }
 }
 
+template <int NS>
 struct LgRegs {
-  uint4 rx[4];
-  uint4 rt[4];
-  uint32_t rm[3];
+  uint4 rx[4];    // X: row srow, 16-B chunks (tid & 3) * 4 + c4 of the 128 columns
+  uint4 rt[NS];   // T: piece tid + 256 q of the [64][32 NS] tile (row p / (4 NS), chunk p % (4 NS))
+  uint32_t rm[NS];
 };
 
-__global__ __launch_bounds__(256, 2) void lora_grad_kernel(LgArgs a) {
-  __shared__ __attribute__((aligned(16))) char smem[8 * 8192];  // X: 3 sites x 2 panels | T: 2 panels
+// One work item: rows [mb, me) x the 128 columns from c0 of job J (NS sites sharing X; DROP: keep-bit masks).
+// NS and DROP are template parameters so the item loop is straight-line code in which the compiler counts the two
+// sub-chunks in flight (vmcnt(N)) instead of draining both at each commit.
+template <int NS, bool DROP>
+__device__ __forceinline__ void lg_item(const LgJob J, int c0, int mb, int me, char* smem) {
   char* ts = smem + 6 * 8192;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
   const int srow = tid >> 2;
-  for (int item = blockIdx.x; item < a.nitems; item += gridDim.x) {
-    int jb = 0;
+  const int mycol = c0 + 32 * w + (lane & 31);
+  f32x16 acc[NS];
 #pragma unroll
-    for (int q = 1; q < kLgMaxJobs; ++q) jb += (q < a.njobs && item >= lg_job(a, q).item0) ? 1 : 0;
-    const LgJob J = lg_job(a, jb);
-    const int li = item - J.item0, cb = li % J.ncb, kc = li / J.ncb;
-    const int c0 = cb * 128, mb = kc * J.kch, me = min(a.M, mb + J.kch);
-    const int mycol = c0 + 32 * w + (lane & 31);
-    const bool drop = J.bits[0] != nullptr;
-    const int ns = J.ns;
-    f32x16 acc[3];
+  for (int j = 0; j < NS; ++j)
 #pragma unroll
-    for (int j = 0; j < 3; ++j)
+    for (int i = 0; i < 16; ++i) acc[j][i] = 0.f;
+  // branch-free loads: rows past the chunk clamped to its last row (zeroed at commit), T columns past the sites
+  // clamped to the last site's
+  auto load = [&](int mm, LgRegs<NS>& R) {
+    const int gm = min(mm + srow, me - 1);
 #pragma unroll
-      for (int i = 0; i < 16; ++i) acc[j][i] = 0.f;
-    auto load = [&](int mm, LgRegs& R) {
-      const int gm = mm + srow;
-      const bool ok = gm < me;
+    for (int c4 = 0; c4 < 4; ++c4) {
+      const int c = (tid & 3) * 4 + c4;
+      R.rx[c4] = *reinterpret_cast<const uint4*>(J.X + (long)gm * J.ldx + c0 + 8 * c);
+    }
 #pragma unroll
-      for (int c4 = 0; c4 < 4; ++c4) {
-        const int c = (tid & 3) * 4 + c4;
-        R.rx[c4] = ok ? *reinterpret_cast<const uint4*>(J.X + (long)gm * J.ldx + c0 + 8 * c) : make_uint4(0u, 0u, 0u, 0u);
-        if (8 * c < 32 * ns)
-          R.rt[c4] = ok ? *reinterpret_cast<const uint4*>(J.T + (long)gm * J.ldt + 8 * c) : make_uint4(0u, 0u, 0u, 0u);
+    for (int q = 0; q < NS; ++q) {
+      const int pc = tid + 256 * q, tr = min(mm + pc / (4 * NS), me - 1);
+      R.rt[q] = *reinterpret_cast<const uint4*>(J.T + (long)tr * J.ldt + 8 * (pc % (4 * NS)));
+    }
+    if constexpr (DROP) {
+#pragma unroll
+      for (int j = 0; j < NS; ++j) R.rm[j] = J.bits[j][(long)gm * J.ldbits + (c0 >> 5) + (tid & 3)];
+    }
+  };
+  auto commit = [&](const LgRegs<NS>& R, int mm) {
+    const bool ok = mm + srow < me;
+#pragma unroll
+    for (int c4 = 0; c4 < 4; ++c4) {
+      const int c = (tid & 3) * 4 + c4;
+      uint4 v = ok ? R.rx[c4] : make_uint4(0u, 0u, 0u, 0u);
+      uint32_t* u = reinterpret_cast<uint32_t*>(&v);
+      if constexpr (DROP) {  // bf16(x / (1-p)), the rounding of peft's dropout output
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+          bf16x2 o;
+          o[0] = (bf16)(__uint_as_float(u[d] << 16) * J.sc);
+          o[1] = (bf16)(__uint_as_float(u[d] & 0xFFFF0000u) * J.sc);
+          u[d] = __builtin_bit_cast(uint32_t, o);
+        }
       }
 #pragma unroll
-      for (int j = 0; j < 3; ++j)
-        R.rm[j] = (drop && j < ns) ? (ok ? J.bits[j][(long)gm * J.ldbits + (c0 >> 5) + (tid & 3)] : 0u) : 0xFFFFFFFFu;
-    };
-    auto commit = [&](const LgRegs& R) {
-#pragma unroll
-      for (int c4 = 0; c4 < 4; ++c4) {
-        const int c = (tid & 3) * 4 + c4;
-        uint4 v = R.rx[c4];
-        uint32_t* u = reinterpret_cast<uint32_t*>(&v);
-        if (drop) {  // bf16(x / (1-p)), the rounding of peft's dropout output
+      for (int j = 0; j < NS; ++j) {
+        uint4 m = v;
+        if constexpr (DROP) {
+          uint32_t* mu = reinterpret_cast<uint32_t*>(&m);
 #pragma unroll
           for (int d = 0; d < 4; ++d) {
-            bf16x2 o;
-            o[0] = (bf16)(__uint_as_float(u[d] << 16) * J.sc);
-            o[1] = (bf16)(__uint_as_float(u[d] & 0xFFFF0000u) * J.sc);
-            u[d] = __builtin_bit_cast(uint32_t, o);
+            const uint32_t lo = (uint32_t)__builtin_amdgcn_sbfe((int)R.rm[j], 8 * c4 + 2 * d, 1);
+            const uint32_t hi = (uint32_t)__builtin_amdgcn_sbfe((int)R.rm[j], 8 * c4 + 2 * d + 1, 1);
+            mu[d] &= (lo & 0xFFFFu) | (hi & 0xFFFF0000u);
           }
         }
-#pragma unroll
-        for (int j = 0; j < 3; ++j) {
-          if (j < ns) {
-            uint4 m = v;
-            if (drop) {
-              uint32_t* mu = reinterpret_cast<uint32_t*>(&m);
-#pragma unroll
-              for (int d = 0; d < 4; ++d) {
-                const uint32_t lo = (uint32_t)__builtin_amdgcn_sbfe((int)R.rm[j], 8 * c4 + 2 * d, 1);
-                const uint32_t hi = (uint32_t)__builtin_amdgcn_sbfe((int)R.rm[j], 8 * c4 + 2 * d + 1, 1);
-                mu[d] &= (lo & 0xFFFFu) | (hi & 0xFFFF0000u);
-              }
-            }
-            *reinterpret_cast<uint4*>(smem + (2 * j + (c >> 3)) * 8192 + la_sw(srow, c & 7)) = m;
-          }
-        }
-        if (8 * c < 32 * ns) *reinterpret_cast<uint4*>(ts + (c >> 3) * 8192 + la_sw(srow, c & 7)) = R.rt[c4];
+        *reinterpret_cast<uint4*>(smem + (2 * j + (c >> 3)) * 8192 + la_sw(srow, c & 7)) = m;
       }
-    };
-    auto mma = [&]() {
+    }
 #pragma unroll
-      for (int ms = 0; ms < 4; ++ms)
+    for (int q = 0; q < NS; ++q) {
+      const int pc = tid + 256 * q, tr = pc / (4 * NS), ch = pc % (4 * NS);
+      *reinterpret_cast<uint4*>(ts + (ch >> 3) * 8192 + la_sw(tr, ch & 7)) =
+          mm + tr < me ? R.rt[q] : make_uint4(0u, 0u, 0u, 0u);
+    }
+  };
+  auto mma = [&]() {
+    // the lane index laundered per call: its LDS addresses are recomputed (a few VALU per sub-chunk) instead of
+    // hoisted out of the sub-chunk loop for every site and slice, which spilled at NS = 3
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
 #pragma unroll
-        for (int j = 0; j < 3; ++j)
-          if (j < ns) {
-            const bf16x8 xm = la_tr(smem + (2 * j + (w >> 1)) * 8192, 16 * ms, 32 * (w & 1), lane);
-            const bf16x8 ta = la_tr(ts + ((32 * j) >> 6) * 8192, 16 * ms, (32 * j) & 63, lane);
-            acc[j] = mfma32x32(ta, xm, acc[j]);
-          }
-    };
-    const int nsub = (me - mb + 63) / 64;
-    LgRegs R0, R1;
-    if (nsub > 0) load(mb, R0);
-    if (nsub > 1) load(mb + 64, R1);
-    for (int sb = 0; sb < nsub; sb += 2) {
-      commit(R0);
+    for (int ms = 0; ms < 4; ++ms)
+#pragma unroll
+      for (int j = 0; j < NS; ++j) {
+        const bf16x8 xm = la_tr(smem + (2 * j + (w >> 1)) * 8192, 16 * ms, 32 * (w & 1), ln);
+        const bf16x8 ta = la_tr(ts + ((32 * j) >> 6) * 8192, 16 * ms, (32 * j) & 63, ln);
+        acc[j] = mfma32x32(ta, xm, acc[j]);
+      }
+  };
+  const int nsub = (me - mb + 63) / 64;
+  LgRegs<NS> R0, R1;
+  load(mb, R0);
+  if (nsub > 1) load(mb + 64, R1);
+  for (int sb = 0; sb < nsub; sb += 2) {
+    commit(R0, mb + 64 * sb);
+    __syncthreads();
+    if (sb + 2 < nsub) load(mb + 64 * (sb + 2), R0);
+    mma();
+    __syncthreads();
+    if (sb + 1 >= nsub) break;
+    commit(R1, mb + 64 * (sb + 1));
+    __syncthreads();
+    if (sb + 3 < nsub) load(mb + 64 * (sb + 3), R1);
+    mma();
+    __syncthreads();
+  }
+  if (!J.nr) {
+#pragma unroll
+    for (int j = 0; j < NS; ++j)
+#pragma unroll
+      for (int g = 0; g < 16; ++g) {
+        const int rr = (g & 3) + 8 * (g >> 2) + 4 * h;
+        atomicAdd(J.out[j] + (long)rr * J.N + mycol, J.alpha * acc[j][g]);
+      }
+  } else {  // out[n][32]: transpose through LDS ([32][129] f32), then 32 consecutive r per 32 lanes
+    float* red = reinterpret_cast<float*>(smem);
+#pragma unroll
+    for (int j = 0; j < NS; ++j) {
+#pragma unroll
+      for (int g = 0; g < 16; ++g) {
+        const int rr = (g & 3) + 8 * (g >> 2) + 4 * h;
+        red[rr * 129 + 32 * w + (lane & 31)] = acc[j][g];
+      }
       __syncthreads();
-      if (sb + 2 < nsub) load(mb + 64 * (sb + 2), R0);
-      mma();
-      __syncthreads();
-      if (sb + 1 >= nsub) break;
-      commit(R1);
-      __syncthreads();
-      if (sb + 3 < nsub) load(mb + 64 * (sb + 3), R1);
-      mma();
+      for (int e = tid; e < 32 * 128; e += 256) {
+        const int col = e >> 5, r = e & 31;
+        atomicAdd(J.out[j] + (long)(c0 + col) * 32 + r, J.alpha * red[r * 129 + col]);
+      }
       __syncthreads();
     }
-    if (!J.nr) {
+  }
+}
+
+// one block per work item (the host sizes the items to about one per block slot, so the grid is one round)
+__global__ __launch_bounds__(256, 2) void lora_grad_kernel(LgArgs a) {
+  __shared__ __attribute__((aligned(16))) char smem[8 * 8192];  // X: 3 sites x 2 panels | T: 2 panels
+  const int item = blockIdx.x;
+  int jb = 0;
 #pragma unroll
-      for (int j = 0; j < 3; ++j)
-        if (j < ns) {
-#pragma unroll
-          for (int g = 0; g < 16; ++g) {
-            const int rr = (g & 3) + 8 * (g >> 2) + 4 * h;
-            atomicAdd(J.out[j] + (long)rr * J.N + mycol, J.alpha * acc[j][g]);
-          }
-        }
-    } else {  // out[n][32]: transpose through LDS ([32][129] f32), then 32 consecutive r per 32 lanes
-      float* red = reinterpret_cast<float*>(smem);
-#pragma unroll
-      for (int j = 0; j < 3; ++j)
-        if (j < ns) {
-#pragma unroll
-          for (int g = 0; g < 16; ++g) {
-            const int rr = (g & 3) + 8 * (g >> 2) + 4 * h;
-            red[rr * 129 + 32 * w + (lane & 31)] = acc[j][g];
-          }
-          __syncthreads();
-          for (int e = tid; e < 32 * 128; e += 256) {
-            const int col = e >> 5, r = e & 31;
-            atomicAdd(J.out[j] + (long)(c0 + col) * 32 + r, J.alpha * red[r * 129 + col]);
-          }
-          __syncthreads();
-        }
-    }
-    __syncthreads();  // the next item overwrites the panels
+  for (int q = 1; q < kLgMaxJobs; ++q) jb += (q < a.njobs && item >= lg_job(a, q).item0) ? 1 : 0;
+  const LgJob J = lg_job(a, jb);
+  const int li = item - J.item0, cb = li % J.ncb, kc = li / J.ncb;
+  const int c0 = cb * 128, mb = kc * J.kch, me = min(a.M, mb + J.kch);
+  const bool drop = J.bits[0] != nullptr;
+  switch (J.ns * 2 + (drop ? 1 : 0)) {
+    case 2: lg_item<1, false>(J, c0, mb, me, smem); break;
+    case 3: lg_item<1, true>(J, c0, mb, me, smem); break;
+    case 4: lg_item<2, false>(J, c0, mb, me, smem); break;
+    case 5: lg_item<2, true>(J, c0, mb, me, smem); break;
+    case 6: lg_item<3, false>(J, c0, mb, me, smem); break;
+    default: lg_item<3, true>(J, c0, mb, me, smem); break;
   }
 }
 
@@ -899,8 +922,7 @@ extern "C" int slx_lora_grad(const slx_lora_grad_job* jobs, int njobs, int64_t M
     items += a.j[i].ncb * (int)nkc;
   }
   a.nitems = items;
-  const int grid = items < 512 ? items : 512;
-  hipLaunchKernelGGL(lora_grad_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, a);
+  hipLaunchKernelGGL(lora_grad_kernel, dim3(items), dim3(256), 0, (hipStream_t)stream, a);
   SLX_LAUNCH_CHECK("slx_lora_grad");
   return 0;
 }
