@@ -2338,9 +2338,12 @@ static int gemm_launch(const slx_gemm_desc* d, int v, hipStream_t st, int mshift
   }
   {  // more than one round of 256^2 tiles: the FE member (the next tile's loads overlap this tile's epilogue; on a
      // single round there is no next tile and the LDS-staged epilogue is as fast or faster: gemm_epi_bench proj)
+    // SLX_GEMM_FE1=1: also single-round launches with the plain STORE epilogue (register-direct stores measured
+    // 824 vs 711 TF on the InternViT proj dgrad shape and 1247 vs 1176 on the fc1 dgrad shape, tools/gemm_bench.py)
     static const bool fe_on = [] { const char* e = getenv("SLX_GEMM_FE"); return !e || atoi(e) != 0; }();
+    static const bool fe1 = [] { const char* e = getenv("SLX_GEMM_FE1"); return e && atoi(e) != 0; }();
     const long t3 = (long)(((rem_r0 > 0 ? rem_r0 : d->M) + V3_BM - 1) / V3_BM) * ((d->N + V3_BN - 1) / V3_BN);
-    if (v == 7 && fe_on && batch == 1 && t3 > 256 && !d->rope_cos) v = 11;
+    if (v == 7 && fe_on && batch == 1 && (t3 > 256 || (fe1 && d->epilogue == SLX_EPI_STORE)) && !d->rope_cos) v = 11;
   }
   SLX_CHECK_ARG(!d->colsum || (d->colsum_ws && a.vec_ok && a.ksplit == 1 && v != 1 && d->N % 8 == 0 &&
                                 (d->epilogue == SLX_EPI_STORE || d->epilogue == SLX_EPI_GELU_BWD ||
