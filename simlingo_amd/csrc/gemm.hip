@@ -2338,12 +2338,14 @@ static int gemm_launch(const slx_gemm_desc* d, int v, hipStream_t st, int mshift
   }
   {  // more than one round of 256^2 tiles: the FE member (the next tile's loads overlap this tile's epilogue; on a
      // single round there is no next tile and the LDS-staged epilogue is as fast or faster: gemm_epi_bench proj)
-    // SLX_GEMM_FE1=1: also single-round launches with the plain STORE epilogue (register-direct stores measured
-    // 824 vs 711 TF on the InternViT proj dgrad shape and 1247 vs 1176 on the fc1 dgrad shape, tools/gemm_bench.py)
+    // Single-round launches too with the plain STORE epilogue (SLX_GEMM_FE1=1, default): register-direct stores
+    // measured 824 vs 711 TF on the InternViT proj dgrad shape and 1247 vs 1176 on the fc1 dgrad shape
+    // (tools/gemm_bench.py), +0.7 % on the step (profiles/round4_fe1_ab.txt); SLX_GEMM_FE1=2 adds every epilogue
     static const bool fe_on = [] { const char* e = getenv("SLX_GEMM_FE"); return !e || atoi(e) != 0; }();
-    static const bool fe1 = [] { const char* e = getenv("SLX_GEMM_FE1"); return e && atoi(e) != 0; }();
+    static const int fe1 = [] { const char* e = getenv("SLX_GEMM_FE1"); return e ? atoi(e) : 1; }();
     const long t3 = (long)(((rem_r0 > 0 ? rem_r0 : d->M) + V3_BM - 1) / V3_BM) * ((d->N + V3_BN - 1) / V3_BN);
-    if (v == 7 && fe_on && batch == 1 && (t3 > 256 || (fe1 && d->epilogue == SLX_EPI_STORE)) && !d->rope_cos) v = 11;
+    const bool single_ok = fe1 >= 2 || (fe1 == 1 && d->epilogue == SLX_EPI_STORE);
+    if (v == 7 && fe_on && batch == 1 && (t3 > 256 || single_ok) && !d->rope_cos) v = 11;
   }
   SLX_CHECK_ARG(!d->colsum || (d->colsum_ws && a.vec_ok && a.ksplit == 1 && v != 1 && d->N % 8 == 0 &&
                                 (d->epilogue == SLX_EPI_STORE || d->epilogue == SLX_EPI_GELU_BWD ||
