@@ -13,6 +13,7 @@ cat gpurun_out/${TAG}_bench.json
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_prof -o run -- python3 bench.py --steps 4 --warmup 2 --no-cpu-baseline --no-extras > gpurun_out/${TAG}_prof.log 2>&1
 python3 tools/prof_steps.py gpurun_out/${TAG}_prof --warmup 2 --grid --top 70 > gpurun_out/${TAG}_steps.txt
 python3 tools/prof_steps.py gpurun_out/${TAG}_prof --warmup 2 --top 40 > gpurun_out/${TAG}_steps_byname.txt
+python3 tools/prof_steps.py gpurun_out/${TAG}_prof --warmup 2 --top 12 --alternate v3_pair_kernel > gpurun_out/${TAG}_steps_pairs.txt
 head -12 gpurun_out/${TAG}_steps.txt
 find gpurun_out/${TAG}_prof -name '*kernel_stats.csv' -exec cp {} gpurun_out/${TAG}_kernel_stats.csv \;
 rm -rf gpurun_out/${TAG}_prof

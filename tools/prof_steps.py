@@ -19,6 +19,9 @@ ap.add_argument("--top", type=int, default=45)
 ap.add_argument("--grid", action="store_true", help="split kernels by launch grid (GEMM shape attribution)")
 ap.add_argument("--marker", default="adamw_kernel")
 ap.add_argument("--gaps", type=int, default=0, help="also list the N largest idle gaps between kernels")
+ap.add_argument("--alternate", default="", help="split the calls of kernels whose name contains this string by "
+                "occurrence parity within the steady steps (#0, #1): the two InternViT weight-gradient pairs share one "
+                "kernel and one grid, and alternate fc2.w+fc1.w (#0), proj.w+qkv.w (#1) in every layer's backward")
 args = ap.parse_args()
 path = args.path
 if os.path.isdir(path):
@@ -38,8 +41,12 @@ t0, t1 = marks[args.warmup - 1] if args.warmup > 0 else rows[0][1] - 1, marks[-1
 steps = len(marks) - args.warmup
 sel = [r for r in rows if t0 < r[1] <= t1]
 agg = defaultdict(lambda: [0, 0.0])
+alt = 0
 for name, s, e, dur, gx, gy, gz, wx in sel:
     short = name.replace("void ", "").replace("slx::", "")[:120]
+    if args.alternate and args.alternate in name:
+        short = f"#{alt % 2} " + short
+        alt += 1
     key = (short, (gx // max(wx, 1), gy, gz)) if args.grid else (short, None)
     agg[key][0] += 1
     agg[key][1] += dur
