@@ -644,22 +644,25 @@ __device__ __forceinline__ void lg_item(const LgJob J, int c0, int mb, int me, c
         acc[j] = mfma32x32(ta, xm, acc[j]);
       }
   };
+  // D sub-chunks in flight behind the one being multiplied: 4 for single-site items (the B gradients and the
+  // o / down A gradients: 20 VGPRs per register set), 2 for the two- and three-site A gradients
+  constexpr int D = NS == 1 ? 4 : 3;
   const int nsub = (me - mb + 63) / 64;
-  LgRegs<NS> R0, R1;
-  load(mb, R0);
-  if (nsub > 1) load(mb + 64, R1);
-  for (int sb = 0; sb < nsub; sb += 2) {
-    commit(R0, mb + 64 * sb);
-    __syncthreads();
-    if (sb + 2 < nsub) load(mb + 64 * (sb + 2), R0);
-    mma();
-    __syncthreads();
-    if (sb + 1 >= nsub) break;
-    commit(R1, mb + 64 * (sb + 1));
-    __syncthreads();
-    if (sb + 3 < nsub) load(mb + 64 * (sb + 3), R1);
-    mma();
-    __syncthreads();
+  LgRegs<NS> R[D];
+#pragma unroll
+  for (int q = 0; q < D; ++q)
+    if (q < nsub) load(mb + 64 * q, R[q]);
+  for (int sb = 0; sb < nsub; sb += D) {
+#pragma unroll
+    for (int q = 0; q < D; ++q) {
+      if (sb + q < nsub) {
+        commit(R[q], mb + 64 * (sb + q));
+        __syncthreads();
+        if (sb + q + D < nsub) load(mb + 64 * (sb + q + D), R[q]);
+        mma();
+        __syncthreads();
+      }
+    }
   }
   if (!J.nr) {
 #pragma unroll
