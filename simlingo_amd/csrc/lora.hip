@@ -644,9 +644,9 @@ __device__ __forceinline__ void lg_item(const LgJob J, int c0, int mb, int me, c
         acc[j] = mfma32x32(ta, xm, acc[j]);
       }
   };
-  // D sub-chunks in flight behind the one being multiplied: 4 for single-site items (the B gradients and the
-  // o / down A gradients: 20 VGPRs per register set), 2 for the two- and three-site A gradients
-  constexpr int D = NS == 1 ? 4 : 3;
+  // D sub-chunks in flight behind the one being multiplied (depths 4 / 3 for single- / multi-site items measured the
+  // same on the step as 2, profiles/round4_lora_grad_depth_ab.txt)
+  constexpr int D = 2;
   const int nsub = (me - mb + 63) / 64;
   LgRegs<NS> R[D];
 #pragma unroll
