@@ -39,7 +39,7 @@ BF16, F32 = torch.bfloat16, torch.float32
 FUSE_O = os.environ.get("SLX_DEC_FUSE_O", "0") == "1"
 # the attention split over keys (Hkv x 8 workgroups) with its partials merged by the O GEMV's prologue
 # (slx_dec_attn_o_split) instead of one MFMA workgroup per kv head + the O GEMV: 0.71 vs 0.80 ms per token in
-# alternating bench_infer runs (tools/r4_dec_ab.sh, profiles/round4_knobs_ab.txt); SLX_DEC_SPLIT_O=0 restores the old pair
+# alternating bench_infer runs (tools/ab/r4_dec_ab.sh, profiles/round4_knobs_ab.txt); SLX_DEC_SPLIT_O=0 restores the old pair
 SPLIT_O = os.environ.get("SLX_DEC_SPLIT_O", "1") == "1"
 DEC_STORE_ROW, DEC_RESID, DEC_SWIGLU, DEC_ARGMAX = 0, 1, 2, 3
 

@@ -2,6 +2,6 @@
 set -e
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-bash tools/r4_knobs2.sh
-bash tools/r4_traffic.sh
-bash tools/r4_attn_pmc.sh
+bash tools/ab/r4_knobs2.sh
+bash tools/traffic.sh
+bash tools/attn_pmc.sh

@@ -8,4 +8,4 @@ for cfg in "SLX_LORA_DA_SLAB=0" "SLX_LORA_DA_SLAB=1" "SLX_LORA_DA_SLAB=1 SLX_LOR
   echo "== $cfg"
   env $cfg timeout -k 10 120 python3 tools/lora_bench.py 2>/dev/null
 done
-bash tools/r4_step_ab.sh "SLX_LORA_DA_SLAB=0" "SLX_LORA_DA_SLAB=1" 2
+bash tools/step_ab.sh "SLX_LORA_DA_SLAB=0" "SLX_LORA_DA_SLAB=1" 2
