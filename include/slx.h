@@ -91,6 +91,9 @@ typedef struct slx_gemm_desc {
                        f32 as slx_rope takes them), applied to alpha*acc + bias before the bf16 rounding: the Qwen2
                        q|k projection (modeling_qwen2 apply_rotary_pos_emb) fused into its GEMM                       */
   int rope_S; int rope_ncols;
+  int aux_grad;     /* GELU / QGELU: aux_out receives the activation's derivative at the pre-activation,
+                       bf16(gelu'(h)), instead of h; GELU_BWD / QGELU_BWD: aux holds that derivative and is multiplied
+                       in directly (the backward epilogue then evaluates no transcendental)                           */
 } slx_gemm_desc;
 int slx_gemm_bf16(const slx_gemm_desc* d, slx_stream_t stream);
 /* Two independent accumulating f32 STORE GEMMs (same layout and K, no bias / colsum / batch) in one launch:

@@ -42,6 +42,24 @@ __device__ __forceinline__ float qgelu_grad(float x) {
   const float s = 1.0f / (1.0f + __expf(-1.702f * x));
   return s * (1.0f + 1.702f * x * (1.0f - s));
 }
+// act(h) and, with p.aux_grad, the value stored as aux: the derivative act'(h) instead of h
+template <int EPI>
+__device__ __forceinline__ float act_fwd(float h, bool aux_grad, float& aux) {
+  if constexpr (EPI == EPI_GELU) {
+    const GeluTerms g = gelu_terms(h);
+    aux = aux_grad ? __builtin_fmaf(h * 0.39894228040143268f, g.e, g.cdf) : h;
+    return h * g.cdf;
+  } else {
+    aux = aux_grad ? qgelu_grad(h) : h;
+    return qgelu(h);
+  }
+}
+template <int EPI>
+__device__ __forceinline__ float act_bwd(float aux, bool aux_grad) {
+  if (aux_grad) return aux;
+  if constexpr (EPI == EPI_GELU_BWD) return gelu_erf_grad(aux);
+  else return qgelu_grad(aux);
+}
 
 struct GemmArgs {
   const bf16* A;
@@ -98,6 +116,8 @@ struct GemmArgs {
   const float* rope_cos;
   const float* rope_sin;
   int rope_S, rope_ncols;
+  // GELU / QGELU store the derivative at h as aux; GELU_BWD / QGELU_BWD multiply the aux in directly
+  int aux_grad;
 };
 
 // Dropout applied while loading an operand (LoRA dropout, regenerated bit-exactly in backward):
@@ -224,8 +244,10 @@ __device__ __forceinline__ void epilogue_elem(const GemmArgs& p, OutT* __restric
   } else if constexpr (EPI == EPI_GELU) {
     if (p.bias) v += p.bias[n];
     const bf16 hb = (bf16)v;
-    p.aux_out[(long)m * p.ldaux_out + n] = hb;
-    C[ci] = (OutT)gelu_erf((float)hb);
+    float ax;
+    const float y = act_fwd<EPI_GELU>((float)hb, p.aux_grad, ax);
+    p.aux_out[(long)m * p.ldaux_out + n] = (bf16)ax;
+    C[ci] = (OutT)y;
   } else if constexpr (EPI == EPI_RESID_LS) {
     if (p.bias) v += p.bias[n];
     const bf16 yb = (bf16)v;
@@ -234,14 +256,16 @@ __device__ __forceinline__ void epilogue_elem(const GemmArgs& p, OutT* __restric
   } else if constexpr (EPI == EPI_QGELU) {
     if (p.bias) v += p.bias[n];
     const bf16 hb = (bf16)v;
-    p.aux_out[(long)m * p.ldaux_out + n] = hb;
-    C[ci] = (OutT)qgelu((float)hb);
+    float ax;
+    const float y = act_fwd<EPI_QGELU>((float)hb, p.aux_grad, ax);
+    p.aux_out[(long)m * p.ldaux_out + n] = (bf16)ax;
+    C[ci] = (OutT)y;
   } else if constexpr (EPI == EPI_QGELU_BWD) {
     const float h = (float)p.aux[(long)m * p.ldaux + n];
-    C[ci] = (OutT)(v * qgelu_grad(h));
+    C[ci] = (OutT)(v * act_bwd<EPI_QGELU_BWD>(h, p.aux_grad));
   } else if constexpr (EPI == EPI_GELU_BWD) {
     const float h = (float)p.aux[(long)m * p.ldaux + n];
-    C[ci] = (OutT)(v * gelu_erf_grad(h));
+    C[ci] = (OutT)(v * act_bwd<EPI_GELU_BWD>(h, p.aux_grad));
   } else if constexpr (EPI == EPI_SWIGLU_BWD) {
     const long ai = (long)m * p.ldaux + n;
     const float g = (float)p.aux[ai], u = (float)p.aux[ai + p.N];
@@ -321,9 +345,10 @@ __device__ __forceinline__ void epilogue_vec8(const GemmArgs& p, OutT* __restric
     float h[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) h[e] = (float)(bf16)(v[e] + (p.bias ? p.bias[n + e] : 0.f));
-    st8(p.aux_out + (long)m * p.ldaux_out + n, h);
+    float ax[8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) h[e] = gelu_erf(h[e]);
+    for (int e = 0; e < 8; ++e) h[e] = act_fwd<EPI_GELU>(h[e], p.aux_grad, ax[e]);
+    st8(p.aux_out + (long)m * p.ldaux_out + n, ax);
     st8(C + ci, h);
   } else if constexpr (EPI == EPI_RESID_LS) {
     if (p.bias) {
@@ -340,21 +365,22 @@ __device__ __forceinline__ void epilogue_vec8(const GemmArgs& p, OutT* __restric
     float h[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) h[e] = (float)(bf16)(v[e] + (p.bias ? p.bias[n + e] : 0.f));
-    st8(p.aux_out + (long)m * p.ldaux_out + n, h);
+    float ax[8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) h[e] = qgelu(h[e]);
+    for (int e = 0; e < 8; ++e) h[e] = act_fwd<EPI_QGELU>(h[e], p.aux_grad, ax[e]);
+    st8(p.aux_out + (long)m * p.ldaux_out + n, ax);
     st8(C + ci, h);
   } else if constexpr (EPI == EPI_QGELU_BWD) {
     float h[8];
     ld8(p.aux + (long)m * p.ldaux + n, h);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] *= qgelu_grad(h[e]);
+    for (int e = 0; e < 8; ++e) v[e] *= act_bwd<EPI_QGELU_BWD>(h[e], p.aux_grad);
     st8(C + ci, v);
   } else if constexpr (EPI == EPI_GELU_BWD) {
     float h[8];
     ld8(p.aux + (long)m * p.ldaux + n, h);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] *= gelu_erf_grad(h[e]);
+    for (int e = 0; e < 8; ++e) v[e] *= act_bwd<EPI_GELU_BWD>(h[e], p.aux_grad);
     st8(C + ci, v);
   } else if constexpr (EPI == EPI_SWIGLU_BWD) {
     float g[8], u[8], o[8];
@@ -814,9 +840,10 @@ __device__ __forceinline__ void epi_finish(const GemmArgs& p, OutT* __restrict__
     float h[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) h[e] = (float)(bf16)(v[e] + (p.bias ? p.bias[n + e] : 0.f));
-    st8(p.aux_out + (long)m * p.ldaux_out + n, h);
+    float ax[8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) h[e] = EPI == EPI_GELU ? gelu_erf(h[e]) : qgelu(h[e]);
+    for (int e = 0; e < 8; ++e) h[e] = act_fwd<EPI>(h[e], p.aux_grad, ax[e]);
+    st8(p.aux_out + (long)m * p.ldaux_out + n, ax);
     st8(C + ci, h);
   } else if constexpr (EPI == EPI_RESID_LS) {
     if (p.bias) {
@@ -833,7 +860,7 @@ __device__ __forceinline__ void epi_finish(const GemmArgs& p, OutT* __restrict__
     float h[8];
     unpack_bf8(L[0], h);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] *= EPI == EPI_GELU_BWD ? gelu_erf_grad(h[e]) : qgelu_grad(h[e]);
+    for (int e = 0; e < 8; ++e) v[e] *= act_bwd<EPI>(h[e], p.aux_grad);
     st8(C + ci, v);
   } else if constexpr (EPI == EPI_SWIGLU_BWD) {
     float g[8], u[8], o[8];
@@ -1415,12 +1442,26 @@ __device__ __forceinline__ void fe_epilogue(const GemmArgs& p, OutT* __restrict_
       for (int b = 0; b < 4; ++b)
 #pragma unroll
         for (int r = 0; r < 4; ++r) y[b][r] = (float)(bf16)y[b][r];
-      fe_st_bf16(scr, ra, va, a * sa, sa / 2, lane, y);
+      if (p.aux_grad) {  // aux = act'(h): the derivative replaces h in y for the aux store, act(h) kept aside
+        float g[4][4];
 #pragma unroll
-      for (int b = 0; b < 4; ++b)
+        for (int b = 0; b < 4; ++b)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) y[b][r] = EPI == EPI_GELU ? gelu_erf(y[b][r]) : qgelu(y[b][r]);
-      fe_st_bf16(scr, rc, vc, a * sc, sc / 2, lane, y);
+          for (int r = 0; r < 4; ++r) {
+            float ax;
+            g[b][r] = act_fwd<EPI>(y[b][r], true, ax);
+            y[b][r] = ax;
+          }
+        fe_st_bf16(scr, ra, va, a * sa, sa / 2, lane, y);
+        fe_st_bf16(scr, rc, vc, a * sc, sc / 2, lane, g);
+      } else {
+        fe_st_bf16(scr, ra, va, a * sa, sa / 2, lane, y);
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) y[b][r] = EPI == EPI_GELU ? gelu_erf(y[b][r]) : qgelu(y[b][r]);
+        fe_st_bf16(scr, rc, vc, a * sc, sc / 2, lane, y);
+      }
     } else if constexpr (EPI == EPI_RESID_LS) {
       if (p.aux_out) fe_st_bf16(scr, ra, va, a * sa, sa / 2, lane, y);
 #pragma unroll
@@ -1433,7 +1474,7 @@ __device__ __forceinline__ void fe_epilogue(const GemmArgs& p, OutT* __restrict_
       for (int b = 0; b < 4; ++b) {
         const bf16x4 hv = __builtin_bit_cast(bf16x4, ax[a & 3][b]);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) y[b][r] *= EPI == EPI_GELU_BWD ? gelu_erf_grad((float)hv[r]) : qgelu_grad((float)hv[r]);
+        for (int r = 0; r < 4; ++r) y[b][r] *= act_bwd<EPI>((float)hv[r], p.aux_grad);
       }
       fe_st_bf16(scr, rc, vc, a * sc, sc / 2, lane, y);
 #pragma unroll
@@ -1717,8 +1758,8 @@ __device__ __forceinline__ void v3_remainder(const GemmArgs& p, int u) {
         const float a = ((a8[0] + a8[1]) + (a8[2] + a8[3])) + ((a8[4] + a8[5]) + (a8[6] + a8[7]));
         epilogue_elem<EPI, OutT>(p, C, r0 + m, n, a);
         if constexpr (EPI == EPI_STORE) cs += a * p.alpha + (p.bias ? p.bias[n] : 0.f);
-        else if constexpr (EPI == EPI_GELU_BWD) cs += a * p.alpha * gelu_erf_grad((float)p.aux[(long)(r0 + m) * p.ldaux + n]);
-        else if constexpr (EPI == EPI_QGELU_BWD) cs += a * p.alpha * qgelu_grad((float)p.aux[(long)(r0 + m) * p.ldaux + n]);
+        else if constexpr (EPI == EPI_GELU_BWD) cs += a * p.alpha * act_bwd<EPI_GELU_BWD>((float)p.aux[(long)(r0 + m) * p.ldaux + n], p.aux_grad);
+        else if constexpr (EPI == EPI_QGELU_BWD) cs += a * p.alpha * act_bwd<EPI_QGELU_BWD>((float)p.aux[(long)(r0 + m) * p.ldaux + n], p.aux_grad);
       }
     }
   }
@@ -2236,8 +2277,8 @@ __global__ __launch_bounds__(256) void rows_epilogue_kernel(GemmArgs p, const fl
       const float acc = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
       epilogue_elem<EPI, OutT>(p, C, m, n, acc);
       if constexpr (EPI == EPI_STORE) cs += acc * p.alpha + (p.bias ? p.bias[n] : 0.f);
-      else if constexpr (EPI == EPI_GELU_BWD) cs += acc * p.alpha * gelu_erf_grad((float)p.aux[(long)m * p.ldaux + n]);
-      else if constexpr (EPI == EPI_QGELU_BWD) cs += acc * p.alpha * qgelu_grad((float)p.aux[(long)m * p.ldaux + n]);
+      else if constexpr (EPI == EPI_GELU_BWD) cs += acc * p.alpha * act_bwd<EPI_GELU_BWD>((float)p.aux[(long)m * p.ldaux + n], p.aux_grad);
+      else if constexpr (EPI == EPI_QGELU_BWD) cs += acc * p.alpha * act_bwd<EPI_QGELU_BWD>((float)p.aux[(long)m * p.ldaux + n], p.aux_grad);
     }
   }
   if (p.colsum) {
@@ -2299,6 +2340,7 @@ static int gemm_launch(const slx_gemm_desc* d, int v, hipStream_t st, int mshift
   a.colsum_row0 = colsum_row0;
   a.split_ws = nullptr; a.split_cnt = nullptr; a.split_tile0 = 0;
   a.rope_cos = d->rope_cos; a.rope_sin = d->rope_sin; a.rope_S = d->rope_S; a.rope_ncols = d->rope_ncols;
+  a.aux_grad = d->aux_grad;
   a.mshift_last = 0;
   a.tilesM = (d->M + BM - 1) / BM;
   a.tilesN = (d->N + BN - 1) / BN;

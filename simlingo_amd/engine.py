@@ -58,6 +58,9 @@ PAIR_SIDE = os.environ.get("SLX_PAIR_SIDE", "0") == "1"
 # operand, instead of a split-K GEMM per B gradient and a dA pass per site group: +1.75 % on the step (102.0 -> 103.8
 # samples/s in alternating runs, profiles/round4_lora_grad_group_ab.txt); SLX_LORA_GRAD_GROUP=0 restores the per-site path
 LORA_GRAD_GROUP = os.environ.get("SLX_LORA_GRAD_GROUP", "1") == "1"
+# SLX_GELU_AUX_GRAD=1: the InternViT fc1 GEMM stores gelu'(h) (bf16) as its aux instead of h, so the fc2 data-gradient
+# epilogue multiplies it in instead of evaluating gelu' (an rcp, an exp2 and ~10 FMA per element of 16400 x 4096)
+GELU_AUX_GRAD = os.environ.get("SLX_GELU_AUX_GRAD", "0") == "1"
 ALIGN = 64  # elements; keeps every parameter view 256-B aligned
 
 
@@ -474,14 +477,16 @@ class VLAEngine(EngineOps):
             h2, n2 = self._norm(xm, self.P[p + "ln2.w"], self.P[p + "ln2.b"], Mv, D, cfg.vit_eps)
             hpre = self._e(Mv, F_)
             hact = self._e(Mv, F_)
+            hgrad = GELU_AUX_GRAD and not self.precise  # hpre then holds gelu'(h) (see GELU_AUX_GRAD)
             with self._probe("vit.fc1"):
-                K.mm(h2, self.W[p + "fc1.w"], hact, bias=self.P[p + "fc1.b"], epi=K.EPI_GELU, aux_out=hpre, ldaux_out=F_)
+                K.mm(h2, self.W[p + "fc1.w"], hact, bias=self.P[p + "fc1.b"], epi=K.EPI_GELU, aux_out=hpre, ldaux_out=F_,
+                     aux_grad=hgrad)
             xo = self._e(Mv, D, dtype=F32)
             y2 = self._e(Mv, D)
             K.mm(hact, self.W[p + "fc2.w"], xo, bias=self.P[p + "fc2.b"], epi=K.EPI_RESID_LS, resid=xm, ldr=D,
                  ls=self.P[p + "ls2"], aux_out=y2, ldaux_out=D)
             vit_saved.append(dict(x=x, h1=h1, n1=n1, qkv=qkv, o=o, lse=lse, y1=y1, xm=xm, h2=h2, n2=n2, hpre=hpre,
-                                  hact=hact, y2=y2))
+                                  hact=hact, y2=y2, hgrad=hgrad))
             x = xo
         sv["vit"] = vit_saved
         sv["vit_out"] = x
@@ -758,7 +763,8 @@ class VLAEngine(EngineOps):
                 K.mm(g, Ls["hact"], self.G[p + "fc2.w"], ta=True, tb=False, accumulate=True)
             dh = self._e(Mv, F_)
             self._mm_dx(g, self.W[p + "fc2.w"], self.WT.get(p + "fc2.w"), dh, epi=K.EPI_GELU_BWD, aux=Ls["hpre"],
-                        ldaux=F_, colsum=self.G[p + "fc1.b"])  # fc1.b grad = column sums of dh, in the same epilogue
+                        ldaux=F_, colsum=self.G[p + "fc1.b"],  # fc1.b grad = column sums of dh, in the same epilogue
+                        aux_grad=Ls["hgrad"])
             side = PAIR_WGRAD and PAIR_SIDE and not self.precise
             if side:
                 ev_side = self._side_fork()

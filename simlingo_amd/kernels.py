@@ -43,7 +43,7 @@ class GemmDesc(ctypes.Structure):
         ("ksplit_max", c_int), ("variant", c_int), ("drop_operand", c_int),
         ("colsum", c_vp), ("colsum_ws", c_vp), ("maskbits", c_vp), ("ldbits", c_i64), ("rem_ws", c_vp),
         ("rem_ws_floats", c_i64), ("resid_bf16", c_int), ("split_ws", c_vp), ("split_ws_floats", c_i64),
-        ("rope_cos", c_vp), ("rope_sin", c_vp), ("rope_S", c_int), ("rope_ncols", c_int),
+        ("rope_cos", c_vp), ("rope_sin", c_vp), ("rope_S", c_int), ("rope_ncols", c_int), ("aux_grad", c_int),
     ]
 
 
@@ -142,9 +142,13 @@ def gemm(A, B, C, M, N, K, layout, lda, ldb, ldc, **kw):
 def _gemm_desc(A, B, C, M, N, K, layout, lda, ldb, ldc, *, epi=EPI_STORE, alpha=1.0, bias=None, ls=None,
                aux=None, ldaux=0, aux_out=None, ldaux_out=0, resid=None, ldr=0, accumulate=False,
                seed=0, drop_p=0.0, ldmask=0, batch=1, sA=0, sB=0, sC=0, ksplit_max=0, variant=None, drop_operand=0,
-               colsum=None, maskbits=None, split_ws=True, rope=None):
+               colsum=None, maskbits=None, split_ws=True, rope=None, aux_grad=False):
     _require_cuda(A, B, C)
+    if aux_grad and A.dtype == torch.float32:
+        raise RuntimeError("aux_grad (derivative stored as the GELU aux) is a bf16-path option; the fp32 parity "
+                           "kernels store the pre-activation")
     d = GemmDesc()
+    d.aux_grad = 1 if aux_grad else 0
     d.layout, d.epilogue = layout, epi
     d.out_f32 = 1 if C.dtype == torch.float32 else 0
     d.M, d.N, d.K, d.batch = int(M), int(N), int(K), int(batch)

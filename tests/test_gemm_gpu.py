@@ -516,3 +516,37 @@ def test_gemm_pair_xcd_split_full_shape(dev, shapes):
     for (_, _, C), ref in zip(ops, refs):
         err = (C - ref).abs().max().item()
         assert err < 4e-3 * T ** 0.5, err
+
+
+@pytest.mark.parametrize("M,v", [(8208, 11), (8208, 8), (1000, 0), (77, 1)])
+def test_gelu_aux_grad(dev, M, v):
+    """aux_grad: the GELU / QGELU forward epilogue stores bf16(act'(h)) at the bf16-rounded pre-activation h as its aux
+    (output unchanged), and the GELU_BWD / QGELU_BWD epilogue multiplies that aux in directly: against torch on the
+    same bf16 h, for the FE (11), LDS-staged v3 (8), automatic and scalar (1) epilogues."""
+    N, Kd = 2304, 512
+    g = torch.Generator(device=dev).manual_seed(M + v)
+    x = torch.randn(M, Kd, device=dev, generator=g).bfloat16()
+    w = (torch.randn(N, Kd, device=dev, generator=g) * (2.0 / Kd ** 0.5)).bfloat16()
+    bias = torch.randn(N, device=dev, generator=g)
+    wt = w.t().contiguous()
+    dy = torch.randn(M, Kd, device=dev, generator=g).bfloat16()
+    for epi, bepi in ((K.EPI_GELU, K.EPI_GELU_BWD), (K.EPI_QGELU, K.EPI_QGELU_BWD)):
+        h0, hpre = (torch.empty(M, N, device=dev, dtype=torch.bfloat16) for _ in range(2))
+        K.gemm(x, w, h0, M, N, Kd, K.GEMM_NT, Kd, Kd, N, epi=epi, bias=bias, aux_out=hpre, ldaux_out=N, variant=v)
+        h1, gpre = (torch.empty(M, N, device=dev, dtype=torch.bfloat16) for _ in range(2))
+        K.gemm(x, w, h1, M, N, Kd, K.GEMM_NT, Kd, Kd, N, epi=epi, bias=bias, aux_out=gpre, ldaux_out=N, variant=v,
+               aux_grad=True)
+        torch.cuda.synchronize()
+        assert torch.equal(h0, h1)  # the activation output does not change
+        hp = hpre.float().requires_grad_(True)
+        act = torch.nn.functional.gelu(hp) if epi == K.EPI_GELU else hp * torch.sigmoid(1.702 * hp)
+        (ref_g,) = torch.autograd.grad(act.sum(), hp)
+        torch.testing.assert_close(gpre.float(), ref_g, atol=2e-3, rtol=8e-3)
+        d0, d1 = (torch.empty(M, N, device=dev, dtype=torch.bfloat16) for _ in range(2))
+        K.gemm(dy, wt, d0, M, N, Kd, K.GEMM_NN, Kd, N, N, epi=bepi, aux=hpre, ldaux=N, variant=v)
+        K.gemm(dy, wt, d1, M, N, Kd, K.GEMM_NN, Kd, N, N, epi=bepi, aux=gpre, ldaux=N, variant=v, aux_grad=True)
+        torch.cuda.synchronize()
+        dv = dy.float() @ wt.float()
+        torch.testing.assert_close(d1.float(), dv * gpre.float(), atol=3e-2, rtol=2e-2)
+        # against the h-aux path: the only difference is the bf16 rounding of act'(h)
+        torch.testing.assert_close(d1.float(), d0.float(), atol=3e-2, rtol=2e-2)
