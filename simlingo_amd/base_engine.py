@@ -21,6 +21,7 @@ import os
 import numpy as np
 import torch
 
+from . import engine as _engine
 from . import kernels as K
 from .base_config import BaseConfig
 from .base_params import flat_layout, init_base_params
@@ -165,13 +166,14 @@ class BaseEngine(EngineOps):
                  ls=self.ones_D)
             h2, n2 = self._norm(xm, self.P[p + "ln2.w"], self.P[p + "ln2.b"], Mv, D, cfg.vit_eps)
             hpre, hact = self._e(Mv, F_), self._e(Mv, F_)
+            hgrad = _engine.GELU_AUX_GRAD and not self.precise  # hpre then holds qgelu'(h)
             with self._probe("vit.fc1"):
                 K.mm(h2, self.W[p + "fc1.w"], hact, bias=self.P[p + "fc1.b"], epi=K.EPI_QGELU, aux_out=hpre,
-                     ldaux_out=F_)
+                     ldaux_out=F_, aux_grad=hgrad)
             xo = self._e(Mv, D, dtype=F32)
             K.mm(hact, self.W[p + "fc2.w"], xo, bias=self.P[p + "fc2.b"], epi=K.EPI_RESID_LS, resid=xm, ldr=D,
                  ls=self.ones_D)
-            vit_saved.append(dict(h1=h1, n1=n1, qkv=qkv, o=o, lse=lse, h2=h2, n2=n2, hpre=hpre, hact=hact))
+            vit_saved.append(dict(h1=h1, n1=n1, qkv=qkv, o=o, lse=lse, h2=h2, n2=n2, hpre=hpre, hact=hact, hgrad=hgrad))
             x = xo
         sv["vit"] = vit_saved
         # ---- projector + spatial merge + projection ----
@@ -388,7 +390,7 @@ class BaseEngine(EngineOps):
             K.mm(gb, L["hact"], self.G[p + "fc2.w"], ta=True, tb=False, accumulate=True)
             dh = self._e(Mv, F_)
             self._mm_dx(gb, self.W[p + "fc2.w"], self.WT.get(p + "fc2.w"), dh, epi=K.EPI_QGELU_BWD, aux=L["hpre"], ldaux=F_,
-                 colsum=self.G[p + "fc1.b"])
+                 colsum=self.G[p + "fc1.b"], aux_grad=L["hgrad"])
             K.mm(dh, L["h2"], self.G[p + "fc1.w"], ta=True, tb=False, accumulate=True)
             dh2 = self._e(Mv, D, dtype=F32)
             self._mm_dx(dh, self.W[p + "fc1.w"], self.WT.get(p + "fc1.w"), dh2)

@@ -58,9 +58,11 @@ PAIR_SIDE = os.environ.get("SLX_PAIR_SIDE", "0") == "1"
 # operand, instead of a split-K GEMM per B gradient and a dA pass per site group: +1.75 % on the step (102.0 -> 103.8
 # samples/s in alternating runs, profiles/round4_lora_grad_group_ab.txt); SLX_LORA_GRAD_GROUP=0 restores the per-site path
 LORA_GRAD_GROUP = os.environ.get("SLX_LORA_GRAD_GROUP", "1") == "1"
-# SLX_GELU_AUX_GRAD=1: the InternViT fc1 GEMM stores gelu'(h) (bf16) as its aux instead of h, so the fc2 data-gradient
-# epilogue multiplies it in instead of evaluating gelu' (an rcp, an exp2 and ~10 FMA per element of 16400 x 4096)
-GELU_AUX_GRAD = os.environ.get("SLX_GELU_AUX_GRAD", "0") == "1"
+# The InternViT fc1 GEMM (and SimLingo-Base's CLIP fc1) stores act'(h) (bf16) as its aux instead of h, so the fc2
+# data-gradient epilogue multiplies it in instead of evaluating act' (an rcp, an exp2 and ~10 FMA per element of
+# 16400 x 4096): +0.5 % on the step (104.27 -> 104.83 samples/s, profiles/round4_gelu_aux_grad_ab.txt);
+# SLX_GELU_AUX_GRAD=0 stores the pre-activation as before
+GELU_AUX_GRAD = os.environ.get("SLX_GELU_AUX_GRAD", "1") == "1"
 ALIGN = 64  # elements; keeps every parameter view 256-B aligned
 
 
