@@ -63,6 +63,10 @@ LORA_GRAD_GROUP = os.environ.get("SLX_LORA_GRAD_GROUP", "1") == "1"
 # 16400 x 4096): +0.5 % on the step (104.27 -> 104.83 samples/s, profiles/round4_gelu_aux_grad_ab.txt);
 # SLX_GELU_AUX_GRAD=0 stores the pre-activation as before
 GELU_AUX_GRAD = os.environ.get("SLX_GELU_AUX_GRAD", "1") == "1"
+# SLX_LORA_GRAD_DEFER=1: a layer's attention-half LoRA gradient jobs ride in the NEXT layer's (in backward order)
+# MLP-half slx_lora_grad launch instead of a launch of their own (~50 MB, latency-bound alone); the norm backwards
+# then write a fresh bf16 dX buffer, so the deferred o-site job keeps the one it read
+LORA_GRAD_DEFER = os.environ.get("SLX_LORA_GRAD_DEFER", "0") == "1"
 ALIGN = 64  # elements; keeps every parameter view 256-B aligned
 
 
@@ -644,6 +648,8 @@ class VLAEngine(EngineOps):
         ws = K.attn_ws(B, S, Hq, Hk, self.device)
         lora = cfg.lora
         r = cfg.lora_r
+        defer = (lora and LORA_GRAD_GROUP and LORA_GRAD_DEFER and not self.precise and self._lg_shapes_ok())
+        done_pending = None
         for i in reversed(range(cfg.llm_layers)):
             p = f"llm.{i}."
             Ls = sv["llm"][i]
@@ -685,6 +691,11 @@ class VLAEngine(EngineOps):
                                dh2x[:, :d], sv, skip_db=side)
             del dgu
             self._lg_flush(Ml)  # before dxb (the down site's dy) is overwritten
+            if done_pending is not None:  # the previous layer's deferred attention-half jobs were in that launch
+                self._group_done(done_pending)
+                done_pending = None
+            if defer:
+                dxb = self._e(Ml, d)
             K.norm_bwd(Ls["n2"], dh2x, dX, dx_accumulate=True, dx_bf16=dxb)
             # o projection
             dox = self._e(Ml, qn + Po, dtype=F32)
@@ -705,12 +716,21 @@ class VLAEngine(EngineOps):
             if lora:
                 self._lora_bwd(i, ("q", "k", "v"), [dqkv[:, :qn], dqkv[:, qn:qn + kn], dqkv[:, qn + kn:]], hx[:, d:],
                                hx[:, :d], dhx[:, d:], dhx[:, :d], sv)
-            self._lg_flush(Ml)  # before dxb (the o site's dy) is overwritten
+            if defer:  # the attention-half jobs wait for the next layer's MLP-half launch; the o site keeps its dxb
+                dxb = self._e(Ml, d)
+            else:
+                self._lg_flush(Ml)  # before dxb (the o site's dy) is overwritten
             K.norm_bwd(Ls["n1"], dhx, dX, dx_accumulate=True, dx_bf16=dxb)
             del dqkv, dhx, dh2x
             if lora:
                 self._join_side()  # the layer's gradients are complete before its bucket can be exchanged
-                self._group_done(f"llm{i}")
+                if defer:
+                    done_pending = f"llm{i}"
+                else:
+                    self._group_done(f"llm{i}")
+        if done_pending is not None:
+            self._lg_flush(Ml)
+            self._group_done(done_pending)
         # ---------------- token assembly backward ----------------
         qg = self.G["drv.query_route"]  # [20, d] followed by [10, d] (adjacent)
         K.call("slx_gather_sum", K.P(dX), d, K.P(dplan["query_pos"]), B, cfg.n_queries, d, K.P(qg), 0, K.stream_ptr())

@@ -13,10 +13,11 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def _step(dev, side, monkeypatch, pair_side=False, group=False):
+def _step(dev, side, monkeypatch, pair_side=False, group=False, defer=False):
     import simlingo_amd.engine as E
     monkeypatch.setattr(E, "PAIR_SIDE", pair_side)
     monkeypatch.setattr(E, "LORA_GRAD_GROUP", group)  # the side-stream knobs act on the per-site LoRA path
+    monkeypatch.setattr(E, "LORA_GRAD_DEFER", defer)
     from simlingo_amd.config import full_config
     from simlingo_amd.params import init_params
     from simlingo_amd.plan import plan_from_example
@@ -78,3 +79,8 @@ def test_lora_grad_group_matches(dev, monkeypatch):
     o1, g1, _ = _step(dev, False, monkeypatch, group=True)
     assert torch.equal(o0, o1)
     _check(g0, g0b, g1)
+    # SLX_LORA_GRAD_DEFER: the attention-half jobs in the next layer's launch; every layer's group still marked done
+    o2, g2, marks = _step(dev, False, monkeypatch, group=True, defer=True)
+    assert torch.equal(o0, o2)
+    _check(g0, g0b, g2)
+    assert [g for g, _ in marks if g.startswith("llm")] == ["llm1", "llm0"], marks
