@@ -67,6 +67,10 @@ GELU_AUX_GRAD = os.environ.get("SLX_GELU_AUX_GRAD", "1") == "1"
 # MLP-half slx_lora_grad launch instead of a launch of their own (~50 MB, latency-bound alone); the norm backwards
 # then write a fresh bf16 dX buffer, so the deferred o-site job keeps the one it read
 LORA_GRAD_DEFER = os.environ.get("SLX_LORA_GRAD_DEFER", "0") == "1"
+# SLX_VIT_RESID_VARIANT / SLX_LLM_RESID_VARIANT: main-loop member for the residual-epilogue GEMMs (InternViT proj / fc2
+# forward, Qwen2 o / down forward); 0 = the cost model's choice (A/B hook)
+VIT_RESID_VARIANT = int(os.environ.get("SLX_VIT_RESID_VARIANT", "0"))
+LLM_RESID_VARIANT = int(os.environ.get("SLX_LLM_RESID_VARIANT", "0"))
 ALIGN = 64  # elements; keeps every parameter view 256-B aligned
 
 
@@ -424,7 +428,8 @@ class VLAEngine(EngineOps):
             if lora:
                 L.update(self._lora_down(o, i, ("o",), ox[:, qn:], sv))
             Xm = self._e(Ml, d, dtype=F32)
-            K.mm(ox, cat["o"] if lora else self.W[p + "o_w"], Xm, epi=K.EPI_RESID_LS, resid=X, ldr=d, ls=self.ones_d)
+            K.mm(ox, cat["o"] if lora else self.W[p + "o_w"], Xm, epi=K.EPI_RESID_LS, resid=X, ldr=d, ls=self.ones_d,
+                 variant=LLM_RESID_VARIANT or None)
             h2x = self._buf(("h2x", i), Ml, d + Pg, zero=lora)
             h2, nrm2 = self._norm(Xm, self.P[p + "ln2"], None, Ml, d, cfg.rms_eps, rms=True, out=h2x[:, :d])
             if lora:
@@ -438,7 +443,7 @@ class VLAEngine(EngineOps):
                 L.update(self._lora_down(act, i, ("down",), ax[:, Fl:], sv))
             Xo = self._e(Ml, d, dtype=F32)
             K.mm(ax, cat["down"] if lora else self.W[p + "down_w"], Xo, epi=K.EPI_RESID_LS, resid=Xm, ldr=d,
-                 ls=self.ones_d)
+                 ls=self.ones_d, variant=LLM_RESID_VARIANT or None)
             llm_saved.append(dict(X=X, hx=hx, n1=nrm1, qkv=qkv, ox=ox, lse=lse, Xm=Xm, h2x=h2x, n2=nrm2, gu=gu, ax=ax,
                                   lora=L))
             X = Xo
@@ -479,7 +484,7 @@ class VLAEngine(EngineOps):
             xm = self._e(Mv, D, dtype=F32)
             y1 = self._e(Mv, D)
             K.mm(o, self.W[p + "proj.w"], xm, bias=self.P[p + "proj.b"], epi=K.EPI_RESID_LS, resid=x, ldr=D,
-                 ls=self.P[p + "ls1"], aux_out=y1, ldaux_out=D)
+                 ls=self.P[p + "ls1"], aux_out=y1, ldaux_out=D, variant=VIT_RESID_VARIANT or None)
             h2, n2 = self._norm(xm, self.P[p + "ln2.w"], self.P[p + "ln2.b"], Mv, D, cfg.vit_eps)
             hpre = self._e(Mv, F_)
             hact = self._e(Mv, F_)
@@ -490,7 +495,7 @@ class VLAEngine(EngineOps):
             xo = self._e(Mv, D, dtype=F32)
             y2 = self._e(Mv, D)
             K.mm(hact, self.W[p + "fc2.w"], xo, bias=self.P[p + "fc2.b"], epi=K.EPI_RESID_LS, resid=xm, ldr=D,
-                 ls=self.P[p + "ls2"], aux_out=y2, ldaux_out=D)
+                 ls=self.P[p + "ls2"], aux_out=y2, ldaux_out=D, variant=VIT_RESID_VARIANT or None)
             vit_saved.append(dict(x=x, h1=h1, n1=n1, qkv=qkv, o=o, lse=lse, y1=y1, xm=xm, h2=h2, n2=n2, hpre=hpre,
                                   hact=hact, y2=y2, hgrad=hgrad))
             x = xo
