@@ -14,9 +14,9 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def _worker(rank, port, ret):
+def _worker(rank, port, ret, geom="tiny"):
     import torch.distributed as dist
-    from simlingo_amd.config import tiny_config
+    from simlingo_amd.config import full_config, tiny_config
     from simlingo_amd.engine import VLAEngine
     from simlingo_amd.plan import plan_from_example
     from simlingo_amd.synthetic import make_batch
@@ -25,8 +25,9 @@ def _worker(rank, port, ret):
     torch.cuda.set_device(0)
     dev = torch.device("cuda:0")
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
-    cfg = tiny_config()
-    ex = make_batch(cfg, B=2, s_text=24, n_loss=4, seed=7)
+    # full: the real widths (1 ViT + 2 Qwen2 layers), where the LoRA gradients take the grouped slx_lora_grad path
+    cfg = tiny_config() if geom == "tiny" else full_config(vit_layers=1, llm_layers=2)
+    ex = make_batch(cfg, B=2, s_text=24 if geom == "tiny" else 64, n_loss=4, seed=7)
     plan = plan_from_example(cfg, ex)
 
     def run(distributed):
@@ -56,13 +57,14 @@ def _worker(rank, port, ret):
     dist.destroy_process_group()
 
 
-def test_rccl_bucketed_exchange_on_hardware(dev):
+@pytest.mark.parametrize("geom", ["tiny", "full"])
+def test_rccl_bucketed_exchange_on_hardware(dev, geom):
     import torch.multiprocessing as mp
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     ret = mp.Manager().dict()
-    mp.spawn(_worker, args=(port, ret), nprocs=1, join=True)
+    mp.spawn(_worker, args=(port, ret, geom), nprocs=1, join=True)
     print(dict(ret))
     assert ret["backend"] == "nccl"
     assert ret["nb"] > 1 and ret["issued"] == ret["nb"] and ret["before_end"] >= ret["nb"] - 1
