@@ -58,6 +58,8 @@ def parse():
     ap.add_argument("--wire", default="auto", choices=["auto", "f32", "bf16"],
                     help="gradient all-reduce wire dtype (bf16: half the xGMI bytes, f32 accumulation kept; "
                          "auto = bf16 at N > 1, SURVEY.md §8e)")
+    ap.add_argument("--no-dropin", action="store_true", help="skip the drop-in loop key (DataLoader + Collate + "
+                    "DrivingModel.training_step + FusedAdamW + OneCycleLR)")
     ap.add_argument("--no-extras", action="store_true",
                     help="skip the config-4 (S_text 512, 128 loss tokens) step, the config-5 agent latency and the "
                          "config-2 SimLingo-Base step that the N = 1 vla line carries as extra keys")
@@ -287,6 +289,72 @@ def agent_latency(dev, frames=5, new_tokens=100, s_text=64):
     return bench_infer.measure(dev, frames=frames, warmup=1, new_tokens=new_tokens, s_text=s_text)
 
 
+def dropin_loader(B=8, steps=10, warmup=3, workers=4, s_text=256, n_loss=16):
+    """The reference's data path for the drop-in step (datamodule.py:275-284: DataLoader(num_workers, collate_fn=
+    dl_collate_fn, pin_memory)): a 'dataset' of (warmup + steps) * B distinct synthetic DatasetOutputs (1024 x 512
+    frames cropped to 359 rows, chat conversations of the config-3 length), batched by a DataLoader whose workers run
+    Collate.host (tokenisation, masks, labels, stacked uint8 frames). Built and its workers forked BEFORE the process
+    touches the GPU, so no worker inherits device state; the training process runs Collate.device (pinned-ring H2D +
+    HIP frame kernel) per batch."""
+    os.environ.setdefault("TOKENIZERS_PARALLELISM", "false")
+    from torch.utils.data import DataLoader
+    from simlingo_amd.collate import Collate
+    from simlingo_amd.config import full_config
+    from simlingo_amd.synthetic import synthetic_samples, synthetic_tokenizer
+    cfg = full_config()
+    col = Collate(synthetic_tokenizer(cfg), num_image_tokens_per_patch=cfg.img_tokens_per_tile,
+                  num_image_patches=cfg.tiles, device="cuda:0")
+    data = synthetic_samples(cfg, (warmup + steps) * B, s_text=s_text, n_loss=n_loss, seed=4242)
+    loader = DataLoader(data, batch_size=B, shuffle=False, num_workers=workers, collate_fn=col.host,
+                        prefetch_factor=2, persistent_workers=False)
+    return dict(col=col, it=iter(loader), B=B, steps=steps, warmup=warmup, workers=workers, cfg=cfg)
+
+
+def dropin_line(dl, dev):
+    """The drop-in training loop, timed: per step one fresh collated batch (Collate.device on the DataLoader's host
+    batch: H2D + HIP frames), DrivingModel.training_step -> loss.backward() -> FusedAdamW.step() ->
+    OneCycleLR.step() -> zero_grad(), exactly the calls Lightning makes (driving.py:263-271, 718-732)."""
+    from simlingo_amd.driving import DrivingModel
+    from simlingo_amd.params import init_params
+    cfg, col, it, B = dl["cfg"], dl["col"], dl["it"], dl["B"]
+    variant = {"variant": "OpenGVLab/InternVL2-1B"}
+    m = DrivingModel(vision_model=dict(variant), language_model=dict(variant, lora=True, lora_r=32, lora_alpha=64,
+                                                                     lora_dropout=0.1),
+                     lr=cfg.lr, init_params=init_params(cfg, seed=0, lora_b_std=0.02, device=dev))
+    m.max_steps = 10000
+    m.build_engine(dev)
+    conf = m.configure_optimizers()
+    opt, sched = conf["optimizer"], conf["lr_scheduler"]["scheduler"]
+
+    def step():
+        ex = col.device(next(it))
+        out = m.training_step(ex, 0)
+        out["loss"].backward()
+        opt.step()
+        sched.step()
+        opt.zero_grad()
+        return out["loss"]
+
+    for _ in range(dl["warmup"]):
+        loss = step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(dl["steps"]):
+        loss = step()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    v = B * dl["steps"] / dt
+    res = {"workload": "drop-in loop: DataLoader(workers run Collate.host) -> Collate.device (pinned H2D + HIP frames) "
+                       "-> DrivingModel.training_step -> loss.backward() -> FusedAdamW.step -> OneCycleLR.step, "
+                       "fresh batch per step, B=8, S_llm 798",
+           "value": round(v, 3), "unit": "samples/s", "ms_per_step": round(dt / dl["steps"] * 1e3, 3),
+           "steps": dl["steps"], "warmup": dl["warmup"], "loader_workers": dl["workers"],
+           "step_mfma_frac": round(v * VLA_GFLOP_PER_SAMPLE / 1e3 / PEAK_BF16_TFLOPS, 4),
+           "loss_last": round(loss.item(), 5)}
+    del m, opt, sched
+    return res
+
+
 def traffic_record(tag, flop_M):
     """PMC-measured HBM bytes per FC1 launch (profiles/*_{tag}_fc1_traffic.json, newest first)."""
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", f"*{tag}_fc1_traffic.json")), reverse=True):
@@ -304,6 +372,12 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    dl = None
+    if world == 1 and args.config == "vla" and not args.no_extras and not args.no_dropin:
+        try:  # forks the loader workers now, before anything touches the GPU
+            dl = dropin_loader()
+        except Exception as e:
+            dl = {"error": repr(e)[:200]}
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
@@ -398,6 +472,14 @@ def main():
             res["comm_exposed_ms"] = cs.pop("comm_exposed_ms")
             res["comm"] = cs
     if rank == 0 and world == 1 and args.config == "vla" and not args.no_extras:
+        if dl is not None and "error" not in dl:
+            try:
+                res["dropin"] = dropin_line(dl, dev)
+                res["dropin"]["vs_value"] = round(res["dropin"]["value"] / value, 4)
+            except Exception as e:
+                res["dropin"] = {"error": repr(e)[:300]}
+        elif dl is not None:
+            res["dropin"] = dl
         try:
             res["config4"] = config4_step(args, dev)
         except Exception as e:  # the bench line must still be printed

@@ -200,7 +200,8 @@ class DrivingModel(_Base):
         opt = BaseFusedAdamW(self, lr=self.lr, vision_lr=self.vision_lr, betas=self.betas,
                              weight_decay=self.weight_decay, eps=self.base_cfg.eps, max_norm=self.base_cfg.grad_clip)
         trainer = getattr(self, "_trainer", None)
-        max_steps = getattr(trainer, "max_steps", -1) if trainer is not None else -1
+        max_steps = getattr(self, "max_steps", None) or (
+            getattr(trainer, "max_steps", -1) if trainer is not None else -1)
         if max_steps is None or max_steps <= 0:
             max_steps = int(getattr(trainer, "estimated_stepping_batches", 10000) or 10000) if trainer is not None else 10000
         lrs = [pg["lr"] for pg in opt.param_groups]

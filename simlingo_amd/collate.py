@@ -161,7 +161,12 @@ class DatasetOutput(NamedTuple):
 class Collate:
     """dl_collate_fn (datamodule.py:310-443) for the VLA: frames -> HIP tiles (`pixel_fn`, default the frame kernel
     of simlingo_amd.frames on `device`), conversations -> chat-template token ids and loss masks, labels -> tensors.
-    `tokenizer` must already carry the placeholder special tokens and left padding (datamodule.py:130-138)."""
+    `tokenizer` must already carry the placeholder special tokens and left padding (datamodule.py:130-138).
+
+    The work splits at the host/device line so the host half can run where the reference runs its whole collate, in
+    the DataLoader workers (datamodule.py:275-284, num_workers = 10): `host(data)` is CPU-only and picklable (token
+    ids, masks, labels, the stacked uint8 frames as `camera_images`), `device(example)` uploads the frames through a
+    pinned ring and tiles them with the HIP kernel in the training process. `__call__` = device(host(data))."""
 
     def __init__(self, tokenizer, num_image_tokens_per_patch: int = 256, num_image_patches: int = 2,
                  device=None, pixel_fn: Optional[Callable] = None, predict: bool = False, input_size: int = 448):
@@ -169,30 +174,43 @@ class Collate:
         self.num_image_patches = num_image_patches
         self.num_image_tokens_total = num_image_tokens_per_patch * num_image_patches
         self.predict = predict
-        if pixel_fn is None:
-            from .frames import FramePreprocessor
-            dev = torch.device(device) if device is not None else torch.device("cuda")
-            pres = {}
-
-            def pixel_fn(frames_u8, max_num_grid):  # preprocess_image_batch, one cached geometry per frame size
-                B, _, H, W = frames_u8.shape
-                key = (H, W, max_num_grid)
-                if key not in pres:
-                    pres[key] = FramePreprocessor(H, W, dev, input_size, max_num_grid, False, cut_bottom=False)
-                pre = pres[key]
-                return {"pixel_values": pre(frames_u8.to(dev, non_blocking=True), channels_first=True),
-                        "image_sizes": pre.image_sizes(B)}
+        self.device_ = device
+        self.input_size = input_size
         self.pixel_fn = pixel_fn
+        self._pres = {}
+        self._uploader = None
 
-    def __call__(self, data: List[DatasetOutput]) -> DrivingExample:
+    def __getstate__(self):  # DataLoader workers get the host half only
+        st = dict(self.__dict__)
+        st["_pres"], st["_uploader"] = {}, None
+        return st
+
+    def _default_pixels(self, frames_u8, max_num_grid):
+        """preprocess_image_batch on the device: pinned-ring upload (no pageable H2D, no host sync) + frame kernel,
+        one cached geometry per frame size."""
+        from .frames import FramePreprocessor, FrameUploader
+        dev = torch.device(self.device_) if self.device_ is not None else torch.device("cuda")
+        B, _, H, W = frames_u8.shape
+        key = (H, W, max_num_grid)
+        if key not in self._pres:
+            self._pres[key] = FramePreprocessor(H, W, dev, self.input_size, max_num_grid, False, cut_bottom=False)
+        pre = self._pres[key]
+        if not frames_u8.is_cuda:
+            if self._uploader is None:
+                self._uploader = FrameUploader(dev)
+            frames_u8 = self._uploader(frames_u8)
+        out = {"pixel_values": pre(frames_u8, channels_first=True), "image_sizes": pre.image_sizes(B)}
+        if self._uploader is not None:
+            self._uploader.release()
+        return out
+
+    def host(self, data: List[DatasetOutput]) -> DrivingExample:
         B = len(data)
         img = data[0].image_ff
         T, C, H, W = img.shape
         assert T == 1, "Only one timestep as input supported"
-        frames = torch.from_numpy(np.stack([d.image_ff if d.image_ff is not None else np.zeros_like(img) for d in data]))
-        processed = self.pixel_fn(frames.view(B, C, H, W), self.num_image_patches)  # [B, C, H, W] uint8
-        pix = processed["pixel_values"]
-        pix = pix.view(B, T, pix.shape[1], C, pix.shape[-2], pix.shape[-1])
+        frames = torch.from_numpy(np.stack([(d.image_ff if d.image_ff is not None else np.zeros_like(img)).reshape(C, H, W)
+                                            for d in data]))
         conv_d, q_d = get_custom_chat_template([d.conversation for d in data], self.tokenizer,
                                                self.num_image_tokens_total)
         placeholders = [{self.tokenizer.convert_tokens_to_ids(k): v for k, v in d.placeholder_values.items()}
@@ -204,7 +222,7 @@ class Collate:
         answer = LanguageLabel(None, None, None, None, [d.answer[0]["content"][0]["text"] for d in data], None)
         f32 = torch.float32
         di = DrivingInput(
-            camera_images=pix, image_sizes=processed["image_sizes"],
+            camera_images=frames, image_sizes=None,
             camera_intrinsics=camera_intrinsics(W, H, 110).unsqueeze(0).repeat(B, 1, 1),
             camera_extrinsics=camera_extrinsics().unsqueeze(0).repeat(B, 1, 1),
             vehicle_speed=torch.tensor(np.asarray([d.speed for d in data]), dtype=f32),
@@ -218,3 +236,17 @@ class Collate:
         qa = [d.qa_templates[0] if d.qa_templates is not None else None for d in data] if self.predict else None
         return DrivingExample(driving_input=di, driving_label=dl,
                               run_id=encode_uint8([d.measurement_path for d in data], 1000), qa_templates=qa)
+
+    def device(self, ex: DrivingExample) -> DrivingExample:
+        """uint8 frames [B, C, H, W] of a host() batch -> pixel tiles [B, T=1, tiles, C, s, s] (device)."""
+        di = ex.driving_input
+        frames = di.camera_images
+        B, C = frames.shape[:2]
+        fn = self.pixel_fn if self.pixel_fn is not None else self._default_pixels
+        processed = fn(frames, self.num_image_patches)
+        pix = processed["pixel_values"]
+        pix = pix.view(B, 1, pix.shape[1], C, pix.shape[-2], pix.shape[-1])
+        return ex._replace(driving_input=di._replace(camera_images=pix, image_sizes=processed["image_sizes"]))
+
+    def __call__(self, data: List[DatasetOutput]) -> DrivingExample:
+        return self.device(self.host(data))

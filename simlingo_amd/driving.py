@@ -52,8 +52,9 @@ class _VLAStep(torch.autograd.Function):
         eng = model.engine
         dev = eng.device
         di, lab = example.driving_input, example.driving_label
-        out4, rp, sp = eng.forward(di.camera_images.to(dev, non_blocking=True), plan, dplan,
-                                   lab.path.to(dev, non_blocking=True), lab.waypoints.to(dev, non_blocking=True),
+        path = dplan["path"] if "path" in dplan else lab.path.to(dev, non_blocking=True)
+        wps = dplan["waypoints"] if "waypoints" in dplan else lab.waypoints.to(dev, non_blocking=True)
+        out4, rp, sp = eng.forward(di.camera_images.to(dev, non_blocking=True), plan, dplan, path, wps,
                                    training=model.training)
         ctx.model = model
         model._last_predictions = {"route": rp, "speed_wps": sp}
@@ -136,9 +137,12 @@ class DrivingModel(_Base):
         """driving.py:236-261 -> (TrainingOutput, loss_logs) or (loss_dict, pred_labels)."""
         eng = self.build_engine()
         plan = plan_from_example(self.vla_cfg, example)
-        dplan = plan.to_device(eng.device)
+        lab = example.driving_label
+        # host-side labels ride in the plan's single pinned H2D copy (no pageable copy, no host sync per step)
+        extra = {k: getattr(lab, k) for k in ("path", "waypoints") if not getattr(lab, k).is_cuda}
+        dplan = plan.to_device(eng.device, extra=extra)
         out4 = _VLAStep.apply(self.anchor, self, example, plan, dplan)
-        values, counts = self._per_sample_losses(eng, plan)
+        values, counts = self._per_sample_losses(eng, plan, dplan)
         averages = {"language_loss": out4[1], "route_loss": out4[2], "speed_wps_loss": out4[3]}
         preds = self._last_predictions
         if per_sample:  # driving.py:256-259: ({key: (values, counts)}, prediction labels)
@@ -147,7 +151,7 @@ class DrivingModel(_Base):
         out = TrainingOutput(loss=out4[0], loss_averages=averages, loss_values=values, loss_counts=counts)
         return out, {}
 
-    def _per_sample_losses(self, eng, plan):
+    def _per_sample_losses(self, eng, plan, dplan):
         """summarise_losses inputs (models/utils.py:7-41, AdaptorList.compute_loss adaptors.py:333-355): language_loss
         CE per shifted label position [B, L-1] with its mask, route_loss [B, 20] and speed_wps_loss [B, 10] with ones
         counts - read from the engine's per-row loss buffers of this step (no host sync)."""
@@ -159,7 +163,7 @@ class DrivingModel(_Base):
         cnt = torch.zeros(B, max(L - 1, 0), dtype=torch.bool, device=dev)
         R = plan.loss_pos.shape[0]
         if R:
-            bt = torch.from_numpy(plan.loss_bt).to(dev)
+            bt = dplan["loss_bt"].long()
             lang[bt[:, 0], bt[:, 1]] = sv["ce_loss"][:R]
             cnt[bt[:, 0], bt[:, 1]] = True
         route = sv["route_loss"].view(B, cfg.n_route)

@@ -244,10 +244,58 @@ class FramePipeline:
         return out, self.pre.image_sizes(self.B)
 
 
+class FrameUploader:
+    """uint8 frames host -> HBM through a ring of (pinned slot, device slot) pairs, the copy on a side stream.
+
+    __call__(frames) copies the stacked uint8 frames into a pinned slot, enqueues the H2D on the copy
+    stream and makes the current stream wait for it; `release(t)` (called by the consumer after the kernel that reads
+    the device slot was enqueued) records when the slot may be overwritten. The host never waits on the GPU except when
+    a slot is still in use `depth` batches later. Collate's default image path."""
+
+    def __init__(self, device, depth: int = 3):
+        self.device = torch.device(device)
+        self.depth = depth
+        self.slots = [None] * depth      # (shape, pinned, device)
+        self.copied = [None] * depth     # event: the H2D that last read the pinned slot is done
+        self.consumed = [None] * depth   # event: the kernel that last read the device slot is done
+        self.i = 0
+        self.copy_stream = torch.cuda.Stream(device=self.device)
+
+    def __call__(self, frames) -> torch.Tensor:
+        """frames: uint8 host tensor / array [B, ...] -> the device slot holding a copy (the current stream waits)."""
+        frames = torch.as_tensor(frames)
+        shape = tuple(frames.shape)
+        s = self.i % self.depth
+        self.i += 1
+        for ev in (self.copied[s], self.consumed[s]):
+            if ev is not None:
+                ev.synchronize()
+        if self.slots[s] is None or self.slots[s][0] != shape:
+            self.slots[s] = (shape, torch.empty(shape, dtype=torch.uint8).pin_memory(),
+                             torch.empty(shape, dtype=torch.uint8, device=self.device))
+        _, host, dev = self.slots[s]
+        host.copy_(frames)
+        cur = torch.cuda.current_stream(self.device)
+        with torch.cuda.stream(self.copy_stream):
+            dev.copy_(host, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(self.copy_stream)
+        self.copied[s] = ev
+        cur.wait_event(ev)
+        self._last = s
+        return dev
+
+    def release(self):
+        """The current stream's work enqueued so far (the tiling kernel) is the last reader of the newest slot."""
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        self.consumed[self._last] = ev
+
+
 def algorithmic_bytes(pre: FramePreprocessor, B: int) -> int:
     """HBM bytes one launch must move: the cropped uint8 frames once + the f32 tiles once."""
     return B * (pre.H * pre.W * 3 + pre.tiles * 3 * pre.tile * pre.tile * 4)
 
 
-__all__ = ["FramePreprocessor", "FramePipeline", "preprocess_image_batch", "bottom_crop_rows", "closest_grid",
+__all__ = ["FramePreprocessor", "FramePipeline", "FrameUploader", "preprocess_image_batch", "bottom_crop_rows", "closest_grid",
            "resample_coeffs", "algorithmic_bytes"]

@@ -70,17 +70,19 @@ def lib():
         for name, args in _SIGS.items():
             f = getattr(_lib, name)
             f.argtypes = args
-            f.restype = c_int
+            f.restype = _RESTYPE.get(name, c_int)
     return _lib
 
 
-def register(name: str, argtypes: list):
-    """Declare a C-ABI entry point (used by modules that add bindings)."""
+def register(name: str, argtypes: list, restype=None):
+    """Declare a C-ABI entry point (used by modules that add bindings); restype defaults to int."""
     _SIGS[name] = argtypes
+    if restype is not None:
+        _RESTYPE[name] = restype
     if _lib is not None:
         f = getattr(_lib, name)
         f.argtypes = argtypes
-        f.restype = c_int
+        f.restype = _RESTYPE.get(name, c_int)
 
 
 def exported_symbols() -> list[str]:
@@ -304,7 +306,6 @@ for _n, _a in {
     "slx_lora_pack_a": [_vp, ctypes.c_int64, ctypes.c_int, ctypes.c_int, _vp, _vp],
     "slx_lora_bwd": [ctypes.POINTER(LoraBwdDesc), _vp],
     "slx_lora_bwd_ws": [ctypes.POINTER(LoraBwdDesc), _vp, _I, _vp],
-    "slx_lora_bwd_ws_floats": [_I, _i, _i],  # int64 result, < 2^31 at every shape used (restype int)
     "slx_lora_grad": [ctypes.POINTER(LoraGradJob), _i, _I, _vp],
     "slx_dropout_bits": [ctypes.POINTER(DropoutBitsDesc), _vp],
     "slx_attn_bwd": [ctypes.POINTER(AttnDesc), ctypes.POINTER(AttnBwdDesc), _vp],
@@ -359,6 +360,7 @@ for _n, _a in {
     "slx_llava_merge_fwd_f32": [_vp, _i, _I, _i, _i, _i, _i, _i, _i, _i, _i, _vp, _vp, _vp],
 }.items():
     register(_n, _a)
+register("slx_lora_bwd_ws_floats", [_I, _i, _i], restype=c_i64)  # int64_t result (include/slx.h)
 
 
 def attn_desc(q, k, v, o, lse, *, B, S, Hq, Hkv, causal=False, seqlens=None, scale=0.125):

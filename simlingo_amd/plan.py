@@ -39,24 +39,81 @@ class Plan:
     loss_bt: np.ndarray | None = None  # [R, 2] (sample, position in the shifted [B, L-1] label grid) of each loss row
     perm: np.ndarray | None = None     # [B, S] AdaptorList.forward's valid-first permutation (adaptors.py:322-325)
 
-    def to_device(self, device) -> dict:
-        t = lambda a, dt=torch.int32: torch.from_numpy(np.ascontiguousarray(a)).to(dt).pin_memory().to(device, non_blocking=True) \
-            if torch.cuda.is_available() and str(device) != "cpu" else torch.from_numpy(np.ascontiguousarray(a)).to(dt)
-        return {"code": t(self.code), "seqlens": t(self.seqlens), "img_pos": t(self.img_pos),
-                "wp_coords": t(self.wp_coords, torch.float32), "wp_pos": t(self.wp_pos),
-                "query_pos": t(self.query_pos.reshape(-1)), "loss_pos": t(self.loss_pos),
-                "loss_labels": t(self.loss_labels)}
+    def to_device(self, device, extra: dict | None = None) -> dict:
+        """Every index array (and the `extra` f32 host tensors, e.g. the step's labels) packed into ONE pinned staging
+        slot and sent to the device in ONE non-blocking copy on the current stream; the returned dict holds views of
+        that device buffer. No host<->device synchronisation: the slot is reused only after the copy that last read it
+        has executed (a ring of events), so the host can build the next batch while the GPU runs this one."""
+        i32 = lambda a: np.ascontiguousarray(a, dtype=np.int32).reshape(-1)
+        f32 = lambda a: np.ascontiguousarray(a, dtype=np.float32).reshape(-1).view(np.int32)
+        bt = self.loss_bt if self.loss_bt is not None else np.zeros((0, 2))
+        parts = [("code", i32(self.code), None, False), ("seqlens", i32(self.seqlens), None, False),
+                 ("img_pos", i32(self.img_pos), None, False), ("wp_coords", f32(self.wp_coords), (-1, 2), True),
+                 ("wp_pos", i32(self.wp_pos), None, False), ("query_pos", i32(self.query_pos), None, False),
+                 ("loss_pos", i32(self.loss_pos), None, False), ("loss_labels", i32(self.loss_labels), None, False),
+                 ("loss_bt", i32(bt), (-1, 2), False)]
+        for k, t in (extra or {}).items():
+            a = t.detach().cpu().numpy() if isinstance(t, torch.Tensor) else np.asarray(t)
+            parts.append((k, f32(a), tuple(a.shape), True))
+        return stage_to_device(parts, device)
 
 
-def build_plan(cfg: VLAConfig, ids, valid, loss_mask, placeholder_values, n_img: int | None = None) -> Plan:
-    ids = np.asarray(ids.cpu() if isinstance(ids, torch.Tensor) else ids, dtype=np.int64)
-    valid = np.asarray(valid.cpu() if isinstance(valid, torch.Tensor) else valid, dtype=bool)
-    loss_mask = np.asarray(loss_mask.cpu() if isinstance(loss_mask, torch.Tensor) else loss_mask, dtype=bool)
+class _PinnedRing:
+    """Pinned int32 staging slots of one device, each guarded by the event of the H2D copy that last read it."""
+
+    def __init__(self, depth: int = 4):
+        self.slots = [None] * depth
+        self.events = [None] * depth
+        self.i = 0
+
+    def take(self, n: int):
+        s = self.i % len(self.slots)
+        self.i += 1
+        if self.events[s] is not None:
+            self.events[s].synchronize()  # normally long done: that copy ran at the start of an earlier step
+        buf = self.slots[s]
+        if buf is None or buf.numel() < n:
+            buf = self.slots[s] = torch.empty(max(n, 1 << 16), dtype=torch.int32).pin_memory()
+        return s, buf
+
+
+_rings: dict = {}
+
+
+def stage_to_device(parts, device) -> dict:
+    """parts: [(name, int32 words (f32 data viewed as int32), shape or None, is_f32)] -> {name: device view}: one pinned
+    slot, one H2D copy on the current stream."""
+    device = torch.device(device)
+    if device.type != "cuda" or not torch.cuda.is_available():
+        raise RuntimeError("the token plan is staged for the MI355X (HIP) path only; there is no CPU path")
+    n = sum(a.size for _, a, _, _ in parts)
+    ring = _rings.setdefault(device, _PinnedRing())
+    s, host = ring.take(n)
+    hv = host.numpy()
+    off, spans = 0, []
+    for name, a, shape, is_f32 in parts:
+        hv[off:off + a.size] = a
+        spans.append((name, off, a.size, shape, is_f32))
+        off += a.size
+    dev = torch.empty(max(n, 1), dtype=torch.int32, device=device)
+    dev[:n].copy_(host[:n], non_blocking=True)
+    ev = torch.cuda.Event()
+    ev.record()
+    ring.events[s] = ev
+    out = {}
+    for name, o, size, shape, is_f32 in spans:
+        v = dev[o:o + size]
+        if is_f32:
+            v = v.view(torch.float32)
+        out[name] = v.view(shape) if shape is not None else v
+    return out
+
+
+def language_codes(cfg: VLAConfig, ids: np.ndarray, placeholder_values, n_img: int):
+    """[B, L] codes of the language rows after replace_placeholder_tokens (before the valid-first permutation), and the
+    waypoint-encoder input coordinates in the reference's row order."""
     B, L = ids.shape
-    NQ = cfg.n_queries
-    S = L + NQ
     V = cfg.vocab
-    n_img = cfg.img_tokens * B if n_img is None else n_img
     # language codes before replacement: embed_tokens(ids.clamp(0, V-1))  (adaptors.py:256)
     lang = _code(KIND_TOKEN, np.clip(ids, 0, V - 1))
     # 2a placeholders (internvl2_model.py:53-91): unique ids >= first added special id; first
@@ -83,19 +140,34 @@ def build_plan(cfg: VLAConfig, ids, valid, loss_mask, placeholder_values, n_img:
     flat = lang.reshape(-1)
     flat[sel] = _code(KIND_IMG, np.arange(n_sel))
     lang = flat.reshape(B, L)
+    return lang, wp_coords
+
+
+def build_plan(cfg: VLAConfig, ids, valid, loss_mask, placeholder_values, n_img: int | None = None) -> Plan:
+    ids = np.asarray(ids.cpu() if isinstance(ids, torch.Tensor) else ids, dtype=np.int64)
+    valid = np.asarray(valid.cpu() if isinstance(valid, torch.Tensor) else valid, dtype=bool)
+    loss_mask = np.asarray(loss_mask.cpu() if isinstance(loss_mask, torch.Tensor) else loss_mask, dtype=bool)
+    B, L = ids.shape
+    NQ = cfg.n_queries
+    S = L + NQ
+    V = cfg.vocab
+    n_img = cfg.img_tokens * B if n_img is None else n_img
+    lang, wp_coords = language_codes(cfg, ids, placeholder_values, n_img)
     # AdaptorList.forward: concat [language | driving queries], stable valid-first permutation
     valid_cat = np.concatenate([valid, np.ones((B, NQ), dtype=bool)], axis=1)
     perm = np.argsort(~valid_cat, axis=1, kind="stable")
     inv = np.argsort(perm, axis=1, kind="stable")
-    code = np.empty((B, S), dtype=np.int64)
-    for b in range(B):
-        i0 = int(perm[b, 0])
-        for s in range(S):
-            if s < L - i0:  # internvl2_model.py:139-142 copy of the replaced language embeddings
-                code[b, s] = lang[b, i0 + s]
-            else:
-                p = int(perm[b, s])
-                code[b, s] = _code(KIND_QUERY, p - L) if p >= L else _code(KIND_TOKEN, min(max(int(ids[b, p]), 0), V - 1))
+    # internvl2_model.py:139-142: row s of sample b takes the replaced language embedding lang[b, i0 + s] while
+    # s < L - i0 (i0 = the first valid position); the rest follow the permutation (driving queries, or the plain
+    # token embedding of the trailing positions)
+    i0 = perm[:, 0]
+    s_idx = np.arange(S)[None, :]
+    take_lang = s_idx < (L - i0)[:, None]
+    src = np.minimum(i0[:, None] + s_idx, L - 1)
+    from_lang = np.take_along_axis(lang, src, axis=1)
+    p_ = perm
+    tok = _code(KIND_TOKEN, np.clip(np.take_along_axis(ids, np.minimum(p_, L - 1), axis=1), 0, V - 1))
+    code = np.where(take_lang, from_lang, np.where(p_ >= L, _code(KIND_QUERY, p_ - L), tok))
     seqlens = valid_cat.sum(1).astype(np.int32)
     # positions of image / waypoint rows in the final sequence (for the backward gathers)
     flat_code = code.reshape(-1)

@@ -67,3 +67,70 @@ def make_batch(cfg: VLAConfig, B: int, s_text: int, n_loss: int, seed: int = 0, 
     dl = DrivingLabel(waypoints=speed.float().to(device), path=route.float().to(device), answer=None,
                       image_ff_org=torch.zeros(B, 2))
     return DrivingExample(driving_input=di, driving_label=dl, run_id=[f"synthetic-{seed}-{b}" for b in range(B)])
+
+
+# ---- synthetic per-sample dataset outputs for the drop-in collate path (bench `dropin` key, config-1 test) --------
+_ROLE_WORDS = ("user", "assistant", "system")
+
+
+def synthetic_tokenizer(cfg: VLAConfig):
+    """A word-level HF tokenizer with the InternVL2-1B id layout of `cfg` (the Qwen2 tokenizer is hub-only): ordinary
+    words below pad_id, <|endoftext|> = pad, <|im_start|>, <|im_end|> = eos, <img>, </img>, <IMG_CONTEXT> at their
+    ids, the SimLingo placeholders from first_added_id (datamodule.py:130-137), left padding (datamodule.py:138).
+    Whitespace splits words, so one word is one token and prompt lengths are exact."""
+    from tokenizers import Tokenizer, models, pre_tokenizers
+    from transformers import PreTrainedTokenizerFast
+
+    from .collate import PLACEHOLDER_TOKENS
+    if not (cfg.img_start_id == cfg.pad_id + 3 and cfg.eos_id == cfg.pad_id + 2 and cfg.img_context_id == cfg.pad_id + 5
+            and cfg.first_added_id == cfg.pad_id + 12):
+        raise ValueError("synthetic_tokenizer follows the InternVL2-1B special-token layout (full_config)")
+    vocab = {w: i for i, w in enumerate(_ROLE_WORDS)}
+    for i in range(len(vocab), cfg.pad_id):
+        vocab[f"w{i}"] = i
+    specials = ["<|endoftext|>", "<|im_start|>", "<|im_end|>", "<img>", "</img>", "<IMG_CONTEXT>"]
+    specials += [f"<spare{j}>" for j in range(cfg.first_added_id - cfg.pad_id - len(specials))]
+    for j, t in enumerate(specials):
+        vocab[t] = cfg.pad_id + j
+    tk = Tokenizer(models.WordLevel(vocab=vocab, unk_token="<|endoftext|>"))
+    tk.pre_tokenizer = pre_tokenizers.WhitespaceSplit()
+    tok = PreTrainedTokenizerFast(tokenizer_object=tk, pad_token="<|endoftext|>", unk_token="<|endoftext|>",
+                                  eos_token="<|im_end|>", additional_special_tokens=specials[1:])
+    tok.add_special_tokens({"additional_special_tokens": specials[1:] + PLACEHOLDER_TOKENS})
+    tok.padding_side = "left"
+    assert tok.convert_tokens_to_ids("<TARGET_POINT>") == cfg.target_point_id
+    assert tok.convert_tokens_to_ids("<IMG_CONTEXT>") == cfg.img_context_id
+    return tok
+
+
+def synthetic_samples(cfg: VLAConfig, B: int, s_text: int = 256, n_loss: int = 16, seed: int = 0,
+                      frame_hw=(512, 1024)):
+    """B per-sample `collate.DatasetOutput`s of the reference's shape: a 1024 x 512 RGB frame with the dataset's bottom
+    crop applied (dataset_base.py:464-467 -> 359 rows, 2 tiles of 448^2), a [user, assistant] conversation whose
+    chat-template token count is exactly s_text + img_tokens (so S_llm = s_text + img_tokens + n_queries, as in
+    make_batch) with n_loss LM-loss tokens (the assistant span) and two <TARGET_POINT> placeholders, and the
+    waypoint / path labels. Words come from synthetic_tokenizer's vocabulary."""
+    from .collate import DatasetOutput
+    from .frames import bottom_crop_rows
+    rng = np.random.default_rng(seed)
+    H0, W0 = frame_hw
+    H = bottom_crop_rows(H0)
+    n_ans = n_loss - 3                       # <|im_start|> assistant {answer} <|im_end|>: the assistant span
+    n_q = s_text - 8 - n_ans                 # everything else but the image block and the role / separator tokens
+    assert n_ans >= 1 and n_q >= 4, "s_text / n_loss too small for the chat template"
+    words = lambda n: " ".join(f"w{int(i)}" for i in rng.integers(len(_ROLE_WORDS), cfg.pad_id, size=n))
+    out = []
+    for _ in range(B):
+        q = words(2) + " <TARGET_POINT> <TARGET_POINT> " + words(n_q - 4)
+        a = words(n_ans)
+        conv = [{"role": "user", "content": [{"type": "text", "text": q}]},
+                {"role": "assistant", "content": [{"type": "text", "text": a}]}]
+        out.append(DatasetOutput(
+            image_ff=rng.integers(0, 256, size=(1, 3, H, W0), dtype=np.uint8), image_ff_org_size=(H0, W0),
+            conversation=conv, answer=[conv[1]],
+            placeholder_values={"<TARGET_POINT>": rng.normal(0.0, 10.0, size=(2, 2)).astype(np.float32)},
+            waypoints=np.cumsum(rng.normal((0.8, 0.0), 0.3, size=(cfg.n_speed, cfg.speed_dims)), 0).astype(np.float32),
+            path=np.cumsum(rng.normal((1.0, 0.0), 0.1, size=(cfg.n_route, 2)), 0).astype(np.float32),
+            speed=np.float32(rng.uniform(0, 10)), target_points=rng.normal(0, 10, size=(2,)).astype(np.float32),
+            measurement_path=f"synthetic/route{int(rng.integers(1000))}/measurements/0000.json.gz"))
+    return out

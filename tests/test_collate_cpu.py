@@ -122,3 +122,42 @@ def test_collate_to_engine_boundary_config1(tok):
     assert all(torch.isfinite(g).all() for g in grads.values())
     # the inference prompt (question only) collates and plans too
     assert plan_from_example(cfg, ex, inference=True).L == di.prompt_inference.phrase_ids.shape[1]
+
+
+def test_collate_host_half_in_dataloader_workers(tok):
+    """Collate.host is the CPU half that runs in DataLoader workers (datamodule.py:275-284): picklable, uint8 frames
+    stacked as camera_images, the same token ids / masks / labels as the in-process call."""
+    from torch.utils.data import DataLoader
+    from simlingo_amd.config import tiny_config
+    cfg = tiny_config()
+    col = C.Collate(tok, num_image_tokens_per_patch=cfg.img_tokens_per_tile, num_image_patches=cfg.tiles)
+    samples = _samples(cfg, 8, seed=3)
+    want = [col.host(samples[:4]), col.host(samples[4:])]
+    dl = DataLoader(samples, batch_size=4, shuffle=False, num_workers=2, collate_fn=col.host)
+    got = list(dl)
+    assert len(got) == 2
+    for g, w in zip(got, want):
+        assert g.driving_input.camera_images.dtype == torch.uint8 and g.driving_input.camera_images.shape == (4, 3, 48, 96)
+        assert torch.equal(g.driving_input.camera_images, w.driving_input.camera_images)
+        for k in ("phrase_ids", "phrase_valid", "loss_masking"):
+            assert torch.equal(getattr(g.driving_input.prompt, k), getattr(w.driving_input.prompt, k))
+        assert torch.equal(g.driving_label.path, w.driving_label.path)
+
+
+def test_synthetic_samples_full_geometry():
+    """simlingo_amd.synthetic.synthetic_samples + synthetic_tokenizer (InternVL2-1B id layout): the collated prompt is
+    exactly s_text + img_tokens long with n_loss LM-loss tokens and two <TARGET_POINT> placeholders, so the plan has
+    the config-3 sequence (S = 798)."""
+    from simlingo_amd.config import full_config
+    from simlingo_amd.plan import plan_from_example
+    from simlingo_amd.synthetic import synthetic_samples, synthetic_tokenizer
+    cfg = full_config()
+    tk = synthetic_tokenizer(cfg)
+    col = C.Collate(tk, num_image_tokens_per_patch=cfg.img_tokens_per_tile, num_image_patches=cfg.tiles)
+    ex = col.host(synthetic_samples(cfg, 3, seed=2))
+    p = ex.driving_input.prompt
+    assert p.phrase_ids.shape == (3, 256 + cfg.img_tokens) and bool(p.phrase_valid.all())
+    assert (p.loss_masking.sum(1) == 16).all()
+    assert ex.driving_input.camera_images.shape == (3, 3, 359, 1024)
+    plan = plan_from_example(cfg, ex)
+    assert plan.S == 798 and plan.loss_pos.shape[0] == 3 * 16 and plan.wp_coords.shape == (6, 2)

@@ -1,0 +1,54 @@
+"""The drop-in training loop (bench.py `dropin` key) is the engine step and nothing else: DataLoader (Collate.host in
+the loader) -> Collate.device (pinned-ring H2D + HIP frame kernel) -> DrivingModel.training_step -> loss.backward()
+-> FusedAdamW.step -> OneCycleLR.step, against VLAEngine stepped directly on the same collated batches at the same
+per-step learning rates (tiny geometry, LoRA dropout on). Losses and the updated parameters agree to f32-atomic
+reduction order (the engine's gradients are not bitwise run-to-run)."""
+import pytest
+import torch
+
+from chat_util import build_tokenizer
+from test_collate_cpu import _samples
+
+pytestmark = [pytest.mark.gpu, pytest.mark.filterwarnings("ignore::UserWarning")]
+
+
+def test_dropin_loop_equals_engine_steps(dev):
+    from torch.utils.data import DataLoader
+    from simlingo_amd.collate import Collate
+    from simlingo_amd.config import tiny_config
+    from simlingo_amd.driving import DrivingModel
+    from simlingo_amd.engine import VLAEngine
+    from simlingo_amd.params import init_params
+    from simlingo_amd.plan import plan_from_example
+    cfg = tiny_config(lora_dropout=0.1)
+    col = Collate(build_tokenizer(), num_image_tokens_per_patch=cfg.img_tokens_per_tile, num_image_patches=cfg.tiles,
+                  device=dev, input_size=cfg.img_size)
+    data = _samples(cfg, 12, seed=5)
+    loader = DataLoader(data, batch_size=4, shuffle=False, num_workers=0, collate_fn=col.host)
+    P = init_params(cfg, seed=3, lora_b_std=0.05, std=0.05)
+    m = DrivingModel(vision_model={"variant": "tiny"}, language_model={"variant": "tiny", "lora_dropout": 0.1},
+                     lr=1e-3, init_params=P)
+    m.max_steps = 8
+    m.build_engine(dev)
+    conf = m.configure_optimizers()
+    opt, sched = conf["optimizer"], conf["lr_scheduler"]["scheduler"]
+    ref = VLAEngine(m.vla_cfg, dev, P)
+    for i, hb in enumerate(loader):
+        ex = col.device(hb)
+        assert ex.driving_input.camera_images.is_cuda
+        g = opt.param_groups[0]
+        lr, betas = g["lr"], g["betas"]
+        out = m.training_step(ex, i)
+        out["loss"].backward()
+        opt.step()
+        sched.step()
+        opt.zero_grad()
+        plan = plan_from_example(m.vla_cfg, ex)
+        lab = ex.driving_label
+        out4, _, _ = ref.forward(ex.driving_input.camera_images, plan, plan.to_device(dev), lab.path.to(dev),
+                                 lab.waypoints.to(dev), training=True)
+        ref.backward(None)
+        ref.adamw_step(lr, i + 1, betas=betas, eps=g["eps"], weight_decay=g["weight_decay"], max_norm=m.vla_cfg.grad_clip)
+        torch.cuda.synchronize()
+        assert abs(out["loss"].item() - out4[0].item()) <= 1e-5 * abs(out4[0].item()), (i, out["loss"].item(), out4[0].item())
+        torch.testing.assert_close(m.engine.master, ref.master, rtol=1e-4, atol=1e-6)
