@@ -1,8 +1,10 @@
 """The drop-in training loop (bench.py `dropin` key) is the engine step and nothing else: DataLoader (Collate.host in
 the loader) -> Collate.device (pinned-ring H2D + HIP frame kernel) -> DrivingModel.training_step -> loss.backward()
 -> FusedAdamW.step -> OneCycleLR.step, against VLAEngine stepped directly on the same collated batches at the same
-per-step learning rates (tiny geometry, LoRA dropout on). Losses and the updated parameters agree to f32-atomic
-reduction order (the engine's gradients are not bitwise run-to-run)."""
+step seed and parameters (tiny geometry, LoRA dropout on): each step's loss agrees to 1e-5 and its gradients to
+f32-atomic reduction order (relative L2 1e-3; the engine's gradients are not bitwise run-to-run, and a first Adam step
+turns that noise into +-lr sign flips, so the parameters after the optimizer are not compared here - the optimizer
+call itself is pinned by test_driving_dropin_gpu / test_adamw_gpu)."""
 import pytest
 import torch
 
@@ -36,19 +38,24 @@ def test_dropin_loop_equals_engine_steps(dev):
     for i, hb in enumerate(loader):
         ex = col.device(hb)
         assert ex.driving_input.camera_images.is_cuda
-        g = opt.param_groups[0]
-        lr, betas = g["lr"], g["betas"]
+        # the reference engine starts every step from the drop-in model's current parameters and step seed
+        ref.master.copy_(m.engine.master)
+        ref.wbf.copy_(m.engine.wbf)
+        ref._refresh_derived()
+        ref.step_seed = m.engine.step_seed
         out = m.training_step(ex, i)
         out["loss"].backward()
-        opt.step()
-        sched.step()
-        opt.zero_grad()
         plan = plan_from_example(m.vla_cfg, ex)
         lab = ex.driving_label
         out4, _, _ = ref.forward(ex.driving_input.camera_images, plan, plan.to_device(dev), lab.path.to(dev),
                                  lab.waypoints.to(dev), training=True)
         ref.backward(None)
-        ref.adamw_step(lr, i + 1, betas=betas, eps=g["eps"], weight_decay=g["weight_decay"], max_norm=m.vla_cfg.grad_clip)
         torch.cuda.synchronize()
         assert abs(out["loss"].item() - out4[0].item()) <= 1e-5 * abs(out4[0].item()), (i, out["loss"].item(), out4[0].item())
-        torch.testing.assert_close(m.engine.master, ref.master, rtol=1e-4, atol=1e-6)
+        g, r = m.engine.grad, ref.grad
+        rel = ((g - r).norm() / r.norm()).item()
+        assert rel <= 1e-3, (i, rel)   # f32-atomic reduction order only
+        opt.step()
+        sched.step()
+        opt.zero_grad()
+    assert i == 2 and opt.step_count == 3
