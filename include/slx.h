@@ -25,6 +25,14 @@ typedef void* slx_stream_t;
 const char* slx_last_error(void);
 int slx_abi_version(void);
 int slx_device_sync(void);
+/* Deterministic-reduction mode (reproducible gradients; off by default). on = 1: every cross-block f32 reduction of
+ * the step (LoRA parameter gradients, column sums, norm parameter gradients, the gradient sum of squares, GEMM split-K)
+ * stores per-block partials in ws and sums them in a fixed order instead of f32 atomics, and GEMM split-K runs only in
+ * its in-launch slab form; two runs on the same inputs then give bitwise-equal gradients. ws (>= 2^20 floats; 16 Mi
+ * floats cover the InternVL2-1B step) is used by one call at a time and must outlive the mode. Process-wide switch,
+ * for one stream at a time (a test / reproducibility mode, not thread-safe against concurrent launches).          */
+int slx_set_deterministic(int on, float* ws, int64_t ws_floats);
+int slx_get_deterministic(void);
 
 /* ---- GEMM ---------------------------------------------------------------------------------
  * C[M,N] = alpha * sum_k A(m,k) B(k,n)   (+ epilogue), bf16 operands, f32 accumulation (MFMA).
@@ -444,8 +452,8 @@ int slx_frames_to_tiles(const slx_frame_desc* d, slx_stream_t stream);
  * engines' own launch sequence with f32 activations and weights, so the forward can be held to the north-star
  * tolerance (waypoint L2 <= 1e-4 m, LM CE <= 1e-4) against the reference fixtures. Same arguments and meaning
  * as the bf16 entry point named; every void* operand is f32. Not tuned.                              */
-int slx_gemm_f32(const slx_gemm_desc* d, slx_stream_t stream);        /* slx_gemm_bf16, forward epilogues
-                                                                         STORE / GELU / QGELU / RESID_LS */
+int slx_gemm_f32(const slx_gemm_desc* d, slx_stream_t stream);        /* slx_gemm_bf16, epilogues STORE /
+                                                       GELU / QGELU / RESID_LS / GELU_BWD / QGELU_BWD (no colsum) */
 int slx_attn_fwd_f32(const slx_attn_desc* d, slx_stream_t stream);    /* slx_attn_fwd                     */
 int slx_rope_f32(void* x, int64_t ldx, int64_t ntok, int S, int nheads, const float* cos_tab,
                  const float* sin_tab, int inverse, slx_stream_t stream);                 /* slx_rope */
@@ -455,6 +463,20 @@ int slx_assemble_tokens_f32(const int* code, int64_t n, int D, const void* embed
                             const float* wp, const float* query, float* out, slx_stream_t s);
 int slx_llava_merge_fwd_f32(const void* src, int C, int64_t n_img, int npatch_h, int npatch_w, int g, int r0,
                             int hu, int c0, int wu, int pool, const float* newline, void* out, slx_stream_t s);
+/* backward twins (the trained path at the north-star tolerance, VLAEngine(precise=True).backward) */
+int slx_attn_bwd_f32(const slx_attn_desc* d, const slx_attn_bwd_desc* g,
+                     slx_stream_t stream);                        /* slx_attn_bwd without RoPE / dbias: dq, dk, dv of the
+                                                                     rotated q / k (callers apply slx_rope_f32 inverse
+                                                                     and slx_colsum); delta_ws [B, Hq, S] required */
+int slx_swiglu_bwd_f32(const float* dact, int64_t ldd, const void* gu, int64_t ldgu, void* dgu, int64_t lddgu,
+                       int64_t M, int F, slx_stream_t s);        /* slx_swiglu_bwd                       */
+int slx_mul_f32(int mode, const float* x, int64_t ldx, const float* y, int64_t ldy, float* out, int64_t ldo,
+                int64_t M, int N, slx_stream_t s);               /* out = x*y (mode 0) or x*y[col] (1): the
+                                                                     layer-scale branch products of slx_ls_branch_bwd */
+int slx_ce_bwd_f32(const float* logits, int64_t ld, const int* labels, const float* lse, int64_t R, int V,
+                   const float* gscale, float* dlogits, int64_t ldd, slx_stream_t s);     /* slx_ce_bwd  */
+int slx_vit_embed_bwd_f32(const float* dx, int N, int T, int D, float* dpos, float* dcls, float* dpatch,
+                          slx_stream_t s);                       /* slx_vit_embed_bwd                    */
 
 #ifdef __cplusplus
 }

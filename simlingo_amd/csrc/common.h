@@ -24,6 +24,10 @@ namespace slx {
 
 // Thread-local error string (the C-ABI's slx_last_error()).
 void set_error(const char* fmt, ...);
+// deterministic-reduction mode (det.hip, slx_set_deterministic): partials in ws + ordered sums instead of f32 atomics
+struct DetMode { int on; float* ws; long ws_floats; };
+DetMode& det_mode();
+int det_reduce(const float* part, int nparts, long n, long stride, float* out, int accumulate, hipStream_t st);
 
 
 #define SLX_CHECK_ARG(cond, ...)            \

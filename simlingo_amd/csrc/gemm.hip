@@ -2201,8 +2201,9 @@ constexpr long kSlabFloats = 65536;    // one 256 x 256 f32 partial
 // last arriver's serial read of three 256 KiB slabs made it slower than the atomics (178 vs 164 us,
 // tools/wgrad_group_bench.py SPLIT_AB=1, profiles/round3_split_ab.txt). SLX_SPLIT_REDUCE_MAX raises the cap (A/B).
 static bool split_ws_fits(const slx_gemm_desc* d, long tiles, int sp) {
-  static const int smax = [] { const char* e = getenv("SLX_SPLIT_REDUCE_MAX"); const int v = e ? atoi(e) : 2;
-                               return v >= 2 && v <= 4 ? v : 2; }();
+  static const int smax_env = [] { const char* e = getenv("SLX_SPLIT_REDUCE_MAX"); const int v = e ? atoi(e) : 2;
+                                   return v >= 2 && v <= 4 ? v : 2; }();
+  const int smax = det_mode().on ? 4 : smax_env;  // deterministic mode: every split count the slab sum supports
   return d->split_ws && sp > 1 && sp <= smax && 2 * tiles <= kSplitCntInts &&
          tiles * sp * kSlabFloats <= d->split_ws_floats - kSplitCntInts;
 }
@@ -2302,6 +2303,8 @@ __global__ __launch_bounds__(256) void colsum_reduce_kernel(const float* __restr
 
 static int colsum_reduce(const slx_gemm_desc* d, hipStream_t st) {
   const int nrows = (d->M + 63) / 64;
+  if (det_mode().on)  // deterministic mode: every column summed by one thread in row order (no atomics)
+    return det_reduce(d->colsum_ws, nrows, d->N, d->N, d->colsum, 1, st);
   hipLaunchKernelGGL(colsum_reduce_kernel, dim3((d->N + 255) / 256, (nrows + 31) / 32), dim3(256), 0, st,
                      (const float*)d->colsum_ws, nrows, d->N, d->colsum);
   SLX_LAUNCH_CHECK("slx_gemm_bf16(colsum reduce)");
@@ -2372,6 +2375,13 @@ static int gemm_launch(const slx_gemm_desc* d, int v, hipStream_t st, int mshift
         a.split_ws = d->split_ws;
         a.split_cnt = reinterpret_cast<int*>(d->split_ws + d->split_ws_floats - kSplitCntInts);
       }
+      if (det_mode().on && !a.split_ws && !split_stride) {  // deterministic mode: no f32-atomic split-K
+        sp = 1;
+        a.ksplit = 1;
+        a.kchunk = d->K;
+      }
+    }
+    if (sp > 1) {
       if (!d->accumulate && !split_stride && !a.split_ws) {
         hipError_t e = hipMemset2DAsync(d->C, d->ldc * sizeof(float), 0, (size_t)d->N * sizeof(float), d->M, st);
         if (e != hipSuccess) { set_error("slx_gemm_bf16: memset2D failed: %s", hipGetErrorString(e)); return -1000 - (int)e; }
@@ -2738,7 +2748,11 @@ extern "C" int slx_gemm_bf16_pair(const slx_gemm_desc* d1, const slx_gemm_desc* 
   // in-launch reduction (slabs in d1's split_ws) when split_ws_fits allows it, else f32 atomics
   const int per = ((ksteps + sp - 1) / sp) * BK;
   sp = (d1->K + per - 1) / per;
-  const bool red = split_ws_fits(d1, tiles, sp);
+  bool red = split_ws_fits(d1, tiles, sp);
+  if (det_mode().on && sp > 1 && !red) {  // deterministic mode: one split (no f32-atomic partials)
+    sp = 1;
+    red = false;
+  }
   a.ksplit = b.ksplit = sp;
   a.kchunk = b.kchunk = sp > 1 ? per : d1->K;
   if (red && sp > 1) {

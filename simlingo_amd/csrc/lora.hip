@@ -532,6 +532,8 @@ struct LgJob {
   float alpha;   // scale of the f32 product
   float* out[3]; int nr;
   int ncb, kch, item0;
+  float* part[3];  // deterministic mode: per-row-chunk partials [nkc][32 N] of each site (same layout as out), summed
+                   // in chunk order by det_reduce after the launch; null = f32 atomics into out
 };
 struct LgArgs { int M, njobs, nitems; LgJob j[kLgMaxJobs]; };
 
@@ -563,7 +565,7 @@ struct LgRegs {
 // NS and DROP are template parameters so the item loop is straight-line code in which the compiler counts the two
 // sub-chunks in flight (vmcnt(N)) instead of draining both at each commit.
 template <int NS, bool DROP>
-__device__ __forceinline__ void lg_item(const LgJob J, int c0, int mb, int me, char* smem) {
+__device__ __forceinline__ void lg_item(const LgJob J, int c0, int mb, int me, int kc, char* smem) {
   char* ts = smem + 6 * 8192;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
   const int srow = tid >> 2;
@@ -664,13 +666,15 @@ __device__ __forceinline__ void lg_item(const LgJob J, int c0, int mb, int me, c
       }
     }
   }
+  const long pofs = (long)kc * 32 * J.N;  // this item's partial slot (deterministic mode)
   if (!J.nr) {
 #pragma unroll
     for (int j = 0; j < NS; ++j)
 #pragma unroll
       for (int g = 0; g < 16; ++g) {
         const int rr = (g & 3) + 8 * (g >> 2) + 4 * h;
-        atomicAdd(J.out[j] + (long)rr * J.N + mycol, J.alpha * acc[j][g]);
+        if (J.part[0]) J.part[j][pofs + (long)rr * J.N + mycol] = J.alpha * acc[j][g];
+        else atomicAdd(J.out[j] + (long)rr * J.N + mycol, J.alpha * acc[j][g]);
       }
   } else {  // out[n][32]: transpose through LDS ([32][129] f32), then 32 consecutive r per 32 lanes
     float* red = reinterpret_cast<float*>(smem);
@@ -684,7 +688,8 @@ __device__ __forceinline__ void lg_item(const LgJob J, int c0, int mb, int me, c
       __syncthreads();
       for (int e = tid; e < 32 * 128; e += 256) {
         const int col = e >> 5, r = e & 31;
-        atomicAdd(J.out[j] + (long)(c0 + col) * 32 + r, J.alpha * red[r * 129 + col]);
+        if (J.part[0]) J.part[j][pofs + (long)(c0 + col) * 32 + r] = J.alpha * red[r * 129 + col];
+        else atomicAdd(J.out[j] + (long)(c0 + col) * 32 + r, J.alpha * red[r * 129 + col]);
       }
       __syncthreads();
     }
@@ -703,12 +708,12 @@ __global__ __launch_bounds__(256, 2) void lora_grad_kernel(LgArgs a) {
   const int c0 = cb * 128, mb = kc * J.kch, me = min(a.M, mb + J.kch);
   const bool drop = J.bits[0] != nullptr;
   switch (J.ns * 2 + (drop ? 1 : 0)) {
-    case 2: lg_item<1, false>(J, c0, mb, me, smem); break;
-    case 3: lg_item<1, true>(J, c0, mb, me, smem); break;
-    case 4: lg_item<2, false>(J, c0, mb, me, smem); break;
-    case 5: lg_item<2, true>(J, c0, mb, me, smem); break;
-    case 6: lg_item<3, false>(J, c0, mb, me, smem); break;
-    default: lg_item<3, true>(J, c0, mb, me, smem); break;
+    case 2: lg_item<1, false>(J, c0, mb, me, kc, smem); break;
+    case 3: lg_item<1, true>(J, c0, mb, me, kc, smem); break;
+    case 4: lg_item<2, false>(J, c0, mb, me, kc, smem); break;
+    case 5: lg_item<2, true>(J, c0, mb, me, kc, smem); break;
+    case 6: lg_item<3, false>(J, c0, mb, me, kc, smem); break;
+    default: lg_item<3, true>(J, c0, mb, me, kc, smem); break;
   }
 }
 
@@ -863,6 +868,12 @@ static int lora_bwd_impl(const slx_lora_bwd_desc* d, float* ws, int64_t ws_float
   SLX_CHECK_ARG(!ws || !d->dA[0] || ws_floats >= slx_lora_bwd_ws_floats(d->M, d->Kin, d->nsites),
                 "slx_lora_bwd_ws: workspace holds %lld floats, slx_lora_bwd_ws_floats asks for %lld", (long long)ws_floats,
                 (long long)slx_lora_bwd_ws_floats(d->M, d->Kin, d->nsites));
+  if (!ws && d->dA[0] && det_mode().on &&  // deterministic mode: the slab path, in the mode's workspace
+      det_mode().ws_floats >= slx_lora_bwd_ws_floats(d->M, d->Kin, d->nsites)) {
+    ws = det_mode().ws;
+    ws_floats = det_mode().ws_floats;
+  }
+  SLX_CHECK_ARG(!d->dA[0] || ws || !det_mode().on, "slx_lora_bwd: deterministic workspace too small for the dA partials");
   a.dA_part = (ws && d->dA[0]) ? ws : nullptr;
   SLX_CHECK_ARG(!a.dA_part || (long)grid.y <= (long)kDaRedLanes * kDaRedPer,
                 "slx_lora_bwd_ws: %u row chunks, at most %d (SLX_LORA_DA_BLOCKS too high for M)", grid.y,
@@ -925,7 +936,23 @@ extern "C" int slx_lora_grad(const slx_lora_grad_job* jobs, int njobs, int64_t M
     items += a.j[i].ncb * (int)nkc;
   }
   a.nitems = items;
-  hipLaunchKernelGGL(lora_grad_kernel, dim3(items), dim3(256), 0, (hipStream_t)stream, a);
+  const DetMode& dm = det_mode();
+  if (dm.on) {  // partial slots [nkc][32 N] per (job, site) in the deterministic workspace
+    long off = 0;
+    for (int i = 0; i < njobs; ++i)
+      for (int j = 0; j < a.j[i].ns; ++j) {
+        a.j[i].part[j] = dm.ws + off;
+        off += nkc * 32L * a.j[i].N;
+      }
+    SLX_CHECK_ARG(off <= dm.ws_floats, "slx_lora_grad: deterministic workspace holds %ld floats, the partials need %ld",
+                  dm.ws_floats, off);
+  }
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(lora_grad_kernel, dim3(items), dim3(256), 0, st, a);
   SLX_LAUNCH_CHECK("slx_lora_grad");
+  if (dm.on)
+    for (int i = 0; i < njobs; ++i)
+      for (int j = 0; j < a.j[i].ns; ++j)
+        if (det_reduce(a.j[i].part[j], (int)nkc, 32L * a.j[i].N, 32L * a.j[i].N, a.j[i].out[j], 1, st)) return -1000;
   return 0;
 }

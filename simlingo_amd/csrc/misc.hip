@@ -85,7 +85,8 @@ __global__ void swiglu_fwd_kernel(const bf16* gu, long ldgu, bf16* out, long ldo
 //   out0[c] += sum dres*y (d ls), out1[c] += sum dres*ls (d bias)
 template <int MODE>
 __global__ __launch_bounds__(256) void colsum_kernel(const void* xv, long ldx, long M, int N, float* out0, float* out1,
-                                                     const float* ls, const bf16* y, long ldy, bf16* g, long ldg) {
+                                                     const float* ls, const bf16* y, long ldy, bf16* g, long ldg,
+                                                     float* part) {
   const int c0 = (blockIdx.y * 256 + threadIdx.x) * 4;
   const bool live = c0 < N;
   float s[4] = {0, 0, 0, 0}, s2[4] = {0, 0, 0, 0};
@@ -133,6 +134,11 @@ __global__ __launch_bounds__(256) void colsum_kernel(const void* xv, long ldx, l
   __syncthreads();
   const int cb = blockIdx.y * 1024;
   for (int c = threadIdx.x; c < 1024 && cb + c < N; c += 256) {
+    if (part) {  // deterministic mode: per-block partial rows, summed in block order by det_reduce
+      if (out0) part[(long)blockIdx.x * N + cb + c] = cs[0][c];
+      if (MODE == 2) part[((long)gridDim.x + blockIdx.x) * N + cb + c] = cs[1][c];
+      continue;
+    }
     if (out0) atomicAdd(out0 + cb + c, cs[0][c]);
     if (MODE == 2) atomicAdd(out1 + cb + c, cs[1][c]);
   }
@@ -361,7 +367,7 @@ __global__ void loss_gscale_kernel(const float* dl, int nl, int nr, int ns, floa
 // ---------------------------------------------------------------------------------------------
 // Optimizer: global grad-norm (sum of squares, partials + atomics) and fused clip + AdamW
 // (torch.optim.AdamW semantics, decoupled weight decay; driving.py:718-724, clip train.py:206).
-__global__ __launch_bounds__(256) void sumsq_kernel(const float* g, long n, float* out) {
+__global__ __launch_bounds__(256) void sumsq_kernel(const float* g, long n, float* out, float* part) {
   __shared__ float sh[16];
   float s = 0.f;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n / 4; i += (long)gridDim.x * blockDim.x) {
@@ -371,7 +377,10 @@ __global__ __launch_bounds__(256) void sumsq_kernel(const float* g, long n, floa
   if (blockIdx.x == 0)
     for (long i = (n / 4) * 4 + threadIdx.x; i < n; i += blockDim.x) s += g[i] * g[i];
   s = block_sum(s, sh);
-  if (threadIdx.x == 0) atomicAdd(out, s);
+  if (threadIdx.x == 0) {
+    if (part) part[blockIdx.x] = s;  // deterministic mode: summed in block order by det_reduce
+    else atomicAdd(out, s);
+  }
 }
 
 __global__ __launch_bounds__(256) void adamw_kernel(float* p, const float* g, float* m, float* v, bf16* pbf, long n,
@@ -679,11 +688,19 @@ int slx_colsum(int mode, const void* x, int64_t ldx, int64_t M, int N, float* ou
   (void)ws;
   hipStream_t st = (hipStream_t)s;
   if (!accumulate) hipMemsetAsync(out, 0, (size_t)N * sizeof(float), st);
-  const int nblk = (int)(M < 512 ? (M > 0 ? M : 1) : 512);
+  int nblk = (int)(M < 512 ? (M > 0 ? M : 1) : 512);
+  const DetMode& dm = det_mode();
+  float* part = nullptr;
+  if (dm.on) {
+    SLX_CHECK_ARG(dm.ws_floats >= N, "slx_colsum: deterministic workspace too small");
+    if ((long)nblk * N > dm.ws_floats) nblk = (int)(dm.ws_floats / N);
+    part = dm.ws;
+  }
   dim3 grid(nblk, (N / 4 + 255) / 256);
-  if (mode == 0) hipLaunchKernelGGL((colsum_kernel<0>), grid, dim3(256), 0, st, x, ldx, M, N, out, (float*)nullptr, nullptr, nullptr, 0L, nullptr, 0L);
-  else hipLaunchKernelGGL((colsum_kernel<1>), grid, dim3(256), 0, st, x, ldx, M, N, out, (float*)nullptr, nullptr, nullptr, 0L, nullptr, 0L);
+  if (mode == 0) hipLaunchKernelGGL((colsum_kernel<0>), grid, dim3(256), 0, st, x, ldx, M, N, out, (float*)nullptr, nullptr, nullptr, 0L, nullptr, 0L, part);
+  else hipLaunchKernelGGL((colsum_kernel<1>), grid, dim3(256), 0, st, x, ldx, M, N, out, (float*)nullptr, nullptr, nullptr, 0L, nullptr, 0L, part);
   SLX_LAUNCH_CHECK("slx_colsum");
+  if (part) return det_reduce(part, nblk, N, N, out, 1, st);
   return 0;
 }
 
@@ -698,10 +715,21 @@ int slx_ls_branch_bwd(const float* dres, int64_t ldr, const float* ls, const voi
     if (dls) hipMemsetAsync(dls, 0, (size_t)N * sizeof(float), st);
     hipMemsetAsync(dbias, 0, (size_t)N * sizeof(float), st);
   }
-  const int nblk = (int)(M < 512 ? (M > 0 ? M : 1) : 512);
+  int nblk = (int)(M < 512 ? (M > 0 ? M : 1) : 512);
+  const DetMode& dm = det_mode();
+  float* part = nullptr;
+  if (dm.on) {
+    SLX_CHECK_ARG(dm.ws_floats >= 2L * N, "slx_ls_branch_bwd: deterministic workspace too small");
+    if (2L * nblk * N > dm.ws_floats) nblk = (int)(dm.ws_floats / (2L * N));
+    part = dm.ws;
+  }
   dim3 grid(nblk, (N / 4 + 255) / 256);
-  hipLaunchKernelGGL((colsum_kernel<2>), grid, dim3(256), 0, st, (const void*)dres, ldr, M, N, dls, dbias, ls, (const bf16*)y, ldy, (bf16*)g, ldg);
+  hipLaunchKernelGGL((colsum_kernel<2>), grid, dim3(256), 0, st, (const void*)dres, ldr, M, N, dls, dbias, ls, (const bf16*)y, ldy, (bf16*)g, ldg, part);
   SLX_LAUNCH_CHECK("slx_ls_branch_bwd");
+  if (part) {
+    if (dls && det_reduce(part, nblk, N, N, dls, 1, st)) return -1000;
+    return det_reduce(part + (long)nblk * N, nblk, N, N, dbias, 1, st);
+  }
   return 0;
 }
 
@@ -809,8 +837,11 @@ int slx_sumsq(const float* g, int64_t n, float* out, int zero_first, slx_stream_
   long blocks = (n / 4 + 255) / 256;
   if (blocks > 2048) blocks = 2048;
   if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(sumsq_kernel, dim3((unsigned)blocks), dim3(256), 0, st, g, n, out);
+  const DetMode& dm = det_mode();
+  float* part = dm.on ? dm.ws : nullptr;
+  hipLaunchKernelGGL(sumsq_kernel, dim3((unsigned)blocks), dim3(256), 0, st, g, n, out, part);
   SLX_LAUNCH_CHECK("slx_sumsq");
+  if (part) return det_reduce(part, (int)blocks, 1, 1, out, 1, st);
   return 0;
 }
 

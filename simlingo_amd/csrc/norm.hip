@@ -33,10 +33,18 @@ struct NormArgs {
   float* dx; long lddx; int dx_accumulate;
   bf16* dxb; long lddxb;  // optional bf16 copy of dx (non-pixel-shuffle rows only)
   float* partial;   // unused (kept for ABI workspace sizing)
+  float* detp;      // deterministic mode: per-block partial rows [4][gridDim.x][D] (dgamma, dbeta, dls, dlsb)
   float* dgamma; float* dbeta;
   // fused layer-scale branch backward on the updated dx (slx_norm_desc.ls*)
   const float* ls; const bf16* lsy; long ldlsy; bf16* lsg; long ldlsg; float* dls; float* dlsb;
 };
+
+// one block's column partial of parameter gradient q (0 dgamma, 1 dbeta, 2 dls, 3 dlsb) into its output: an f32 atomic,
+// or (deterministic mode) a plain store into the partial rows summed in block order afterwards
+__device__ __forceinline__ void norm_param_out(const NormArgs& a, int q, float* out, int c, float v) {
+  if (a.detp) a.detp[((long)q * gridDim.x + blockIdx.x) * a.D + c] = v;
+  else atomicAdd(out + c, v);
+}
 
 // 4 consecutive dy values of a row (f32 rows, or bf16 rows when a.dy_bf16; DYB: decided at compile time)
 template <int DYB = -1>
@@ -314,11 +322,13 @@ __global__ __launch_bounds__(256) void norm_bwd_wave_kernel(NormArgs a) {
   if (a.dgamma || a.dbeta || LS) {  // 4 waves' column partials summed through LDS, then contiguous f32 atomics
     __syncthreads();
     for (int c = threadIdx.x; c < a.D; c += 256) {
-      if (a.dgamma) atomicAdd(a.dgamma + c, cs[0][0][c] + cs[1][0][c] + cs[2][0][c] + cs[3][0][c]);
-      if (a.dbeta) atomicAdd(a.dbeta + c, cs[0][1][c] + cs[1][1][c] + cs[2][1][c] + cs[3][1][c]);
+      if (a.dgamma) norm_param_out(a, 0, a.dgamma, c, cs[0][0][c] + cs[1][0][c] + cs[2][0][c] + cs[3][0][c]);
+      if (a.dbeta) norm_param_out(a, 1, a.dbeta, c, cs[0][1][c] + cs[1][1][c] + cs[2][1][c] + cs[3][1][c]);
       if constexpr (LS) {
-        atomicAdd(a.dls + c, cs[0][LS ? 2 : 0][c] + cs[1][LS ? 2 : 0][c] + cs[2][LS ? 2 : 0][c] + cs[3][LS ? 2 : 0][c]);
-        atomicAdd(a.dlsb + c, cs[0][LS ? 3 : 0][c] + cs[1][LS ? 3 : 0][c] + cs[2][LS ? 3 : 0][c] + cs[3][LS ? 3 : 0][c]);
+        norm_param_out(a, 2, a.dls, c,
+                       cs[0][LS ? 2 : 0][c] + cs[1][LS ? 2 : 0][c] + cs[2][LS ? 2 : 0][c] + cs[3][LS ? 2 : 0][c]);
+        norm_param_out(a, 3, a.dlsb, c,
+                       cs[0][LS ? 3 : 0][c] + cs[1][LS ? 3 : 0][c] + cs[2][LS ? 3 : 0][c] + cs[3][LS ? 3 : 0][c]);
       }
     }
   }
@@ -432,11 +442,13 @@ __global__ __launch_bounds__(256) void norm_bwd_row_kernel(NormArgs a) {
     }
     __syncthreads();
     for (int c = threadIdx.x; c < a.D; c += 256) {
-      if (a.dgamma) atomicAdd(a.dgamma + c, cs[0][0][c] + cs[1][0][c] + cs[2][0][c] + cs[3][0][c]);
-      if (a.dbeta) atomicAdd(a.dbeta + c, cs[0][1][c] + cs[1][1][c] + cs[2][1][c] + cs[3][1][c]);
+      if (a.dgamma) norm_param_out(a, 0, a.dgamma, c, cs[0][0][c] + cs[1][0][c] + cs[2][0][c] + cs[3][0][c]);
+      if (a.dbeta) norm_param_out(a, 1, a.dbeta, c, cs[0][1][c] + cs[1][1][c] + cs[2][1][c] + cs[3][1][c]);
       if constexpr (LS) {
-        atomicAdd(a.dls + c, cs[0][LS ? 2 : 0][c] + cs[1][LS ? 2 : 0][c] + cs[2][LS ? 2 : 0][c] + cs[3][LS ? 2 : 0][c]);
-        atomicAdd(a.dlsb + c, cs[0][LS ? 3 : 0][c] + cs[1][LS ? 3 : 0][c] + cs[2][LS ? 3 : 0][c] + cs[3][LS ? 3 : 0][c]);
+        norm_param_out(a, 2, a.dls, c,
+                       cs[0][LS ? 2 : 0][c] + cs[1][LS ? 2 : 0][c] + cs[2][LS ? 2 : 0][c] + cs[3][LS ? 2 : 0][c]);
+        norm_param_out(a, 3, a.dlsb, c,
+                       cs[0][LS ? 3 : 0][c] + cs[1][LS ? 3 : 0][c] + cs[2][LS ? 3 : 0][c] + cs[3][LS ? 3 : 0][c]);
       }
     }
   }
@@ -527,8 +539,8 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(NormArgs a) {
     }
     __syncthreads();
     for (int c = tid; c < a.D; c += 256) {
-      if (a.dgamma) atomicAdd(a.dgamma + c, cs[0][c]);
-      if (a.dbeta) atomicAdd(a.dbeta + c, cs[1][c]);
+      if (a.dgamma) norm_param_out(a, 0, a.dgamma, c, cs[0][c]);
+      if (a.dbeta) norm_param_out(a, 1, a.dbeta, c, cs[1][c]);
     }
   }
 }
@@ -553,7 +565,14 @@ static int norm_fwd(NormArgs& a, hipStream_t st) {
 
 template <bool RMS>
 static int norm_bwd(NormArgs& a, float* dgamma, float* dbeta, int accumulate, hipStream_t st) {
-  const int nblk = (int)(a.rows < kBwdBlocks ? a.rows : kBwdBlocks);
+  int nblk = (int)(a.rows < kBwdBlocks ? a.rows : kBwdBlocks);
+  const DetMode& dm = det_mode();
+  a.detp = nullptr;
+  if (dm.on && (dgamma || dbeta || a.ls)) {  // partial rows [4][nblk][D], summed in block order below
+    SLX_CHECK_ARG(dm.ws_floats >= 4L * a.D, "slx_norm_bwd: deterministic workspace too small");
+    if (4L * nblk * a.D > dm.ws_floats) nblk = (int)(dm.ws_floats / (4L * a.D));
+    a.detp = dm.ws;
+  }
   SLX_CHECK_ARG(a.D % 4 == 0 && a.D <= 4096, "norm bwd: D=%d must be a multiple of 4 and <= 4096", a.D);
   a.dgamma = dgamma;
   a.dbeta = dbeta;
@@ -578,6 +597,11 @@ static int norm_bwd(NormArgs& a, float* dgamma, float* dbeta, int accumulate, hi
   else if (a.D <= 2048) hipLaunchKernelGGL((norm_bwd_kernel<8, RMS>), dim3(nblk), dim3(256), 0, st, a);
   else hipLaunchKernelGGL((norm_bwd_kernel<16, RMS>), dim3(nblk), dim3(256), 0, st, a);
   SLX_LAUNCH_CHECK("slx_norm_bwd");
+  if (a.detp) {
+    float* outs[4] = {dgamma, dbeta, a.ls ? a.dls : nullptr, a.ls ? a.dlsb : nullptr};
+    for (int q = 0; q < 4; ++q)
+      if (outs[q] && det_reduce(a.detp + (long)q * nblk * a.D, nblk, a.D, a.D, outs[q], 1, st)) return -1000;
+  }
   return 0;
 }
 

@@ -71,6 +71,9 @@ LORA_GRAD_DEFER = os.environ.get("SLX_LORA_GRAD_DEFER", "0") == "1"
 # forward, Qwen2 o / down forward); 0 = the cost model's choice (A/B hook)
 VIT_RESID_VARIANT = int(os.environ.get("SLX_VIT_RESID_VARIANT", "0"))
 LLM_RESID_VARIANT = int(os.environ.get("SLX_LLM_RESID_VARIANT", "0"))
+# SLX_DETERMINISTIC=1: the library's deterministic-reduction mode (kernels.set_deterministic) from the first engine on:
+# bitwise-reproducible gradients (ordered partial sums instead of f32 atomics), at some speed
+DETERMINISTIC = os.environ.get("SLX_DETERMINISTIC", "0") == "1"
 ALIGN = 64  # elements; keeps every parameter view 256-B aligned
 
 
@@ -92,7 +95,8 @@ class VLAEngine(EngineOps):
     def __init__(self, cfg: VLAConfig, device, params: dict[str, torch.Tensor] | None = None, seed: int = 0,
                  bucket_bytes: int = 32 << 20, precise: bool = False, wire: str = "f32"):
         """precise=True: fp32 parity mode — the same launch sequence with f32 activations and weights (the f32
-        twins of csrc/precise.hip), forward only; used to hold the forward to the north-star tolerance."""
+        twins of csrc/precise.hip), forward, backward and optimizer; used to hold the trained path to the north-star
+        tolerance (LoRA dropout must be 0: the parity mode has no keep masks)."""
         from .params import init_params
         self.cfg = cfg
         self.device = torch.device(device)
@@ -101,6 +105,8 @@ class VLAEngine(EngineOps):
         self.precise = bool(precise)
         self.adt = F32 if self.precise else BF16   # activation / GEMM-operand dtype
         K.lib()  # fail loudly if the HIP library is missing
+        if DETERMINISTIC:
+            K.set_deterministic(True, self.device)
         params = params if params is not None else init_params(cfg, seed)
         self.specs = param_specs(cfg)
         # ---- flat trainable storage ----
@@ -607,8 +613,9 @@ class VLAEngine(EngineOps):
         cfg = self.cfg
         sv = self.saved
         assert sv is not None, "backward() without forward()"
-        if self.precise:
-            raise RuntimeError("the fp32 parity mode is forward-only (it pins the forward outputs)")
+        pr = self.precise  # fp32 parity mode: the same sequence over f32 operands (csrc/precise.hip twins)
+        if pr and sv["drop"] > 0:
+            raise RuntimeError("the fp32 parity mode has no LoRA dropout (lora_dropout = 0)")
         B, S, Ml, Mv, Mi, R = sv["B"], sv["S"], sv["Ml"], sv["Mv"], sv["Mi"], sv["R"]
         d, D = cfg.llm_dim, cfg.vit_dim
         nr, ns = cfg.n_route, cfg.n_speed
@@ -633,7 +640,7 @@ class VLAEngine(EngineOps):
         if R:
             dlog = self._e(R, self.Vp)
             if "logits" in sv:
-                K.call("slx_ce_bwd", K.P(sv["logits"]), self.Vp, K.P(dplan["loss_labels"]), K.P(sv["lse_ce"]), R,
+                K.call("slx_ce_bwd_f32" if pr else "slx_ce_bwd", K.P(sv["logits"]), self.Vp, K.P(dplan["loss_labels"]), K.P(sv["lse_ce"]), R,
                        cfg.vocab, K.P(gs[0:1]), K.P(dlog), self.Vp, K.stream_ptr())
             else:  # the LM-head GEMM recomputed with the softmax-gradient epilogue (slx_lmhead_ce_bwd)
                 K.call("slx_lmhead_ce_bwd", K.P(sv["fl"]), d, K.P(self.W["llm.lm_head"]), d, K.P(dplan["loss_labels"]),
@@ -643,8 +650,10 @@ class VLAEngine(EngineOps):
             K.call("slx_scatter_rows", K.P(dfl), d, K.P(dplan["loss_pos"]), R, d, K.P(dfeat), d, 1, K.stream_ptr())
         # ---------------- final RMSNorm ----------------
         dX = self._z(Ml + 1, d)
-        dxb = self._e(Ml, d)  # bf16 copy of dX, written by every norm backward that updates dX (dgrad operand)
-        K.norm_bwd(sv["nf"], dfeat, dX, dx_bf16=dxb)
+        # bf16 copy of dX, written by every norm backward that updates dX (dgrad operand); parity mode: dX itself
+        dxb = dX[:Ml] if pr else self._e(Ml, d)
+        nb = None if pr else dxb
+        K.norm_bwd(sv["nf"], dfeat, dX, dx_bf16=nb)
         # ---------------- Qwen2 layers ----------------
         Hq, Hk, Fl = cfg.llm_heads, cfg.llm_kv_heads, cfg.llm_ffn
         qn, kn = Hq * 64, Hk * 64
@@ -664,15 +673,15 @@ class VLAEngine(EngineOps):
             # down projection: Xo = Xm + [act | t_d] . [Wd | s B_d]^T   (dxb = bf16(dX), from the last norm backward)
             # bf16 with LoRA: the gradient of act that a bf16 Linear backward produces under autocast (read once by the
             # SwiGLU epilogue and, columns Fl.., as the dT operand); f32 for the plain slx_swiglu_bwd path
-            dax = self._e(Ml, Fl + Pd, dtype=BF16 if lora else F32)
+            dax = self._e(Ml, Fl + Pd, dtype=BF16 if (lora and not pr) else F32)
             self._mm_dx(dxb, *self._dxw(cat, "down", p + "down_w"), dax)
             dgu = self._e(Ml, 2 * Fl)
             if lora:  # the down-site dropout dgrad and the SwiGLU backward share one GEMM epilogue
                 self._lora_bwd(i, ("down",), [dxb], ax[:, Fl:], ax[:, :Fl], dax[:, Fl:], dax[:, :Fl], sv,
                                swiglu=(Ls["gu"], dgu))
             else:
-                K.call("slx_swiglu_bwd", K.P(dax), dax.stride(0), K.P(Ls["gu"]), 2 * Fl, K.P(dgu), 2 * Fl, Ml, Fl,
-                       K.stream_ptr())
+                K.call("slx_swiglu_bwd_f32" if pr else "slx_swiglu_bwd", K.P(dax), dax.stride(0), K.P(Ls["gu"]), 2 * Fl,
+                       K.P(dgu), 2 * Fl, Ml, Fl, K.stream_ptr())
             del dax
             dh2x = self._e(Ml, d + Pg, dtype=F32)
             side = lora and LORA_DB_SIDE and not self.precise and not LORA_GRAD_GROUP
@@ -700,15 +709,16 @@ class VLAEngine(EngineOps):
                 self._group_done(done_pending)
                 done_pending = None
             if defer:
-                dxb = self._e(Ml, d)
-            K.norm_bwd(Ls["n2"], dh2x, dX, dx_accumulate=True, dx_bf16=dxb)
+                dxb = nb = self._e(Ml, d)
+            K.norm_bwd(Ls["n2"], dh2x, dX, dx_accumulate=True, dx_bf16=nb)
             # o projection
             dox = self._e(Ml, qn + Po, dtype=F32)
             self._mm_dx(dxb, *self._dxw(cat, "o", p + "o_w"), dox)
-            dob = self._e(Ml, qn)
+            dob = dox[:, :qn] if pr else self._e(Ml, qn)
             if lora:  # the LoRA dx term and the bf16 cast of dO in one pass
-                self._lora_bwd(i, ("o",), [dxb], ox[:, qn:], ox[:, :qn], dox[:, qn:], dox[:, :qn], sv, dx_bf16=dob)
-            else:
+                self._lora_bwd(i, ("o",), [dxb], ox[:, qn:], ox[:, :qn], dox[:, qn:], dox[:, :qn], sv,
+                               dx_bf16=None if pr else dob)
+            elif not pr:
                 K.call("slx_cast_rows", K.P(dox), dox.stride(0), K.P(dob), qn, Ml, qn, K.stream_ptr())
             del dox
             qkv = Ls["qkv"]
@@ -722,10 +732,10 @@ class VLAEngine(EngineOps):
                 self._lora_bwd(i, ("q", "k", "v"), [dqkv[:, :qn], dqkv[:, qn:qn + kn], dqkv[:, qn + kn:]], hx[:, d:],
                                hx[:, :d], dhx[:, d:], dhx[:, :d], sv)
             if defer:  # the attention-half jobs wait for the next layer's MLP-half launch; the o site keeps its dxb
-                dxb = self._e(Ml, d)
+                dxb = nb = self._e(Ml, d)
             else:
                 self._lg_flush(Ml)  # before dxb (the o site's dy) is overwritten
-            K.norm_bwd(Ls["n1"], dhx, dX, dx_accumulate=True, dx_bf16=dxb)
+            K.norm_bwd(Ls["n1"], dhx, dX, dx_accumulate=True, dx_bf16=nb)
             del dqkv, dhx, dh2x
             if lora:
                 self._join_side()  # the layer's gradients are complete before its bucket can be exchanged
@@ -751,11 +761,11 @@ class VLAEngine(EngineOps):
                 self.G[n].zero_()
         self._group_done("assembly")
         dimg = self._e(Mi, d)
-        K.call("slx_gather_rows", K.P(dX), d, K.P(dplan["img_pos"]), Mi, d, K.P(dimg), d, 1, K.stream_ptr())
+        K.call("slx_gather_rows", K.P(dX), d, K.P(dplan["img_pos"]), Mi, d, K.P(dimg), d, int(not pr), K.stream_ptr())
         del dX, dfeat
         # ---------------- mlp1 backward ----------------
         K.mm(dimg, sv["a1"], self.G["proj.fc2.w"], ta=True, tb=False, accumulate=True)
-        self._colsum(dimg, self.G["proj.fc2.b"], 0)
+        self._colsum(dimg, self.G["proj.fc2.b"])
         da1 = self._e(Mi, d)
         self._mm_dx(dimg, self.W["proj.fc2.w"], self.WT.get("proj.fc2.w"), da1, epi=K.EPI_GELU_BWD, aux=sv["a1pre"],
                     ldaux=d, colsum=self.G["proj.fc1.b"])
@@ -783,19 +793,22 @@ class VLAEngine(EngineOps):
             Ls = sv["vit"][i]
             # x_out = x_mid + ls2 * (fc2(gelu(fc1(ln2(x_mid)))) ); below the top layer this branch backward ran fused
             # into the previous LN1 backward (slx_norm_desc.ls*)
-            if i == cfg.vit_layers - 1:
+            if i == cfg.vit_layers - 1 and pr:
+                self._ls_branch_precise(dxv, self.P[p + "ls2"], Ls["y2"], g, self.G[p + "ls2"], self.G[p + "fc2.b"])
+            elif i == cfg.vit_layers - 1:
                 K.call("slx_ls_branch_bwd", K.P(dxv), D, K.P(self.P[p + "ls2"]), K.P(Ls["y2"]), D, K.P(g), D, Mv, D,
                        K.P(self.G[p + "ls2"]), K.P(self.G[p + "fc2.b"]), 1, K.P(self._ws(2 * 256 * D)), K.stream_ptr())
-            if not PAIR_WGRAD:
+            pair = PAIR_WGRAD and not pr
+            if not pair:
                 K.mm(g, Ls["hact"], self.G[p + "fc2.w"], ta=True, tb=False, accumulate=True)
             dh = self._e(Mv, F_)
             self._mm_dx(g, self.W[p + "fc2.w"], self.WT.get(p + "fc2.w"), dh, epi=K.EPI_GELU_BWD, aux=Ls["hpre"],
                         ldaux=F_, colsum=self.G[p + "fc1.b"],  # fc1.b grad = column sums of dh, in the same epilogue
                         aux_grad=Ls["hgrad"])
-            side = PAIR_WGRAD and PAIR_SIDE and not self.precise
+            side = pair and PAIR_SIDE
             if side:
                 ev_side = self._side_fork()
-            elif PAIR_WGRAD:  # fc2.w and fc1.w gradients as one launch (two under-filled grids fill the chip together)
+            elif pair:  # fc2.w and fc1.w gradients as one launch (two under-filled grids fill the chip together)
                 with self._probe("vit.wgrad_fc"):
                     K.mm_pair((g, Ls["hact"], self.G[p + "fc2.w"]), (dh, Ls["h2"], self.G[p + "fc1.w"]))
             else:
@@ -810,10 +823,12 @@ class VLAEngine(EngineOps):
             del dh
             # x_mid = x_in + ls1 * proj(attn(ln1(x_in))): its branch backward (g = ls1 * dx_mid, dls1, proj.b grad)
             # fused into the LN2 backward that produces dx_mid
+            lsb = (self.P[p + "ls1"], Ls["y1"], g, self.G[p + "ls1"], self.G[p + "proj.b"])
             K.norm_bwd(Ls["n2"], dh2, dxv, dx_accumulate=True, dgamma=self.G[p + "ln2.w"], dbeta=self.G[p + "ln2.b"],
-                       ws=self._ws(K.norm_ws_floats(D)), param_accumulate=True,
-                       ls_branch=(self.P[p + "ls1"], Ls["y1"], g, self.G[p + "ls1"], self.G[p + "proj.b"]))
-            if not PAIR_WGRAD:
+                       ws=self._ws(K.norm_ws_floats(D)), param_accumulate=True, ls_branch=None if pr else lsb)
+            if pr:
+                self._ls_branch_precise(dxv, *lsb)
+            if not pair:
                 K.mm(g, Ls["o"], self.G[p + "proj.w"], ta=True, tb=False, accumulate=True)
             do = self._e(Mv, D)
             self._mm_dx(g, self.W[p + "proj.w"], self.WT.get(p + "proj.w"), do)
@@ -825,7 +840,7 @@ class VLAEngine(EngineOps):
             del do
             if side:
                 ev_side = self._side_fork()
-            elif PAIR_WGRAD:  # proj.w (g still holds ls1 * dx_mid) and qkv.w gradients as one launch
+            elif pair:  # proj.w (g still holds ls1 * dx_mid) and qkv.w gradients as one launch
                 with self._probe("vit.wgrad_attn"):
                     K.mm_pair((g, Ls["o"], self.G[p + "proj.w"]), (dqkv, Ls["h1"], self.G[p + "qkv.w"]))
             else:
@@ -842,18 +857,20 @@ class VLAEngine(EngineOps):
                 q = f"vit.{i - 1}."
                 nxt = (self.P[q + "ls2"], sv["vit"][i - 1]["y2"], g, self.G[q + "ls2"], self.G[q + "fc2.b"])
             K.norm_bwd(Ls["n1"], dh2, dxv, dx_accumulate=True, dgamma=self.G[p + "ln1.w"], dbeta=self.G[p + "ln1.b"],
-                       ws=self._ws(K.norm_ws_floats(D)), param_accumulate=True, ls_branch=nxt)
+                       ws=self._ws(K.norm_ws_floats(D)), param_accumulate=True, ls_branch=None if pr else nxt)
+            if pr and nxt is not None:
+                self._ls_branch_precise(dxv, *nxt)
             del dh2
             self._group_done(f"vit{i}")
         # ---------------- embeddings ----------------
         g_ = cfg.vit_grid
         dpatch = self._e(N * g_ * g_, D)
-        K.call("slx_vit_embed_bwd", K.P(dxv), N, T, D, K.P(self.G["vit.pos"]), K.P(self.G["vit.cls"]), K.P(dpatch),
-               K.stream_ptr())
+        K.call("slx_vit_embed_bwd_f32" if pr else "slx_vit_embed_bwd", K.P(dxv), N, T, D, K.P(self.G["vit.pos"]),
+               K.P(self.G["vit.cls"]), K.P(dpatch), K.stream_ptr())
         dwp = self._e(D, cfg.patch_kpad, dtype=F32)
         K.mm(dpatch, sv["col"], dwp, ta=True, tb=False)
         self.G["vit.patch.w"].copy_(dwp[:, : cfg.patch_k])
-        self._colsum(dpatch, self.G["vit.patch.b"], 0)
+        self._colsum(dpatch, self.G["vit.patch.b"])
         self._group_done("vit_embed")
         self.bucketer.mark("backward_end")
         self.saved = None
@@ -915,6 +932,9 @@ class VLAEngine(EngineOps):
         swiglu=(gu, dgu) (down projection only): the dx term and the SwiGLU backward run in one GEMM epilogue instead:
         dgu = swiglu'(gu) applied to dx + drop'(dt A)."""
         cfg = self.cfg
+        if self.precise:
+            self._lora_bwd_precise(i, sites, dys, tx, x, dtx, dx, swiglu)
+            return
         drop = sv["drop"]
         keep = sv["llm"][i]["lora"]
         bits = [keep[site] for site in sites]
@@ -943,6 +963,21 @@ class VLAEngine(EngineOps):
                    seed=lora_site_seed(sv["step_seed"], i, LORA_SITES.index("down")), drop_p=drop,
                    ldmask=x.shape[1], maskbits=bits[0], variant=SWIGLU_BWD_VARIANT)
 
+
+    def _lora_bwd_precise(self, i, sites, dys, tx, x, dtx, dx, swiglu):
+        """fp32 parity mode of _lora_bwd (no dropout): dB_j = s dy_j^T t_j, dA_j += dt_j^T x, dx += dt_j A_j as f32 GEMMs,
+        then (down site) the SwiGLU backward of dx."""
+        r = self.cfg.lora_r
+        self._lora_db(i, sites, dys, tx)
+        for j, site in enumerate(sites):
+            dt = dtx[:, r * j:r * (j + 1)]
+            a = f"llm.{i}.lora.{site}.a"
+            K.mm(dt, x, self.G[a], ta=True, tb=False, accumulate=True)
+            K.mm(dt, self.W[a], dx, tb=False, accumulate=True)
+        if swiglu is not None:
+            gu, dgu = swiglu
+            K.call("slx_swiglu_bwd_f32", K.P(dx), dx.stride(0), K.P(gu), gu.stride(0), K.P(dgu), dgu.stride(0), x.shape[0],
+                   gu.shape[1] // 2, K.stream_ptr())
 
     def _lora_bwd_grouped(self, i, sites, dys, tx, x, dtx, dx, swiglu, dx_bf16, drop, bits, As, step_seed):
         """LORA_GRAD_GROUP: the dx term (or the down site's SwiGLU epilogue) now; dB_j and dA_j as slx_lora_grad jobs

@@ -125,10 +125,24 @@ class EngineOps:
             self._wsbuf = self._e(max(nfloats, 1 << 20), dtype=F32)
         return self._wsbuf
 
-    def _colsum(self, x, out, mode):
+    def _colsum(self, x, out, mode=None):
+        """out += column sums of x (mode 0 bf16 rows, 1 f32 rows; inferred from x when None)."""
         M, N = x.shape
+        mode = int(x.dtype == F32) if mode is None else mode
+        assert mode == int(x.dtype == F32), (mode, x.dtype)
         ws = self._ws(K.lib().slx_colsum_ws_floats(N))
         K.call("slx_colsum", mode, K.P(x), x.stride(0), M, N, K.P(out), 1, K.P(ws), K.stream_ptr())
+
+    def _ls_branch_precise(self, dres, ls, y, g, dls, dbias):
+        """fp32 parity mode of slx_ls_branch_bwd (and of the branch fused into slx_norm_bwd): g = dres * ls,
+        dls += colsum(dres * y), dbias += colsum(g) - f32 rows throughout."""
+        M, N = g.shape
+        K.call("slx_mul_f32", 1, K.P(dres), dres.stride(0), K.P(ls), 0, K.P(g), g.stride(0), M, N, K.stream_ptr())
+        self._colsum(g, dbias)
+        if dls is not None:
+            t = self._e(M, N, dtype=F32)
+            K.call("slx_mul_f32", 0, K.P(dres), dres.stride(0), K.P(y), y.stride(0), K.P(t), N, M, N, K.stream_ptr())
+            self._colsum(t, dls)
 
     def _mlp_fwd(self, x, layers):
         """driving head: list of (prefix, out_dim, act) -> saved [(out, pre, in)]"""

@@ -132,7 +132,11 @@ def gemm(A, B, C, M, N, K, layout, lda, ldb, ldc, **kw):
     if A.dtype == torch.float32:  # fp32 parity mode (csrc/precise.hip)
         if B.dtype != torch.float32 or C.dtype != torch.float32:
             raise RuntimeError("fp32 parity-mode GEMM needs f32 A, B and C")
+        colsum = kw.get("colsum")
+        d.colsum = d.colsum_ws = 0  # the f32 twin has no fused colsum: the output's column sums separately
         check(lib().slx_gemm_f32(ctypes.byref(d), stream_ptr()), "slx_gemm_f32")
+        if colsum is not None:
+            call("slx_colsum", 1, C.data_ptr(), int(ldc), int(M), int(N), colsum.data_ptr(), 1, 0, stream_ptr())
         rope = kw.get("rope")
         if rope is not None:  # the f32 kernels have no fused RoPE epilogue: the separate rotation
             cos, sin, rs, rn = rope
@@ -358,6 +362,13 @@ for _n, _a in {
     "slx_im2col_patch_f32": [_vp, _i, _i, _i, _i, _i, _vp, _vp],
     "slx_assemble_tokens_f32": [_vp, _I, _i, _vp, _i, _vp, _vp, _vp, _vp, _vp],
     "slx_llava_merge_fwd_f32": [_vp, _i, _I, _i, _i, _i, _i, _i, _i, _i, _i, _vp, _vp, _vp],
+    "slx_attn_bwd_f32": [ctypes.POINTER(AttnDesc), ctypes.POINTER(AttnBwdDesc), _vp],
+    "slx_swiglu_bwd_f32": [_vp, _I, _vp, _I, _vp, _I, _I, _i, _vp],
+    "slx_mul_f32": [_i, _vp, _I, _vp, _I, _vp, _I, _I, _i, _vp],
+    "slx_ce_bwd_f32": [_vp, _I, _vp, _vp, _I, _i, _vp, _vp, _I, _vp],
+    "slx_vit_embed_bwd_f32": [_vp, _i, _i, _i, _vp, _vp, _vp, _vp],
+    "slx_set_deterministic": [_i, _vp, _I],
+    "slx_get_deterministic": [],
 }.items():
     register(_n, _a)
 register("slx_lora_bwd_ws_floats", [_I, _i, _i], restype=c_i64)  # int64_t result (include/slx.h)
@@ -404,6 +415,26 @@ def attn_bwd(q, k, v, o, lse, dout, dq, dk, dv, ws, *, rope_cos=None, rope_sin=N
         n = d.Hq * 64
         assert dbias.dtype == torch.float32 and dbias.is_contiguous() and dbias.numel() == 3 * n
         g.dbias_q, g.dbias_k, g.dbias_v = dbias.data_ptr(), dbias.data_ptr() + 4 * n, dbias.data_ptr() + 8 * n
+    if q.dtype == torch.float32:  # fp32 parity mode: the plain restatement, then RoPE^T and the bias column sums
+        g.rope_cos = g.rope_sin = g.dbias_q = g.dbias_k = g.dbias_v = 0
+        check(lib().slx_attn_bwd_f32(ctypes.byref(d), ctypes.byref(g), stream_ptr()), "slx_attn_bwd_f32")
+        ntok = d.B * d.S
+        if rope_cos is not None:
+            rope(dq, ntok, d.S, d.Hq, rope_cos, rope_sin, inverse=True)
+            rope(dk, ntok, d.S, d.Hkv, rope_cos, rope_sin, inverse=True)
+        if dbias is not None:
+            n = d.Hq * 64
+            for j, t in enumerate((dq, dk, dv)):
+                call("slx_colsum", 1, P(t), t.stride(0), ntok, n, dbias.data_ptr() + 4 * n * j, 1, 0, stream_ptr())
+        return
+    if dbias is not None and deterministic():  # the fused bias sums end in f32 atomics: ordered column sums instead
+        g.dbias_q = g.dbias_k = g.dbias_v = 0
+        check(lib().slx_attn_bwd(ctypes.byref(d), ctypes.byref(g), stream_ptr()), "slx_attn_bwd")
+        n = d.Hq * 64
+        for j, t in enumerate((dq, dk, dv)):
+            call("slx_colsum", int(t.dtype == torch.float32), P(t), t.stride(0), d.B * d.S, n,
+                 dbias.data_ptr() + 4 * n * j, 1, 0, stream_ptr())
+        return
     check(lib().slx_attn_bwd(ctypes.byref(d), ctypes.byref(g), stream_ptr()), "slx_attn_bwd")
 
 
@@ -415,6 +446,28 @@ def attn_ws(B, S, Hq, Hkv, device, rope=False):
         ws["dk_acc"] = torch.empty(B * S * Hq * 64, device=device)
         ws["dv_acc"] = torch.empty(B * S * Hq * 64, device=device)
     return ws
+
+
+_det_ws: dict = {}
+DET_WS_FLOATS = 16 << 20  # 64 MB: the largest partial set of the InternVL2-1B step (LoRA MLP half, ~2.2 M floats) x 7
+
+
+def set_deterministic(on: bool, device=None):
+    """Deterministic-reduction mode (slx_set_deterministic, process-wide): every cross-block f32 reduction of the step
+    goes through per-block partials and an ordered sum instead of f32 atomics, so two runs on the same inputs give
+    bitwise-equal gradients. The workspace is allocated once per device and kept."""
+    if on:
+        dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        ws = _det_ws.get(dev)
+        if ws is None:
+            ws = _det_ws[dev] = torch.empty(DET_WS_FLOATS, dtype=torch.float32, device=dev)
+        check(lib().slx_set_deterministic(1, P(ws), ws.numel()), "slx_set_deterministic")
+    else:
+        check(lib().slx_set_deterministic(0, None, 0), "slx_set_deterministic")
+
+
+def deterministic() -> bool:
+    return bool(lib().slx_get_deterministic())
 
 
 def rope_rows(x, ntok, S, nheads, cos, sin):

@@ -108,7 +108,10 @@ def test_lora_bwd_grouped(dev, M, kin, nsites, p, mode, dt_bf16, slab, monkeypat
     dx0 = torch.randn(M, kin, device=dev, generator=g)
     dx = dx0.clone()
     dxb = torch.empty(M, kin, device=dev, dtype=torch.bfloat16) if mode == "bf16" else None
-    K.lora_bwd(x, dt, As, bits, dAs, dx=None if mode == "none" else dx, dx_bf16=dxb, p=p)
+    # the dx kernel's bf16 dT side output (slx_lora_grad's operand), a strided view as the engine passes it
+    dto = torch.full((M, 32 * nsites + 16), -7.0, device=dev, dtype=torch.bfloat16) if mode != "none" else None
+    K.lora_bwd(x, dt, As, bits, dAs, dx=None if mode == "none" else dx, dx_bf16=dxb, p=p,
+               dt_out=None if dto is None else dto[:, 8:8 + 32 * nsites])
     dtb = dt.bfloat16().float()
     ref_dx = dx0.clone()
     for j in range(nsites):
@@ -117,6 +120,9 @@ def test_lora_bwd_grouped(dev, M, kin, nsites, p, mode, dt_bf16, slab, monkeypat
         torch.testing.assert_close(dAs[j], 0.5 + dtb[:, 32 * j:32 * (j + 1)].t() @ xd, atol=5e-2 * (M / 300) ** 0.5,
                                    rtol=1e-2)
         ref_dx += mask * (dtb[:, 32 * j:32 * (j + 1)] @ As[j].float())
+    if dto is not None:  # every row (M % 32 != 0 too) and column tile of both column groups, exact
+        assert torch.equal(dto[:, 8:8 + 32 * nsites], dt.bfloat16())
+        assert bool((dto[:, :8] == -7.0).all()) and bool((dto[:, 8 + 32 * nsites:] == -7.0).all())
     lora_term = (ref_dx - dx0).abs().max().item()
     if mode == "f32":  # the kernel sums the same bf16 operands in f32: relative to the LoRA term, ~1e-7
         assert (dx - ref_dx).abs().max().item() <= 1e-5 * lora_term
@@ -150,10 +156,13 @@ def test_lora_da_slab_deterministic(dev, M, kin, nsites, monkeypatch):
         assert ((a - c).norm() / c.norm()).item() < 1e-5
 
 
+@pytest.mark.parametrize("det", [False, True])
 @pytest.mark.parametrize("M,p", [(6384, 0.1), (1000, 0.0), (77, 0.1)])
-def test_lora_grad_jobs(dev, M, p):
+def test_lora_grad_jobs(dev, M, p, det):
     """slx_lora_grad: a B-gradient job (out [n][32] += s dy^T t) and an A-gradient job of 3 sites sharing x with keep
-    bits (out_j [32][n] += dT_j^T bf16(x/(1-p)) & keep_j), against torch fp32 on the same bf16 operands."""
+    bits (out_j [32][n] += dT_j^T bf16(x/(1-p)) & keep_j), against torch fp32 on the same bf16 operands.
+    det: the deterministic-reduction mode (per-row-chunk partials + ordered sum instead of f32 atomics) - the same
+    values, and two launches bitwise equal."""
     from simlingo_amd.dropmask import keep_bits
     g = torch.Generator(device=dev).manual_seed(21)
     s = 2.0
@@ -167,8 +176,19 @@ def test_lora_grad_jobs(dev, M, p):
     dA = [torch.full((32, 896), -0.5, device=dev) for _ in range(3)]
     jobs = [dict(x=dy, t=t[:, 32:64], outs=[dB], out_nr=True, alpha=s),
             dict(x=x, t=dT, outs=dA, out_nr=False, alpha=1.0, p=p, bits=bits)]
-    K.lora_grad(jobs, M)
-    torch.cuda.synchronize()
+    if det:
+        K.set_deterministic(True, dev)
+    try:
+        K.lora_grad(jobs, M)
+        if det:
+            dB2 = torch.full((4864, 32), 0.25, device=dev)
+            dA2 = [torch.full((32, 896), -0.5, device=dev) for _ in range(3)]
+            K.lora_grad([dict(jobs[0], outs=[dB2]), dict(jobs[1], outs=dA2)], M)
+        torch.cuda.synchronize()
+    finally:
+        K.set_deterministic(False)
+    if det:
+        assert torch.equal(dB, dB2) and all(torch.equal(a, b) for a, b in zip(dA, dA2))
     refB = 0.25 + s * dy.float().t() @ t[:, 32:64].float()
     torch.testing.assert_close(dB, refB, atol=2e-3 * refB.abs().max().item(), rtol=1e-4)
     for j in range(3):

@@ -4,7 +4,8 @@ Tolerances (bf16 operands, f32 accumulation, 2+2 tiny layers, weights N(0, 0.05)
 gate: losses rel <= 1e-2; waypoint predictions (cumsum of 20 / 10 head outputs) max |diff| <= 5e-2 m; every
 trainable gradient cosine >= 0.98 and relative L2 error <= 0.2 (tiny widths: a 128-wide bf16 dot product
 carries relatively more rounding than the real 896/1024 widths, which tests/test_fullgeom_parity_gpu.py holds to
-cosine >= 0.99 / rel <= 0.1). The north-star 1e-4 m bound is held by the fp32 parity mode below.
+cosine >= 0.99 / rel <= 0.1). The north-star 1e-4 m bound is held by the fp32 parity mode below, on the forward
+and on a whole training step (forward + backward + clip + AdamW, then the updated model's predictions).
 """
 import numpy as np
 import pytest
@@ -98,8 +99,66 @@ def test_precise_forward_north_star(dev, case):
     print(msg)
     assert d_loss[1].item() <= 1e-4 and d_route <= 1e-4 and d_speed <= 1e-4, msg
     assert torch.allclose(out4, want, rtol=1e-4, atol=1e-5), msg
-    with pytest.raises(RuntimeError):
-        eng.backward(None)
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_precise_train_step_north_star(dev, case):
+    """VERDICT r4 missing #1: the TRAINED path at the north-star tolerance. fp32 parity mode forward + backward +
+    global-norm clip 0.3 + AdamW (driving.py:718-732, train.py:206) against the oracle's autograd gradients and
+    torch.optim.AdamW over the same trainable set: every gradient within 1e-4 relative L2, the updated parameters
+    within 1e-6 absolute (Adam's first step moves each element by ~lr), and the waypoints / route points the updated
+    model predicts within 1e-4 m of the oracle's updated model (losses 1e-4 relative)."""
+    from simlingo_amd.engine import VLAEngine
+    from simlingo_amd.plan import plan_from_example
+    cfg, P, ex, z = load_case(case)
+    assert cfg.lora_dropout == 0.0
+    ref, grads = O.loss_and_grads(P, cfg, ex)
+    eng = VLAEngine(cfg, dev, P, precise=True)
+    plan = plan_from_example(cfg, ex)
+    lab = ex.driving_label
+    args = (ex.driving_input.camera_images.to(dev), plan, plan.to_device(dev), lab.path.to(dev), lab.waypoints.to(dev))
+    out4, _, _ = eng.forward(*args, training=True)
+    eng.backward(None)
+    torch.cuda.synchronize()
+    assert abs(out4[0].item() - ref["loss"].item()) <= 1e-4 * abs(ref["loss"].item())
+    worst, bad = 0.0, []
+    for name, g in grads.items():
+        e = eng.G[name].detach().float().cpu().reshape(-1)
+        r = g.reshape(-1)
+        if r.norm() < 1e-10:
+            assert e.norm() < 1e-6, name
+            continue
+        rel = ((e - r).norm() / r.norm()).item()
+        worst = max(worst, rel)
+        if rel > 1e-4:
+            bad.append((name, rel))
+    print(f"[{case}] worst gradient rel L2 {worst:.3g}")
+    assert not bad, bad
+    # one optimizer step each side
+    lr = 1e-4
+    Pt = {k: v.detach().clone().float() for k, v in P.items()}
+    tr = [k for k in grads]
+    for k in tr:
+        Pt[k].requires_grad_(True)
+        Pt[k].grad = grads[k].clone().float()
+    torch.nn.utils.clip_grad_norm_([Pt[k] for k in tr], cfg.grad_clip)
+    opt = torch.optim.AdamW([Pt[k] for k in tr], lr=lr, betas=cfg.betas, eps=cfg.eps, weight_decay=cfg.weight_decay)
+    opt.step()
+    eng.adamw_step(lr, 1, betas=cfg.betas, eps=cfg.eps, weight_decay=cfg.weight_decay, max_norm=cfg.grad_clip)
+    torch.cuda.synchronize()
+    dmax = max((eng.P[k].detach().cpu() - Pt[k].detach()).abs().max().item() for k in tr)
+    assert dmax <= 1e-6, dmax
+    Pu = {k: v.detach() for k, v in Pt.items()}
+    with torch.no_grad():
+        ref2 = O.forward_loss(Pu, cfg, ex)
+    out4, rp, sp = eng.forward(*args, training=True)
+    torch.cuda.synchronize()
+    d_route = (rp.cpu() - ref2["route_pred"]).abs().max().item()
+    d_speed = (sp.cpu() - ref2["speed_pred"]).abs().max().item()
+    msg = f"after the update: route {d_route:.3g} speed {d_speed:.3g} params {dmax:.3g}"
+    print(f"[{case}] {msg}")
+    assert d_route <= 1e-4 and d_speed <= 1e-4, msg
+    assert abs(out4[0].item() - ref2["loss"].item()) <= 1e-4 * abs(ref2["loss"].item()), msg
 
 
 def test_engine_vocab_not_multiple_of_128(dev):
