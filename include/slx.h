@@ -326,6 +326,13 @@ int slx_sumsq(const float* g, int64_t n, float* out, int zero_first, slx_stream_
 /* grad_scale multiplies the gradient (1/world after a SUM all-reduce); clipping uses the scaled norm */
 int slx_adamw(float* p, const float* g, float* m, float* v, void* p_bf16, int64_t n, float lr, float beta1, float beta2,
               float eps, float weight_decay, int step, const float* sumsq, float max_norm, float grad_scale, slx_stream_t s);
+/* The same clip + AdamW, and the sum of squares, reading the gradients as bf16: the summed data-parallel gradient on
+ * the bf16 all-reduce wire (simlingo_amd/ddp.py wire="bf16"), scaled by grad_scale (1/world) and widened to f32 inside
+ * the kernel, so no cast-back pass runs between the last all-reduce and the optimizer (train.py:160-168).          */
+int slx_adamw_bf16g(float* p, const void* g_bf16, float* m, float* v, void* p_bf16, int64_t n, float lr, float beta1,
+                    float beta2, float eps, float weight_decay, int step, const float* sumsq, float max_norm,
+                    float grad_scale, slx_stream_t s);
+int slx_sumsq_bf16(const void* g_bf16, int64_t n, float* out, int zero_first, slx_stream_t s);
 int slx_cast_f32_bf16(const float* src, void* dst, int64_t n, slx_stream_t s);
 
 /* ---- SimLingo-Base (LLaVA-NeXT CLIP encoder + tiny Llama, BASELINE configs[1]) ----------------- */

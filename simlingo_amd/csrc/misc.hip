@@ -367,15 +367,27 @@ __global__ void loss_gscale_kernel(const float* dl, int nl, int nr, int ns, floa
 // ---------------------------------------------------------------------------------------------
 // Optimizer: global grad-norm (sum of squares, partials + atomics) and fused clip + AdamW
 // (torch.optim.AdamW semantics, decoupled weight decay; driving.py:718-724, clip train.py:206).
-__global__ __launch_bounds__(256) void sumsq_kernel(const float* g, long n, float* out, float* part) {
+// GT = float, or bf16: the summed data-parallel gradients straight from the bf16 all-reduce wire (ddp.py wire="bf16")
+template <typename GT>
+__device__ __forceinline__ float4 load_g4(const GT* g, long i) {
+  if constexpr (sizeof(GT) == 4) {
+    return reinterpret_cast<const float4*>(g)[i];
+  } else {
+    const bf16x4 b = reinterpret_cast<const bf16x4*>(g)[i];
+    return make_float4((float)b[0], (float)b[1], (float)b[2], (float)b[3]);
+  }
+}
+
+template <typename GT>
+__global__ __launch_bounds__(256) void sumsq_kernel(const GT* g, long n, float* out, float* part) {
   __shared__ float sh[16];
   float s = 0.f;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n / 4; i += (long)gridDim.x * blockDim.x) {
-    const float4 v = reinterpret_cast<const float4*>(g)[i];
+    const float4 v = load_g4(g, i);
     s += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
   }
   if (blockIdx.x == 0)
-    for (long i = (n / 4) * 4 + threadIdx.x; i < n; i += blockDim.x) s += g[i] * g[i];
+    for (long i = (n / 4) * 4 + threadIdx.x; i < n; i += blockDim.x) s += (float)g[i] * (float)g[i];
   s = block_sum(s, sh);
   if (threadIdx.x == 0) {
     if (part) part[blockIdx.x] = s;  // deterministic mode: summed in block order by det_reduce
@@ -383,7 +395,8 @@ __global__ __launch_bounds__(256) void sumsq_kernel(const float* g, long n, floa
   }
 }
 
-__global__ __launch_bounds__(256) void adamw_kernel(float* p, const float* g, float* m, float* v, bf16* pbf, long n,
+template <typename GT>
+__global__ __launch_bounds__(256) void adamw_kernel(float* p, const GT* g, float* m, float* v, bf16* pbf, long n,
                                                     float lr, float b1, float b2, float eps, float wd, float bc1,
                                                     float bc2s, const float* sumsq, float max_norm, float gscale) {
   // gscale: 1/world for summed data-parallel gradients; clip on the averaged gradient's norm
@@ -394,7 +407,7 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* p, const float* g, fl
   }
   const float step = lr / bc1;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
-    const float gi = g[i] * coef;
+    const float gi = (float)g[i] * coef;
     float pi = p[i] * (1.f - lr * wd);
     const float mi = m[i] + (1.f - b1) * (gi - m[i]);
     const float vi = v[i] * b2 + (1.f - b2) * gi * gi;
@@ -407,7 +420,8 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* p, const float* g, fl
 
 // The same update four parameters per lane (16-B loads and stores of p / g / m / v, 8-B bf16 stores): n4 quads from
 // 16-B aligned p / g / m / v and an 8-B aligned pbf; the launcher runs the scalar kernel on the tail.
-__global__ __launch_bounds__(256) void adamw_kernel_x4(float4* p, const float4* g, float4* m, float4* v, bf16x4* pbf,
+template <typename GT>
+__global__ __launch_bounds__(256) void adamw_kernel_x4(float4* p, const GT* g, float4* m, float4* v, bf16x4* pbf,
                                                      long n4, float lr, float b1, float b2, float eps, float wd, float bc1,
                                                      float bc2s, const float* sumsq, float max_norm, float gscale) {
   float coef = gscale;
@@ -417,7 +431,7 @@ __global__ __launch_bounds__(256) void adamw_kernel_x4(float4* p, const float4* 
   }
   const float step = lr / bc1;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
-    const float4 g4 = g[i], p4 = p[i], m4 = m[i], v4 = v[i];
+    const float4 g4 = load_g4(g, i), p4 = p[i], m4 = m[i], v4 = v[i];
     float gi[4] = {g4.x, g4.y, g4.z, g4.w}, pi[4] = {p4.x, p4.y, p4.z, p4.w};
     float mi[4] = {m4.x, m4.y, m4.z, m4.w}, vi[4] = {v4.x, v4.y, v4.z, v4.w};
 #pragma unroll
@@ -830,7 +844,9 @@ int slx_loss_gscale(const float* dtotal, int nl, int nr, int ns, float* gs, slx_
   return 0;
 }
 
-int slx_sumsq(const float* g, int64_t n, float* out, int zero_first, slx_stream_t s) {  // out (+)= sum g^2
+extern "C++" {
+template <typename GT>
+static int sumsq_impl(const GT* g, int64_t n, float* out, int zero_first, slx_stream_t s) {  // out (+)= sum g^2
   hipStream_t st = (hipStream_t)s;
   if (zero_first) hipMemsetAsync(out, 0, sizeof(float), st);
   if (!n) return 0;
@@ -839,20 +855,33 @@ int slx_sumsq(const float* g, int64_t n, float* out, int zero_first, slx_stream_
   if (blocks < 1) blocks = 1;
   const DetMode& dm = det_mode();
   float* part = dm.on ? dm.ws : nullptr;
-  hipLaunchKernelGGL(sumsq_kernel, dim3((unsigned)blocks), dim3(256), 0, st, g, n, out, part);
+  hipLaunchKernelGGL(sumsq_kernel<GT>, dim3((unsigned)blocks), dim3(256), 0, st, g, n, out, part);
   SLX_LAUNCH_CHECK("slx_sumsq");
   if (part) return det_reduce(part, (int)blocks, 1, 1, out, 1, st);
   return 0;
 }
+}  // extern "C++"
 
-int slx_adamw(float* p, const float* g, float* m, float* v, void* p_bf16, int64_t n, float lr, float beta1, float beta2,
-              float eps, float weight_decay, int step, const float* sumsq, float max_norm, float grad_scale, slx_stream_t s) {
+int slx_sumsq(const float* g, int64_t n, float* out, int zero_first, slx_stream_t s) {
+  return sumsq_impl(g, n, out, zero_first, s);
+}
+
+int slx_sumsq_bf16(const void* g, int64_t n, float* out, int zero_first, slx_stream_t s) {
+  SLX_CHECK_ARG(((uintptr_t)g & 7) == 0, "slx_sumsq_bf16: 8-B aligned gradients");
+  return sumsq_impl((const bf16*)g, n, out, zero_first, s);
+}
+
+extern "C++" {
+template <typename GT>
+static int adamw_impl(float* p, const GT* g, float* m, float* v, void* p_bf16, int64_t n, float lr, float beta1,
+                      float beta2, float eps, float weight_decay, int step, const float* sumsq, float max_norm,
+                      float grad_scale, slx_stream_t s) {
   SLX_CHECK_ARG(step >= 1, "slx_adamw: step >= 1");
   if (!n) return 0;
   const float bc1 = 1.f - powf(beta1, (float)step);
   const float bc2s = sqrtf(1.f - powf(beta2, (float)step));
-  const bool vec = ((((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) == 0) &&
-                   (((uintptr_t)p_bf16 & 7) == 0);
+  const bool vec = ((((uintptr_t)p | (uintptr_t)m | (uintptr_t)v) & 15) == 0) &&
+                   (((uintptr_t)g & (sizeof(GT) == 4 ? 15 : 7)) == 0) && (((uintptr_t)p_bf16 & 7) == 0);
   long done = 0;
   if (vec && n >= 4) {
     const long n4 = n / 4;
@@ -863,7 +892,7 @@ int slx_adamw(float* p, const float* g, float* m, float* v, void* p_bf16, int64_
     long blocks = (n4 + 255) / 256;
     if (cap > 0 && blocks > cap) blocks = cap;
     if (blocks > 0x7fffffffL) blocks = 0x7fffffffL;
-    hipLaunchKernelGGL(adamw_kernel_x4, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)s, (float4*)p, (const float4*)g,
+    hipLaunchKernelGGL(adamw_kernel_x4<GT>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)s, (float4*)p, g,
                        (float4*)m, (float4*)v, (bf16x4*)p_bf16, n4, lr, beta1, beta2, eps, weight_decay, bc1, bc2s, sumsq,
                        max_norm, grad_scale);
     SLX_LAUNCH_CHECK("slx_adamw");
@@ -873,12 +902,25 @@ int slx_adamw(float* p, const float* g, float* m, float* v, void* p_bf16, int64_
     const long rest = n - done;
     long blocks = (rest + 255) / 256;
     if (blocks > 8192) blocks = 8192;
-    hipLaunchKernelGGL(adamw_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)s, p + done, g + done, m + done,
+    hipLaunchKernelGGL(adamw_kernel<GT>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)s, p + done, g + done, m + done,
                        v + done, p_bf16 ? (bf16*)p_bf16 + done : nullptr, rest, lr, beta1, beta2, eps, weight_decay, bc1,
                        bc2s, sumsq, max_norm, grad_scale);
     SLX_LAUNCH_CHECK("slx_adamw");
   }
   return 0;
+}
+}  // extern "C++"
+
+int slx_adamw(float* p, const float* g, float* m, float* v, void* p_bf16, int64_t n, float lr, float beta1, float beta2,
+              float eps, float weight_decay, int step, const float* sumsq, float max_norm, float grad_scale, slx_stream_t s) {
+  return adamw_impl(p, g, m, v, p_bf16, n, lr, beta1, beta2, eps, weight_decay, step, sumsq, max_norm, grad_scale, s);
+}
+
+int slx_adamw_bf16g(float* p, const void* g, float* m, float* v, void* p_bf16, int64_t n, float lr, float beta1,
+                    float beta2, float eps, float weight_decay, int step, const float* sumsq, float max_norm,
+                    float grad_scale, slx_stream_t s) {
+  return adamw_impl(p, (const bf16*)g, m, v, p_bf16, n, lr, beta1, beta2, eps, weight_decay, step, sumsq, max_norm,
+                    grad_scale, s);
 }
 
 int slx_scatter_rows(const float* src, int64_t lds, const int* idx, int64_t n, int D, float* dst, int64_t ldd, int accumulate, slx_stream_t s) {

@@ -9,8 +9,13 @@ backward of earlier layers keeps running. The optimizer waits on the handles and
 inside the fused AdamW kernel (no extra pass). Device-agnostic (the CPU tests drive it with gloo).
 
 wire="bf16" (SURVEY.md §8e): each bucket is cast to a bf16 staging slice before its all-reduce (half the xGMI
-bytes: 655 MB instead of 1.31 GB for the full model) and cast back into the f32 gradient when the optimizer waits, so
-the optimizer still accumulates in f32. trace=True records (event, bucket, perf_counter) tuples - "issue" when a
+bytes: 655 MB instead of 1.31 GB for the full model). The optimizer reads the summed bf16 wire buffer itself
+(optimizer_grad(): slx_sumsq_bf16 / slx_adamw_bf16g widen it and scale it by 1/world inside the kernels), so no
+cast-back pass runs between the last all-reduce and the optimizer; moments and master weights stay f32. Rounding of
+the wire: each rank's gradient is rounded to bf16 (8 significant bits: relative 2^-8) and the ring's partial sums are
+rounded again after every hop, so an element of the summed gradient over N ranks lies within N * 2^-8 * sum_r |g_r|
+of the exact sum (N = 8: 3.1e-2 of the sum of magnitudes, worst case; tests/test_ddp_gloo.py checks it at world 2 and
+8). wire="f32" keeps the exchange exact to f32 summation order at twice the bytes. trace=True records (event, bucket, perf_counter) tuples - "issue" when a
 bucket's all-reduce is launched, "backward_end" from the engine, "done" when a handle is found complete - the
 evidence that the exchange overlaps the backward (tests/test_ddp_gloo.py).
 
@@ -80,8 +85,8 @@ class GradBucketer:
             import torch.distributed as dist
             src = self.flat[bk.start:bk.end]
             if self.wire == "bf16":
-                if self.wire_buf is None:
-                    self.wire_buf = torch.empty(self.flat.numel(), dtype=torch.bfloat16, device=self.flat.device)
+                if self.wire_buf is None:  # zeroed once: elements in no bucket (alignment gaps) read as 0
+                    self.wire_buf = torch.zeros(self.flat.numel(), dtype=torch.bfloat16, device=self.flat.device)
                 src = self.wire_buf[bk.start:bk.end]
                 src.copy_(self.flat[bk.start:bk.end])
             bk.handle = dist.all_reduce(src, group=self.pg, async_op=True)
@@ -158,12 +163,17 @@ class GradBucketer:
                 if self.timing and not self.flat.is_cuda:
                     self._cur()["done"][i] = time.perf_counter()
                 bk.handle = None
-                if self.wire == "bf16":  # back into the f32 gradient the optimizer reads
-                    self.flat[bk.start:bk.end].copy_(self.wire_buf[bk.start:bk.end])
             bk.done = 0
             bk._seen = False
         if self.timing and waited and self.steps and "wait" not in self.steps[-1]:
             self.steps[-1]["wait"] = self._stamp()
+
+    def optimizer_grad(self):
+        """(gradient buffer, is_bf16) the optimizer reads after wait(): the summed bf16 wire buffer when the exchange
+        ran on the bf16 wire, else the flat f32 gradients."""
+        if self.wire == "bf16" and self.world > 1 and self.wire_buf is not None:
+            return self.wire_buf, True
+        return self.flat, False
 
     def summary(self) -> list[tuple[int, int, int]]:
         """[(start, end, n_groups)] in launch order."""

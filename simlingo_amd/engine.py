@@ -1027,8 +1027,11 @@ class VLAEngine(EngineOps):
             self.m_state = torch.zeros_like(self.master)
             self.v_state = torch.zeros_like(self.master)
             self.sumsq = torch.zeros(1, dtype=F32, device=self.device)
-        K.call("slx_sumsq", K.P(self.grad), self.n_flat, K.P(self.sumsq), 1, K.stream_ptr())
-        K.call("slx_adamw", K.P(self.master), K.P(self.grad), K.P(self.m_state), K.P(self.v_state), K.P(self.wbf),
+        # the summed gradients: the f32 buffer, or (bf16 all-reduce wire) the wire buffer itself, widened in the kernels
+        g, g_bf16 = self.bucketer.optimizer_grad()
+        K.call("slx_sumsq_bf16" if g_bf16 else "slx_sumsq", K.P(g), self.n_flat, K.P(self.sumsq), 1, K.stream_ptr())
+        K.call("slx_adamw_bf16g" if g_bf16 else "slx_adamw", K.P(self.master), K.P(g), K.P(self.m_state),
+               K.P(self.v_state), K.P(self.wbf),
                self.n_flat, float(lr), float(betas[0]), float(betas[1]), float(eps), float(weight_decay), int(step),
                K.P(self.sumsq), float(max_norm if max_norm else 0.0), 1.0 / self.world, K.stream_ptr())
         self._refresh_derived()
