@@ -1,8 +1,8 @@
 """SimLingo-Base training step on the MI355X (BaseEngine, bf16 MFMA / f32 accumulation) vs the CPU fp32
 oracle (oracle/base_oracle.py, itself pinned to the reference fixture tests/golden/base_tiny.npz).
 
-Tolerances (bf16 operands, 2 CLIP + 2 Llama tiny layers): losses rel 3e-2; predictions: every per-point head
-output (the cumsum increment) within 0.02 m and the cumulated waypoints within 0.1 m; every trainable
+Tolerances (bf16 operands, 2 CLIP + 2 Llama tiny layers): SURVEY.md §8d's bf16 gate - losses rel 1e-2, the
+cumulated waypoints within 5e-2 m (3e-2 / 0.1 m before); every trainable
 gradient cosine >= 0.98 and relative L2 error <= 0.2. Plus one optimizer step against torch.optim.AdamW with
 the reference's param groups (decay only on Linear/Conv weights, no decay on route_head) and clip 1.0."""
 import pytest
@@ -32,12 +32,14 @@ def test_base_engine_vs_oracle(dev, case):
     cfg, P, ex, _ = load_base_case(case)
     ref, grads = O.loss_and_grads(P, cfg, ex)
     eng, out4, rp, sp = run(cfg, P, ex, dev)
-    for got, k in ((out4[0], "loss"), (out4[2], "route_loss"), (out4[3], "speed_wps_loss")):
-        assert abs(got.item() - ref[k].item()) <= 3e-2 * abs(ref[k].item()) + 1e-3, (k, got.item(), ref[k].item())
-    for got, want in ((rp, ref["route_pred"]), (sp, ref["speed_pred"])):
-        inc = (torch.diff(got, dim=1, prepend=torch.zeros_like(got[:, :1]))
-               - torch.diff(want, dim=1, prepend=torch.zeros_like(want[:, :1]))).abs()
-        assert (got - want).abs().max().item() <= 0.1 and inc.max().item() <= 0.02, inc.max().item()
+    rels = {k: abs(got.item() - ref[k].item()) / abs(ref[k].item())
+            for got, k in ((out4[0], "loss"), (out4[2], "route_loss"), (out4[3], "speed_wps_loss"))}
+    dists = [(got - want).abs().max().item() for got, want in ((rp, ref["route_pred"]), (sp, ref["speed_pred"]))]
+    print(f"[{case}] loss rel {rels}, waypoints max |diff| route {dists[0]:.4g} m speed {dists[1]:.4g} m")
+    # SURVEY.md §8d's bf16 gate: losses 1e-2 relative, waypoints 5e-2 m
+    for k, r in rels.items():
+        assert r <= 1e-2, (k, r)
+    assert max(dists) <= 5e-2, dists
     bad = []
     for name, r in grads.items():
         e = eng.G[name].detach().float().cpu().reshape(-1)
