@@ -272,6 +272,22 @@ typedef struct slx_lora_grad_job {
   float* out[3]; int out_nr;
 } slx_lora_grad_job;
 int slx_lora_grad(const slx_lora_grad_job* jobs, int njobs, int64_t M, slx_stream_t s);
+/* The down site's LoRA dgrad fused with the SwiGLU backward (Qwen2MLP, llm.py:106-119 peft lora on down_proj):
+ * dgu[m, f] = d * u * silu'(g), dgu[m, F + f] = d * silu(g) with d = resid[m, f] + keep[m, f] (dT . A)[m, f] / (1 - p),
+ * g = gu[m, f], u = gu[m, F + f]. dT bf16 [M][>= 32] (the fused dgrad GEMM's LoRA columns), at = A^T bf16 [F][32]
+ * (lora_A.weight transposed), resid bf16 [M][F] (the base dgrad dact), gu bf16 [M][2F] (the gate|up GEMM output), bits
+ * the forward's keep bits [M][>= F/32] (p > 0). F % 256 == 0, 16-B aligned rows.                                  */
+typedef struct slx_lora_swiglu_bwd_desc {
+  const void* dt; int64_t lddt;
+  const void* at; int64_t ldat;
+  const void* resid; int64_t ldr;
+  const void* gu; int64_t ldgu;
+  const uint32_t* bits; int64_t ldbits;
+  float p;
+  void* dgu; int64_t lddgu;
+  int64_t M; int F;
+} slx_lora_swiglu_bwd_desc;
+int slx_lora_swiglu_bwd(const slx_lora_swiglu_bwd_desc* d, slx_stream_t stream);
 
 /* small strided f32 GEMM (driving heads adaptors.py:113-132, WaypointInputAdaptor :80)        */
 enum { SLX_ACT_NONE = 0, SLX_ACT_RELU = 1, SLX_ACT_SILU = 2 };

@@ -717,6 +717,91 @@ __global__ __launch_bounds__(256, 2) void lora_grad_kernel(LgArgs a) {
   }
 }
 
+
+// ---- the down site's LoRA dgrad fused with the SwiGLU backward (slx_lora_swiglu_bwd) ---------------------------------
+// dgu = [d * u * silu'(g) | d * silu(g)] with d = resid + keep * (dT . A) / (1 - p): the Qwen2MLP backward from the
+// gradient of the activation act = silu(g) * u (resid, the down projection's bf16 base dgrad) plus the down site's LoRA
+// term (dT [M x 32] . A [32 x F], keep bits of the forward's dropout). The GEMM form of the same (a K = 64 DROPMASK_
+// SWIGLU epilogue over the zero-padded A) walks 128 x 128 output tiles whose epilogue streams are the whole cost
+// (~315 MB per layer); here a block owns 32 rows x 256 columns: it issues its 4 x 16 B of resid / gate / up per thread
+// and the keep words first, runs the tiny K = 32 product on the MFMA (4 per wave, operands straight from global: dT
+// rows and the A^T rows of the packed [F][32] copy), exchanges the [32 x 256] f32 tile through LDS and stores 16 B of
+// gate and up gradient per chunk - row-contiguous 512-B streams in and out.
+struct LswArgs {
+  const bf16* dt; long lddt;
+  const bf16* at; long ldat;  // A^T [F][32] bf16
+  const bf16* resid; long ldr;
+  const bf16* gu; long ldgu;
+  const uint32_t* bits; long ldbits;
+  float sc;  // 1 / (1 - p)
+  bf16* dgu; long lddgu;
+  int M, F;
+};
+
+__global__ __launch_bounds__(256) void lora_swiglu_bwd_kernel(LswArgs a) {
+  __shared__ __attribute__((aligned(16))) float acc_s[32][256 + 4];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int m0 = blockIdx.x * 32, n0 = blockIdx.y * 256;
+  // epilogue operands first: chunk i of this thread = row (tid + 256 i) >> 5, 8 columns 8 ((tid + 256 i) & 31)
+  uint4 rr[4], gg[4], uu[4];
+  uint32_t kb[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = tid + 256 * i, row = c >> 5, n = n0 + 8 * (c & 31);
+    const int m = min(m0 + row, a.M - 1);  // rows past M load row M-1 (never stored)
+    rr[i] = *reinterpret_cast<const uint4*>(a.resid + (long)m * a.ldr + n);
+    gg[i] = *reinterpret_cast<const uint4*>(a.gu + (long)m * a.ldgu + n);
+    uu[i] = *reinterpret_cast<const uint4*>(a.gu + (long)m * a.ldgu + a.F + n);
+    kb[i] = a.bits ? (a.bits[(long)m * a.ldbits + (n >> 5)] >> (n & 31)) & 0xFFu : 0xFFu;
+  }
+  // [32 x 256] = dT [32 x 32] . A [32 x 256]: wave w takes column blocks 2w, 2w + 1
+  const int mr = min(m0 + (lane & 31), a.M - 1);
+  bf16x8 af[2], bfr[2][2];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk)
+    af[kk] = *reinterpret_cast<const bf16x8*>(a.dt + (long)mr * a.lddt + 16 * kk + 8 * (lane >> 5));
+#pragma unroll
+  for (int q = 0; q < 2; ++q)
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int n = n0 + 32 * (2 * w + q) + (lane & 31);
+      bfr[q][kk] = *reinterpret_cast<const bf16x8*>(a.at + (long)n * a.ldat + 16 * kk + 8 * (lane >> 5));
+    }
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    f32x16 acc;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) acc[j] = 0.f;
+    acc = mfma32x32(af[0], bfr[q][0], acc);
+    acc = mfma32x32(af[1], bfr[q][1], acc);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) acc_s[8 * (j >> 2) + 4 * (lane >> 5) + (j & 3)][32 * (2 * w + q) + (lane & 31)] = acc[j];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = tid + 256 * i, row = c >> 5, cc = c & 31, n = n0 + 8 * cc;
+    const int m = m0 + row;
+    const float4 v0 = *reinterpret_cast<const float4*>(&acc_s[row][8 * cc]);
+    const float4 v1 = *reinterpret_cast<const float4*>(&acc_s[row][8 * cc + 4]);
+    const float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+    const bf16x8 r8 = __builtin_bit_cast(bf16x8, rr[i]), g8 = __builtin_bit_cast(bf16x8, gg[i]),
+                 u8 = __builtin_bit_cast(bf16x8, uu[i]);
+    bf16x8 og, ou;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float d = ((kb[i] >> e) & 1u ? v[e] * a.sc : 0.f) + (float)r8[e];
+      const float g = (float)g8[e], u = (float)u8[e];
+      og[e] = (bf16)(d * u * silu_grad(g));
+      ou[e] = (bf16)(d * silu(g));
+    }
+    if (m < a.M) {
+      *reinterpret_cast<bf16x8*>(a.dgu + (long)m * a.lddgu + n) = og;
+      *reinterpret_cast<bf16x8*>(a.dgu + (long)m * a.lddgu + a.F + n) = ou;
+    }
+  }
+}
+
 }  // namespace slx
 
 using namespace slx;
@@ -954,5 +1039,28 @@ extern "C" int slx_lora_grad(const slx_lora_grad_job* jobs, int njobs, int64_t M
     for (int i = 0; i < njobs; ++i)
       for (int j = 0; j < a.j[i].ns; ++j)
         if (det_reduce(a.j[i].part[j], (int)nkc, 32L * a.j[i].N, 32L * a.j[i].N, a.j[i].out[j], 1, st)) return -1000;
+  return 0;
+}
+
+extern "C" int slx_lora_swiglu_bwd(const slx_lora_swiglu_bwd_desc* d, slx_stream_t stream) {
+  SLX_CHECK_ARG(d && d->dt && d->at && d->resid && d->gu && d->dgu, "slx_lora_swiglu_bwd: null operand");
+  SLX_CHECK_ARG(d->F > 0 && d->F % 256 == 0 && d->M >= 0, "slx_lora_swiglu_bwd: F %% 256 == 0 (got %d)", d->F);
+  SLX_CHECK_ARG(d->lddt % 8 == 0 && d->ldat % 8 == 0 && d->ldat >= 32 && d->ldr % 8 == 0 && d->ldgu % 8 == 0 &&
+                d->lddgu % 8 == 0 && ((((uintptr_t)d->dt | (uintptr_t)d->at | (uintptr_t)d->resid | (uintptr_t)d->gu |
+                                        (uintptr_t)d->dgu) & 15) == 0),
+                "slx_lora_swiglu_bwd: 16-B aligned rows (leading dims %% 8)");
+  SLX_CHECK_ARG(d->p >= 0.f && d->p < 1.f && (d->p == 0.f || (d->bits && d->ldbits >= d->F / 32)),
+                "slx_lora_swiglu_bwd: 0 <= p < 1, p > 0 needs the keep bits");
+  if (d->M == 0) return 0;
+  LswArgs a;
+  a.dt = (const bf16*)d->dt; a.lddt = d->lddt; a.at = (const bf16*)d->at; a.ldat = d->ldat;
+  a.resid = (const bf16*)d->resid; a.ldr = d->ldr; a.gu = (const bf16*)d->gu; a.ldgu = d->ldgu;
+  a.bits = d->p > 0.f ? d->bits : nullptr; a.ldbits = d->ldbits;
+  a.sc = 1.0f / (1.0f - d->p);
+  a.dgu = (bf16*)d->dgu; a.lddgu = d->lddgu;
+  a.M = (int)d->M; a.F = d->F;
+  hipLaunchKernelGGL(lora_swiglu_bwd_kernel, dim3((unsigned)((d->M + 31) / 32), (unsigned)(d->F / 256)), dim3(256), 0,
+                     (hipStream_t)stream, a);
+  SLX_LAUNCH_CHECK("slx_lora_swiglu_bwd");
   return 0;
 }

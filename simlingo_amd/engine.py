@@ -63,6 +63,10 @@ LORA_GRAD_GROUP = os.environ.get("SLX_LORA_GRAD_GROUP", "1") == "1"
 # 16400 x 4096): +0.5 % on the step (104.27 -> 104.83 samples/s, profiles/round4_gelu_aux_grad_ab.txt);
 # SLX_GELU_AUX_GRAD=0 stores the pre-activation as before
 GELU_AUX_GRAD = os.environ.get("SLX_GELU_AUX_GRAD", "1") == "1"
+# The down site's LoRA dgrad + the SwiGLU backward as one streaming kernel (slx_lora_swiglu_bwd: 32 x 256 tiles, the K = 32
+# product on the MFMA, 16-B row streams) instead of the K = 64 GEMM with the DROPMASK_SWIGLU epilogue over 128^2 tiles;
+# SLX_LORA_SWIGLU_BWD=0 restores the GEMM (A/B)
+LORA_SWIGLU_BWD = os.environ.get("SLX_LORA_SWIGLU_BWD", "1") == "1"
 # SLX_LORA_GRAD_DEFER=1: a layer's attention-half LoRA gradient jobs ride in the NEXT layer's (in backward order)
 # MLP-half slx_lora_grad launch instead of a launch of their own (~50 MB, latency-bound alone); the norm backwards
 # then write a fresh bf16 dX buffer, so the deferred o-site job keeps the one it read
@@ -308,6 +312,11 @@ class VLAEngine(EngineOps):
                         entries.append([a.data_ptr(), a.stride(0), af.data_ptr(), 0, r, a.shape[1],
                                         int(np.float32(1.0).view(np.int32)), mode])
                         cats[key + site] = af
+                    if site == "down":  # A^T [F][32] for slx_lora_swiglu_bwd (mode 4: transposed)
+                        at = torch.empty(a.shape[1], r, dtype=torch.bfloat16, device=self.device)
+                        entries.append([a.data_ptr(), a.stride(0), at.data_ptr(), r, r, a.shape[1],
+                                        int(np.float32(1.0).view(np.int32)), 4])
+                        cats["aT.down"] = at
             self.cat.append(cats)
         self._pack_tab = torch.tensor(entries, dtype=torch.int64, device=self.device)
         self._pack_n = len(entries)
@@ -1002,6 +1011,9 @@ class VLAEngine(EngineOps):
         assert dTb is dtx, "the SwiGLU path takes dT from the bf16 dgrad output"
         gu, dgu = swiglu
         F = gu.shape[1] // 2
+        if LORA_SWIGLU_BWD and F % 256 == 0:
+            K.lora_swiglu_bwd(dtx, self.cat[i]["aT.down"], dx, gu, dgu, bits[0], drop)
+            return
         K.gemm(dtx, self.cat[i]["apad.down"], dgu, M, F, 64, K.GEMM_NN, dtx.stride(0), x.shape[1], dgu.stride(0),
                epi=K.EPI_DROPMASK_SWIGLU, resid=dx, ldr=dx.stride(0), aux=gu, ldaux=gu.stride(0),
                seed=lora_site_seed(step_seed, i, LORA_SITES.index("down")), drop_p=drop,

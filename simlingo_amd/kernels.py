@@ -659,6 +659,34 @@ def lora_bwd(x, dt, As, bits, dAs, dx=None, dx_bf16=None, p=0.0, packed=False, d
     check(lib().slx_lora_bwd(ctypes.byref(d), stream_ptr()), "slx_lora_bwd")
 
 
+class LoraSwigluBwdDesc(ctypes.Structure):
+    _fields_ = [("dt", c_vp), ("lddt", c_i64), ("at", c_vp), ("ldat", c_i64), ("resid", c_vp), ("ldr", c_i64),
+                ("gu", c_vp), ("ldgu", c_i64), ("bits", c_vp), ("ldbits", c_i64), ("p", c_float), ("dgu", c_vp),
+                ("lddgu", c_i64), ("M", c_i64), ("F", c_int)]
+
+
+register("slx_lora_swiglu_bwd", [ctypes.POINTER(LoraSwigluBwdDesc), c_vp])
+
+
+def lora_swiglu_bwd(dt, at, resid, gu, dgu, bits, p):
+    """slx_lora_swiglu_bwd: dgu = SwiGLU'(gu) applied to d = resid + keep * (dT[:, :32] . A) / (1 - p).
+    dt bf16 [M, >= 32] view, at bf16 [F, 32] (A^T), resid bf16 [M, F] view, gu bf16 [M, 2F], dgu bf16 [M, 2F],
+    bits int32 [M, >= F/32] (p > 0)."""
+    M, F = resid.shape
+    for t in (dt, at, resid, gu, dgu):
+        assert t.dtype == torch.bfloat16 and t.is_cuda and t.stride(1) == 1
+    assert at.shape == (F, 32) and gu.shape[0] == M and gu.shape[1] >= 2 * F and dgu.shape[1] >= 2 * F
+    assert dt.shape[0] == M and dt.shape[1] >= 32
+    d = LoraSwigluBwdDesc()
+    d.dt, d.lddt, d.at, d.ldat = dt.data_ptr(), dt.stride(0), at.data_ptr(), at.stride(0)
+    d.resid, d.ldr, d.gu, d.ldgu = resid.data_ptr(), resid.stride(0), gu.data_ptr(), gu.stride(0)
+    if p > 0:
+        assert bits is not None and bits.dtype == torch.int32 and bits.shape[0] == M and bits.shape[1] * 32 >= F
+        d.bits, d.ldbits = bits.data_ptr(), bits.stride(0)
+    d.p, d.dgu, d.lddgu, d.M, d.F = float(p), dgu.data_ptr(), dgu.stride(0), M, F
+    check(lib().slx_lora_swiglu_bwd(ctypes.byref(d), stream_ptr()), "slx_lora_swiglu_bwd")
+
+
 def lora_grad(jobs, M):
     """The LoRA parameter gradients of one layer group in one launch (slx_lora_grad). jobs: dicts with
     x (bf16 [M, n] view, n % 128 == 0), t (bf16 [M, >= 32 * nsites] view), outs (list of f32 gradients, 1..3 sites),

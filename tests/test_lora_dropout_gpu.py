@@ -196,3 +196,35 @@ def test_lora_grad_jobs(dev, M, p, det):
         xd = (x.float() * mask).bfloat16().float()
         refA = -0.5 + dT[:, 32 * j:32 * (j + 1)].float().t() @ xd
         torch.testing.assert_close(dA[j], refA, atol=2e-3 * refA.abs().max().item(), rtol=1e-4)
+
+
+@pytest.mark.parametrize("M,F,p", [(6384, 4864, 0.1), (77, 256, 0.1), (300, 512, 0.0)])
+def test_lora_swiglu_bwd(dev, M, F, p):
+    """slx_lora_swiglu_bwd (the down site's LoRA dgrad fused with the SwiGLU backward) against torch fp32 on the same
+    bf16 operands and against the K = 64 GEMM form it replaces (DROPMASK_SWIGLU epilogue over the zero-padded A):
+    both round the same f32 values to bf16, so they agree to one bf16 ulp."""
+    from simlingo_amd.dropmask import keep_bits
+    import torch.nn.functional as Fn
+    g = torch.Generator(device=dev).manual_seed(31)
+    dtfull = (torch.randn(M, 64, device=dev, generator=g) * 0.5).bfloat16()
+    dtfull[:, 32:] = 0  # the W_cat padding columns are exactly zero
+    A = (torch.randn(32, F, device=dev, generator=g) * 0.1).bfloat16()
+    resid = torch.randn(M, F, device=dev, generator=g).bfloat16()
+    gu = torch.randn(M, 2 * F, device=dev, generator=g).bfloat16()
+    bits = torch.from_numpy(keep_bits(99, M, F, F, p).view("int32")).to(dev) if p > 0 else None
+    dgu = torch.empty(M, 2 * F, device=dev, dtype=torch.bfloat16)
+    K.lora_swiglu_bwd(dtfull, A.t().contiguous(), resid, gu, dgu, bits, p)
+    mask = torch.from_numpy(keep_scale(99, M, F, F, p)).to(dev) if p > 0 else 1.0
+    d = resid.float() + mask * (dtfull[:, :32].float() @ A.float())
+    gg, uu = gu[:, :F].float(), gu[:, F:].float()
+    sg = torch.sigmoid(gg)
+    ref = torch.cat([d * uu * sg * (1 + gg * (1 - sg)), d * Fn.silu(gg)], 1)
+    torch.testing.assert_close(dgu.float(), ref, atol=1e-2, rtol=1e-2)
+    # the GEMM form it replaces
+    apad = torch.zeros(64, F, device=dev, dtype=torch.bfloat16)
+    apad[:32] = A
+    dg2 = torch.empty_like(dgu)
+    K.gemm(dtfull, apad, dg2, M, F, 64, K.GEMM_NN, 64, F, 2 * F, epi=K.EPI_DROPMASK_SWIGLU, resid=resid, ldr=F,
+           aux=gu, ldaux=2 * F, seed=0, drop_p=p, ldmask=F, maskbits=bits)
+    diff = (dgu.float() - dg2.float()).abs()
+    assert (diff <= dg2.float().abs() * 2 ** -7 + 1e-6).all(), diff.max().item()
