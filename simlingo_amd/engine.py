@@ -67,6 +67,12 @@ GELU_AUX_GRAD = os.environ.get("SLX_GELU_AUX_GRAD", "1") == "1"
 # product on the MFMA, 16-B row streams) instead of the K = 64 GEMM with the DROPMASK_SWIGLU epilogue over 128^2 tiles;
 # SLX_LORA_SWIGLU_BWD=0 restores the GEMM (A/B)
 LORA_SWIGLU_BWD = os.environ.get("SLX_LORA_SWIGLU_BWD", "1") == "1"
+# The LoRA dropout keep bits of every Qwen2 layer (they depend on the step seed only) generated at the start of the step
+# on a side stream, beside the InternViT forward, instead of one slx_dropout_bits launch per layer on the critical path
+# (~19 us each); the compute stream waits for them before the first LoRA down-projection. Off by default: -0.3 % on the
+# step in alternating runs (106.4 vs 106.1 samples/s, profiles/round5_bits_side_ab.txt) - the VALU-bound hash slows
+# the InternViT GEMMs it runs beside by more than the launches it removes from the critical path.
+BITS_SIDE = os.environ.get("SLX_BITS_SIDE", "0") == "1"
 # SLX_LORA_GRAD_DEFER=1: a layer's attention-half LoRA gradient jobs ride in the NEXT layer's (in backward order)
 # MLP-half slx_lora_grad launch instead of a launch of their own (~50 MB, latency-bound alone); the norm backwards
 # then write a fresh bf16 dX buffer, so the deferred o-site job keeps the one it read
@@ -348,6 +354,8 @@ class VLAEngine(EngineOps):
         self.step_seed += 1
         sv["step_seed"] = self.step_seed
         sv["drop"] = cfg.lora_dropout if (training and cfg.lora) else 0.0
+        if BITS_SIDE and sv["drop"] > 0 and not self.precise:
+            self._bits_side(plan.B * plan.S, sv)
         X = self.encode_inputs(pix, plan, dplan, sv)
         S, d = plan.S, cfg.llm_dim
         Ml = B * S
@@ -599,19 +607,40 @@ class VLAEngine(EngineOps):
                     packed=True)
         return dict(zip(sites, bits))
 
+    def _bits_side(self, M, sv):
+        """Every layer's keep bits (slx_dropout_bits, one launch per layer) on the side stream; the compute stream
+        waits for them at the first _lora_bits of the step."""
+        if self._side is None:
+            self._side = torch.cuda.Stream(device=self.device)
+        cur = torch.cuda.current_stream(self.device)
+        self._side.wait_stream(cur)  # the bit buffers' previous readers (last step's backward) are done
+        with torch.cuda.stream(self._side):
+            for i in range(self.cfg.llm_layers):
+                self._bits_layer(i, M, sv)
+            ev = torch.cuda.Event()
+            ev.record(self._side)
+        sv["bits_event"] = ev
+        sv["bits_done"] = set(range(self.cfg.llm_layers))
+
+    def _bits_layer(self, i, M, sv):
+        jobs = []
+        for j, s in enumerate(LORA_SITES):
+            kin = lora_io(self.cfg, s)[0]
+            b = self._buf(("bits", i, s), M, kin // 32, dtype=torch.int32)
+            jobs.append((lora_site_seed(sv["step_seed"], i, j), b, kin, kin))
+        K.dropout_bits(jobs, M, sv["drop"])
+
     def _lora_bits(self, i, site, M, sv):
         """Keep-bit mask of one (layer, site) for this step (persistent buffer; None without dropout). The 7 sites of
         a layer are generated by one slx_dropout_bits launch, the first time any of them is asked for in a step."""
         if sv["drop"] <= 0:
             return None
+        ev = sv.pop("bits_event", None)
+        if ev is not None:  # the side stream's bits (BITS_SIDE) are needed from here on
+            torch.cuda.current_stream(self.device).wait_event(ev)
         key = sv.setdefault("bits_done", set())
         if i not in key:
-            jobs = []
-            for j, s in enumerate(LORA_SITES):
-                kin = lora_io(self.cfg, s)[0]
-                b = self._buf(("bits", i, s), M, kin // 32, dtype=torch.int32)
-                jobs.append((lora_site_seed(sv["step_seed"], i, j), b, kin, kin))
-            K.dropout_bits(jobs, M, sv["drop"])
+            self._bits_layer(i, M, sv)
             key.add(i)
         return self._buf(("bits", i, site), M, lora_io(self.cfg, site)[0] // 32, dtype=torch.int32)
 
