@@ -288,6 +288,24 @@ typedef struct slx_lora_swiglu_bwd_desc {
   int64_t M; int F;
 } slx_lora_swiglu_bwd_desc;
 int slx_lora_swiglu_bwd(const slx_lora_swiglu_bwd_desc* d, slx_stream_t stream);
+/* The SwiGLU forward fused with the down site's LoRA down-projection (Qwen2MLP act_fn(gate) * up, then peft lora_A
+ * on down_proj with its dropout; llm.py:106-119): act = bf16(silu(g) * u) from gu bf16 [M][2F] (the gate|up GEMM
+ * output), written to act [M][F], and t = drop(act) . A^T written as bf16 to t [M][32], drop(x) = bf16(x / (1 - p)) &
+ * keep (the forward's keep bits [M][>= F/32], p > 0). A = lora_A bf16 [32][F]. ws: f32 scratch of
+ * slx_swiglu_lora_down_ws_floats(M, F) floats (per-column-block partials of t, summed in order by a second launch).
+ * F % 256 == 0.                                                                                                      */
+typedef struct slx_swiglu_lora_down_desc {
+  const void* gu; int64_t ldgu;
+  void* act; int64_t ldact;
+  const void* A; int64_t lda;
+  const uint32_t* bits; int64_t ldbits;
+  float p;
+  void* t; int64_t ldt;
+  float* ws; int64_t ws_floats;
+  int64_t M; int F;
+} slx_swiglu_lora_down_desc;
+int slx_swiglu_lora_down(const slx_swiglu_lora_down_desc* d, slx_stream_t stream);
+int64_t slx_swiglu_lora_down_ws_floats(int64_t M, int F);
 
 /* small strided f32 GEMM (driving heads adaptors.py:113-132, WaypointInputAdaptor :80)        */
 enum { SLX_ACT_NONE = 0, SLX_ACT_RELU = 1, SLX_ACT_SILU = 2 };

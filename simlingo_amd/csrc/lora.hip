@@ -741,7 +741,8 @@ struct LswArgs {
 __global__ __launch_bounds__(256) void lora_swiglu_bwd_kernel(LswArgs a) {
   __shared__ __attribute__((aligned(16))) float acc_s[32][256 + 4];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int m0 = blockIdx.x * 32, n0 = blockIdx.y * 256;
+  // column block fastest in dispatch order: the blocks in flight together cover whole rows (DRAM page locality)
+  const int m0 = blockIdx.y * 32, n0 = blockIdx.x * 256;
   // epilogue operands first: chunk i of this thread = row (tid + 256 i) >> 5, 8 columns 8 ((tid + 256 i) & 31)
   uint4 rr[4], gg[4], uu[4];
   uint32_t kb[4];
@@ -800,6 +801,85 @@ __global__ __launch_bounds__(256) void lora_swiglu_bwd_kernel(LswArgs a) {
       *reinterpret_cast<bf16x8*>(a.dgu + (long)m * a.lddgu + a.F + n) = ou;
     }
   }
+}
+
+// ---- the SwiGLU forward fused with the down site's LoRA down-projection (slx_swiglu_lora_down) ----------------------
+// act = silu(g) * u (bf16, the Qwen2MLP activation the down projection reads) and t = drop(act) . A^T [M x 32] (peft's
+// lora_A on down_proj, drop(act) = bf16(act / (1 - p)) & keep), in one pass over gu: a block owns 32 rows x 256
+// columns, streams g / u as 16-B row chunks, stores act, stages drop(act) in LDS ([32][256] bf16, 16-B chunks XOR-
+// swizzled by the row) and one wave runs its 32 x 32 x 256 slice of t on the MFMA (16 MFMAs, A rows straight from
+// global, L2-resident) and stores the block's [32 x 32] f32 partial to the workspace; a second launch adds the F / 256 partials of every row in column-block order (deterministic) and writes t
+// as bf16. Replaces slx_swiglu_fwd + slx_lora_down(down), which read act back from HBM with only M / 32 blocks.
+struct SldArgs {
+  const bf16* gu; long ldgu;
+  bf16* act; long ldact;
+  const bf16* A; long lda;        // lora_A [32][F] bf16
+  const uint32_t* bits; long ldbits;
+  float sc;
+  bf16* t; long ldt;
+  float* part;                    // [F / 256][M][32] f32 partials
+  int M, F;
+};
+
+__global__ __launch_bounds__(256) void swiglu_lora_down_kernel(SldArgs a) {
+  __shared__ __attribute__((aligned(16))) char xs[32 * 512];  // drop(act) [32][256] bf16
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  // column block fastest in dispatch order: the blocks in flight together cover whole rows (DRAM page locality)
+  const int m0 = blockIdx.y * 32, n0 = blockIdx.x * 256;
+  uint4 gg[4], uu[4];
+  uint32_t kb[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = tid + 256 * i, row = c >> 5, n = n0 + 8 * (c & 31);
+    const int m = min(m0 + row, a.M - 1);
+    gg[i] = *reinterpret_cast<const uint4*>(a.gu + (long)m * a.ldgu + n);
+    uu[i] = *reinterpret_cast<const uint4*>(a.gu + (long)m * a.ldgu + a.F + n);
+    kb[i] = a.bits ? (a.bits[(long)m * a.ldbits + (n >> 5)] >> (n & 31)) & 0xFFu : 0xFFu;
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = tid + 256 * i, row = c >> 5, cc = c & 31, n = n0 + 8 * cc;
+    const bf16x8 g8 = __builtin_bit_cast(bf16x8, gg[i]), u8 = __builtin_bit_cast(bf16x8, uu[i]);
+    bf16x8 o, d;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      o[e] = (bf16)(silu((float)g8[e]) * (float)u8[e]);  // slx_swiglu_fwd's rounding
+      d[e] = (kb[i] >> e) & 1u ? (bf16)((float)o[e] * a.sc) : (bf16)0.f;
+    }
+    if (m0 + row < a.M) *reinterpret_cast<bf16x8*>(a.act + (long)(m0 + row) * a.ldact + n) = o;
+    *reinterpret_cast<bf16x8*>(xs + row * 512 + ((cc ^ (row & 31)) << 4)) = d;
+  }
+  __syncthreads();
+  if (w != 0) return;
+  // wave 0: the block's [32 x 32] partial over its 256 columns, 16 MFMAs; A rows j = lane & 31 straight from global
+  f32x16 acc;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) acc[j] = 0.f;
+#pragma unroll
+  for (int kk = 0; kk < 16; ++kk) {
+    const bf16x8 bfr = *reinterpret_cast<const bf16x8*>(a.A + (long)(lane & 31) * a.lda + n0 + 16 * kk + 8 * (lane >> 5));
+    const int row = lane & 31, cc = 2 * kk + (lane >> 5);
+    const bf16x8 af = *reinterpret_cast<const bf16x8*>(xs + row * 512 + ((cc ^ (row & 31)) << 4));
+    acc = mfma32x32(af, bfr, acc);
+  }
+  float* pb = a.part + ((long)blockIdx.x * a.M) * 32;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int row = 8 * (j >> 2) + 4 * (lane >> 5) + (j & 3);
+    if (m0 + row < a.M) pb[(long)(m0 + row) * 32 + (lane & 31)] = acc[j];
+  }
+}
+
+// t[m][j] = bf16(sum over the column blocks y of part[y][m][j]), y in order: the kernel boundary makes every partial
+// visible (an in-launch last-arriver hand-off needs an agent-scope release per block, i.e. an L2 write-back behind
+// the block's act stores, which cost far more than this launch)
+__global__ __launch_bounds__(256) void swiglu_lora_down_reduce_kernel(const float* part, int ny, long M, bf16* t,
+                                                                      long ldt) {
+  const long e = (long)blockIdx.x * 256 + threadIdx.x;
+  if (e >= M * 32) return;
+  float v = 0.f;
+  for (int y = 0; y < ny; ++y) v += part[(long)y * M * 32 + e];
+  t[(e >> 5) * ldt + (e & 31)] = (bf16)v;
 }
 
 }  // namespace slx
@@ -1059,8 +1139,42 @@ extern "C" int slx_lora_swiglu_bwd(const slx_lora_swiglu_bwd_desc* d, slx_stream
   a.sc = 1.0f / (1.0f - d->p);
   a.dgu = (bf16*)d->dgu; a.lddgu = d->lddgu;
   a.M = (int)d->M; a.F = d->F;
-  hipLaunchKernelGGL(lora_swiglu_bwd_kernel, dim3((unsigned)((d->M + 31) / 32), (unsigned)(d->F / 256)), dim3(256), 0,
+  hipLaunchKernelGGL(lora_swiglu_bwd_kernel, dim3((unsigned)(d->F / 256), (unsigned)((d->M + 31) / 32)), dim3(256), 0,
                      (hipStream_t)stream, a);
   SLX_LAUNCH_CHECK("slx_lora_swiglu_bwd");
+  return 0;
+}
+
+extern "C" int64_t slx_swiglu_lora_down_ws_floats(int64_t M, int F) {
+  return (M <= 0 || F <= 0 || F % 256 != 0) ? 0 : (int64_t)(F / 256) * M * 32;
+}
+
+extern "C" int slx_swiglu_lora_down(const slx_swiglu_lora_down_desc* d, slx_stream_t stream) {
+  SLX_CHECK_ARG(d && d->gu && d->act && d->A && d->t && d->ws, "slx_swiglu_lora_down: null operand");
+  SLX_CHECK_ARG(d->F > 0 && d->F % 256 == 0 && d->M >= 0 && d->M < (1LL << 31), "slx_swiglu_lora_down: F %% 256 (got %d)",
+                d->F);
+  SLX_CHECK_ARG(d->ldgu % 8 == 0 && d->ldact % 8 == 0 && d->lda % 8 == 0 && d->lda >= d->F &&
+                ((((uintptr_t)d->gu | (uintptr_t)d->act | (uintptr_t)d->A) & 15) == 0),
+                "slx_swiglu_lora_down: 16-B aligned rows (leading dims %% 8)");
+  SLX_CHECK_ARG(d->p >= 0.f && d->p < 1.f && (d->p == 0.f || (d->bits && d->ldbits >= d->F / 32)),
+                "slx_swiglu_lora_down: 0 <= p < 1, p > 0 needs the keep bits");
+  SLX_CHECK_ARG(d->ws_floats >= slx_swiglu_lora_down_ws_floats(d->M, d->F),
+                "slx_swiglu_lora_down: workspace holds %lld floats, needs %lld", (long long)d->ws_floats,
+                (long long)slx_swiglu_lora_down_ws_floats(d->M, d->F));
+  if (d->M == 0) return 0;
+  SldArgs a;
+  a.gu = (const bf16*)d->gu; a.ldgu = d->ldgu; a.act = (bf16*)d->act; a.ldact = d->ldact;
+  a.A = (const bf16*)d->A; a.lda = d->lda;
+  a.bits = d->p > 0.f ? d->bits : nullptr; a.ldbits = d->ldbits;
+  a.sc = 1.0f / (1.0f - d->p);
+  a.t = (bf16*)d->t; a.ldt = d->ldt;
+  a.part = d->ws;
+  a.M = (int)d->M; a.F = d->F;
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(swiglu_lora_down_kernel, dim3((unsigned)(d->F / 256), (unsigned)((d->M + 31) / 32)), dim3(256), 0,
+                     st, a);
+  hipLaunchKernelGGL(swiglu_lora_down_reduce_kernel, dim3((unsigned)((d->M * 32 + 255) / 256)), dim3(256), 0, st,
+                     (const float*)d->ws, d->F / 256, (long)d->M, (bf16*)d->t, (long)d->ldt);
+  SLX_LAUNCH_CHECK("slx_swiglu_lora_down");
   return 0;
 }

@@ -73,6 +73,9 @@ LORA_SWIGLU_BWD = os.environ.get("SLX_LORA_SWIGLU_BWD", "1") == "1"
 # step in alternating runs (106.4 vs 106.1 samples/s, profiles/round5_bits_side_ab.txt) - the VALU-bound hash slows
 # the InternViT GEMMs it runs beside by more than the launches it removes from the critical path.
 BITS_SIDE = os.environ.get("SLX_BITS_SIDE", "0") == "1"
+# The SwiGLU forward and the down site's LoRA down-projection as one streaming kernel (slx_swiglu_lora_down: act is
+# written once and never read back for t); SLX_SWIGLU_LORA_DOWN=0 runs slx_swiglu_fwd + slx_lora_down (A/B)
+SWIGLU_LORA_DOWN = os.environ.get("SLX_SWIGLU_LORA_DOWN", "1") == "1"
 # SLX_LORA_GRAD_DEFER=1: a layer's attention-half LoRA gradient jobs ride in the NEXT layer's (in backward order)
 # MLP-half slx_lora_grad launch instead of a launch of their own (~50 MB, latency-bound alone); the norm backwards
 # then write a fresh bf16 dX buffer, so the deferred o-site job keeps the one it read
@@ -461,9 +464,15 @@ class VLAEngine(EngineOps):
             K.mm(h2x, cat["gu"] if lora else self.W[p + "gate_up_w"], gu)
             ax = self._buf(("ax", i), Ml, Fl + Pd, zero=lora)
             act = ax[:, :Fl]
-            self._swiglu(gu, act, Ml, Fl)
-            if lora:
-                L.update(self._lora_down(act, i, ("down",), ax[:, Fl:], sv))
+            if lora and SWIGLU_LORA_DOWN and not self.precise and Fl % 256 == 0:
+                bits = self._lora_bits(i, "down", Ml, sv)
+                ws = self._buf(("sld_ws",), K.lib().slx_swiglu_lora_down_ws_floats(Ml, Fl), dtype=F32)
+                K.swiglu_lora_down(gu, act, self.cat[i]["apad.down"], ax[:, Fl:Fl + cfg.lora_r], bits, sv["drop"], ws)
+                L["down"] = bits
+            else:
+                self._swiglu(gu, act, Ml, Fl)
+                if lora:
+                    L.update(self._lora_down(act, i, ("down",), ax[:, Fl:], sv))
             Xo = self._e(Ml, d, dtype=F32)
             K.mm(ax, cat["down"] if lora else self.W[p + "down_w"], Xo, epi=K.EPI_RESID_LS, resid=Xm, ldr=d,
                  ls=self.ones_d, variant=LLM_RESID_VARIANT or None)

@@ -687,6 +687,36 @@ def lora_swiglu_bwd(dt, at, resid, gu, dgu, bits, p):
     check(lib().slx_lora_swiglu_bwd(ctypes.byref(d), stream_ptr()), "slx_lora_swiglu_bwd")
 
 
+class SwigluLoraDownDesc(ctypes.Structure):
+    _fields_ = [("gu", c_vp), ("ldgu", c_i64), ("act", c_vp), ("ldact", c_i64), ("A", c_vp), ("lda", c_i64),
+                ("bits", c_vp), ("ldbits", c_i64), ("p", c_float), ("t", c_vp), ("ldt", c_i64), ("ws", c_vp),
+                ("ws_floats", c_i64), ("M", c_i64), ("F", c_int)]
+
+
+register("slx_swiglu_lora_down", [ctypes.POINTER(SwigluLoraDownDesc), c_vp])
+register("slx_swiglu_lora_down_ws_floats", [c_i64, c_int], restype=c_i64)
+
+
+def swiglu_lora_down(gu, act, A, t, bits, p, ws):
+    """slx_swiglu_lora_down: act = bf16(silu(g) u) from gu bf16 [M, 2F], t = drop(act) A^T (bf16 [M, 32] view).
+    A bf16 [>= 32, F] rows (lora_A), bits int32 [M, >= F/32] keep bits (p > 0), ws f32 scratch of
+    slx_swiglu_lora_down_ws_floats(M, F) floats (engine-owned, reused)."""
+    M, F = act.shape
+    for x in (gu, act, A, t):
+        assert x.dtype == torch.bfloat16 and x.is_cuda and x.stride(1) == 1
+    assert gu.shape[0] == M and gu.shape[1] >= 2 * F and A.shape[1] == F and A.shape[0] >= 32 and t.shape == (M, 32)
+    need = lib().slx_swiglu_lora_down_ws_floats(M, F)
+    assert ws.dtype == torch.float32 and ws.numel() >= need
+    d = SwigluLoraDownDesc()
+    d.gu, d.ldgu, d.act, d.ldact = gu.data_ptr(), gu.stride(0), act.data_ptr(), act.stride(0)
+    d.A, d.lda = A.data_ptr(), A.stride(0)
+    if p > 0:
+        assert bits is not None and bits.dtype == torch.int32 and bits.shape[0] == M and bits.shape[1] * 32 >= F
+        d.bits, d.ldbits = bits.data_ptr(), bits.stride(0)
+    d.p, d.t, d.ldt, d.ws, d.ws_floats, d.M, d.F = float(p), t.data_ptr(), t.stride(0), ws.data_ptr(), ws.numel(), M, F
+    check(lib().slx_swiglu_lora_down(ctypes.byref(d), stream_ptr()), "slx_swiglu_lora_down")
+
+
 def lora_grad(jobs, M):
     """The LoRA parameter gradients of one layer group in one launch (slx_lora_grad). jobs: dicts with
     x (bf16 [M, n] view, n % 128 == 0), t (bf16 [M, >= 32 * nsites] view), outs (list of f32 gradients, 1..3 sites),

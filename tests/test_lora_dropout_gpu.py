@@ -228,3 +228,38 @@ def test_lora_swiglu_bwd(dev, M, F, p):
            aux=gu, ldaux=2 * F, seed=0, drop_p=p, ldmask=F, maskbits=bits)
     diff = (dgu.float() - dg2.float()).abs()
     assert (diff <= dg2.float().abs() * 2 ** -7 + 1e-6).all(), diff.max().item()
+
+
+@pytest.mark.parametrize("M,F,p", [(6384, 4864, 0.1), (77, 256, 0.1), (300, 512, 0.0)])
+def test_swiglu_lora_down(dev, M, F, p):
+    """slx_swiglu_lora_down (SwiGLU forward + the down site's LoRA down-projection in one pass) against the two launches
+    it replaces: act bit-identical to slx_swiglu_fwd, t equal to slx_lora_down's up to f32 summation order (one bf16
+    ulp), both against torch fp32; two calls on the same workspace agree bitwise."""
+    from simlingo_amd.dropmask import keep_bits
+    import torch.nn.functional as Fn
+    g = torch.Generator(device=dev).manual_seed(41)
+    gu = torch.randn(M, 2 * F, device=dev, generator=g).bfloat16()
+    A = (torch.randn(32, F, device=dev, generator=g) * 0.05).bfloat16()
+    bits = torch.from_numpy(keep_bits(123, M, F, F, p).view("int32")).to(dev) if p > 0 else None
+    ws = torch.zeros(K.lib().slx_swiglu_lora_down_ws_floats(M, F), device=dev)
+    outs = []
+    for _ in range(2):
+        act = torch.empty(M, F, device=dev, dtype=torch.bfloat16)
+        t = torch.full((M, 48), 7.0, device=dev, dtype=torch.bfloat16)
+        K.swiglu_lora_down(gu, act, A, t[:, 8:40], bits, p, ws)
+        outs.append((act, t))
+    torch.cuda.synchronize()
+    (act, t), (act2, t2) = outs
+    assert torch.equal(act, act2) and torch.equal(t, t2)
+    assert bool((t[:, :8] == 7.0).all()) and bool((t[:, 40:] == 7.0).all())
+    ref_act = torch.empty_like(act)
+    K.call("slx_swiglu_fwd", K.P(gu), 2 * F, K.P(ref_act), F, M, F, K.stream_ptr())
+    assert torch.equal(act, ref_act)
+    torch.testing.assert_close(act.float(), (Fn.silu(gu[:, :F].float()) * gu[:, F:].float()), atol=2e-2, rtol=1e-2)
+    tl = torch.empty(M, 32, device=dev, dtype=torch.bfloat16)
+    K.lora_down(act, [A], tl, [0], p=p, bits=[bits])
+    diff = (t[:, 8:40].float() - tl.float()).abs()
+    assert (diff <= tl.float().abs() * 2 ** -7 + 1e-4).all(), diff.max().item()
+    mask = torch.from_numpy(keep_scale(123, M, F, F, p)).to(dev) if p > 0 else 1.0
+    xd = (act.float() * mask).bfloat16().float()
+    torch.testing.assert_close(t[:, 8:40].float(), xd @ A.float().t(), atol=3e-2, rtol=2e-2)
