@@ -326,6 +326,8 @@ def dropin_line(dl, dev):
     conf = m.configure_optimizers()
     opt, sched = conf["optimizer"], conf["lr_scheduler"]["scheduler"]
 
+    sync = os.environ.get("SLX_DROPIN_SYNC", "0") == "1"  # debugging aid: synchronise after every step
+
     def step():
         ex = col.device(next(it))
         out = m.training_step(ex, 0)
@@ -333,16 +335,20 @@ def dropin_line(dl, dev):
         opt.step()
         sched.step()
         opt.zero_grad()
+        if sync:
+            torch.cuda.synchronize()
         return out["loss"]
 
+    losses = []
     for _ in range(dl["warmup"]):
-        loss = step()
+        losses.append(step())
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(dl["steps"]):
-        loss = step()
+        losses.append(step())
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    loss = losses[-1]
     v = B * dl["steps"] / dt
     res = {"workload": "drop-in loop: DataLoader(workers run Collate.host) -> Collate.device (pinned H2D + HIP frames) "
                        "-> DrivingModel.training_step -> loss.backward() -> FusedAdamW.step -> OneCycleLR.step, "
@@ -350,7 +356,7 @@ def dropin_line(dl, dev):
            "value": round(v, 3), "unit": "samples/s", "ms_per_step": round(dt / dl["steps"] * 1e3, 3),
            "steps": dl["steps"], "warmup": dl["warmup"], "loader_workers": dl["workers"],
            "step_mfma_frac": round(v * VLA_GFLOP_PER_SAMPLE / 1e3 / PEAK_BF16_TFLOPS, 4),
-           "loss_last": round(loss.item(), 5)}
+           "loss_last": round(loss.item(), 5), "losses": [round(x.item(), 4) for x in losses]}
     del m, opt, sched
     return res
 

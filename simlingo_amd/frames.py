@@ -215,6 +215,9 @@ class FramePipeline:
         self.out = [torch.empty(B, 1, self.pre.tiles, 3, self.pre.tile, self.pre.tile, dtype=torch.float32,
                                 device=dev) for _ in range(depth)]
         self.copy_stream = torch.cuda.Stream(device=dev)
+        # the device slots come from the current stream's pool (possibly memory its queued kernels still use): the
+        # copy stream's first writes wait for the work enqueued so far (see FrameUploader)
+        self.copy_stream.wait_stream(torch.cuda.current_stream(dev))
         self.ready = [torch.cuda.Event() for _ in range(depth)]
         self.consumed = [torch.cuda.Event() for _ in range(depth)]
         self.put_i = self.get_i = 0
@@ -270,12 +273,16 @@ class FrameUploader:
         for ev in (self.copied[s], self.consumed[s]):
             if ev is not None:
                 ev.synchronize()
+        cur = torch.cuda.current_stream(self.device)
         if self.slots[s] is None or self.slots[s][0] != shape:
             self.slots[s] = (shape, torch.empty(shape, dtype=torch.uint8).pin_memory(),
                              torch.empty(shape, dtype=torch.uint8, device=self.device))
+            # the caching allocator hands out blocks in the CURRENT stream's order: the new device slot may be memory
+            # the current stream freed while kernels still queued on it read or write it. The copy stream is not
+            # ordered after those kernels, so its first write into the slot waits for everything enqueued so far.
+            self.copy_stream.wait_stream(cur)
         _, host, dev = self.slots[s]
         host.copy_(frames)
-        cur = torch.cuda.current_stream(self.device)
         with torch.cuda.stream(self.copy_stream):
             dev.copy_(host, non_blocking=True)
             ev = torch.cuda.Event()
