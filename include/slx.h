@@ -455,6 +455,9 @@ int slx_dec_attn_o(void* cache, int64_t ld, int Hq, int Hkv, const float* cos_ta
 int slx_dec_attn_o_split(void* cache, int64_t ld, int Hq, int Hkv, const float* cos_tab, const float* sin_tab,
                          int lmax, float* ws, void* out, const slx_dec_state* st, const void* Wo, int64_t ldwo, int N,
                          int K, float* X, slx_stream_t s);
+/* 1 if slx_dec_attn_o_split supports a cache of lmax rows under this process's SLX_DEC_SPLIT_NS, else 0 (the caller
+ * then runs slx_dec_attn + the O GEMV)                                                                           */
+int slx_dec_attn_o_split_ok(int lmax);
 int slx_dec_attn_ws_floats(int Hq, int Hkv, int lmax);
 int slx_dec_attn(void* cache, int64_t ld, int Hq, int Hkv, const float* cos_tab, const float* sin_tab, int lmax,
                  float* ws, void* out, const slx_dec_state* st, slx_stream_t s);

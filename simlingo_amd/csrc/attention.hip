@@ -1258,27 +1258,39 @@ __global__ __launch_bounds__(256, ATTN_KV_OCC) void attn_bwd_kv_dma_kernel(AttnA
   int qo[2], qr_[2], doo[2], dr_[2];
   dma_lane_offsets(a.ldq, wu, lane, qo, qr_);
   dma_lane_offsets(a.lddo, wu, lane, doo, dr_);
+  // (q-head, chunk) of the next stage to issue, advanced by one per issue: issue() is called for it = 0, 1, 2, ...
+  // in order, so no per-iteration integer division by nch (a ~40-instruction scalar sequence each)
+  int ih = 0, ic = 0;
+  // the q-head's buffer descriptors (Q, dO, lse | delta rows), rebuilt only when the issued head changes
+  int rh = -1;
+  __amdgpu_buffer_rsrc_t rsq = slice_rsrc(a.q, a.ldq, S, 2), rsd = rsq, rsl = rsq;
   auto issue = [&](int it) {
     char* slot = smem + (it % NS) * KV_SLOT;
     const bool real = it < nit;
-    const int h = hk * G + hg0 + (real ? it / nch : 0), qc = real ? qstart + (it % nch) * 64 : S;
-    const bf16* qb_ = a.q + (long)b * S * a.ldq + h * 64;
-    const bf16* db_ = a.dout + (long)b * S * a.lddo + h * 64;
-    dma_tile64(slice_rsrc(qb_, a.ldq, S, 2), slot, a.ldq, qc, S, wu, qo, qr_);
-    dma_tile64(slice_rsrc(db_, a.lddo, S, 2), slot + 8192, a.lddo, qc, S, wu, doo, dr_);
-    const long base = ((long)b * a.Hq + h) * S;
-    const float* src = wu == 0 ? a.lse + base : a.delta + base;
-    dma_row64_f32(__builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(src), (short)0, S * 4, 0x00020000),
-                  slot + 16384 + 256 * wu, qc, wu < 2 ? S : 0, lane);
+    const int h = hk * G + hg0 + (real ? ih : 0), qc = real ? qstart + ic * 64 : S;
+    if (++ic == nch) { ic = 0; ++ih; }
+    if (h != rh) {
+      rh = h;
+      rsq = slice_rsrc(a.q + (long)b * S * a.ldq + h * 64, a.ldq, S, 2);
+      rsd = slice_rsrc(a.dout + (long)b * S * a.lddo + h * 64, a.lddo, S, 2);
+      const long base = ((long)b * a.Hq + h) * S;
+      rsl = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(wu == 0 ? a.lse + base : a.delta + base), (short)0,
+                                              S * 4, 0x00020000);
+    }
+    dma_tile64(rsq, slot, a.ldq, qc, S, wu, qo, qr_);
+    dma_tile64(rsd, slot + 8192, a.lddo, qc, S, wu, doo, dr_);
+    dma_row64_f32(rsl, slot + 16384 + 256 * wu, qc, wu < 2 ? S : 0, lane);
   };
 
 
 #pragma unroll
   for (int j = 0; j < NS - 1; ++j) issue(j);
+  int cc = 0;  // chunk index of stage `it` (it % nch, advanced incrementally)
   for (int it = 0; it < nit; ++it) {
     wait_vmcnt<5 * (NS - 2)>();
     __syncthreads();
-    const int qc = qstart + (it % nch) * 64;
+    const int qc = qstart + cc * 64;
+    if (++cc == nch) cc = 0;
     const char* slot = smem + (it % NS) * KV_SLOT;
     const char* Ql = slot;
     const char* Dl = slot + 8192;
@@ -1777,7 +1789,7 @@ struct RopeArgs {
 };
 
 // One thread per (token, head, i<32 pair-group of 4): 8 pairs per thread -> 256 threads per row
-__global__ void rope_kernel(RopeArgs r) {
+__device__ __forceinline__ void rope_rows(const RopeArgs& r) {
   const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const long total = (long)r.ntok * r.nheads * 4;
   if (idx >= total) return;
@@ -1814,6 +1826,9 @@ __global__ void rope_kernel(RopeArgs r) {
   *reinterpret_cast<bf16x8*>(x + i0) = oa;
   *reinterpret_cast<bf16x8*>(x + 32 + i0) = ob;
 }
+__global__ void rope_kernel(RopeArgs r) { rope_rows(r); }
+// the dK and dV finalizes of one backward as one launch (blockIdx.y selects the tensor)
+__global__ void rope2_kernel(RopeArgs r0, RopeArgs r1) { rope_rows(blockIdx.y ? r1 : r0); }
 
 // GQA finalize: dst[t, hk, :] = sum_{j<G} src[t, hk*G + j, :] (f32 per-q-head partials, row stride
 // Hq*64) -> optional RoPE^T -> bf16. One thread per (token, kv head, quarter of the pairs).
@@ -2413,15 +2428,27 @@ extern "C" int slx_attn_bwd(const slx_attn_desc* d, const slx_attn_bwd_desc* g, 
   else hipLaunchKernelGGL(attn_bwd_kv_kernel, dim3(nblk * a.Hkv * a.nsplit * a.B), dim3(256), 0, st, a);
   SLX_LAUNCH_CHECK("slx_attn_bwd(dk/dv)");
   // finalize: f32 -> bf16, summing head-split partials and applying the RoPE transpose where asked
+  auto rope_args = [&](const float* src, int heads, bf16* dst, long ld, bool rope, int nsplit) {
+    RopeArgs r;
+    memset(&r, 0, sizeof(r));
+    r.ntok = ntok; r.S = a.S; r.inverse = 1;
+    r.cos = rope ? g->rope_cos : nullptr;
+    r.sin = rope ? g->rope_sin : nullptr;
+    r.x = dst; r.ldx = ld; r.nheads = heads; r.src_f32 = src; r.ldsrc = (long)heads * 64;
+    r.nsplit = nsplit; r.split_stride = ntok * heads * 64;
+    return r;
+  };
+  if (f32kv && a.nsplit > 1) {  // GQA: dK (RoPE^T) and dV finalized by one launch
+    const RopeArgs rk = rope_args(a.dk_acc, a.Hkv, (bf16*)g->dk, g->lddk, true, a.nsplit);
+    const RopeArgs rv = rope_args(a.dv_acc, a.Hkv, (bf16*)g->dv, g->lddv, false, a.nsplit);
+    const long total = ntok * a.Hkv * 4;
+    hipLaunchKernelGGL(rope2_kernel, dim3((total + 255) / 256, 2), dim3(256), 0, st, rk, rv);
+    SLX_LAUNCH_CHECK("slx_attn_bwd(finalize dk+dv)");
+    return 0;
+  }
   auto conv = [&](const float* src, int heads, bf16* dst, long ld, bool rope, int nsplit) -> int {
     if ((rope && g->rope_cos) || nsplit > 1) {
-      RopeArgs r;
-      memset(&r, 0, sizeof(r));
-      r.ntok = ntok; r.S = a.S; r.inverse = 1;
-      r.cos = rope ? g->rope_cos : nullptr;
-      r.sin = rope ? g->rope_sin : nullptr;
-      r.x = dst; r.ldx = ld; r.nheads = heads; r.src_f32 = src; r.ldsrc = (long)heads * 64;
-      r.nsplit = nsplit; r.split_stride = ntok * heads * 64;
+      const RopeArgs r = rope_args(src, heads, dst, ld, rope, nsplit);
       const long total = ntok * heads * 4;
       hipLaunchKernelGGL(rope_kernel, dim3((total + 255) / 256), dim3(256), 0, st, r);
     } else {

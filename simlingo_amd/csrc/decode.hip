@@ -628,13 +628,22 @@ int slx_dec_attn(void* cache, int64_t ld, int Hq, int Hkv, const float* cos_tab,
 
 // split attention + O projection: dec_attn_mfma_split_kernel (Hkv x ns workgroups, partials in ws), then the O GEMV
 // (+ residual) merging the partials in its prologue (dec_gemv_kernel MG); ns = SLX_DEC_SPLIT_NS (default 8)
+static int dec_split_ns() {
+  static const int ns_env = [] { const char* e = getenv("SLX_DEC_SPLIT_NS"); return e ? atoi(e) : 8; }();
+  return ns_env;
+}
+
+int slx_dec_attn_o_split_ok(int lmax) {
+  const int ns = dec_split_ns();
+  return ns >= 1 && ns <= kMergeMaxNs && lmax > 0 && lmax <= 256 * ns && ns <= slx_dec_attn_nsplit(lmax);
+}
+
 int slx_dec_attn_o_split(void* cache, int64_t ld, int Hq, int Hkv, const float* cos_tab, const float* sin_tab,
                          int lmax, float* ws, void* out, const slx_dec_state* st, const void* Wo, int64_t ldwo, int N,
                          int K, float* X, slx_stream_t s) {
-  static const int ns_env = [] { const char* e = getenv("SLX_DEC_SPLIT_NS"); return e ? atoi(e) : 8; }();
-  const int ns = ns_env;
+  const int ns = dec_split_ns();
   SLX_CHECK_ARG(cache && cos_tab && sin_tab && ws && st && Wo && X, "slx_dec_attn_o_split: null argument");
-  SLX_CHECK_ARG(ns >= 1 && ns <= kMergeMaxNs && lmax > 0 && lmax <= 256 * ns && ns <= slx_dec_attn_nsplit(lmax),
+  SLX_CHECK_ARG(slx_dec_attn_o_split_ok(lmax),
                 "slx_dec_attn_o_split: 1 <= ns <= %d splits of at most 8 key blocks (lmax %d, ns %d)", kMergeMaxNs,
                 lmax, ns);
   SLX_CHECK_ARG(Hkv > 0 && Hq % Hkv == 0 && Hq / Hkv <= 32 && K == Hq * 64 && K <= 1024 && K % 8 == 0,

@@ -59,6 +59,7 @@ K.register("slx_dec_attn_nsplit", [K.c_int])
 K.register("slx_dec_attn_ws_floats", [K.c_int, K.c_int, K.c_int])
 K.register("slx_dec_attn", [K.c_vp, K.c_i64, K.c_int, K.c_int, K.c_vp, K.c_vp, K.c_int, K.c_vp, K.c_vp, K.c_vp, K.c_vp])
 K.register("slx_dec_sync_ints", [])
+K.register("slx_dec_attn_o_split_ok", [K.c_int])
 K.register("slx_dec_attn_o", [K.c_vp, K.c_i64, K.c_int, K.c_int, K.c_vp, K.c_vp, K.c_int, K.c_vp, K.c_vp, K.c_vp, K.c_vp,
                               K.c_i64, K.c_int, K.c_int, K.c_vp, K.c_vp, K.c_vp])
 K.register("slx_dec_attn_o_split", [K.c_vp, K.c_i64, K.c_int, K.c_int, K.c_vp, K.c_vp, K.c_int, K.c_vp, K.c_vp, K.c_vp,
@@ -104,6 +105,8 @@ class GreedyDecoder:
         self.ones_d = torch.ones(d, dtype=F32, device=dev)
         nws = K.lib().slx_dec_attn_ws_floats(cfg.llm_heads, cfg.llm_kv_heads, self.max_len)
         self.attn_ws = torch.zeros(max(nws, 1), dtype=F32, device=dev)
+        # the split path's cache-length limit depends on SLX_DEC_SPLIT_NS (C side); past it, attention + O GEMV
+        self.split_ok = bool(K.lib().slx_dec_attn_o_split_ok(self.max_len))
         # attention + O projection hand-off counters, one 128-B line per layer (slx_dec_attn_o resets them per call)
         assert K.lib().slx_dec_sync_ints() <= 32
         self.sync = torch.zeros(cfg.llm_layers, 32, dtype=torch.int32, device=dev)
@@ -174,7 +177,7 @@ class GreedyDecoder:
         lib = K.lib()
         for i, (qkv, cache, o, gu, down) in enumerate(self._steps):
             K.check(lib.slx_dec_gemv(ctypes.byref(qkv), s), "slx_dec_gemv")
-            if SPLIT_O and self.max_len <= 2048:  # split attention, merged by the O GEMV (+ residual)
+            if SPLIT_O and self.split_ok:  # split attention, merged by the O GEMV (+ residual)
                 wo = self.Wm[i]["o_w"]
                 K.check(lib.slx_dec_attn_o_split(K.P(cache), cache.stride(0), cfg.llm_heads, cfg.llm_kv_heads,
                                                  K.P(self.cos), K.P(self.sin), self.max_len, K.P(self.attn_ws), None,

@@ -19,6 +19,7 @@ ap.add_argument("--top", type=int, default=45)
 ap.add_argument("--grid", action="store_true", help="split kernels by launch grid (GEMM shape attribution)")
 ap.add_argument("--marker", default="adamw_kernel")
 ap.add_argument("--gaps", type=int, default=0, help="also list the N largest idle gaps between kernels")
+ap.add_argument("--dump", default="", help="write the first steady step's dispatch sequence (name, us, grid) to FILE")
 ap.add_argument("--alternate", default="", help="split the calls of kernels whose name contains this string by "
                 "occurrence parity within the steady steps (#0, #1): the two InternViT weight-gradient pairs share one "
                 "kernel and one grid, and alternate fc2.w+fc1.w (#0), proj.w+qkv.w (#1) in every layer's backward")
@@ -77,3 +78,11 @@ if args.gaps:
         hist[k][1] += g
     for (a, b), (n, g) in sorted(hist.items(), key=lambda kv: -kv[1][1])[:args.gaps]:
         print(f"{g / 1e6 / steps:7.3f} ms/step {n / steps:5.1f}x avg {g / n / 1e3:6.1f} us  {a}  ->  {b}")
+
+if args.dump:
+    # the first steady step in dispatch order: site attribution by position (kernels are shared by many sites)
+    t_end = marks[args.warmup] if len(marks) > args.warmup else t1
+    with open(args.dump, "w") as f:
+        for i, (name, s_, e_, dur, gx, gy, gz, wx) in enumerate(r for r in sel if r[1] <= t_end):
+            f.write(f"{i:5d} {dur / 1e3:9.1f} us grid ({gx // max(wx, 1)},{gy},{gz})  "
+                    f"{name.replace('void ', '').replace('slx::', '')[:110]}\n")
