@@ -384,10 +384,19 @@ def main():
             dl = dropin_loader()
         except Exception as e:
             dl = {"error": repr(e)[:200]}
+    # rehearsal of the N > 1 path on a one-GPU box (the driver's scaling runs use one GPU per rank over RCCL):
+    # SLX_BENCH_ONE_DEVICE=1 puts every rank on cuda:0 and SLX_BENCH_BACKEND=gloo exchanges the buckets through gloo
+    # (RCCL refuses two ranks on one GPU)
+    if os.environ.get("SLX_BENCH_ONE_DEVICE", "0") == "1":
+        local = 0
+    backend = os.environ.get("SLX_BENCH_BACKEND", "nccl")
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local)
     args.wire_eff = ("bf16" if world > 1 else "f32") if args.wire == "auto" else args.wire
     w = (setup_base if args.config.startswith("base") else setup_vla)(args, dev, world, rank)
@@ -473,6 +482,7 @@ def main():
                 res["roofline"]["traffic_source"] = psrc
             res["roofline_fc1"] = fc1
     if world > 1:
+        res["dist_backend"] = "rccl" if backend == "nccl" else backend
         cs = eng.bucketer.comm_summary()
         if cs:
             res["comm_exposed_ms"] = cs.pop("comm_exposed_ms")
