@@ -7,9 +7,11 @@ rounding. Token check (teacher forced on the HIP tokens, one oracle pass gives e
 chosen token's oracle logit is within 3e-2 x std(logits) of the oracle maximum at every step, and wherever
 the oracle's top-2 margin exceeds 0.2 x std the tokens are identical. Driving predictions from the oracle's
 final forward over the same prompt + tokens + queries: every per-point head output (the increment the
-cumsum adds) within 0.015 m and the cumulated waypoints within 0.1 m (the training parity bound; with a
-random-init head the 20 increments carry near-identical bf16 errors, so the cumsum's error grows linearly). EOS stopping, the graph-replayed and the eager step, and the single-forward mode are
-checked for exact agreement.
+cumsum adds) within 0.015 m and the cumulated waypoints within 0.1 m of the fp32 oracle (observed 0.074 m: with a
+random-init head the 20 increments carry near-identical bf16 errors, so the cumsum's error grows linearly), and
+within SURVEY §8d's bf16 gate of 5e-2 m of the oracle evaluated on the decoder's own bf16 operands (every weight
+rounded as the engine holds it, the LoRA-merged Qwen2 projections; observed <= 0.018 m). EOS stopping, the
+graph-replayed and the eager step, and the single-forward mode are checked for exact agreement.
 """
 import pytest
 import torch
@@ -66,7 +68,26 @@ def test_greedy_decode_vs_oracle(dev):
             diff = (got - want).abs()
             inc = (torch.diff(got, dim=0, prepend=torch.zeros(1, got.shape[1]))
                    - torch.diff(want, dim=0, prepend=torch.zeros(1, want.shape[1]))).abs()
+            print(f"[decode b={b}] cumulated max |diff| {diff.max().item():.4g} m, per-point increment {inc.max().item():.4g} m")
             assert diff.max().item() <= 0.1 and inc.max().item() <= 0.015, (b, diff.max().item(), inc.max().item())
+    # SURVEY §8d's bf16 gate (5e-2 m) against the oracle evaluated with the decoder's own bf16 GEMM operands: every
+    # engine weight rounded to bf16 as the engine holds it, the Qwen2 projections replaced by the decoder's merged
+    # bf16 W + s B A (LoRA B zeroed in the oracle so the merged term is not added twice); what remains is the bf16
+    # rounding of activations
+    Pq = {k: (v.detach().float().cpu().bfloat16().float() if k in eng.W else v) for k, v in P.items()}
+    groups = (("qkv_w", ("q", "k", "v")), ("o_w", ("o",)), ("gate_up_w", ("gate", "up")), ("down_w", ("down",)))
+    for i, layer in enumerate(dec.Wm):
+        for name, sites in groups:
+            Pq[f"llm.{i}.{name}"] = layer[name].float().cpu()
+            if cfg.lora:
+                for site in sites:
+                    Pq[f"llm.{i}.lora.{site}.b"] = torch.zeros_like(P[f"llm.{i}.lora.{site}.b"])
+    refq = _oracle_teacher(Pq, cfg, ex, toks)
+    for b, (_, r_q, s_q) in enumerate(refq):
+        for got, want in ((rp[b].cpu(), r_q), (sp[b].cpu(), s_q)):
+            dq = (got - want).abs().max().item()
+            print(f"[decode b={b}] vs the oracle on the decoder's bf16 operands: cumulated max |diff| {dq:.4g} m")
+            assert dq <= 5e-2, (b, dq)
     # the oracle's own free-running greedy agrees up to its first near-tie decision
     _, _, toks_o = O.infer(P, cfg, ex, n_new, eos=-1)
     for b in range(len(toks)):
