@@ -92,6 +92,7 @@ struct AttnArgs {
   bf16* dq; long lddq;           // dQ pass output: bf16, RoPE^T applied with rcos/rsin (pos = query index) if given
   const float* rcos; const float* rsin;
   int tail_first;                // non-causal: each XCD's partial last row blocks dispatched first (SLX_ATTN_TAIL_FIRST)
+  int tailv;                     // non-causal DMA forms: a short last key / query tile (<= kTailMax rows) on the VALU
 };
 
 // Stage 64 rows x 64 cols (bf16) of a token-major matrix into a swizzled LDS tile (8 KB).
@@ -777,6 +778,51 @@ __device__ __forceinline__ void dma_row64_f32(__amdgpu_buffer_rsrc_t rs, char* l
   __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)lds, 4, off, 0, 0, 0);
 }
 
+// ---- short tails on the VALU (non-causal; InternViT: T = 1025 = 16 * 64 + 1) ----------------------------------
+// A 64-row tile holding one valid key (forward / dQ) or query (dK/dV) costs the MFMAs and the masked softmax of a
+// whole tile: 1/17 of each pass. Up to kTailMax such rows are instead folded in after the tile loop, one row at a time
+// on the VALU: the same bf16 operands, f32 products, and P / dS rounded to bf16 exactly where the MFMA forms round
+// them (only the f32 summation order differs). Operand rows come straight from global memory (every lane of a half
+// reads the same 16-B pieces: broadcast loads).
+constexpr int kTailMax = 4;
+
+// Tail rows are copied to LDS when the workgroup starts (their global latency then hides under the tile loop, whose
+// first barrier publishes them): rows[2 * j] = a[j], rows[2 * j + 1] = b[j] for j < n (64 bf16 each)
+__device__ __forceinline__ void tail_stage(bf16* rows, const bf16* a0, long lda, const bf16* b0, long ldb, int n) {
+  const int t = threadIdx.x;
+  if (t < 16 * n) {
+    const int j = t >> 4, which = (t >> 3) & 1, piece = t & 7;
+    const bf16* src = which ? b0 + (long)j * ldb : a0 + (long)j * lda;
+    *reinterpret_cast<uint4*>(rows + (2 * j + which) * 64 + 8 * piece) = *reinterpret_cast<const uint4*>(src + 8 * piece);
+  }
+}
+
+// sum over the 64 dims of row . (the lane's fragments): lane (i, half hl) holds dims 16kk + 8hl + j of its own row
+__device__ __forceinline__ float tail_dot(const bf16* row, const bf16x8 (&f)[4], int hl) {
+  float sum = 0.f;
+#pragma unroll
+  for (int kk = 0; kk < 4; ++kk) {
+    const bf16x8 x = *reinterpret_cast<const bf16x8*>(row + 16 * kk + 8 * hl);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) sum = __builtin_fmaf((float)f[kk][j], (float)x[j], sum);
+  }
+  return sum + __shfl_xor(sum, 32, 64);
+}
+
+// acc0[r] += w * row[dim(r)], acc1[r] += w * row[32 + dim(r)] for the accumulator layout dim(r) = 8(r >> 2) + 4hl + (r & 3)
+__device__ __forceinline__ void tail_axpy(const bf16* row, float w, f32x16& acc0, f32x16& acc1, int hl) {
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const bf16x4 lo = *reinterpret_cast<const bf16x4*>(row + 8 * g + 4 * hl);
+    const bf16x4 hi = *reinterpret_cast<const bf16x4*>(row + 32 + 8 * g + 4 * hl);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      acc0[4 * g + e] = __builtin_fmaf(w, (float)lo[e], acc0[4 * g + e]);
+      acc1[4 * g + e] = __builtin_fmaf(w, (float)hi[e], acc1[4 * g + e]);
+    }
+  }
+}
+
 #ifndef ATTN_NSLOT
 #define ATTN_NSLOT 2  // one tile ahead: fastest of 2 / 3 / 4 slots on both shapes (profiles/round4_attn_dma_ab.txt)
 #endif
@@ -814,7 +860,11 @@ __global__ __launch_bounds__(256, ATTN_FWD_OCC) void attn_fwd_dma_kernel(AttnArg
   }
   int kend = kvlen;
   if (a.causal) kend = min(kend, qb * 128 + 128);
-  const int nt = (kend + 63) / 64;
+  const int ntail = (!a.causal && a.tailv && (kend & 63) <= kTailMax) ? (kend & 63) : 0;  // keys on the VALU
+  const int nt = (kend - ntail + 63) / 64;
+  __shared__ __attribute__((aligned(16))) bf16 trows[2 * kTailMax * 64];
+  tail_stage(trows, kbase + (long)(kend - ntail) * a.ldk, a.ldk, vbase + (long)(kend - ntail) * a.ldv, a.ldv, ntail);
+  if (nt == 0) __syncthreads();
   int ko[2], kr_[2], vo[2], vr_[2];
   dma_lane_offsets(a.ldk, wu, lane, ko, kr_);
   dma_lane_offsets(a.ldv, wu, lane, vo, vr_);
@@ -845,6 +895,21 @@ __global__ __launch_bounds__(256, ATTN_FWD_OCC) void attn_fwd_dma_kernel(AttnArg
     }
   }
   wait_vmcnt<0>();  // the trailing sentinel pieces have landed before the workgroup's LDS is released
+  if (active) {
+    for (int j = 0; j < ntail; ++j) {  // the short key tail: s, the online max, bf16 p, O += p v, l += p
+      const float sc = tail_dot(trows + 2 * j * 64, qf, hl) * c;
+      if (__builtin_amdgcn_ballot_w64(sc > m + LAZY)) {
+        const float mnew = fmaxf(m, sc);
+        const float alpha = __builtin_amdgcn_exp2f(m - mnew);
+        m = mnew;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) { o0[r] *= alpha; o1[r] *= alpha; lacc[r] *= alpha; }
+      }
+      const float pb = (float)(bf16)__builtin_amdgcn_exp2f(sc - m);
+      lacc[0] += pb;
+      tail_axpy(trows + (2 * j + 1) * 64, pb, o0, o1, hl);
+    }
+  }
   if (!active || myq >= S) return;
   const float lt = lacc[0];
   const float inv = 1.0f / lt;
@@ -912,7 +977,11 @@ __global__ __launch_bounds__(256, ATTN_DQ_OCC) void attn_bwd_dq_dma_kernel(AttnA
   for (int r = 0; r < 16; ++r) negd[r] = -dlt;
   int kend = kvlen;
   if (a.causal) kend = min(kend, qb * 128 + 128);
-  const int nt = (kend + 63) / 64;
+  const int ntail = (!a.causal && a.tailv && (kend & 63) <= kTailMax) ? (kend & 63) : 0;  // keys on the VALU
+  const int nt = (kend - ntail + 63) / 64;
+  __shared__ __attribute__((aligned(16))) bf16 trows[2 * kTailMax * 64];
+  tail_stage(trows, kbase + (long)(kend - ntail) * a.ldk, a.ldk, vbase + (long)(kend - ntail) * a.ldv, a.ldv, ntail);
+  if (nt == 0) __syncthreads();
   int ko[2], kr_[2], vo[2], vr_[2];
   dma_lane_offsets(a.ldk, wu, lane, ko, kr_);
   dma_lane_offsets(a.ldv, wu, lane, vo, vr_);
@@ -946,6 +1015,15 @@ __global__ __launch_bounds__(256, ATTN_DQ_OCC) void attn_bwd_dq_dma_kernel(AttnA
     }
   }
   wait_vmcnt<0>();
+  if (active) {
+    for (int j = 0; j < ntail; ++j) {  // the short key tail: dS = p (dP - delta) in bf16, dQ += dS k
+      const bf16* krow = trows + 2 * j * 64;
+      const float sv = tail_dot(krow, qf, hl);
+      const float dpv = tail_dot(trows + (2 * j + 1) * 64, df, hl);
+      const float pv = __builtin_amdgcn_exp2f(__builtin_fmaf(sv, c, -lse));
+      tail_axpy(krow, (float)(bf16)(pv * (dpv - dlt)), dq0, dq1, hl);
+    }
+  }
   __syncthreads();  // the ring is free for the bias column sums' LDS tiles
   const bool qvalid = active && myq < S;
   float c0[16], c1[16];
@@ -1253,7 +1331,16 @@ __global__ __launch_bounds__(256, ATTN_KV_OCC) void attn_bwd_kv_dma_kernel(AttnA
   for (int r = 0; r < 16; ++r) { dk0[r] = dk1[r] = dv0[r] = dv1[r] = 0.f; }
 
   const int qstart = a.causal ? (k0 / 64) * 64 : 0;
-  const int nch = qstart < S ? (S - qstart + 63) / 64 : 0;
+  // queries on the VALU (one q-head per workgroup: InternViT)
+  const int qtail = (!a.causal && a.tailv && ng == 1 && (S & 63) <= kTailMax) ? (S & 63) : 0;
+  const int nch = qstart < S ? (S - qtail - qstart + 63) / 64 : 0;
+  __shared__ __attribute__((aligned(16))) bf16 trows[2 * kTailMax * 64];
+  {
+    const int h = hk * G + hg0;
+    tail_stage(trows, a.q + ((long)b * S + S - qtail) * a.ldq + h * 64, a.ldq,
+               a.dout + ((long)b * S + S - qtail) * a.lddo + h * 64, a.lddo, qtail);
+    if (nch == 0) __syncthreads();
+  }
   const int nit = nch * ng;
   int qo[2], qr_[2], doo[2], dr_[2];
   dma_lane_offsets(a.ldq, wu, lane, qo, qr_);
@@ -1302,6 +1389,20 @@ __global__ __launch_bounds__(256, ATTN_KV_OCC) void attn_bwd_kv_dma_kernel(AttnA
     issue(it + NS - 1);  // into slot (it - 1) % NS: every wave finished stage it - 1 before this iteration's barrier
   }
   wait_vmcnt<0>();
+  if (qtail && kw0 < kvlen) {  // the short query tail: dV += p dO, dK += dS q (bf16 p, dS)
+    const int h = hk * G + hg0;
+    for (int j = 0; j < qtail; ++j) {
+      const long li = ((long)b * a.Hq + h) * S + S - qtail + j;
+      const bf16* qrow = trows + 2 * j * 64;
+      const bf16* drow = trows + (2 * j + 1) * 64;
+      const float sv = tail_dot(qrow, kf, hl);
+      const float dpv = tail_dot(drow, vf, hl);
+      float pv = __builtin_amdgcn_exp2f(__builtin_fmaf(sv, c, -a.lse[li]));
+      pv = mykey < kvlen ? pv : 0.f;
+      tail_axpy(drow, (float)(bf16)pv, dv0, dv1, hl);
+      tail_axpy(qrow, (float)(bf16)(pv * (dpv + a.delta[li])), dk0, dk1, hl);  // a.delta holds -delta
+    }
+  }
   __syncthreads();  // ring free for the bias column sums' LDS tiles
 
   const bool kvalid = mykey < S;
@@ -2351,6 +2452,8 @@ static int fill_common(AttnArgs& a, const slx_attn_desc* d) {
   // default on: +0.1-0.2 % on the VLA step (profiles/round2_s3_tail_swiglu_ab.txt)
   static const int tf = [] { const char* e = getenv("SLX_ATTN_TAIL_FIRST"); return e ? atoi(e) : 1; }();
   a.tail_first = (!d->causal && d->S % 128 != 0) ? tf : 0;
+  static const int tv = [] { const char* e = getenv("SLX_ATTN_TAILV"); return e ? atoi(e) : 1; }();
+  a.tailv = tv;
   return 0;
 }
 
