@@ -31,6 +31,7 @@ from __future__ import annotations
 import argparse
 import glob
 import json
+import math
 import os
 import sys
 import time
@@ -357,6 +358,7 @@ def dropin_line(dl, dev):
            "steps": dl["steps"], "warmup": dl["warmup"], "loader_workers": dl["workers"],
            "step_mfma_frac": round(v * VLA_GFLOP_PER_SAMPLE / 1e3 / PEAK_BF16_TFLOPS, 4),
            "loss_last": round(loss.item(), 5), "losses": [round(x.item(), 4) for x in losses]}
+    res["losses_finite"] = all(math.isfinite(x) for x in res["losses"])
     del m, opt, sched
     return res
 
