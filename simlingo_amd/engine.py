@@ -45,14 +45,6 @@ FUSED_ROPE = os.environ.get("SLX_FUSED_ROPE", "1") != "0"
 # Data-gradient GEMMs dX = dY W over [in][out] copies of the weights (NT main loop, 6-21% faster than NN on the step's
 # shapes: profiles/round3_nn_vs_nt.txt); 0 runs them NN over W itself (A/B hook)
 NT_DGRAD = os.environ.get("SLX_NT_DGRAD", "1") != "0"
-# The Qwen2 gate/up data-gradient GEMM is one round of 200 v3 blocks (100 tiles x 2 K splits; 56 CUs idle for ~150
-# us). SLX_LORA_DB_SIDE=1 runs the gate/up LoRA B-gradient GEMM (it reads the same dgu, nothing reads its output before
-# the optimizer) on a side stream launched right after the dgrad, so its blocks take the idle CUs.
-LORA_DB_SIDE = os.environ.get("SLX_LORA_DB_SIDE", "0") == "1"
-# SLX_PAIR_SIDE=1: each InternViT weight-gradient pair runs on the side stream beside its independent data-gradient GEMM
-# (fc2.w + fc1.w beside the fc1 dgrad, proj.w + qkv.w beside the qkv dgrad); the compute stream waits for it before
-# the next LayerNorm backward, which rewrites the g buffer the pair reads.
-PAIR_SIDE = os.environ.get("SLX_PAIR_SIDE", "0") == "1"
 # Every LoRA parameter gradient (dB_j = s dy_j^T t_j, dA_j = dT_j^T drop_j(x)) of a layer half (the MLP sites, then the
 # attention sites) is deferred to ONE slx_lora_grad launch issued before the norm backward that overwrites their shared
 # operand, instead of a split-K GEMM per B gradient and a dA pass per site group: +1.75 % on the step (102.0 -> 103.8
@@ -67,12 +59,6 @@ GELU_AUX_GRAD = os.environ.get("SLX_GELU_AUX_GRAD", "1") == "1"
 # product on the MFMA, 16-B row streams) instead of the K = 64 GEMM with the DROPMASK_SWIGLU epilogue over 128^2 tiles;
 # SLX_LORA_SWIGLU_BWD=0 restores the GEMM (A/B)
 LORA_SWIGLU_BWD = os.environ.get("SLX_LORA_SWIGLU_BWD", "1") == "1"
-# The LoRA dropout keep bits of every Qwen2 layer (they depend on the step seed only) generated at the start of the step
-# on a side stream, beside the InternViT forward, instead of one slx_dropout_bits launch per layer on the critical path
-# (~19 us each); the compute stream waits for them before the first LoRA down-projection. Off by default: -0.3 % on the
-# step in alternating runs (106.4 vs 106.1 samples/s, profiles/round5_bits_side_ab.txt) - the VALU-bound hash slows
-# the InternViT GEMMs it runs beside by more than the launches it removes from the critical path.
-BITS_SIDE = os.environ.get("SLX_BITS_SIDE", "0") == "1"
 # The SwiGLU forward and the down site's LoRA down-projection as one streaming kernel (slx_swiglu_lora_down: act is
 # written once and never read back for t); SLX_SWIGLU_LORA_DOWN=0 runs slx_swiglu_fwd + slx_lora_down (A/B)
 SWIGLU_LORA_DOWN = os.environ.get("SLX_SWIGLU_LORA_DOWN", "1") == "1"
@@ -181,8 +167,6 @@ class VLAEngine(EngineOps):
         self._cos_sin = {}
         self._build_lora_cat()
         self._build_transposes()
-        self._side = None          # side stream of the LORA_DB_SIDE overlap, and its pending completion events
-        self._side_pending = []
         self._lg_jobs = []         # deferred slx_lora_grad jobs of the current layer half (LORA_GRAD_GROUP)
         self.probe_site = None     # name of a call site to bracket with HIP events (bench roofline)
         self.probe_events = []
@@ -357,8 +341,6 @@ class VLAEngine(EngineOps):
         self.step_seed += 1
         sv["step_seed"] = self.step_seed
         sv["drop"] = cfg.lora_dropout if (training and cfg.lora) else 0.0
-        if BITS_SIDE and sv["drop"] > 0 and not self.precise:
-            self._bits_side(plan.B * plan.S, sv)
         X = self.encode_inputs(pix, plan, dplan, sv)
         S, d = plan.S, cfg.llm_dim
         Ml = B * S
@@ -616,21 +598,6 @@ class VLAEngine(EngineOps):
                     packed=True)
         return dict(zip(sites, bits))
 
-    def _bits_side(self, M, sv):
-        """Every layer's keep bits (slx_dropout_bits, one launch per layer) on the side stream; the compute stream
-        waits for them at the first _lora_bits of the step."""
-        if self._side is None:
-            self._side = torch.cuda.Stream(device=self.device)
-        cur = torch.cuda.current_stream(self.device)
-        self._side.wait_stream(cur)  # the bit buffers' previous readers (last step's backward) are done
-        with torch.cuda.stream(self._side):
-            for i in range(self.cfg.llm_layers):
-                self._bits_layer(i, M, sv)
-            ev = torch.cuda.Event()
-            ev.record(self._side)
-        sv["bits_event"] = ev
-        sv["bits_done"] = set(range(self.cfg.llm_layers))
-
     def _bits_layer(self, i, M, sv):
         jobs = []
         for j, s in enumerate(LORA_SITES):
@@ -644,9 +611,6 @@ class VLAEngine(EngineOps):
         a layer are generated by one slx_dropout_bits launch, the first time any of them is asked for in a step."""
         if sv["drop"] <= 0:
             return None
-        ev = sv.pop("bits_event", None)
-        if ev is not None:  # the side stream's bits (BITS_SIDE) are needed from here on
-            torch.cuda.current_stream(self.device).wait_event(ev)
         key = sv.setdefault("bits_done", set())
         if i not in key:
             self._bits_layer(i, M, sv)
@@ -731,25 +695,10 @@ class VLAEngine(EngineOps):
                        K.P(dgu), 2 * Fl, Ml, Fl, K.stream_ptr())
             del dax
             dh2x = self._e(Ml, d + Pg, dtype=F32)
-            side = lora and LORA_DB_SIDE and not self.precise and not LORA_GRAD_GROUP
-            if side:
-                ev_dgu = torch.cuda.Event()
-                ev_dgu.record()
             self._mm_dx(dgu, *self._dxw(cat, "gu", p + "gate_up_w"), dh2x)
-            if side:  # the gate/up B gradients beside the dgrad's single round (see LORA_DB_SIDE)
-                if self._side is None:
-                    self._side = torch.cuda.Stream(device=self.device)
-                self._side.wait_event(ev_dgu)
-                with torch.cuda.stream(self._side):
-                    self._lora_db(i, ("gate", "up"), [dgu[:, :Fl], dgu[:, Fl:]], h2x[:, d:])
-                    ev_db = torch.cuda.Event()
-                    ev_db.record()
-                dgu.record_stream(self._side)
-                h2x.record_stream(self._side)
-                self._side_pending.append(ev_db)
             if lora:
                 self._lora_bwd(i, ("gate", "up"), [dgu[:, :Fl], dgu[:, Fl:]], h2x[:, d:], h2x[:, :d], dh2x[:, d:],
-                               dh2x[:, :d], sv, skip_db=side)
+                               dh2x[:, :d], sv)
             del dgu
             self._lg_flush(Ml)  # before dxb (the down site's dy) is overwritten
             if done_pending is not None:  # the previous layer's deferred attention-half jobs were in that launch
@@ -785,7 +734,6 @@ class VLAEngine(EngineOps):
             K.norm_bwd(Ls["n1"], dhx, dX, dx_accumulate=True, dx_bf16=nb)
             del dqkv, dhx, dh2x
             if lora:
-                self._join_side()  # the layer's gradients are complete before its bucket can be exchanged
                 if defer:
                     done_pending = f"llm{i}"
                 else:
@@ -852,21 +800,13 @@ class VLAEngine(EngineOps):
             self._mm_dx(g, self.W[p + "fc2.w"], self.WT.get(p + "fc2.w"), dh, epi=K.EPI_GELU_BWD, aux=Ls["hpre"],
                         ldaux=F_, colsum=self.G[p + "fc1.b"],  # fc1.b grad = column sums of dh, in the same epilogue
                         aux_grad=Ls["hgrad"])
-            side = pair and PAIR_SIDE
-            if side:
-                ev_side = self._side_fork()
-            elif pair:  # fc2.w and fc1.w gradients as one launch (two under-filled grids fill the chip together)
+            if pair:  # fc2.w and fc1.w gradients as one launch (two under-filled grids fill the chip together)
                 with self._probe("vit.wgrad_fc"):
                     K.mm_pair((g, Ls["hact"], self.G[p + "fc2.w"]), (dh, Ls["h2"], self.G[p + "fc1.w"]))
             else:
                 K.mm(dh, Ls["h2"], self.G[p + "fc1.w"], ta=True, tb=False, accumulate=True)
             dh2 = self._e(Mv, D)  # bf16: the gradient a bf16 Linear backward hands the fp32 LayerNorm under autocast
             self._mm_dx(dh, self.W[p + "fc1.w"], self.WT.get(p + "fc1.w"), dh2)
-            if side:  # the pair beside the fc1 dgrad (issued after it, so the dgrad's blocks are dispatched first)
-                with torch.cuda.stream(self._side):
-                    self._side.wait_event(ev_side)
-                    K.mm_pair((g, Ls["hact"], self.G[p + "fc2.w"]), (dh, Ls["h2"], self.G[p + "fc1.w"]))
-                self._side_join_now([g, dh, Ls["hact"], Ls["h2"]])
             del dh
             # x_mid = x_in + ls1 * proj(attn(ln1(x_in))): its branch backward (g = ls1 * dx_mid, dls1, proj.b grad)
             # fused into the LN2 backward that produces dx_mid
@@ -885,19 +825,12 @@ class VLAEngine(EngineOps):
                        dqkv[:, :D], dqkv[:, D:2 * D], dqkv[:, 2 * D:], vws, B=N, S=T, Hq=H, Hkv=H, causal=False,
                        dbias=self.G[p + "qkv.b"])  # qkv.b grad = column sums of dq | dk | dv, in the same kernels
             del do
-            if side:
-                ev_side = self._side_fork()
-            elif pair:  # proj.w (g still holds ls1 * dx_mid) and qkv.w gradients as one launch
+            if pair:  # proj.w (g still holds ls1 * dx_mid) and qkv.w gradients as one launch
                 with self._probe("vit.wgrad_attn"):
                     K.mm_pair((g, Ls["o"], self.G[p + "proj.w"]), (dqkv, Ls["h1"], self.G[p + "qkv.w"]))
             else:
                 K.mm(dqkv, Ls["h1"], self.G[p + "qkv.w"], ta=True, tb=False, accumulate=True)
             self._mm_dx(dqkv, self.W[p + "qkv.w"], self.WT.get(p + "qkv.w"), dh2)
-            if side:
-                with torch.cuda.stream(self._side):
-                    self._side.wait_event(ev_side)
-                    K.mm_pair((g, Ls["o"], self.G[p + "proj.w"]), (dqkv, Ls["h1"], self.G[p + "qkv.w"]))
-                self._side_join_now([g, dqkv, Ls["o"], Ls["h1"]])
             del dqkv
             nxt = None
             if i > 0:  # the next (lower) layer's ls2 branch backward, fused onto dx_in
@@ -921,29 +854,6 @@ class VLAEngine(EngineOps):
         self._group_done("vit_embed")
         self.bucketer.mark("backward_end")
         self.saved = None
-
-    def _side_fork(self):
-        """An event on the compute stream that side-stream work issued next waits for."""
-        if self._side is None:
-            self._side = torch.cuda.Stream(device=self.device)
-        ev = torch.cuda.Event()
-        ev.record()
-        return ev
-
-    def _side_join_now(self, tensors):
-        """The compute stream waits here for everything issued on the side stream so far."""
-        ev = torch.cuda.Event()
-        ev.record(self._side)
-        torch.cuda.current_stream(self.device).wait_event(ev)
-        for t in tensors:
-            t.record_stream(self._side)
-
-    def _join_side(self):
-        """The compute stream waits for the side-stream LoRA B-gradient GEMMs issued so far."""
-        cur = torch.cuda.current_stream(self.device)
-        for ev in self._side_pending:
-            cur.wait_event(ev)
-        self._side_pending = []
 
     def _lora_db(self, i, sites, dys, tx):
         """dB_j = s dy_j^T t_j. Sites of equal width whose dy columns are adjacent (k|v, gate|up) and whose B-gradient
@@ -969,7 +879,7 @@ class VLAEngine(EngineOps):
                  ksplit_max=LORA_DB_SPLIT)
             j += 1
 
-    def _lora_bwd(self, i, sites, dys, tx, x, dtx, dx, sv, swiglu=None, dx_bf16=None, skip_db=False):
+    def _lora_bwd(self, i, sites, dys, tx, x, dtx, dx, sv, swiglu=None, dx_bf16=None):
         """LoRA sites of one group sharing the input x. dys[j] bf16 [M, out_j] (views of the output grad),
         tx bf16 [M, P] (forward down-projections t_j in columns 32j..), x bf16 [M, in] (undropped input),
         dtx f32 [M, P] (columns 32j.. hold dt_j = s dy_j B_j, produced by the fused dgrad GEMM; padding columns
@@ -989,8 +899,7 @@ class VLAEngine(EngineOps):
         if LORA_GRAD_GROUP and not self.precise and self._lg_shapes_ok():
             self._lora_bwd_grouped(i, sites, dys, tx, x, dtx, dx, swiglu, dx_bf16, drop, bits, As, sv["step_seed"])
             return
-        if not skip_db:
-            self._lora_db(i, sites, dys, tx)
+        self._lora_db(i, sites, dys, tx)
         # dA and the dx term in one launch. (Running the parameter-only part - dB GEMMs, dA - on a side stream was
         # measured 6 ms/step slower: per-call event/stream overhead on the host and slower main-stream GEMMs.)
         K.lora_bwd(x, dtx, As, bits, [self.G[f"llm.{i}.lora.{site}.a"] for site in sites],
