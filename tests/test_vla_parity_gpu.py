@@ -108,9 +108,27 @@ def test_precise_train_step_north_star(dev, case):
     torch.optim.AdamW over the same trainable set: every gradient within 1e-4 relative L2, the parameter update within
     1e-3 relative L2 (and each element within Adam's step size), and the waypoints / route points the updated
     model predicts within 1e-4 m of the oracle's updated model (losses 1e-4 relative)."""
+    cfg, P, ex, _ = load_case(case)
+    _precise_step(dev, cfg, P, ex, case)
+
+
+def test_precise_train_step_north_star_full_width(dev):
+    """The same north-star step at the REAL InternVL2-1B widths (2 InternViT + 2 Qwen2 layers, T = 1025, GQA 14/2,
+    V = 151655, LoRA r32 on the 7 sites, S_text 256 with 16 loss tokens): fp32 parity mode vs the fp32 oracle through
+    forward, backward, clip and one AdamW update, then the updated model's route / waypoints within 1e-4 m."""
+    from simlingo_amd.config import full_config
+    from simlingo_amd.params import init_params
+    from simlingo_amd.synthetic import make_batch
+    torch.set_num_threads(16)
+    cfg = full_config(vit_layers=2, llm_layers=2, lora_dropout=0.0)
+    P = init_params(cfg, seed=7, lora_b_std=0.02)
+    ex = make_batch(cfg, B=1, s_text=256, n_loss=16, seed=100)
+    _precise_step(dev, cfg, P, ex, "full-width")
+
+
+def _precise_step(dev, cfg, P, ex, case):
     from simlingo_amd.engine import VLAEngine
     from simlingo_amd.plan import plan_from_example
-    cfg, P, ex, z = load_case(case)
     assert cfg.lora_dropout == 0.0
     ref, grads = O.loss_and_grads(P, cfg, ex)
     eng = VLAEngine(cfg, dev, P, precise=True)
