@@ -458,11 +458,6 @@ int slx_dec_attn_o_split(void* cache, int64_t ld, int Hq, int Hkv, const float* 
 /* 1 if slx_dec_attn_o_split supports a cache of lmax rows under this process's SLX_DEC_SPLIT_NS, else 0 (the caller
  * then runs slx_dec_attn + the O GEMV)                                                                           */
 int slx_dec_attn_o_split_ok(int lmax);
-/* read n <= 4 byte ranges (16-B aligned; sizes rounded down to 16 B) with nblocks workgroups, results discarded:
- * run on a second stream it stages the next layer's weights in the Infinity Cache while the current layer computes.
- * Early-exits when st->done. sink: 256 device uints, never written in practice (keeps the loads alive).          */
-int slx_dec_prefetch(const void* const* ptrs, const int64_t* bytes, int n, int nblocks, const slx_dec_state* st,
-                     unsigned* sink, slx_stream_t s);
 int slx_dec_attn_ws_floats(int Hq, int Hkv, int lmax);
 int slx_dec_attn(void* cache, int64_t ld, int Hq, int Hkv, const float* cos_tab, const float* sin_tab, int lmax,
                  float* ws, void* out, const slx_dec_state* st, slx_stream_t s);

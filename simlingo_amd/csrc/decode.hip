@@ -561,42 +561,6 @@ static int gemv_launch(int mode, GemvArgs& a, hipStream_t st) {
   return 0;
 }
 
-// Warm the die-level Infinity Cache with the weights of a layer that runs next, from a second stream while the
-// current layer's launches (latency-bound: 5-7 us each at 1.4-2.4 TB/s) leave HBM bandwidth and CUs idle. Loads only:
-// each lane reads 8 coalesced 16-B chunks per round (a full 128-B line per 8 lanes, so the whole line is fetched) and
-// folds them into one word that is stored (vector store) only on an impossible value, which keeps the loads.
-constexpr int kPrefetchRanges = 4;
-struct PrefetchArgs {
-  const uint4* p[kPrefetchRanges];
-  long long n16[kPrefetchRanges];
-  int nr;
-  const slx_dec_state* st;
-  unsigned* sink;
-};
-
-__global__ __launch_bounds__(256) void dec_prefetch_kernel(PrefetchArgs a) {
-  if (a.st && a.st->done) return;
-  unsigned acc = 0;
-  const long long stride = (long long)gridDim.x * 256;
-  for (int r = 0; r < a.nr; ++r) {
-    const uint4* p = a.p[r];
-    const long long n = a.n16[r];
-    long long i = (long long)blockIdx.x * 256 + threadIdx.x;
-    for (; i + 7 * stride < n; i += 8 * stride) {
-      uint4 v[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = p[i + u * stride];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
-    }
-    for (; i < n; i += stride) {
-      const uint4 v = p[i];
-      acc ^= v.x ^ v.y ^ v.z ^ v.w;
-    }
-  }
-  if (acc == 0x5bd1e995u) a.sink[threadIdx.x] = acc;
-}
-
 }  // namespace slx
 
 using namespace slx;
@@ -700,23 +664,6 @@ int slx_dec_attn_o_split(void* cache, int64_t ld, int Hq, int Hkv, const float* 
 }
 
 int slx_dec_sync_ints(void) { return 4; }
-
-int slx_dec_prefetch(const void* const* ptrs, const int64_t* bytes, int n, int nblocks, const slx_dec_state* st,
-                     unsigned* sink, slx_stream_t s) {
-  SLX_CHECK_ARG(ptrs && bytes && sink && n >= 1 && n <= kPrefetchRanges && nblocks >= 1 && nblocks <= 4096,
-                "slx_dec_prefetch: 1..%d ranges, 1..4096 workgroups, sink of 256 uints", kPrefetchRanges);
-  PrefetchArgs a;
-  memset(&a, 0, sizeof(a));
-  a.nr = n; a.st = st; a.sink = sink;
-  for (int r = 0; r < n; ++r) {
-    SLX_CHECK_ARG(ptrs[r] && ((uintptr_t)ptrs[r] & 15) == 0 && bytes[r] >= 0, "slx_dec_prefetch: 16-B aligned ranges");
-    a.p[r] = (const uint4*)ptrs[r];
-    a.n16[r] = bytes[r] / 16;  // a trailing partial chunk is not worth a load
-  }
-  hipLaunchKernelGGL(dec_prefetch_kernel, dim3(nblocks), dim3(256), 0, (hipStream_t)s, a);
-  SLX_LAUNCH_CHECK("slx_dec_prefetch");
-  return 0;
-}
 
 int slx_dec_attn_o(void* cache, int64_t ld, int Hq, int Hkv, const float* cos_tab, const float* sin_tab, int lmax,
                    float* ws, void* out, const slx_dec_state* st, const void* Wo, int64_t ldwo, int N, int K, float* X,

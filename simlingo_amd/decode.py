@@ -41,10 +41,6 @@ FUSE_O = os.environ.get("SLX_DEC_FUSE_O", "0") == "1"
 # (slx_dec_attn_o_split) instead of one MFMA workgroup per kv head + the O GEMV: 0.71 vs 0.80 ms per token in
 # alternating bench_infer runs (tools/ab/r4_dec_ab.sh, profiles/round4_knobs_ab.txt); SLX_DEC_SPLIT_O=0 restores the old pair
 SPLIT_O = os.environ.get("SLX_DEC_SPLIT_O", "1") == "1"
-# Infinity Cache prefetch of the next layer's weights (slx_dec_prefetch) from a second captured stream, forked at the
-# start of each layer: SLX_DEC_PREFETCH workgroups (0 = off), SLX_DEC_PREFETCH_LAG layers ahead
-PREFETCH = int(os.environ.get("SLX_DEC_PREFETCH", "0"))
-PREFETCH_LAG = int(os.environ.get("SLX_DEC_PREFETCH_LAG", "1"))
 DEC_STORE_ROW, DEC_RESID, DEC_SWIGLU, DEC_ARGMAX = 0, 1, 2, 3
 
 
@@ -64,7 +60,6 @@ K.register("slx_dec_attn_ws_floats", [K.c_int, K.c_int, K.c_int])
 K.register("slx_dec_attn", [K.c_vp, K.c_i64, K.c_int, K.c_int, K.c_vp, K.c_vp, K.c_int, K.c_vp, K.c_vp, K.c_vp, K.c_vp])
 K.register("slx_dec_sync_ints", [])
 K.register("slx_dec_attn_o_split_ok", [K.c_int])
-K.register("slx_dec_prefetch", [K.c_vp, K.c_vp, K.c_int, K.c_int, K.c_vp, K.c_vp, K.c_vp])
 K.register("slx_dec_attn_o", [K.c_vp, K.c_i64, K.c_int, K.c_int, K.c_vp, K.c_vp, K.c_int, K.c_vp, K.c_vp, K.c_vp, K.c_vp,
                               K.c_i64, K.c_int, K.c_int, K.c_vp, K.c_vp, K.c_vp])
 K.register("slx_dec_attn_o_split", [K.c_vp, K.c_i64, K.c_int, K.c_int, K.c_vp, K.c_vp, K.c_int, K.c_vp, K.c_vp, K.c_vp,
@@ -169,23 +164,6 @@ class GreedyDecoder:
             ))
         self._head = _gemv_desc(DEC_ARGMAX, eng.W["llm.lm_head"], cfg.vocab, d, X=self.X, gamma=eng.P["llm.norm"],
                                 eps=cfg.rms_eps, keys=self.keys, state=st)
-        self._pf = []
-        if PREFETCH > 0:  # per layer: its four weight matrices in the order the step reads them
-            self.pf_stream = torch.cuda.Stream(self.dev)
-            self.pf_sink = torch.zeros(256, dtype=torch.int32, device=self.dev)
-            for W in self.Wm:
-                ws = [W[n] for n in ("qkv_w", "o_w", "gate_up_w", "down_w")]
-                self._pf.append(((ctypes.c_void_p * 4)(*[w.data_ptr() for w in ws]),
-                                 (ctypes.c_int64 * 4)(*[w.numel() * w.element_size() for w in ws])))
-
-    def _prefetch(self, j):
-        """Fork the prefetch stream off the current one and read layer j's weights there (joined in _step)."""
-        cur = torch.cuda.current_stream(self.dev)
-        self.pf_stream.wait_stream(cur)
-        ptrs, nbytes = self._pf[j]
-        with torch.cuda.stream(self.pf_stream):
-            K.check(K.lib().slx_dec_prefetch(ptrs, nbytes, 4, PREFETCH, K.P(self.state), K.P(self.pf_sink),
-                                             K.stream_ptr()), "slx_dec_prefetch")
 
     def _begin(self):
         K.call("slx_dec_begin", K.P(self.state), K.P(self.keys), K.P(self.eng.W["llm.embed"]), self.cfg.llm_dim,
@@ -197,10 +175,7 @@ class GreedyDecoder:
         self._begin()
         s = K.stream_ptr()
         lib = K.lib()
-        L = len(self._steps)
         for i, (qkv, cache, o, gu, down) in enumerate(self._steps):
-            if self._pf and i + PREFETCH_LAG < L:
-                self._prefetch(i + PREFETCH_LAG)
             K.check(lib.slx_dec_gemv(ctypes.byref(qkv), s), "slx_dec_gemv")
             if SPLIT_O and self.split_ok:  # split attention, merged by the O GEMV (+ residual)
                 wo = self.Wm[i]["o_w"]
@@ -221,12 +196,7 @@ class GreedyDecoder:
                 K.check(lib.slx_dec_gemv(ctypes.byref(o), s), "slx_dec_gemv")
             K.check(lib.slx_dec_gemv(ctypes.byref(gu), s), "slx_dec_gemv")
             K.check(lib.slx_dec_gemv(ctypes.byref(down), s), "slx_dec_gemv")
-        if self._pf:  # the next token's first layers, beside the LM head (whose 272 MB stream flushes the cache)
-            for j in range(min(PREFETCH_LAG, L)):
-                self._prefetch(j)
         K.check(lib.slx_dec_gemv(ctypes.byref(self._head), s), "slx_dec_gemv")
-        if self._pf:
-            torch.cuda.current_stream(self.dev).wait_stream(self.pf_stream)
 
     def _capture(self):
         """Capture one decode step in a hipGraph. Run once first with done=1 (every kernel early-exits; the
