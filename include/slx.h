@@ -288,6 +288,23 @@ typedef struct slx_lora_swiglu_bwd_desc {
   int64_t M; int F;
 } slx_lora_swiglu_bwd_desc;
 int slx_lora_swiglu_bwd(const slx_lora_swiglu_bwd_desc* d, slx_stream_t stream);
+/* slx_lora_swiglu_bwd plus three LoRA parameter gradients from the same pass (the peft lora_A / lora_B weight grads of
+ * Qwen2MLP's down and gate/up sites, llm.py:106-119), so neither the 2F-wide dgu nor act is read again:
+ *   dA_down [32][F] += dT^T . drop(act),  act = bf16(silu(g) * u) (the forward's activation, recomputed bit-exactly),
+ *                      drop(act) = bf16(act / (1 - p)) & keep (the down site's keep bits, as in the dgrad term);
+ *   dB_gate [F][32] += alpha_b * dgu[:, :F]^T . tg,  dB_up [F][32] += alpha_b * dgu[:, F:]^T . tu  (bf16 dgu as stored);
+ * tg / tu bf16 [M][32]: the gate / up sites' forward t = drop(x) . A^T. Row-group partials go to ws (size from
+ * slx_lora_swiglu_bwd_grads_ws_floats) and are summed in row-group order by a second launch (deterministic in every
+ * mode); F % 128 == 0. dgu is bitwise what slx_lora_swiglu_bwd writes.                                           */
+typedef struct slx_lora_swiglu_bwd_grads_desc {
+  slx_lora_swiglu_bwd_desc sw;
+  const void* tg; const void* tu; int64_t ldtg;
+  float* dA_down; float* dB_gate; float* dB_up;
+  float alpha_b;
+  float* ws; int64_t ws_floats;
+} slx_lora_swiglu_bwd_grads_desc;
+int64_t slx_lora_swiglu_bwd_grads_ws_floats(int64_t M, int F);
+int slx_lora_swiglu_bwd_grads(const slx_lora_swiglu_bwd_grads_desc* d, slx_stream_t stream);
 /* The SwiGLU forward fused with the down site's LoRA down-projection (Qwen2MLP act_fn(gate) * up, then peft lora_A
  * on down_proj with its dropout; llm.py:106-119): act = bf16(silu(g) * u) from gu bf16 [M][2F] (the gate|up GEMM
  * output), written to act [M][F], and t = drop(act) . A^T written as bf16 to t [M][32], drop(x) = bf16(x / (1 - p)) &

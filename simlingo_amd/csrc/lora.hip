@@ -421,28 +421,27 @@ struct DxRegs {
   uint32_t kw[NS];
 };
 
-template <int NS, bool DTB>  // DTB: dt rows are bf16
+// Every global load is unconditional (rows past M read row M - 1 and are never stored; DROP is a template switch):
+// a load inside a branch makes hipcc drain vmcnt(0) behind it, which serialised the dT row loads into 8 round trips.
+template <int NS, bool DTB, bool DROP>  // DTB: dt rows are bf16; DROP: keep bits given
 __global__ __launch_bounds__(512) void lora_dx_kernel(LoraBwdArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, r = lane & 31;
   const int row = blockIdx.x * 32 + r;
   const bool rok = row < a.M;
-  const bool drop = a.bits[0] != nullptr;
+  const long rowc = rok ? row : a.M - 1;
   const int nct = a.Kin / 32;
   bf16x8 tb[NS][2];  // B operand: lane (row r, half h) holds dT_j[row][16 kb + 8 h + i]
 #pragma unroll
   for (int j = 0; j < NS; ++j)
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {
-      const long off = (long)(rok ? row : 0) * a.lddt + 32 * j + 16 * kb + 8 * h;
+      const long off = rowc * a.lddt + 32 * j + 16 * kb + 8 * h;
       if constexpr (DTB) {
-        bf16x8 z;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) z[e] = (bf16)0.f;
-        tb[j][kb] = rok ? *reinterpret_cast<const bf16x8*>(reinterpret_cast<const bf16*>(a.dt) + off) : z;
+        tb[j][kb] = *reinterpret_cast<const bf16x8*>(reinterpret_cast<const bf16*>(a.dt) + off);
       } else {
         const float* tp = a.dt + off;
-        const float4 f0 = rok ? *reinterpret_cast<const float4*>(tp) : make_float4(0.f, 0.f, 0.f, 0.f);
-        const float4 f1 = rok ? *reinterpret_cast<const float4*>(tp + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+        const float4 f0 = *reinterpret_cast<const float4*>(tp);
+        const float4 f1 = *reinterpret_cast<const float4*>(tp + 4);
         tb[j][kb][0] = (bf16)f0.x; tb[j][kb][1] = (bf16)f0.y; tb[j][kb][2] = (bf16)f0.z; tb[j][kb][3] = (bf16)f0.w;
         tb[j][kb][4] = (bf16)f1.x; tb[j][kb][5] = (bf16)f1.y; tb[j][kb][6] = (bf16)f1.z; tb[j][kb][7] = (bf16)f1.w;
       }
@@ -460,12 +459,11 @@ __global__ __launch_bounds__(512) void lora_dx_kernel(LoraBwdArgs a) {
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb)
         R.af[j][kb] = *reinterpret_cast<const bf16x8*>(a.A[j] + ((long)(2 * ct + kb) * 64 + lane) * 8);
-      R.kw[j] = (drop && rok) ? a.bits[j][(long)row * a.ldbits + ct] : 0u;
+      R.kw[j] = DROP ? a.bits[j][rowc * a.ldbits + ct] : 0u;
     }
 #pragma unroll
     for (int g = 0; g < 4; ++g)
-      R.dxv[g] = rok ? *reinterpret_cast<const float4*>(a.dx + (long)row * a.lddx + 32 * ct + 8 * g + 4 * h)
-                     : make_float4(0.f, 0.f, 0.f, 0.f);
+      R.dxv[g] = *reinterpret_cast<const float4*>(a.dx + rowc * a.lddx + 32 * ct + 8 * g + 4 * h);
   };
   auto process = [&](int ct, const DxRegs<NS>& R) {
     f32x16 o[NS];
@@ -484,7 +482,7 @@ __global__ __launch_bounds__(512) void lora_dx_kernel(LoraBwdArgs a) {
         float sum = 0.f;
 #pragma unroll
         for (int j = 0; j < NS; ++j) {
-          const float k = drop ? (((R.kw[j] >> (8 * g + 4 * h + e)) & 1u) ? a.sc : 0.f) : 1.0f;
+          const float k = DROP ? (((R.kw[j] >> (8 * g + 4 * h + e)) & 1u) ? a.sc : 0.f) : 1.0f;
           sum += k * o[j][4 * g + e];
         }
         v[e] += sum;
@@ -502,14 +500,16 @@ __global__ __launch_bounds__(512) void lora_dx_kernel(LoraBwdArgs a) {
   };
   // the block's column tiles: wave w takes w + 8 y, then every 8 * gridDim.y-th (gridDim.y column groups per row tile)
   const int c0 = w + 8 * blockIdx.y, cs = 8 * gridDim.y;
+  // a load for a tile past nct reads the wave's current tile again (L1/L2-hot) and is never processed: no branch
+  // around a load
   DxRegs<NS> R0, R1;
-  if (c0 < nct) load(c0, R0);
+  load(min(c0, nct - 1), R0);
   for (int ct = c0; ct < nct; ct += 2 * cs) {
     const bool more = ct + cs < nct;
-    if (more) load(ct + cs, R1);
+    load(more ? ct + cs : ct, R1);
     process(ct, R0);
     if (!more) break;
-    if (ct + 2 * cs < nct) load(ct + 2 * cs, R0);
+    load(ct + 2 * cs < nct ? ct + 2 * cs : ct + cs, R0);
     process(ct + cs, R1);
   }
 }
@@ -739,6 +739,9 @@ struct LswArgs {
   int M, F;
 };
 
+// DROP: keep bits given (a compile-time switch: a keep-word load behind `a.bits ? ... :` was a branch around a load,
+// after which hipcc drains vmcnt(0), serialising the block's four chunks of loads)
+template <bool DROP>
 __global__ __launch_bounds__(256) void lora_swiglu_bwd_kernel(LswArgs a) {
   __shared__ __attribute__((aligned(16))) float acc_s[32][256 + 4];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -754,7 +757,7 @@ __global__ __launch_bounds__(256) void lora_swiglu_bwd_kernel(LswArgs a) {
     rr[i] = *reinterpret_cast<const uint4*>(a.resid + (long)m * a.ldr + n);
     gg[i] = *reinterpret_cast<const uint4*>(a.gu + (long)m * a.ldgu + n);
     uu[i] = *reinterpret_cast<const uint4*>(a.gu + (long)m * a.ldgu + a.F + n);
-    kb[i] = a.bits ? (a.bits[(long)m * a.ldbits + (n >> 5)] >> (n & 31)) & 0xFFu : 0xFFu;
+    kb[i] = DROP ? (a.bits[(long)m * a.ldbits + (n >> 5)] >> (n & 31)) & 0xFFu : 0xFFu;
   }
   // [32 x 256] = dT [32 x 32] . A [32 x 256]: wave w takes column blocks 2w, 2w + 1
   const int mr = min(m0 + (lane & 31), a.M - 1);
@@ -804,6 +807,192 @@ __global__ __launch_bounds__(256) void lora_swiglu_bwd_kernel(LswArgs a) {
   }
 }
 
+// ---- the same pass with the down site's dA and the gate / up sites' dB (slx_lora_swiglu_bwd_grads) ------------------
+// slx_lora_grad's MLP-half launch streamed dgu (2F wide, 124 MB at the InternVL2-1B step) for dB_gate / dB_up and act
+// (62 MB) for dA_down once more, after this kernel had both in registers. Here a block owns 128 columns of F and a
+// group of 32-row chunks, two chunks' loads in flight (register sets R[0] / R[1]: resid / gate / up / keep, 2 x 16 B
+// each per thread, and the three [32 x 32] LoRA operand tiles dT, tg, tu on the first 128 threads). Per chunk it forms
+// the dgrad term (dT . A on the MFMA, 2 per wave, A^T fragments loaded once per block) and exchanges it through LDS;
+// computes dgu exactly as lora_swiglu_bwd_kernel does and act / drop(act) exactly as the forward's
+// swiglu_lora_down_kernel does; stores dgu and issues the loads of the chunk after next into the freed registers;
+// stages dgu_gate, dgu_up, drop(act) and the operand tiles as [32][64] la_sw panels; and accumulates the three
+// [32 x 128] products with lora_grad's transposed fragment reads (la_tr) on v_mfma_f32_32x32x16_bf16, 6 per wave.
+// The block's three f32 partials go to ws [G][3][32 F] (the B gradients transposed through LDS to their [F][32]
+// layout) and lsw_grads_reduce_kernel adds them in row-group order.
+struct LswgArgs {
+  LswArgs s;
+  const bf16* tg; const bf16* tu; long ldtg;
+  int kch;         // rows per block (a multiple of 32)
+  float* part;     // [gridDim.y][3][32 F]
+};
+
+struct LswgRegs {
+  uint4 rr[2], gg[2], uu[2], td, tgv, tuv;
+  uint32_t kb[2];
+  bf16x8 af[2];
+};
+
+// DROP: keep bits given (p > 0); a compile-time switch, so every load of the chunk loop is an unconditional global load
+template <bool DROP>
+__global__ __launch_bounds__(256, 2) void lora_swiglu_bwd_grads_kernel(LswgArgs g) {
+  // region P (24 KiB): the [32][132] f32 dgrad-term exchange, then per chunk the panels og (0, 1), ou (2, 3),
+  // drop(act) (4, 5) of 4 KiB each; region T (12 KiB): the dT, tg, tu panels (columns 0-31 used)
+  constexpr int PB = 4096;
+  __shared__ __attribute__((aligned(16))) char smem[9 * PB];  // >= the [32][129] f32 transpose of the partials
+  float* acc_s = reinterpret_cast<float*>(smem);
+  char* tp = smem + 6 * PB;
+  const LswArgs& a = g.s;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
+  const int n0 = blockIdx.x * 128;
+  const int mb = blockIdx.y * g.kch, me = min(a.M, mb + g.kch);
+  // A^T fragments of the dgrad term: wave w's column tile 32 w
+  bf16x8 bfr[2];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk)
+    bfr[kk] = *reinterpret_cast<const bf16x8*>(a.at + (long)(n0 + 32 * w + (lane & 31)) * a.ldat + 16 * kk + 8 * h);
+  f32x16 accA, accG, accU;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) accA[j] = accG[j] = accU[j] = 0.f;
+  // piece c = tid + 256 i (i = 0, 1) is row c >> 4, columns n0 + 8 (c & 15); operand tiles (tid < 128): row tid >> 2,
+  // 16-B chunk tid & 3; af: dT rows m0 + (lane & 31)
+  auto load = [&](int m0, LswgRegs& R) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = tid + 256 * i, n = n0 + 8 * (c & 15);
+      const int m = min(m0 + (c >> 4), a.M - 1);  // rows past M load row M-1 (zeroed in the panels, never stored)
+      R.rr[i] = *reinterpret_cast<const uint4*>(a.resid + (long)m * a.ldr + n);
+      R.gg[i] = *reinterpret_cast<const uint4*>(a.gu + (long)m * a.ldgu + n);
+      R.uu[i] = *reinterpret_cast<const uint4*>(a.gu + (long)m * a.ldgu + a.F + n);
+      R.kb[i] = DROP ? a.bits[(long)m * a.ldbits + (n >> 5)] : 0xFFFFFFFFu;  // shifted at use
+    }
+    {  // every thread loads (threads 128.. duplicate 0..127's pieces, L2 hits): no branch around a load
+      const int tm = min(m0 + ((tid & 127) >> 2), a.M - 1), tc = 8 * (tid & 3);
+      R.td = *reinterpret_cast<const uint4*>(a.dt + (long)tm * a.lddt + tc);
+      R.tgv = *reinterpret_cast<const uint4*>(g.tg + (long)tm * g.ldtg + tc);
+      R.tuv = *reinterpret_cast<const uint4*>(g.tu + (long)tm * g.ldtg + tc);
+    }
+    const int mr = min(m0 + (lane & 31), a.M - 1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+      R.af[kk] = *reinterpret_cast<const bf16x8*>(a.dt + (long)mr * a.lddt + 16 * kk + 8 * h);
+  };
+  auto process = [&](LswgRegs& R, int m0, bool more) {
+    {  // dgrad term [32 x 128] = dT [32 x 32] . A [32 x 128]: wave w columns 32 w
+      f32x16 acc;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) acc[j] = 0.f;
+      acc = mfma32x32(R.af[0], bfr[0], acc);
+      acc = mfma32x32(R.af[1], bfr[1], acc);
+#pragma unroll
+      for (int j = 0; j < 16; ++j) acc_s[(8 * (j >> 2) + 4 * h + (j & 3)) * 132 + 32 * w + (lane & 31)] = acc[j];
+    }
+    __syncthreads();
+    float v[2][8];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = tid + 256 * i, row = c >> 4, cc = c & 15;
+      const float4 v0 = *reinterpret_cast<const float4*>(&acc_s[row * 132 + 8 * cc]);
+      const float4 v1 = *reinterpret_cast<const float4*>(&acc_s[row * 132 + 8 * cc + 4]);
+      v[i][0] = v0.x; v[i][1] = v0.y; v[i][2] = v0.z; v[i][3] = v0.w;
+      v[i][4] = v1.x; v[i][5] = v1.y; v[i][6] = v1.z; v[i][7] = v1.w;
+    }
+    __syncthreads();  // region P is rewritten as panels below
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = tid + 256 * i, row = c >> 4, cc = c & 15, n = n0 + 8 * cc;
+      const int m = m0 + row;
+      const bool ok = m < me;
+      const bf16x8 r8 = __builtin_bit_cast(bf16x8, R.rr[i]), g8 = __builtin_bit_cast(bf16x8, R.gg[i]),
+                   u8 = __builtin_bit_cast(bf16x8, R.uu[i]);
+      bf16x8 og, ou, dk;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const bool keep = (R.kb[i] >> ((8 * cc + e) & 31)) & 1u;
+        const float d = (keep ? v[i][e] * a.sc : 0.f) + (float)r8[e];  // lora_swiglu_bwd_kernel's arithmetic
+        const float gf = (float)g8[e], uf = (float)u8[e];
+        og[e] = (bf16)(d * uf * silu_grad(gf));
+        ou[e] = (bf16)(d * silu(gf));
+        const bf16 act = (bf16)(silu(gf) * uf);  // swiglu_lora_down_kernel's (and slx_swiglu_fwd's) rounding
+        dk[e] = keep ? (bf16)((float)act * a.sc) : (bf16)0.f;
+      }
+      if (ok) {
+        *reinterpret_cast<bf16x8*>(a.dgu + (long)m * a.lddgu + n) = og;
+        *reinterpret_cast<bf16x8*>(a.dgu + (long)m * a.lddgu + a.F + n) = ou;
+      }
+      const uint4 z = make_uint4(0u, 0u, 0u, 0u);
+      const int po = (cc >> 3) * PB + la_sw(row, cc & 7);
+      *reinterpret_cast<uint4*>(smem + po) = ok ? __builtin_bit_cast(uint4, og) : z;
+      *reinterpret_cast<uint4*>(smem + 2 * PB + po) = ok ? __builtin_bit_cast(uint4, ou) : z;
+      *reinterpret_cast<uint4*>(smem + 4 * PB + po) = ok ? __builtin_bit_cast(uint4, dk) : z;
+    }
+    if (tid < 128) {
+      const int to = la_sw(tid >> 2, tid & 3);
+      *reinterpret_cast<uint4*>(tp + to) = R.td;
+      *reinterpret_cast<uint4*>(tp + PB + to) = R.tgv;
+      *reinterpret_cast<uint4*>(tp + 2 * PB + to) = R.tuv;
+    }
+    // the chunk after next into the registers just consumed (past the block's rows: this chunk again, L2-hot; every
+    // load of the loop is unconditional, so the compiler counts the loads in flight instead of draining them)
+    __builtin_amdgcn_sched_barrier(0);
+    load(more ? m0 + 64 : m0, R);
+    __builtin_amdgcn_sched_barrier(0);
+    __syncthreads();
+    {  // [32 x 32] per product and wave: columns 32 w of the block (panel w >> 1, panel columns 32 (w & 1))
+      int ln = lane;
+      asm volatile("" : "+v"(ln));
+      const int pc = 32 * (w & 1), pn = (w >> 1) * PB;
+#pragma unroll
+      for (int ms = 0; ms < 2; ++ms) {
+        accA = mfma32x32(la_tr(tp, 16 * ms, 0, ln), la_tr(smem + 4 * PB + pn, 16 * ms, pc, ln), accA);
+        accG = mfma32x32(la_tr(tp + PB, 16 * ms, 0, ln), la_tr(smem + pn, 16 * ms, pc, ln), accG);
+        accU = mfma32x32(la_tr(tp + 2 * PB, 16 * ms, 0, ln), la_tr(smem + 2 * PB + pn, 16 * ms, pc, ln), accU);
+      }
+    }
+    __syncthreads();
+  };
+  LswgRegs R[2];
+  load(mb, R[0]);
+  __builtin_amdgcn_sched_barrier(0);  // R[0]'s loads all before R[1]'s: the in-loop waits then count R[1]'s as newer
+  load(mb + 32 < me ? mb + 32 : mb, R[1]);
+  __builtin_amdgcn_sched_barrier(0);
+  for (int m0 = mb; m0 < me; m0 += 64) {  // a pair of chunks per trip (a chunk past me only adds zeros)
+    process(R[0], m0, m0 + 64 < me);
+    process(R[1], m0 + 32, m0 + 96 < me);
+  }
+  // partials: A in its [32][F] layout straight from the accumulators; G / U through an LDS transpose to [F][32]
+  const long F32n = 32L * a.F;
+  float* pb = g.part + (long)blockIdx.y * 3 * F32n;
+  const int mycol = n0 + 32 * w + (lane & 31);
+#pragma unroll
+  for (int j = 0; j < 16; ++j) pb[(long)((j & 3) + 8 * (j >> 2) + 4 * h) * a.F + mycol] = accA[j];
+  float* red = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const f32x16& acc = q == 0 ? accG : accU;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) red[((j & 3) + 8 * (j >> 2) + 4 * h) * 129 + 32 * w + (lane & 31)] = acc[j];
+    __syncthreads();
+    for (int e = tid; e < 32 * 128; e += 256) {
+      const int col = e >> 5, r = e & 31;
+      pb[(1 + q) * F32n + (long)(n0 + col) * 32 + r] = red[r * 129 + col];
+    }
+    __syncthreads();
+  }
+}
+
+// out_q[k] += alpha_q * sum over the row groups y (in order) of part[y][q][k], q = 0 (dA_down), 1 (dB_gate), 2 (dB_up)
+__global__ __launch_bounds__(256) void lsw_grads_reduce_kernel(const float* part, int ny, long n, float* o0, float* o1,
+                                                               float* o2, float al0, float al12) {
+  const long e = (long)blockIdx.x * 256 + threadIdx.x;
+  if (e >= 3 * n) return;
+  const int q = (int)(e / n);
+  const long k = e - q * n;
+  float s = 0.f;
+  for (int y = 0; y < ny; ++y) s += part[(long)y * 3 * n + e];
+  float* o = q == 0 ? o0 : (q == 1 ? o1 : o2);
+  o[k] += (q == 0 ? al0 : al12) * s;
+}
+
 // ---- the SwiGLU forward fused with the down site's LoRA down-projection (slx_swiglu_lora_down) ----------------------
 // act = silu(g) * u (bf16, the Qwen2MLP activation the down projection reads) and t = drop(act) . A^T [M x 32] (peft's
 // lora_A on down_proj, drop(act) = bf16(act / (1 - p)) & keep), in one pass over gu: a block owns 32 rows x 256
@@ -822,6 +1011,7 @@ struct SldArgs {
   int M, F;
 };
 
+template <bool DROP>  // as lora_swiglu_bwd_kernel's
 __global__ __launch_bounds__(256) void swiglu_lora_down_kernel(SldArgs a) {
   __shared__ __attribute__((aligned(16))) char xs[32 * 512];  // drop(act) [32][256] bf16
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -835,7 +1025,7 @@ __global__ __launch_bounds__(256) void swiglu_lora_down_kernel(SldArgs a) {
     const int m = min(m0 + row, a.M - 1);
     gg[i] = *reinterpret_cast<const uint4*>(a.gu + (long)m * a.ldgu + n);
     uu[i] = *reinterpret_cast<const uint4*>(a.gu + (long)m * a.ldgu + a.F + n);
-    kb[i] = a.bits ? (a.bits[(long)m * a.ldbits + (n >> 5)] >> (n & 31)) & 0xFFu : 0xFFu;
+    kb[i] = DROP ? (a.bits[(long)m * a.ldbits + (n >> 5)] >> (n & 31)) & 0xFFu : 0xFFu;
   }
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -960,12 +1150,16 @@ static void launch_bwd_t(const LoraBwdArgs& a, dim3 grid, hipStream_t st) {
                          (int)grid.y);
     }
   }
-  // column groups per 32-row tile: 200 row tiles alone (Qwen2, M = 6384) under-fill the 256 CUs
-  static const int dxg = [] { const char* e = getenv("SLX_LORA_DX_GROUPS"); return e ? atoi(e) : 2; }();
+  // column groups per 32-row tile (SLX_LORA_DX_GROUPS): 1. The 512-thread blocks hold 150-200 VGPRs, so one fits a CU;
+  // two groups (400 blocks at Qwen2's M = 6384) ran as 1.56 rounds and measured 0.25 % slower on the step than one
+  // group's 200 blocks of 3-4 pipelined tiles per wave (profiles/round5_lora_dx_groups_ab.txt)
+  static const int dxg = [] { const char* e = getenv("SLX_LORA_DX_GROUPS"); return e ? atoi(e) : 1; }();
   const int nct = a.Kin / 32;
   int g = dxg < 1 ? 1 : dxg;
   while (g > 1 && 8 * g > nct) --g;
-  if (a.dx) hipLaunchKernelGGL((lora_dx_kernel<NS, DTB>), dim3((unsigned)((a.M + 31) / 32), (unsigned)g), dim3(512), 0, st, a);
+  const dim3 dgrid((unsigned)((a.M + 31) / 32), (unsigned)g);
+  if (a.dx && a.bits[0]) hipLaunchKernelGGL((lora_dx_kernel<NS, DTB, true>), dgrid, dim3(512), 0, st, a);
+  else if (a.dx) hipLaunchKernelGGL((lora_dx_kernel<NS, DTB, false>), dgrid, dim3(512), 0, st, a);
 }
 template <int NS>
 static void launch_bwd(const LoraBwdArgs& a, dim3 grid, hipStream_t st) {
@@ -1142,9 +1336,64 @@ extern "C" int slx_lora_swiglu_bwd(const slx_lora_swiglu_bwd_desc* d, slx_stream
   a.sc = 1.0f / (1.0f - d->p);
   a.dgu = (bf16*)d->dgu; a.lddgu = d->lddgu;
   a.M = (int)d->M; a.F = d->F;
-  hipLaunchKernelGGL(lora_swiglu_bwd_kernel, dim3((unsigned)(d->F / 256), (unsigned)((d->M + 31) / 32)), dim3(256), 0,
-                     (hipStream_t)stream, a);
+  const dim3 grid((unsigned)(d->F / 256), (unsigned)((d->M + 31) / 32));
+  if (a.bits) hipLaunchKernelGGL(lora_swiglu_bwd_kernel<true>, grid, dim3(256), 0, (hipStream_t)stream, a);
+  else hipLaunchKernelGGL(lora_swiglu_bwd_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream, a);
   SLX_LAUNCH_CHECK("slx_lora_swiglu_bwd");
+  return 0;
+}
+
+// rows per block of slx_lora_swiglu_bwd_grads: about two blocks per CU over the F / 128 column blocks
+static int lswg_kch(int64_t M, int F) {
+  const long nch = (M + 63) / 64, ncb = F / 128;
+  long groups = (512 + ncb - 1) / ncb;
+  groups = groups < 1 ? 1 : (groups > nch ? nch : groups);
+  return (int)(((nch + groups - 1) / groups) * 64);
+}
+
+extern "C" int64_t slx_lora_swiglu_bwd_grads_ws_floats(int64_t M, int F) {
+  if (M <= 0 || F <= 0 || F % 128 != 0) return 0;
+  const int kch = lswg_kch(M, F);
+  return (int64_t)((M + kch - 1) / kch) * 3 * 32 * F;
+}
+
+extern "C" int slx_lora_swiglu_bwd_grads(const slx_lora_swiglu_bwd_grads_desc* d, slx_stream_t stream) {
+  SLX_CHECK_ARG(d && d->sw.dt && d->sw.at && d->sw.resid && d->sw.gu && d->sw.dgu && d->tg && d->tu && d->dA_down &&
+                d->dB_gate && d->dB_up && d->ws, "slx_lora_swiglu_bwd_grads: null operand");
+  const slx_lora_swiglu_bwd_desc& s = d->sw;
+  SLX_CHECK_ARG(s.F > 0 && s.F % 128 == 0 && s.M >= 0 && s.M < (1LL << 31), "slx_lora_swiglu_bwd_grads: F %% 128 (got %d)",
+                s.F);
+  SLX_CHECK_ARG(s.lddt % 8 == 0 && s.ldat % 8 == 0 && s.ldat >= 32 && s.ldr % 8 == 0 && s.ldgu % 8 == 0 &&
+                s.lddgu % 8 == 0 && d->ldtg % 8 == 0 &&
+                ((((uintptr_t)s.dt | (uintptr_t)s.at | (uintptr_t)s.resid | (uintptr_t)s.gu | (uintptr_t)s.dgu |
+                   (uintptr_t)d->tg | (uintptr_t)d->tu) & 15) == 0),
+                "slx_lora_swiglu_bwd_grads: 16-B aligned rows (leading dims %% 8)");
+  SLX_CHECK_ARG(s.p >= 0.f && s.p < 1.f && (s.p == 0.f || (s.bits && s.ldbits >= s.F / 32)),
+                "slx_lora_swiglu_bwd_grads: 0 <= p < 1, p > 0 needs the keep bits");
+  SLX_CHECK_ARG(d->ws_floats >= slx_lora_swiglu_bwd_grads_ws_floats(s.M, s.F),
+                "slx_lora_swiglu_bwd_grads: workspace holds %lld floats, needs %lld", (long long)d->ws_floats,
+                (long long)slx_lora_swiglu_bwd_grads_ws_floats(s.M, s.F));
+  if (s.M == 0) return 0;
+  LswgArgs g;
+  LswArgs& a = g.s;
+  a.dt = (const bf16*)s.dt; a.lddt = s.lddt; a.at = (const bf16*)s.at; a.ldat = s.ldat;
+  a.resid = (const bf16*)s.resid; a.ldr = s.ldr; a.gu = (const bf16*)s.gu; a.ldgu = s.ldgu;
+  a.bits = s.p > 0.f ? s.bits : nullptr; a.ldbits = s.ldbits;
+  a.sc = 1.0f / (1.0f - s.p);
+  a.dgu = (bf16*)s.dgu; a.lddgu = s.lddgu;
+  a.M = (int)s.M; a.F = s.F;
+  g.tg = (const bf16*)d->tg; g.tu = (const bf16*)d->tu; g.ldtg = d->ldtg;
+  g.kch = lswg_kch(s.M, s.F);
+  g.part = d->ws;
+  const int groups = (int)((s.M + g.kch - 1) / g.kch);
+  hipStream_t st = (hipStream_t)stream;
+  const dim3 grid((unsigned)(s.F / 128), (unsigned)groups);
+  if (a.bits) hipLaunchKernelGGL(lora_swiglu_bwd_grads_kernel<true>, grid, dim3(256), 0, st, g);
+  else hipLaunchKernelGGL(lora_swiglu_bwd_grads_kernel<false>, grid, dim3(256), 0, st, g);
+  const long n = 32L * s.F;
+  hipLaunchKernelGGL(lsw_grads_reduce_kernel, dim3((unsigned)((3 * n + 255) / 256)), dim3(256), 0, st,
+                     (const float*)d->ws, groups, n, d->dA_down, d->dB_gate, d->dB_up, 1.0f, d->alpha_b);
+  SLX_LAUNCH_CHECK("slx_lora_swiglu_bwd_grads");
   return 0;
 }
 
@@ -1174,8 +1423,9 @@ extern "C" int slx_swiglu_lora_down(const slx_swiglu_lora_down_desc* d, slx_stre
   a.part = d->ws;
   a.M = (int)d->M; a.F = d->F;
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(swiglu_lora_down_kernel, dim3((unsigned)(d->F / 256), (unsigned)((d->M + 31) / 32)), dim3(256), 0,
-                     st, a);
+  const dim3 grid((unsigned)(d->F / 256), (unsigned)((d->M + 31) / 32));
+  if (a.bits) hipLaunchKernelGGL(swiglu_lora_down_kernel<true>, grid, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL(swiglu_lora_down_kernel<false>, grid, dim3(256), 0, st, a);
   hipLaunchKernelGGL(swiglu_lora_down_reduce_kernel, dim3((unsigned)((d->M * 32 + 255) / 256)), dim3(256), 0, st,
                      (const float*)d->ws, d->F / 256, (long)d->M, (bf16*)d->t, (long)d->ldt);
   SLX_LAUNCH_CHECK("slx_swiglu_lora_down");

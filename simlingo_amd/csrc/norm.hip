@@ -126,16 +126,21 @@ __global__ __launch_bounds__(256) void norm_fwd_wave_kernel(NormArgs a) {
   const int lane = threadIdx.x & 63;
   const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= a.rows) return;
+  // every load unconditional (columns past D read column 0 and are zeroed by a select): a load inside a branch makes
+  // hipcc drain vmcnt(0) behind it; gamma / beta are issued with x, so the row costs one round trip
   float v[16];
+  float4 gm[4], bt[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int col = (lane + 64 * i) * 4;
-    float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (col < a.D) {
-      const float* src = a.ps ? a.x + ps_src_row(row, col / a.C, a.G, a.tok_per_img) * a.ldx + (col % a.C)
-                              : a.x + row * a.ldx + col;
-      t = *reinterpret_cast<const float4*>(src);
-    }
+    const bool ok = col < a.D;
+    const int cl = ok ? col : 0;
+    const float* src = a.ps ? a.x + ps_src_row(row, cl / a.C, a.G, a.tok_per_img) * a.ldx + (cl % a.C)
+                            : a.x + row * a.ldx + cl;
+    float4 t = *reinterpret_cast<const float4*>(src);
+    gm[i] = *reinterpret_cast<const float4*>(a.gamma + cl);
+    if (!RMS) bt[i] = *reinterpret_cast<const float4*>(a.beta + cl);
+    if (!ok) t = make_float4(0.f, 0.f, 0.f, 0.f);
     v[4 * i] = t.x; v[4 * i + 1] = t.y; v[4 * i + 2] = t.z; v[4 * i + 3] = t.w;
   }
   float mu = 0.f;
@@ -161,10 +166,13 @@ __global__ __launch_bounds__(256) void norm_fwd_wave_kernel(NormArgs a) {
     const int col = (lane + 64 * i) * 4;
     if (col >= a.D) continue;
     float yv[4];
+    const float gv[4] = {gm[i].x, gm[i].y, gm[i].z, gm[i].w};
+    float bv[4] = {0.f, 0.f, 0.f, 0.f};
+    if (!RMS) { bv[0] = bt[i].x; bv[1] = bt[i].y; bv[2] = bt[i].z; bv[3] = bt[i].w; }
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const float xh = (v[4 * i + e] - mu) * rs;
-      yv[e] = RMS ? (a.y_f32 ? xh : (float)(bf16)xh) * a.gamma[col + e] : xh * a.gamma[col + e] + a.beta[col + e];
+      yv[e] = RMS ? (a.y_f32 ? xh : (float)(bf16)xh) * gv[e] : xh * gv[e] + bv[e];
     }
     if (a.y_f32) {
       *reinterpret_cast<float4*>(reinterpret_cast<float*>(a.y) + row * a.ldy + col) = make_float4(yv[0], yv[1], yv[2], yv[3]);

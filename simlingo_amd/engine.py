@@ -59,6 +59,9 @@ GELU_AUX_GRAD = os.environ.get("SLX_GELU_AUX_GRAD", "1") == "1"
 # product on the MFMA, 16-B row streams) instead of the K = 64 GEMM with the DROPMASK_SWIGLU epilogue over 128^2 tiles;
 # SLX_LORA_SWIGLU_BWD=0 restores the GEMM (A/B)
 LORA_SWIGLU_BWD = os.environ.get("SLX_LORA_SWIGLU_BWD", "1") == "1"
+# ... and that pass also forms dA_down, dB_gate and dB_up (slx_lora_swiglu_bwd_grads), which slx_lora_grad's MLP-half
+# launch otherwise computes by streaming dgu and act again; SLX_LORA_SWIGLU_GRADS=0 restores those jobs (A/B)
+LORA_SWIGLU_GRADS = os.environ.get("SLX_LORA_SWIGLU_GRADS", "1") == "1"
 # The SwiGLU forward and the down site's LoRA down-projection as one streaming kernel (slx_swiglu_lora_down: act is
 # written once and never read back for t); SLX_SWIGLU_LORA_DOWN=0 runs slx_swiglu_fwd + slx_lora_down (A/B)
 SWIGLU_LORA_DOWN = os.environ.get("SLX_SWIGLU_LORA_DOWN", "1") == "1"
@@ -689,7 +692,7 @@ class VLAEngine(EngineOps):
             dgu = self._e(Ml, 2 * Fl)
             if lora:  # the down-site dropout dgrad and the SwiGLU backward share one GEMM epilogue
                 self._lora_bwd(i, ("down",), [dxb], ax[:, Fl:], ax[:, :Fl], dax[:, Fl:], dax[:, :Fl], sv,
-                               swiglu=(Ls["gu"], dgu))
+                               swiglu=(Ls["gu"], dgu), gu_t=h2x[:, d:])
             else:
                 K.call("slx_swiglu_bwd_f32" if pr else "slx_swiglu_bwd", K.P(dax), dax.stride(0), K.P(Ls["gu"]), 2 * Fl,
                        K.P(dgu), 2 * Fl, Ml, Fl, K.stream_ptr())
@@ -879,7 +882,7 @@ class VLAEngine(EngineOps):
                  ksplit_max=LORA_DB_SPLIT)
             j += 1
 
-    def _lora_bwd(self, i, sites, dys, tx, x, dtx, dx, sv, swiglu=None, dx_bf16=None):
+    def _lora_bwd(self, i, sites, dys, tx, x, dtx, dx, sv, swiglu=None, dx_bf16=None, gu_t=None):
         """LoRA sites of one group sharing the input x. dys[j] bf16 [M, out_j] (views of the output grad),
         tx bf16 [M, P] (forward down-projections t_j in columns 32j..), x bf16 [M, in] (undropped input),
         dtx f32 [M, P] (columns 32j.. hold dt_j = s dy_j B_j, produced by the fused dgrad GEMM; padding columns
@@ -887,7 +890,8 @@ class VLAEngine(EngineOps):
         dB_j = s dy_j^T t_j (GEMMs) ; dA_j = dt_j^T drop_j(x) and dx += drop_j'(dt_j A_j) in one slx_lora_bwd launch
         (dx_bf16: write bf16(dx + ...) there instead of updating dx).
         swiglu=(gu, dgu) (down projection only): the dx term and the SwiGLU backward run in one GEMM epilogue instead:
-        dgu = swiglu'(gu) applied to dx + drop'(dt A)."""
+        dgu = swiglu'(gu) applied to dx + drop'(dt A). gu_t (with swiglu): the gate / up sites' forward t [M, 64], for
+        slx_lora_swiglu_bwd_grads (the grouped path then forms dA_down, dB_gate and dB_up in the SwiGLU pass)."""
         cfg = self.cfg
         if self.precise:
             self._lora_bwd_precise(i, sites, dys, tx, x, dtx, dx, swiglu)
@@ -897,7 +901,8 @@ class VLAEngine(EngineOps):
         bits = [keep[site] for site in sites]
         As = [self.cat[i]["axfrag." + site] for site in sites]
         if LORA_GRAD_GROUP and not self.precise and self._lg_shapes_ok():
-            self._lora_bwd_grouped(i, sites, dys, tx, x, dtx, dx, swiglu, dx_bf16, drop, bits, As, sv["step_seed"])
+            self._lora_bwd_grouped(i, sites, dys, tx, x, dtx, dx, swiglu, dx_bf16, drop, bits, As, sv["step_seed"],
+                                   gu_t)
             return
         self._lora_db(i, sites, dys, tx)
         # dA and the dx term in one launch. (Running the parameter-only part - dB GEMMs, dA - on a side stream was
@@ -935,20 +940,35 @@ class VLAEngine(EngineOps):
             K.call("slx_swiglu_bwd_f32", K.P(dx), dx.stride(0), K.P(gu), gu.stride(0), K.P(dgu), dgu.stride(0), x.shape[0],
                    gu.shape[1] // 2, K.stream_ptr())
 
-    def _lora_bwd_grouped(self, i, sites, dys, tx, x, dtx, dx, swiglu, dx_bf16, drop, bits, As, step_seed):
+    def _lora_bwd_grouped(self, i, sites, dys, tx, x, dtx, dx, swiglu, dx_bf16, drop, bits, As, step_seed, gu_t=None):
         """LORA_GRAD_GROUP: the dx term (or the down site's SwiGLU epilogue) now; dB_j and dA_j as slx_lora_grad jobs
         deferred to the layer half's _lg_flush. A dT that lives in f32 (the fused dgrad GEMM's extra columns) is
-        written as bf16 by the dx kernel, the rounding the dA pass applied to it."""
+        written as bf16 by the dx kernel, the rounding the dA pass applied to it. With LORA_SWIGLU_GRADS the down site's
+        SwiGLU pass forms dA_down, dB_gate and dB_up itself (the gate / up sites, which come next, then skip their dB)."""
         cfg = self.cfg
         r = cfg.lora_r
         M = x.shape[0]
+        F = swiglu[0].shape[1] // 2 if swiglu is not None else 0
+        fuse = (swiglu is not None and gu_t is not None and LORA_SWIGLU_BWD and LORA_SWIGLU_GRADS and F % 128 == 0
+                and dtx.dtype == torch.bfloat16)
+        skip_db = sites == ("gate", "up") and getattr(self, "_gu_db_fused", None) == i
+        if sites == ("gate", "up"):
+            self._gu_db_fused = None
         for j, site in enumerate(sites):
-            self._lg_jobs.append(dict(x=dys[j], t=tx[:, r * j:r * (j + 1)], outs=[self.G[f"llm.{i}.lora.{site}.b"]],
-                                      out_nr=True, alpha=float(cfg.lora_scale)))
+            if not skip_db:
+                self._lg_jobs.append(dict(x=dys[j], t=tx[:, r * j:r * (j + 1)], outs=[self.G[f"llm.{i}.lora.{site}.b"]],
+                                          out_nr=True, alpha=float(cfg.lora_scale)))
         if dtx.dtype == torch.bfloat16:
             dTb = dtx
         else:
             dTb = self._buf(("lg_dT",) + tuple(sites), M, r * len(sites), dtype=torch.bfloat16)
+        if fuse:
+            gu, dgu = swiglu
+            K.lora_swiglu_bwd_grads(dtx, self.cat[i]["aT.down"], dx, gu, dgu, bits[0], drop, gu_t[:, :r],
+                                    gu_t[:, r:2 * r], self.G[f"llm.{i}.lora.down.a"], self.G[f"llm.{i}.lora.gate.b"],
+                                    self.G[f"llm.{i}.lora.up.b"], float(cfg.lora_scale))
+            self._gu_db_fused = i
+            return
         self._lg_jobs.append(dict(x=x, t=dTb, outs=[self.G[f"llm.{i}.lora.{site}.a"] for site in sites], out_nr=False,
                                   alpha=1.0, p=drop, bits=bits))
         if swiglu is None:

@@ -687,6 +687,49 @@ def lora_swiglu_bwd(dt, at, resid, gu, dgu, bits, p):
     check(lib().slx_lora_swiglu_bwd(ctypes.byref(d), stream_ptr()), "slx_lora_swiglu_bwd")
 
 
+class LoraSwigluBwdGradsDesc(ctypes.Structure):
+    _fields_ = [("sw", LoraSwigluBwdDesc), ("tg", c_vp), ("tu", c_vp), ("ldtg", c_i64), ("dA_down", c_vp),
+                ("dB_gate", c_vp), ("dB_up", c_vp), ("alpha_b", c_float), ("ws", c_vp), ("ws_floats", c_i64)]
+
+
+register("slx_lora_swiglu_bwd_grads_ws_floats", [c_i64, c_int], restype=c_i64)
+register("slx_lora_swiglu_bwd_grads", [ctypes.POINTER(LoraSwigluBwdGradsDesc), c_vp])
+_lswg_ws = {}
+
+
+def lora_swiglu_bwd_grads(dt, at, resid, gu, dgu, bits, p, tg, tu, dA_down, dB_gate, dB_up, alpha_b):
+    """slx_lora_swiglu_bwd_grads: lora_swiglu_bwd's dgu, and from the same pass dA_down [32, F] += dT^T drop(act),
+    dB_gate / dB_up [F, 32] += alpha_b dgu[:, :F]^T tg / dgu[:, F:]^T tu. tg, tu bf16 [M, 32] views (same stride),
+    the three outputs f32 contiguous."""
+    M, F = resid.shape
+    for t in (dt, at, resid, gu, dgu, tg, tu):
+        assert t.dtype == torch.bfloat16 and t.is_cuda and t.stride(1) == 1
+    assert at.shape == (F, 32) and gu.shape[0] == M and gu.shape[1] >= 2 * F and dgu.shape[1] >= 2 * F
+    assert dt.shape[0] == M and dt.shape[1] >= 32
+    assert tg.shape == (M, 32) and tu.shape == (M, 32) and tg.stride(0) == tu.stride(0)
+    assert dA_down.shape == (32, F) and dB_gate.shape == (F, 32) and dB_up.shape == (F, 32)
+    for t in (dA_down, dB_gate, dB_up):
+        assert t.dtype == torch.float32 and t.is_contiguous()
+    need = int(lib().slx_lora_swiglu_bwd_grads_ws_floats(M, F))
+    key = (dt.device, torch.cuda.current_stream(dt.device).cuda_stream)
+    ws = _lswg_ws.get(key)
+    if ws is None or ws.numel() < need:
+        ws = _lswg_ws[key] = torch.empty(need, dtype=torch.float32, device=dt.device)
+    s = LoraSwigluBwdDesc()
+    s.dt, s.lddt, s.at, s.ldat = dt.data_ptr(), dt.stride(0), at.data_ptr(), at.stride(0)
+    s.resid, s.ldr, s.gu, s.ldgu = resid.data_ptr(), resid.stride(0), gu.data_ptr(), gu.stride(0)
+    if p > 0:
+        assert bits is not None and bits.dtype == torch.int32 and bits.shape[0] == M and bits.shape[1] * 32 >= F
+        s.bits, s.ldbits = bits.data_ptr(), bits.stride(0)
+    s.p, s.dgu, s.lddgu, s.M, s.F = float(p), dgu.data_ptr(), dgu.stride(0), M, F
+    d = LoraSwigluBwdGradsDesc()
+    d.sw = s
+    d.tg, d.tu, d.ldtg = tg.data_ptr(), tu.data_ptr(), tg.stride(0)
+    d.dA_down, d.dB_gate, d.dB_up = dA_down.data_ptr(), dB_gate.data_ptr(), dB_up.data_ptr()
+    d.alpha_b, d.ws, d.ws_floats = float(alpha_b), ws.data_ptr(), ws.numel()
+    check(lib().slx_lora_swiglu_bwd_grads(ctypes.byref(d), stream_ptr()), "slx_lora_swiglu_bwd_grads")
+
+
 class SwigluLoraDownDesc(ctypes.Structure):
     _fields_ = [("gu", c_vp), ("ldgu", c_i64), ("act", c_vp), ("ldact", c_i64), ("A", c_vp), ("lda", c_i64),
                 ("bits", c_vp), ("ldbits", c_i64), ("p", c_float), ("t", c_vp), ("ldt", c_i64), ("ws", c_vp),

@@ -230,6 +230,49 @@ def test_lora_swiglu_bwd(dev, M, F, p):
     assert (diff <= dg2.float().abs() * 2 ** -7 + 1e-6).all(), diff.max().item()
 
 
+@pytest.mark.parametrize("M,F,p", [(6384, 4864, 0.1), (77, 256, 0.1), (300, 512, 0.0), (130, 384, 0.1)])
+def test_lora_swiglu_bwd_grads(dev, M, F, p):
+    """slx_lora_swiglu_bwd_grads: dgu bitwise equal to slx_lora_swiglu_bwd's; dA_down = dT^T drop(act) with act the
+    forward's activation (slx_swiglu_fwd, bit-exact) and dB_gate / dB_up = s dgu^T t against float64 products of the same
+    bf16 operands, accumulated onto non-zero gradients; two calls give bitwise-equal results (ordered partial sums)."""
+    from simlingo_amd.dropmask import keep_bits
+    g = torch.Generator(device=dev).manual_seed(53)
+    dtfull = (torch.randn(M, 64, device=dev, generator=g) * 0.5).bfloat16()
+    dtfull[:, 32:] = 0
+    A = (torch.randn(32, F, device=dev, generator=g) * 0.1).bfloat16()
+    AT = A.t().contiguous()
+    resid = torch.randn(M, F, device=dev, generator=g).bfloat16()
+    gu = torch.randn(M, 2 * F, device=dev, generator=g).bfloat16()
+    tx = (torch.randn(M, 80, device=dev, generator=g) * 0.3).bfloat16()  # t_gate | t_up at columns 8.., 40..
+    tg, tu = tx[:, 8:40], tx[:, 40:72]
+    bits = torch.from_numpy(keep_bits(77, M, F, F, p).view("int32")).to(dev) if p > 0 else None
+    s = 2.0
+    outs = []
+    for _ in range(2):
+        dgu = torch.empty(M, 2 * F, device=dev, dtype=torch.bfloat16)
+        dA = torch.full((32, F), 0.5, device=dev)
+        dBg, dBu = torch.full((F, 32), -0.25, device=dev), torch.full((F, 32), 0.125, device=dev)
+        K.lora_swiglu_bwd_grads(dtfull, AT, resid, gu, dgu, bits, p, tg, tu, dA, dBg, dBu, s)
+        outs.append((dgu, dA, dBg, dBu))
+    torch.cuda.synchronize()
+    for a_, b_ in zip(*outs):
+        assert torch.equal(a_, b_)
+    dgu, dA, dBg, dBu = outs[0]
+    if F % 256 == 0:
+        ref_dgu = torch.empty_like(dgu)
+        K.lora_swiglu_bwd(dtfull, AT, resid, gu, ref_dgu, bits, p)
+        assert torch.equal(dgu, ref_dgu)
+    act = torch.empty(M, F, device=dev, dtype=torch.bfloat16)
+    K.call("slx_swiglu_fwd", K.P(gu), 2 * F, K.P(act), F, M, F, K.stream_ptr())
+    mask = torch.from_numpy(keep_scale(77, M, F, F, p)).to(dev) if p > 0 else 1.0
+    xd = (act.float() * mask).bfloat16().double()
+    refA = 0.5 + dtfull[:, :32].double().t() @ xd
+    refG = -0.25 + s * dgu[:, :F].double().t() @ tg.double()
+    refU = 0.125 + s * dgu[:, F:].double().t() @ tu.double()
+    for got, ref in ((dA, refA), (dBg, refG), (dBu, refU)):
+        torch.testing.assert_close(got.double(), ref, atol=1e-4 * ref.abs().max().item(), rtol=1e-5)
+
+
 @pytest.mark.parametrize("M,F,p", [(6384, 4864, 0.1), (77, 256, 0.1), (300, 512, 0.0)])
 def test_swiglu_lora_down(dev, M, F, p):
     """slx_swiglu_lora_down (SwiGLU forward + the down site's LoRA down-projection in one pass) against the two launches
