@@ -747,6 +747,34 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t slice_rsrc(const void* base, l
                                            (int)(((long)(nrows > 0 ? nrows - 1 : 0) * ld + 64) * esize), 0x00020000);
 }
 
+// One LDS-DMA piece (buffer_load_dword[x4] ... lds; M0 = the wave-uniform LDS destination) issued by inline asm.
+// hipcc's wait-count pass cannot tell which LDS bytes a builtin LDS DMA writes, so it drained vmcnt(0) before the next
+// ds_read of any address: right after each loop trip issued the next tile, before the current tile's fragment reads,
+// so no DMA ever overlapped the MFMAs (and deeper rings could not help). Issued here, the pieces are ordered only by
+// the ring's own protocol (counted wait_vmcnt before the barrier that publishes a slot). Every LDS DMA of this file
+// goes through this helper, so hipcc keeps no value of its own in M0 (checked in the .s: M0 is written only here).
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+template <int BYTES>
+__device__ __forceinline__ void lds_dma(__amdgpu_buffer_rsrc_t rs, const char* lds, unsigned off) {
+  static_assert(BYTES == 16 || BYTES == 4, "dwordx4 or dword pieces");
+  const unsigned m = __builtin_amdgcn_readfirstlane(
+      (unsigned)(uintptr_t)(__attribute__((address_space(3))) const char*)lds);
+  if constexpr (BYTES == 16)
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(m), "v"(off), "s"(rs)
+                 : "memory", "m0");
+  else
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dword %1, %2, 0 offen lds" ::"s"(m), "v"(off), "s"(rs)
+                 : "memory", "m0");
+}
+#pragma clang diagnostic pop
+
+// vmcnt(0) through the intrinsic hipcc's wait-count pass understands (lgkmcnt / expcnt left at their maxima), placed
+// before a ring's first pieces: the loads issued before it (Q / dO fragments, lse) are then known complete at the tile
+// loop's header. Without it the pass re-waits for them inside the loop, and those counted waits (vmcnt(3) .. (0))
+// also wait for the asm-issued pieces in flight, which the hardware counter includes.
+__device__ __forceinline__ void drain_known_vm() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+
 // Wave w's two of the eight 1-KiB pieces of a 64-row x 64-column bf16 tile (rows row0 .. row0 + 63 of the slice)
 // into the sw_off image at lds: lane l of piece p carries row 8p + (l >> 3) into physical chunk l & 7, i.e. logical
 // (source) chunk (l & 7) ^ sw_xor(row) - the swizzle is applied on the source side. lane_off[i] = the lane's byte
@@ -766,8 +794,7 @@ __device__ __forceinline__ void dma_tile64(__amdgpu_buffer_rsrc_t rs, char* lds,
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const unsigned off = lane_row[i] < lim ? (unsigned)(tile_off + lane_off[i]) : kAttnSent;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(lds + (2 * w + i) * 1024), 16,
-                                             off, 0, 0, 0);
+    lds_dma<16>(rs, lds + (2 * w + i) * 1024, off);
   }
 }
 
@@ -775,7 +802,7 @@ __device__ __forceinline__ void dma_tile64(__amdgpu_buffer_rsrc_t rs, char* lds,
 __device__ __forceinline__ void dma_row64_f32(__amdgpu_buffer_rsrc_t rs, char* lds, int i0, int n, int lane) {
   const int i = i0 + lane;
   const unsigned off = i < n ? (unsigned)(i * 4) : kAttnSent;
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)lds, 4, off, 0, 0, 0);
+  lds_dma<4>(rs, lds, off);
 }
 
 // ---- short tails on the VALU (non-causal; InternViT: T = 1025 = 16 * 64 + 1) ----------------------------------
@@ -824,7 +851,9 @@ __device__ __forceinline__ void tail_axpy(const bf16* row, float w, f32x16& acc0
 }
 
 #ifndef ATTN_NSLOT
+#ifndef ATTN_NSLOT
 #define ATTN_NSLOT 2  // one tile ahead: fastest of 2 / 3 / 4 slots on both shapes (profiles/round4_attn_dma_ab.txt)
+#endif
 #endif
 
 // forward: attn_fwd_kernel with the K/V tiles of the (b, kv-head) streamed through an NSLOT ring (16 KiB per slot)
@@ -880,6 +909,7 @@ __global__ __launch_bounds__(256, ATTN_FWD_OCC) void attn_fwd_dma_kernel(AttnArg
 #pragma unroll
   for (int r = 0; r < 16; ++r) { o0[r] = 0.f; o1[r] = 0.f; lacc[r] = 0.f; }
   float m = -1e30f;
+  drain_known_vm();
 #pragma unroll
   for (int j = 0; j < NS - 1; ++j) issue(j);
   for (int t = 0; t < nt; ++t) {
@@ -995,6 +1025,7 @@ __global__ __launch_bounds__(256, ATTN_DQ_OCC) void attn_bwd_dq_dma_kernel(AttnA
   f32x16 dq0, dq1;
 #pragma unroll
   for (int r = 0; r < 16; ++r) { dq0[r] = 0.f; dq1[r] = 0.f; }
+  drain_known_vm();
 #pragma unroll
   for (int j = 0; j < NS - 1; ++j) issue(j);
   for (int t = 0; t < nt; ++t) {
@@ -1185,6 +1216,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dq_pp_kernel(AttnArgs a) {
   bf16x8 dsb[2][2];
 #pragma unroll
   for (int r = 0; r < 16; ++r) { dq0[r] = 0.f; dq1[r] = 0.f; }
+  drain_known_vm();
 #pragma unroll
   for (int j = 0; j < D; ++j) issue(j);
   // phases: group g's tile j (key tile 2j + g) has its MFMA phase at ph = 2j + g + 2j... (local phase 2j), its VALU
@@ -1370,6 +1402,7 @@ __global__ __launch_bounds__(256, ATTN_KV_OCC) void attn_bwd_kv_dma_kernel(AttnA
   };
 
 
+  drain_known_vm();
 #pragma unroll
   for (int j = 0; j < NS - 1; ++j) issue(j);
   int cc = 0;  // chunk index of stage `it` (it % nch, advanced incrementally)
@@ -1517,6 +1550,7 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_pp_kernel(AttnArgs a) {
   for (int j = 0; j < 8; ++j) ones[j] = (bf16)1.0f;
   bool prev_on = false;
   int prev_t = 0;
+  drain_known_vm();
 #pragma unroll
   for (int j = 0; j < D; ++j) issue(j);
   const int nph = max(2 * ((nt + 1) / 2) + 1, 2 * (nt / 2) + 2);
@@ -1724,6 +1758,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_kv_pp_kernel(AttnArgs a) {
   f32x16 spa[2], dpa[2];
   int prev_qc = 0;
   bool prev_on = false;
+  drain_known_vm();
 #pragma unroll
   for (int j = 0; j < D; ++j) issue(j);
   const int nph = max(2 * ((nit + 1) / 2) + 1, 2 * (nit / 2) + 2);
