@@ -1075,10 +1075,9 @@ __global__ __launch_bounds__(BMv * 2, 1) void gemm_bf16_dma_kernel(GemmArgs p) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) ep[(i * 16 + (lane >> 4) * 4 + r) * EP_LD + j * 16 + (lane & 15)] = acc[i][j][r];
   __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS writes done (wave-private region)
-  if constexpr (EPI == EPI_DROPMASK_SWIGLU || EPI == EPI_DROPMASK_SWIGLU_B || EPI == EPI_SWIGLU_BWD)
-    epilogue_tile64_pf<EPI, OutT>(p, C, ep, lane, m0 + wm * 64, n0 + wn * 64);  // HBM-bound K = 64 SwiGLU' GEMMs
-  else
-    epilogue_tile64<EPI, OutT>(p, C, ep, lane, m0 + wm * 64, n0 + wn * 64);
+  // the batched-load epilogue for every kind (it falls back to epilogue_tile64 for partial column tiles): the Qwen2
+  // o / down residual GEMMs' per-row load round trips were the tail of their single round
+  epilogue_tile64_pf<EPI, OutT>(p, C, ep, lane, m0 + wm * 64, n0 + wn * 64);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1652,8 +1651,9 @@ __device__ __forceinline__ void v3_tile(const GemmArgs& p, int bid, long z, char
           for (int r = 0; r < 4; ++r) ep[(i * 16 + (lane >> 4) * 4 + r) * EP_LD + j * 16 + (lane & 15)] = acc[4 * mh + i][j][r];
     }
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): wave-private region written
-    if constexpr (SW) epilogue_tile64_pf<EPI, OutT>(p, C, ep, lane, m0 + arow + 64 * mh, n0 + bcol, reduced);
-    else epilogue_tile64<EPI, OutT>(p, C, ep, lane, m0 + arow + 64 * mh, n0 + bcol, reduced);
+    // the staged image is row-major in both layouts, so the batched-load epilogue serves SW = false too (InternViT
+    // proj / fc2 residual GEMMs: +0.35 % on the step, profiles/round5_gemm_pf_epilogue_ab.txt)
+    epilogue_tile64_pf<EPI, OutT>(p, C, ep, lane, m0 + arow + 64 * mh, n0 + bcol, reduced);
     __builtin_amdgcn_s_waitcnt(0xC07F);
   }
 }
