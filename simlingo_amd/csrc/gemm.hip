@@ -971,6 +971,22 @@ __device__ __forceinline__ void epilogue_tile64_pf(const GemmArgs& p, OutT* __re
   epilogue_tile64<EPI, OutT>(p, C, ep, lane, m_base, n_base, reduced);
 }
 
+// The staged-tile epilogue of the v2 / v3 kernels: the batched-load form where the epilogue reads global data per row
+// (residual, aux, an accumulated C), the row loop where it reads none (plain STORE, GELU: through the batched form the
+// Qwen2 down / gate-up data-gradient GEMMs ran 4-15 % slower, profiles/round5_gemm_pf_epilogue_ab.txt)
+template <int EPI, typename OutT>
+__device__ __forceinline__ void epilogue_tile64_auto(const GemmArgs& p, OutT* __restrict__ C, const float* ep, int lane,
+                                                     int m_base, int n_base, bool reduced = false) {
+  if constexpr (EPI == EPI_GELU || EPI == EPI_QGELU) {
+    epilogue_tile64<EPI, OutT>(p, C, ep, lane, m_base, n_base, reduced);
+  } else if constexpr (EPI == EPI_STORE) {
+    if (p.accumulate) epilogue_tile64_pf<EPI, OutT>(p, C, ep, lane, m_base, n_base, reduced);
+    else epilogue_tile64<EPI, OutT>(p, C, ep, lane, m_base, n_base, reduced);
+  } else {
+    epilogue_tile64_pf<EPI, OutT>(p, C, ep, lane, m_base, n_base, reduced);
+  }
+}
+
 template <bool AK, bool BKc, int EPI, typename OutT, int BMv, int NS>
 __global__ __launch_bounds__(BMv * 2, 1) void gemm_bf16_dma_kernel(GemmArgs p) {
   constexpr int NW = BMv / 32;                 // waves: (BM/64) x 2
@@ -1075,9 +1091,9 @@ __global__ __launch_bounds__(BMv * 2, 1) void gemm_bf16_dma_kernel(GemmArgs p) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) ep[(i * 16 + (lane >> 4) * 4 + r) * EP_LD + j * 16 + (lane & 15)] = acc[i][j][r];
   __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS writes done (wave-private region)
-  // the batched-load epilogue for every kind (it falls back to epilogue_tile64 for partial column tiles): the Qwen2
-  // o / down residual GEMMs' per-row load round trips were the tail of their single round
-  epilogue_tile64_pf<EPI, OutT>(p, C, ep, lane, m0 + wm * 64, n0 + wn * 64);
+  // the batched-load epilogue where the epilogue reads global data (the Qwen2 o / down residual GEMMs' per-row load
+  // round trips were the tail of their single round)
+  epilogue_tile64_auto<EPI, OutT>(p, C, ep, lane, m0 + wm * 64, n0 + wn * 64);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1653,7 +1669,8 @@ __device__ __forceinline__ void v3_tile(const GemmArgs& p, int bid, long z, char
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): wave-private region written
     // the staged image is row-major in both layouts, so the batched-load epilogue serves SW = false too (InternViT
     // proj / fc2 residual GEMMs: +0.35 % on the step, profiles/round5_gemm_pf_epilogue_ab.txt)
-    epilogue_tile64_pf<EPI, OutT>(p, C, ep, lane, m0 + arow + 64 * mh, n0 + bcol, reduced);
+    if constexpr (SW) epilogue_tile64_pf<EPI, OutT>(p, C, ep, lane, m0 + arow + 64 * mh, n0 + bcol, reduced);
+    else epilogue_tile64_auto<EPI, OutT>(p, C, ep, lane, m0 + arow + 64 * mh, n0 + bcol, reduced);
     __builtin_amdgcn_s_waitcnt(0xC07F);
   }
 }
