@@ -971,20 +971,18 @@ __device__ __forceinline__ void epilogue_tile64_pf(const GemmArgs& p, OutT* __re
   epilogue_tile64<EPI, OutT>(p, C, ep, lane, m_base, n_base, reduced);
 }
 
-// The staged-tile epilogue of the v2 / v3 kernels: the batched-load form where the epilogue reads global data per row
-// (residual, aux, an accumulated C), the row loop where it reads none (plain STORE, GELU: through the batched form the
-// Qwen2 down / gate-up data-gradient GEMMs ran 4-15 % slower, profiles/round5_gemm_pf_epilogue_ab.txt)
+// The staged-tile epilogue of the v2 / v3 kernels: the batched-load form for the residual and SwiGLU' kinds (their
+// per-row load round trips were the tail of the single-round residual GEMMs: +0.35 % on the VLA step), the row loop for
+// the others. Through the batched form the Qwen2 down / gate-up data-gradient GEMMs (plain STORE) ran 4-15 % slower and
+// SimLingo-Base's accumulating f32 weight-gradient GEMMs 22 % slower (profiles/round5_gemm_pf_epilogue_ab.txt).
 template <int EPI, typename OutT>
 __device__ __forceinline__ void epilogue_tile64_auto(const GemmArgs& p, OutT* __restrict__ C, const float* ep, int lane,
                                                      int m_base, int n_base, bool reduced = false) {
-  if constexpr (EPI == EPI_GELU || EPI == EPI_QGELU) {
-    epilogue_tile64<EPI, OutT>(p, C, ep, lane, m_base, n_base, reduced);
-  } else if constexpr (EPI == EPI_STORE) {
-    if (p.accumulate) epilogue_tile64_pf<EPI, OutT>(p, C, ep, lane, m_base, n_base, reduced);
-    else epilogue_tile64<EPI, OutT>(p, C, ep, lane, m_base, n_base, reduced);
-  } else {
+  if constexpr (EPI == EPI_RESID_LS || EPI == EPI_SWIGLU_BWD || EPI == EPI_DROPMASK_SWIGLU ||
+                EPI == EPI_DROPMASK_SWIGLU_B)
     epilogue_tile64_pf<EPI, OutT>(p, C, ep, lane, m_base, n_base, reduced);
-  }
+  else
+    epilogue_tile64<EPI, OutT>(p, C, ep, lane, m_base, n_base, reduced);
 }
 
 template <bool AK, bool BKc, int EPI, typename OutT, int BMv, int NS>
