@@ -618,6 +618,17 @@ __device__ __forceinline__ void bwd_dq_tile_ser(const char* Kl, const char* Vl, 
 #define ATTN_DQ_SER 0
 #endif
 
+// The RoPE table entries of a lane's 16 dQ dims (d = 8 g + 4 hl + e, as float4 per g), issued together: read per
+// element inside `if (a.rcos)`, each load was drained (vmcnt(0)) before the next, 16 round trips per dQ store
+__device__ __forceinline__ void rope_lane_tables(const float* rcos, const float* rsin, long qi, int hl, float4 (&cs)[4],
+                                                 float4 (&sn)[4]) {
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    cs[g] = *reinterpret_cast<const float4*>(rcos + qi * 32 + 8 * g + 4 * hl);
+    sn[g] = *reinterpret_cast<const float4*>(rsin + qi * 32 + 8 * g + 4 * hl);
+  }
+}
+
 __global__ __launch_bounds__(256, ATTN_DQ_OCC) void attn_bwd_dq_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) char smem[2 * 2 * 8192];
   const BlockCoord bc = attn_block((a.S + 127) / 128, a.Hq, a.Hkv, a.B, a.causal ? 1 : 0, a.tail_first);
@@ -699,6 +710,8 @@ __global__ __launch_bounds__(256, ATTN_DQ_OCC) void attn_bwd_dq_kernel(AttnArgs 
   // rotation and the bf16 store need no exchange (no f32 workspace, no finalize launch)
   const long qi = qvalid ? myq : 0;  // rows past S (no store) index row 0 of dq and of the RoPE tables
   bf16* qrow = a.dq + ((long)b * S + qi) * a.lddq + h * 64;
+  float4 rtc[4], rts[4];
+  if (a.rcos) rope_lane_tables(a.rcos, a.rsin, qi, hl, rtc, rts);
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
     const int d = 8 * g + 4 * hl;
@@ -707,7 +720,7 @@ __global__ __launch_bounds__(256, ATTN_DQ_OCC) void attn_bwd_dq_kernel(AttnArgs 
     for (int e = 0; e < 4; ++e) {
       float x0 = dq0[4 * g + e] * a.scale, x1 = dq1[4 * g + e] * a.scale;
       if (a.rcos) {
-        const float cs = a.rcos[qi * 32 + d + e], sn = a.rsin[qi * 32 + d + e];
+        const float cs = reinterpret_cast<const float*>(&rtc[g])[e], sn = reinterpret_cast<const float*>(&rts[g])[e];
         const float y0 = x0 * cs + x1 * sn, y1 = x1 * cs - x0 * sn;  // RoPE^T (rope_pair, inverse)
         x0 = y0;
         x1 = y1;
@@ -1060,6 +1073,8 @@ __global__ __launch_bounds__(256, ATTN_DQ_OCC) void attn_bwd_dq_dma_kernel(AttnA
   float c0[16], c1[16];
   const long qi = qvalid ? myq : 0;
   bf16* qrow = a.dq + ((long)b * S + qi) * a.lddq + h * 64;
+  float4 rtc[4], rts[4];
+  if (a.rcos) rope_lane_tables(a.rcos, a.rsin, qi, hl, rtc, rts);
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
     const int d = 8 * g + 4 * hl;
@@ -1068,7 +1083,7 @@ __global__ __launch_bounds__(256, ATTN_DQ_OCC) void attn_bwd_dq_dma_kernel(AttnA
     for (int e = 0; e < 4; ++e) {
       float x0 = dq0[4 * g + e] * a.scale, x1 = dq1[4 * g + e] * a.scale;
       if (a.rcos) {
-        const float cs = a.rcos[qi * 32 + d + e], sn = a.rsin[qi * 32 + d + e];
+        const float cs = reinterpret_cast<const float*>(&rtc[g])[e], sn = reinterpret_cast<const float*>(&rts[g])[e];
         const float y0 = x0 * cs + x1 * sn, y1 = x1 * cs - x0 * sn;
         x0 = y0;
         x1 = y1;
@@ -1272,6 +1287,8 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dq_pp_kernel(AttnArgs a) {
     }
     const long qi = qvalid ? myq : 0;
     bf16* qrow = a.dq + ((long)b * S + qi) * a.lddq + h * 64;
+    float4 rtc[4], rts[4];
+    if (a.rcos) rope_lane_tables(a.rcos, a.rsin, qi, hl, rtc, rts);
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       const int d = 8 * g + 4 * hl;
@@ -1280,7 +1297,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dq_pp_kernel(AttnArgs a) {
       for (int e = 0; e < 4; ++e) {
         float x0 = dq0[4 * g + e] * a.scale, x1 = dq1[4 * g + e] * a.scale;
         if (a.rcos) {
-          const float cs = a.rcos[qi * 32 + d + e], sn = a.rsin[qi * 32 + d + e];
+          const float cs = reinterpret_cast<const float*>(&rtc[g])[e], sn = reinterpret_cast<const float*>(&rts[g])[e];
           const float y0 = x0 * cs + x1 * sn, y1 = x1 * cs - x0 * sn;
           x0 = y0;
           x1 = y1;
