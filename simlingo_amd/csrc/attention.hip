@@ -1941,7 +1941,17 @@ struct RopeArgs {
   int nsplit; long split_stride;     // f32 source: sum of nsplit partials split_stride floats apart
 };
 
-// One thread per (token, head, i<32 pair-group of 4): 8 pairs per thread -> 256 threads per row
+// One thread per (token, head, i<32 pair-group of 4): 8 pairs per thread -> 256 threads per row. The table entries and
+// the f32 partials are read as float4 groups, all issued before use (a table read per element inside `if (r.cos)` was
+// drained before the next: 16 round trips); same sums in the same order
+__device__ __forceinline__ void set8(float (&v)[8], const float* p) {
+  const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+__device__ __forceinline__ void add8(float (&v)[8], const float* p) {
+  const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+  v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w; v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
+}
 __device__ __forceinline__ void rope_rows(const RopeArgs& r) {
   const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const long total = (long)r.ntok * r.nheads * 4;
@@ -1953,15 +1963,23 @@ __device__ __forceinline__ void rope_rows(const RopeArgs& r) {
   const int pos = tok % r.S;
   bf16* x = r.x + tok * r.ldx + hh * 64;
   const int i0 = part * 8;
+  float cs[8], sn[8];
+  if (r.cos) {
+    const float* c = r.cos + (long)pos * 32 + i0;
+    const float* q = r.sin + (long)pos * 32 + i0;
+    const float4 c0 = *reinterpret_cast<const float4*>(c), c1 = *reinterpret_cast<const float4*>(c + 4);
+    const float4 s0 = *reinterpret_cast<const float4*>(q), s1 = *reinterpret_cast<const float4*>(q + 4);
+    cs[0] = c0.x; cs[1] = c0.y; cs[2] = c0.z; cs[3] = c0.w; cs[4] = c1.x; cs[5] = c1.y; cs[6] = c1.z; cs[7] = c1.w;
+    sn[0] = s0.x; sn[1] = s0.y; sn[2] = s0.z; sn[3] = s0.w; sn[4] = s1.x; sn[5] = s1.y; sn[6] = s1.z; sn[7] = s1.w;
+  }
   float v0[8], v1[8];
   if (r.src_f32) {
     const float* s = r.src_f32 + tok * r.ldsrc + hh * 64;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) { v0[j] = s[i0 + j]; v1[j] = s[32 + i0 + j]; }
+    set8(v0, s + i0);
+    set8(v1, s + 32 + i0);
     for (int p = 1; p < r.nsplit; ++p) {
-      const float* t = s + p * r.split_stride;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) { v0[j] += t[i0 + j]; v1[j] += t[32 + i0 + j]; }
+      add8(v0, s + p * r.split_stride + i0);
+      add8(v1, s + p * r.split_stride + 32 + i0);
     }
   } else {
     const bf16x8 a = *reinterpret_cast<const bf16x8*>(x + i0);
@@ -1972,7 +1990,7 @@ __device__ __forceinline__ void rope_rows(const RopeArgs& r) {
   bf16x8 oa, ob;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    if (r.cos) rope_pair(v0[j], v1[j], r.cos[(long)pos * 32 + i0 + j], r.sin[(long)pos * 32 + i0 + j], r.inverse != 0);
+    if (r.cos) rope_pair(v0[j], v1[j], cs[j], sn[j], r.inverse != 0);
     oa[j] = (bf16)v0[j];
     ob[j] = (bf16)v1[j];
   }

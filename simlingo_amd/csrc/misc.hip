@@ -95,32 +95,46 @@ __global__ __launch_bounds__(256) void colsum_kernel(const void* xv, long ldx, l
 #pragma unroll
     for (int e = 0; e < 4; ++e) lsv[e] = ls[c0 + e];
   }
-#pragma unroll 4
-  for (long r = blockIdx.x; live && r < M; r += gridDim.x) {  // unrolled: 4 rows of loads in flight per thread
-    float v[4];
-    if (MODE == 0) {
-      const bf16x4 t = *reinterpret_cast<const bf16x4*>((const bf16*)xv + r * ldx + c0);
+  // 4 rows per trip, every load unconditional (rows past M read row M - 1 and are not summed; a missing y reads x's
+  // bytes and is not used): a load behind `r < M` or `if (y)` made hipcc drain vmcnt(0) before the next row
+  const long G = gridDim.x;
+  const bf16* yb = y ? y : reinterpret_cast<const bf16*>(xv);
+  const long ldyb = y ? ldy : (MODE == 0 ? ldx : 2 * ldx);
+  const int cl = live ? c0 : 0;
+  for (long r0 = blockIdx.x; r0 < M; r0 += 4 * G) {
+    float v[4][4];
+    bf16x4 yy[4];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = (float)t[e];
-    } else {
-      const float4 t = *reinterpret_cast<const float4*>((const float*)xv + r * ldx + c0);
-      v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
-    }
-    if (MODE == 2) {
-      bf16x4 yy;
-      if (y) yy = *reinterpret_cast<const bf16x4*>(y + r * ldy + c0);
-      bf16x4 go;
+    for (int k = 0; k < 4; ++k) {
+      const long r = min(r0 + k * G, M - 1);
+      if (MODE == 0) {
+        const bf16x4 t = *reinterpret_cast<const bf16x4*>((const bf16*)xv + r * ldx + cl);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        if (y) s2[e] += v[e] * (float)yy[e];
-        const float gv = v[e] * lsv[e];
-        go[e] = (bf16)gv;
-        s[e] += gv;
+        for (int e = 0; e < 4; ++e) v[k][e] = (float)t[e];
+      } else {
+        const float4 t = *reinterpret_cast<const float4*>((const float*)xv + r * ldx + cl);
+        v[k][0] = t.x; v[k][1] = t.y; v[k][2] = t.z; v[k][3] = t.w;
       }
-      *reinterpret_cast<bf16x4*>(g + r * ldg + c0) = go;
-    } else {
+      if (MODE == 2) yy[k] = *reinterpret_cast<const bf16x4*>(yb + r * ldyb + cl);
+    }
 #pragma unroll
-      for (int e = 0; e < 4; ++e) s[e] += v[e];
+    for (int k = 0; k < 4; ++k) {
+      const long r = r0 + k * G;
+      if (!live || r >= M) continue;
+      if (MODE == 2) {
+        bf16x4 go;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          if (y) s2[e] += v[k][e] * (float)yy[k][e];
+          const float gv = v[k][e] * lsv[e];
+          go[e] = (bf16)gv;
+          s[e] += gv;
+        }
+        *reinterpret_cast<bf16x4*>(g + r * ldg + c0) = go;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) s[e] += v[k][e];
+      }
     }
   }
   // transpose through LDS: each atomic wave-instruction then covers 256 contiguous bytes
