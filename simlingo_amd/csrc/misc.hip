@@ -434,7 +434,33 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* p, const GT* g, float
 
 // The same update four parameters per lane (16-B loads and stores of p / g / m / v, 8-B bf16 stores): n4 quads from
 // 16-B aligned p / g / m / v and an 8-B aligned pbf; the launcher runs the scalar kernel on the tail.
-template <typename GT>
+typedef float f32x4nt __attribute__((ext_vector_type(4)));
+// NT: p / m / v (and an f32 g) streamed with nontemporal loads and stores (each touched once per step; SLX_ADAMW_NT)
+template <bool NT>
+__device__ __forceinline__ float4 ld4(const float4* q) {
+  if constexpr (NT) {
+    const f32x4nt t = __builtin_nontemporal_load(reinterpret_cast<const f32x4nt*>(q));
+    return make_float4(t[0], t[1], t[2], t[3]);
+  } else {
+    return *q;
+  }
+}
+template <bool NT>
+__device__ __forceinline__ void st4(float4* q, float a, float b, float c, float d) {
+  if constexpr (NT) {
+    const f32x4nt t = {a, b, c, d};
+    __builtin_nontemporal_store(t, reinterpret_cast<f32x4nt*>(q));
+  } else {
+    *q = {a, b, c, d};
+  }
+}
+template <typename GT, bool NT>
+__device__ __forceinline__ float4 load_g4n(const GT* g, long i) {
+  if constexpr (sizeof(GT) == 4) return ld4<NT>(reinterpret_cast<const float4*>(g) + i);
+  else return load_g4(g, i);
+}
+
+template <typename GT, bool NT>
 __global__ __launch_bounds__(256) void adamw_kernel_x4(float4* p, const GT* g, float4* m, float4* v, bf16x4* pbf,
                                                      long n4, float lr, float b1, float b2, float eps, float wd, float bc1,
                                                      float bc2s, const float* sumsq, float max_norm, float gscale) {
@@ -445,7 +471,7 @@ __global__ __launch_bounds__(256) void adamw_kernel_x4(float4* p, const GT* g, f
   }
   const float step = lr / bc1;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
-    const float4 g4 = load_g4(g, i), p4 = p[i], m4 = m[i], v4 = v[i];
+    const float4 g4 = load_g4n<GT, NT>(g, i), p4 = ld4<NT>(p + i), m4 = ld4<NT>(m + i), v4 = ld4<NT>(v + i);
     float gi[4] = {g4.x, g4.y, g4.z, g4.w}, pi[4] = {p4.x, p4.y, p4.z, p4.w};
     float mi[4] = {m4.x, m4.y, m4.z, m4.w}, vi[4] = {v4.x, v4.y, v4.z, v4.w};
 #pragma unroll
@@ -457,9 +483,9 @@ __global__ __launch_bounds__(256) void adamw_kernel_x4(float4* p, const GT* g, f
       const float den = sqrtf(vi[j]) / bc2s + eps;
       pi[j] -= step * mi[j] / den;
     }
-    p[i] = {pi[0], pi[1], pi[2], pi[3]};
-    m[i] = {mi[0], mi[1], mi[2], mi[3]};
-    v[i] = {vi[0], vi[1], vi[2], vi[3]};
+    st4<NT>(p + i, pi[0], pi[1], pi[2], pi[3]);
+    st4<NT>(m + i, mi[0], mi[1], mi[2], mi[3]);
+    st4<NT>(v + i, vi[0], vi[1], vi[2], vi[3]);
     if (pbf) pbf[i] = {(bf16)pi[0], (bf16)pi[1], (bf16)pi[2], (bf16)pi[3]};
   }
 }
@@ -906,9 +932,17 @@ static int adamw_impl(float* p, const GT* g, float* m, float* v, void* p_bf16, i
     long blocks = (n4 + 255) / 256;
     if (cap > 0 && blocks > cap) blocks = cap;
     if (blocks > 0x7fffffffL) blocks = 0x7fffffffL;
-    hipLaunchKernelGGL(adamw_kernel_x4<GT>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)s, (float4*)p, g,
-                       (float4*)m, (float4*)v, (bf16x4*)p_bf16, n4, lr, beta1, beta2, eps, weight_decay, bc1, bc2s, sumsq,
-                       max_norm, grad_scale);
+    // nontemporal p / m / v streams (SLX_ADAMW_NT, default 1): 1675 vs 1733 us at 315M parameters
+    // (tools/adamw_bench.py, profiles/round5_adamw_nt_ab.txt), the same arithmetic
+    static const bool nt = [] { const char* e = getenv("SLX_ADAMW_NT"); return !e || atoi(e) != 0; }();
+    if (nt)
+      hipLaunchKernelGGL((adamw_kernel_x4<GT, true>), dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)s, (float4*)p,
+                         g, (float4*)m, (float4*)v, (bf16x4*)p_bf16, n4, lr, beta1, beta2, eps, weight_decay, bc1, bc2s,
+                         sumsq, max_norm, grad_scale);
+    else
+      hipLaunchKernelGGL((adamw_kernel_x4<GT, false>), dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)s, (float4*)p,
+                         g, (float4*)m, (float4*)v, (bf16x4*)p_bf16, n4, lr, beta1, beta2, eps, weight_decay, bc1, bc2s,
+                         sumsq, max_norm, grad_scale);
     SLX_LAUNCH_CHECK("slx_adamw");
     done = n4 * 4;
   }
