@@ -185,6 +185,21 @@ __global__ __launch_bounds__(256) void norm_fwd_wave_kernel(NormArgs a) {
   }
 }
 
+// read-once streams of the LayerNorm backward (x, dy, the accumulated dx input, the layer-scale branch rows) as
+// nontemporal loads: +0.2 % on the step (the next GEMM's operands are not evicted by them), although the isolated
+// microbenchmark, which re-reads the same MALL-resident buffers every call, runs 7-13 % slower
+// (profiles/round5_norm_bwd_nt_ab.txt)
+typedef float nt_f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned nt_u32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ float4 ldnt_f4(const float* p) {
+  const nt_f32x4 t = __builtin_nontemporal_load(reinterpret_cast<const nt_f32x4*>(p));
+  return make_float4(t[0], t[1], t[2], t[3]);
+}
+__device__ __forceinline__ bf16x4 ldnt_b4(const bf16* p) {
+  const nt_u32x2 t = __builtin_nontemporal_load(reinterpret_cast<const nt_u32x2*>(p));
+  return __builtin_bit_cast(bf16x4, t);
+}
+
 template <bool RMS, bool LS, bool DYB>
 __global__ __launch_bounds__(256) void norm_bwd_wave_kernel(NormArgs a) {
   // column sums (dgamma, dbeta; dls, dbias of the layer-scale branch) accumulate in wave-private LDS rows: each lane
@@ -238,13 +253,18 @@ __global__ __launch_bounds__(256) void norm_bwd_wave_kernel(NormArgs a) {
         if (a.dx_accumulate) {
           const float* dsrc = a.ps ? a.dx + ps_src_row(row, col / a.C, a.G, a.tok_per_img) * a.lddx + (col % a.C)
                                    : a.dx + row * a.lddx + col;
-          r.dxo[i] = *reinterpret_cast<const float4*>(dsrc);
+          r.dxo[i] = ldnt_f4(dsrc);
         }
-        if constexpr (LS) r.lyv[i] = *reinterpret_cast<const bf16x4*>(a.lsy + row * a.ldlsy + col);
+        if constexpr (LS) r.lyv[i] = ldnt_b4(a.lsy + row * a.ldlsy + col);
         const float* src = a.ps ? a.x + ps_src_row(row, col / a.C, a.G, a.tok_per_img) * a.ldx + (col % a.C)
                                 : a.x + row * a.ldx + col;
-        r.t[i] = *reinterpret_cast<const float4*>(src);
-        r.d[i] = load_dy4<DYB ? 1 : 0>(a, row, col);
+        r.t[i] = ldnt_f4(src);
+        if constexpr (DYB) {
+          const bf16x4 b = ldnt_b4(reinterpret_cast<const bf16*>(a.dy) + row * a.lddy + col);
+          r.d[i] = make_float4((float)b[0], (float)b[1], (float)b[2], (float)b[3]);
+        } else {
+          r.d[i] = ldnt_f4(a.dy + row * a.lddy + col);
+        }
       }
     }
   };
