@@ -18,7 +18,10 @@ for src in "$ROOT"/simlingo_amd/csrc/*.hip; do
   o="$OUT/$(basename "${src%.hip}").o"
   objs+=("$o")
   if [ ! -f "$o" ] || [ "$src" -nt "$o" ]; then
-    "$CLANG" "${FL[@]}" -c "$src" -o "$o" &
+    # attention.hip issues its LDS DMA by inline asm with SGPR ("s") operands, which device -O0 cannot allocate
+    extra=()
+    [ "$(basename "$src")" = "attention.hip" ] && extra=(-Xarch_device -O1)
+    "$CLANG" "${FL[@]}" "${extra[@]}" -c "$src" -o "$o" &
     pids+=($!)
   fi
 done
