@@ -387,7 +387,7 @@ __global__ __launch_bounds__(256) void norm_bwd_row_kernel(NormArgs a) {
       if (col < a.D && a.dx_accumulate) {
         const float* dsrc = a.ps ? a.dx + ps_src_row(row, col / a.C, a.G, a.tok_per_img) * a.lddx + (col % a.C)
                                  : a.dx + row * a.lddx + col;
-        dxo[i] = *reinterpret_cast<const float4*>(dsrc);
+        dxo[i] = ldnt_f4(dsrc);
       }
       if constexpr (LS) {
         if (col < a.D) lyv[i] = *reinterpret_cast<const bf16x4*>(a.lsy + row * a.ldlsy + col);
@@ -400,8 +400,13 @@ __global__ __launch_bounds__(256) void norm_bwd_row_kernel(NormArgs a) {
       if (col < a.D) {
         const float* src = a.ps ? a.x + ps_src_row(row, col / a.C, a.G, a.tok_per_img) * a.ldx + (col % a.C)
                                 : a.x + row * a.ldx + col;
-        t = *reinterpret_cast<const float4*>(src);
-        d = load_dy4<DYB ? 1 : 0>(a, row, col);
+        t = ldnt_f4(src);
+        if constexpr (DYB) {
+          const bf16x4 b = ldnt_b4(reinterpret_cast<const bf16*>(a.dy) + row * a.lddy + col);
+          d = make_float4((float)b[0], (float)b[1], (float)b[2], (float)b[3]);
+        } else {
+          d = ldnt_f4(a.dy + row * a.lddy + col);
+        }
         g = *reinterpret_cast<const float4*>(a.gamma + col);
       }
       const float tv[4] = {t.x, t.y, t.z, t.w}, dv[4] = {d.x, d.y, d.z, d.w}, gv[4] = {g.x, g.y, g.z, g.w};
