@@ -57,8 +57,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--wire", default="auto", choices=["auto", "f32", "bf16"],
-                    help="gradient all-reduce wire dtype (bf16: half the xGMI bytes, f32 accumulation kept; "
-                         "auto = bf16 at N > 1, SURVEY.md §8e)")
+                    help="gradient all-reduce wire dtype (auto = f32: the exchange is exact to f32 summation order, "
+                         "stricter than the reference's fp16 ZeRO-2 reduce; bf16: half the xGMI bytes, opt-in)")
     ap.add_argument("--no-dropin", action="store_true", help="skip the drop-in loop key (DataLoader + Collate + "
                     "DrivingModel.training_step + FusedAdamW + OneCycleLR)")
     ap.add_argument("--no-extras", action="store_true",
@@ -400,7 +400,7 @@ def main():
         else:
             dist.init_process_group(backend)
     dev = torch.device("cuda", local)
-    args.wire_eff = ("bf16" if world > 1 else "f32") if args.wire == "auto" else args.wire
+    args.wire_eff = "f32" if args.wire == "auto" else args.wire
     w = (setup_base if args.config.startswith("base") else setup_vla)(args, dev, world, rank)
     eng, step, B = w["eng"], w["step"], w["B"]
     if world > 1:
@@ -485,6 +485,7 @@ def main():
             res["roofline_fc1"] = fc1
     if world > 1:
         res["dist_backend"] = "rccl" if backend == "nccl" else backend
+        res["grad_wire"] = args.wire_eff
         cs = eng.bucketer.comm_summary()
         if cs:
             res["comm_exposed_ms"] = cs.pop("comm_exposed_ms")

@@ -250,3 +250,16 @@ class BaseFusedAdamW(torch.optim.Optimizer):
     def zero_grad(self, set_to_none: bool = True):
         # gradients are overwritten by every backward (no accumulation across steps)
         self.model.anchor.grad = None
+
+    def _names(self):
+        return {sp.name: (sp.ref, tuple(sp.shape)) for sp in self.model.build_engine().specs}
+
+    def state_dict(self):
+        """The four groups' AdamW moments and step keyed by the reference's state-dict names (simlingo_amd.optstate),
+        for Lightning's ckpt_path resume."""
+        from .optstate import export_state
+        return export_state(self, self.model.engine, self._names())
+
+    def load_state_dict(self, state_dict):
+        from .optstate import import_state
+        import_state(self, self.model.build_engine(), self._names(), state_dict)

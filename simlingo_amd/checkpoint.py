@@ -104,6 +104,44 @@ def to_reference(P: dict, cfg: VLAConfig, aliases: bool = True) -> "OrderedDict[
     return sd
 
 
+def trainable_ref_keys(cfg: VLAConfig) -> "OrderedDict[str, tuple[str, tuple]]":
+    """{internal trainable name: (reference state-dict key, reference shape)} — the keys to_reference gives each
+    trainable tensor (its class / position / patch / query reshapes included). Optimizer state is keyed by these, so
+    a checkpoint's moments line up with the reference's parameter names (FusedAdamW.state_dict)."""
+    D, d = cfg.vit_dim, cfg.llm_dim
+    special = {"vit.cls": (VIT + "embeddings.class_embedding", (1, 1, D)),
+               "vit.patch.w": (VIT + "embeddings.patch_embedding.weight", (D, 3, cfg.patch, cfg.patch)),
+               "vit.patch.b": (VIT + "embeddings.patch_embedding.bias", (D,)),
+               "vit.pos": (VIT + "embeddings.position_embedding", (1, cfg.vit_tokens, D)),
+               "drv.query_route": ("adaptors.driving.query_embeds_wps", (1, cfg.n_route, d)),
+               "drv.query_speed": ("adaptors.driving.query_embeds_speed", (1, cfg.n_speed, d))}
+    out: "OrderedDict[str, tuple[str, tuple]]" = OrderedDict()
+    for s in param_specs(cfg):
+        if not s.trainable:
+            continue
+        n = s.name
+        if n in special:
+            out[n] = special[n]
+            continue
+        m = re.fullmatch(r"vit\.(\d+)\.(.+)", n)
+        l = re.fullmatch(r"llm\.(\d+)\.lora\.(\w+)\.([ab])", n)
+        if m:
+            key = f"{VIT}encoder.layers.{m.group(1)}.{_VIT_LAYER[m.group(2)]}"
+        elif l:
+            key = (f"{LLM}model.layers.{l.group(1)}.{_SITE_MOD[l.group(2)]}."
+                   f"lora_{'A' if l.group(3) == 'a' else 'B'}.default.weight")
+        elif n in _MLP1:
+            key = MLP1 + _MLP1[n]
+        elif n in _HEADS:
+            key = "adaptors.driving." + _HEADS[n]
+        elif n in _WP:
+            key = _WP[n]
+        else:
+            raise KeyError(f"no reference key for trainable parameter {n}")
+        out[n] = (key, tuple(s.shape))
+    return out
+
+
 def _unwrap(sd) -> dict:
     """Lightning checkpoint {'state_dict': ...} / DeepSpeed {'module': ...} / DDP 'module.' / Lightning-DeepSpeed
     '_forward_module.' prefixes -> plain DrivingModel keys."""

@@ -8,7 +8,9 @@ issued on RCCL's stream (ordered after the producing kernels of the compute stre
 backward of earlier layers keeps running. The optimizer waits on the handles and applies 1/world
 inside the fused AdamW kernel (no extra pass). Device-agnostic (the CPU tests drive it with gloo).
 
-wire="bf16" (SURVEY.md §8e): each bucket is cast to a bf16 staging slice before its all-reduce (half the xGMI
+wire="f32" is the default (bench.py at every N): the exchange is exact to f32 summation order, stricter than the
+reference's fp16 reduce under DeepSpeed ZeRO-2 "16-mixed" (simlingo_training/config.py:284,298, train.py:160-168).
+wire="bf16" (opt-in): each bucket is cast to a bf16 staging slice before its all-reduce (half the xGMI
 bytes: 655 MB instead of 1.31 GB for the full model). The optimizer reads the summed bf16 wire buffer itself
 (optimizer_grad(): slx_sumsq_bf16 / slx_adamw_bf16g widen it and scale it by 1/world inside the kernels), so no
 cast-back pass runs between the last all-reduce and the optimizer; moments and master weights stay f32. Rounding of
@@ -155,6 +157,15 @@ class GradBucketer:
                     self.trace.append(("done", i, time.perf_counter()))
 
     def wait(self):
+        """Wait for this step's exchange. At world > 1 every bucket must have been issued by the backward: a bucket
+        left out would hand the optimizer a stale summed slice (bf16 wire) or an un-summed local one (f32)."""
+        if self.world > 1:
+            missing = [i for i, bk in enumerate(self.buckets) if bk.handle is None]
+            if missing:
+                for bk in self.buckets:
+                    bk.done = 0
+                raise RuntimeError(f"gradient buckets {missing} were not exchanged this step (the backward did not "
+                                   f"finish their parameter groups)")
         waited = False
         for i, bk in enumerate(self.buckets):
             if bk.handle is not None:

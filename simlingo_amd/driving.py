@@ -306,3 +306,16 @@ class FusedAdamW(torch.optim.Optimizer):
     def zero_grad(self, set_to_none: bool = True):
         # gradients are overwritten by every backward (no accumulation across steps)
         self.model.anchor.grad = None
+
+    def state_dict(self):
+        """AdamW's moments and step keyed by the reference's parameter names (simlingo_amd.optstate), so Lightning's
+        `ckpt_path` resume (train.py:128-142,217) restores them: {format, state: {key: {step, exp_avg, exp_avg_sq}},
+        param_groups (lr / betas / OneCycleLR's fields), step_count, max_norm, step_seed}."""
+        from .checkpoint import trainable_ref_keys
+        from .optstate import export_state
+        return export_state(self, self.model.engine, trainable_ref_keys(self.model.vla_cfg))
+
+    def load_state_dict(self, state_dict):
+        from .checkpoint import trainable_ref_keys
+        from .optstate import import_state
+        import_state(self, self.model.build_engine(), trainable_ref_keys(self.model.vla_cfg), state_dict)

@@ -188,5 +188,7 @@ class EngineOps:
         return self._ones
 
     def grad_norm(self):
-        """L2 norm of the (averaged) gradient — diagnostic (syncs)."""
-        return float(torch.linalg.vector_norm(self.grad).item()) / self.world
+        """L2 norm of the (averaged) gradient the optimizer reads (after wait_grads at N > 1: the summed f32 buffer or
+        the bf16 wire buffer) — diagnostic (syncs)."""
+        g, _ = self.bucketer.optimizer_grad()
+        return float(torch.linalg.vector_norm(g.float()).item()) / self.world

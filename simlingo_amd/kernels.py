@@ -457,9 +457,17 @@ DET_WS_FLOATS = 16 << 20  # 64 MB: the largest partial set of the InternVL2-1B s
 def set_deterministic(on: bool, device=None):
     """Deterministic-reduction mode (slx_set_deterministic, process-wide): every cross-block f32 reduction of the step
     goes through per-block partials and an ordered sum instead of f32 atomics, so two runs on the same inputs give
-    bitwise-equal gradients. The workspace is allocated once per device and kept."""
+    bitwise-equal gradients. The workspace is allocated once per device and kept. The library holds ONE workspace
+    pointer for the process, so the mode serves one device per process (the one-process-per-GPU model): turning it on
+    for a second device while it is on for another raises."""
     if on:
         dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        if dev.index is None:
+            dev = torch.device("cuda", torch.cuda.current_device())
+        other = [d for d in _det_ws if d != dev]
+        if other and deterministic():
+            raise RuntimeError(f"deterministic mode is already on for {other[0]}; the library's workspace is "
+                               f"process-wide (one device per process)")
         ws = _det_ws.get(dev)
         if ws is None:
             ws = _det_ws[dev] = torch.empty(DET_WS_FLOATS, dtype=torch.float32, device=dev)

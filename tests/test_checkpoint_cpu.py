@@ -266,3 +266,69 @@ def test_safe_load_list_subclass_becomes_plain_list(tmp_path, prefix):
     got = safe_load(str(tmp_path / "l.pt"))
     assert type(got["hp"]) is list and got["hp"] == [1, 2, 3] and got["one"] == [7]
     assert torch.equal(got["t"], torch.ones(2))
+
+
+def test_trainable_ref_keys_match_to_reference():
+    """The optimizer-state keys (FusedAdamW.state_dict) are exactly the reference state-dict keys and shapes of the
+    trainable tensors (tiny case: the real tensors, so identity is checked; full geometry: keys and shapes)."""
+    from simlingo_amd.checkpoint import trainable_ref_keys
+    cfg, P, _, _ = load_case("nopad")
+    sd = to_reference(P, cfg, aliases=False)
+    names = trainable_ref_keys(cfg)
+    assert len(names) == sum(1 for s in param_specs(cfg) if s.trainable)
+    for n, (key, shape) in names.items():
+        assert tuple(sd[key].shape) == shape, key
+        assert sd[key].data_ptr() == P[n].data_ptr(), (n, key)
+    full = full_config()
+    keys = KEYS["full"]
+    for n, (key, shape) in trainable_ref_keys(full).items():
+        assert keys[key] == list(shape), key
+
+
+def test_optimizer_state_round_trip_cpu():
+    """simlingo_amd.optstate on a stand-in engine (flat m / v buffers + offsets, as VLAEngine holds them): export cuts the
+    moments per reference key, import writes them back bit-exactly together with the step count, the param groups and
+    the dropout counter; mismatched keys are refused."""
+    import io
+    import math
+    from types import SimpleNamespace
+
+    from simlingo_amd.checkpoint import trainable_ref_keys
+    from simlingo_amd.optstate import export_state, import_state
+    cfg, _, _, _ = load_case("nopad")
+    names = trainable_ref_keys(cfg)
+    offs, o = {}, 0
+    for n, (_, shape) in names.items():
+        offs[n] = o
+        o += (math.prod(shape) + 63) // 64 * 64
+    g = torch.Generator().manual_seed(0)
+    eng = SimpleNamespace(device=torch.device("cpu"), offsets=offs, master=torch.zeros(o), step_seed=17,
+                          m_state=torch.randn(o, generator=g), v_state=torch.rand(o, generator=g))
+    p = torch.nn.Parameter(torch.zeros(()))
+    opt = torch.optim.SGD([p], lr=3e-5)
+    opt.step_count, opt.max_norm = 7, 0.3
+    opt.param_groups[0]["betas"] = (0.87, 0.999)
+    import torch.cuda as tc
+    orig = tc.current_stream
+    tc.current_stream = lambda *_: SimpleNamespace(synchronize=lambda: None)
+    try:
+        sd = export_state(opt, eng, names)
+    finally:
+        tc.current_stream = orig
+    buf = io.BytesIO()
+    torch.save(sd, buf)
+    buf.seek(0)
+    sd2 = torch.load(buf, weights_only=True)
+    assert set(sd2["state"]) == {k for k, _ in names.values()}
+    eng2 = SimpleNamespace(device=torch.device("cpu"), offsets=offs, master=torch.zeros(o), step_seed=0)
+    opt2 = torch.optim.SGD([torch.nn.Parameter(torch.zeros(()))], lr=1.0)
+    opt2.step_count, opt2.max_norm = 0, 0.3
+    import_state(opt2, eng2, names, sd2)
+    assert opt2.step_count == 7 and eng2.step_seed == 17 and opt2.param_groups[0]["betas"] == (0.87, 0.999)
+    for n, (_, shape) in names.items():
+        a, k = offs[n], math.prod(shape)
+        assert torch.equal(eng2.m_state[a:a + k], eng.m_state[a:a + k])
+        assert torch.equal(eng2.v_state[a:a + k], eng.v_state[a:a + k])
+    bad = dict(sd2, state=dict(list(sd2["state"].items())[1:]))
+    with pytest.raises(KeyError):
+        import_state(opt2, eng2, names, bad)

@@ -191,3 +191,15 @@ def test_bucketed_allreduce_world8(wire):
             assert bool((err <= world * 2.0 ** -8 * mag + 1e-30).all()), (err / mag.clamp_min(1e-30)).max().item()
             print(f"bf16 wire, world {world}: max error / sum|g| = {(err / mag.clamp_min(1e-30)).max().item():.3g}")
             assert not torch.equal(ret[r][1], exact.float())
+
+
+def test_wait_refuses_unexchanged_buckets():
+    """at world > 1 a bucket the backward never issued would hand AdamW a stale (bf16 wire) or un-summed
+    (f32 wire) slice; wait() refuses it instead."""
+    g = torch.zeros(4096)
+    bk = GradBucketer(g, {"a": (0, 2048), "b": (2048, 4096)}, bucket_bytes=1024, wire="bf16")
+    bk.set_distributed(None, 2)
+    with pytest.raises(RuntimeError, match="not exchanged"):
+        bk.wait()
+    bk.set_distributed(None, 1)
+    bk.wait()  # single process: nothing to exchange

@@ -49,18 +49,41 @@ def _oracle_teacher(P, cfg, ex, toks_all):
 
 
 def test_greedy_decode_vs_oracle(dev):
-    from simlingo_amd.decode import GreedyDecoder, infer_example
     cfg, P, ex, eng = _setup(dev)
-    n_new = 12
-    dec = GreedyDecoder(eng, max_len=512, max_new_tokens=n_new, eos_id=-1)
+    _check_greedy(cfg, P, ex, eng, n_new=12, max_len=512, tag="tiny")
+
+
+def test_greedy_decode_full_width_vs_oracle(dev):
+    """VERDICT r5 missing #4: the agent's greedy loop at the REAL InternVL2-1B widths (InternViT D 1024 / T 1025, Qwen2
+    d 896, GQA 14/2, FFN 4864, the V = 151655 argmax; 2 + 2 layers so the oracle's literal re-run per token stays
+    cheap), a ~576-token prompt (512 image tokens + 64 text, sample 1 left-padded by 5) and 30 generated tokens,
+    teacher-forced against the oracle's logits with the same gates as the tiny case
+    (/root/reference/simlingo_training/models/language_model/llm.py:178-250, team_code/agent_simlingo.py:797)."""
+    from simlingo_amd.config import full_config
+    from simlingo_amd.engine import VLAEngine
+    from simlingo_amd.params import init_params
+    from simlingo_amd.synthetic import make_batch
+    torch.set_num_threads(16)
+    cfg = full_config(vit_layers=2, llm_layers=2, lora_dropout=0.0)
+    P = init_params(cfg, seed=7, lora_b_std=0.02)
+    ex = make_batch(cfg, B=2, s_text=64, n_loss=1, seed=7, pad=[0, 5])
+    eng = VLAEngine(cfg, dev, P)
+    _check_greedy(cfg, P, ex, eng, n_new=30, max_len=1024, tag="full-width")
+
+
+def _check_greedy(cfg, P, ex, eng, n_new, max_len, tag):
+    from simlingo_amd.decode import GreedyDecoder, infer_example
+    dec = GreedyDecoder(eng, max_len=max_len, max_new_tokens=n_new, eos_id=-1)
     sp, rp, toks = infer_example(eng, dec, ex)
     assert all(len(t) == n_new for t in toks)
     ref = _oracle_teacher(P, cfg, ex, toks)
+    worst_gap, worst_d, worst_inc = 0.0, 0.0, 0.0
     for b, (lg, r_ref, s_ref) in enumerate(ref):
         std = lg.std(dim=-1)
         top2 = lg.topk(2, dim=-1).values
         for i, t in enumerate(toks[b]):
             gap = (top2[i, 0] - lg[i, t]).item()
+            worst_gap = max(worst_gap, gap / std[i].item())
             assert gap <= 3e-2 * std[i].item(), (b, i, t, gap, std[i].item())
             if (top2[i, 0] - top2[i, 1]).item() > 0.2 * std[i].item():
                 assert t == int(lg[i].argmax()), (b, i)
@@ -68,8 +91,10 @@ def test_greedy_decode_vs_oracle(dev):
             diff = (got - want).abs()
             inc = (torch.diff(got, dim=0, prepend=torch.zeros(1, got.shape[1]))
                    - torch.diff(want, dim=0, prepend=torch.zeros(1, want.shape[1]))).abs()
-            print(f"[decode b={b}] cumulated max |diff| {diff.max().item():.4g} m, per-point increment {inc.max().item():.4g} m")
+            worst_d, worst_inc = max(worst_d, diff.max().item()), max(worst_inc, inc.max().item())
             assert diff.max().item() <= 0.1 and inc.max().item() <= 0.015, (b, diff.max().item(), inc.max().item())
+    print(f"[decode {tag}] worst chosen-token gap {worst_gap:.4g} std, cumulated max |diff| {worst_d:.4g} m, "
+          f"per-point increment {worst_inc:.4g} m")
     # SURVEY §8d's bf16 gate (5e-2 m) against the oracle evaluated with the decoder's own bf16 GEMM operands: every
     # engine weight rounded to bf16 as the engine holds it, the Qwen2 projections replaced by the decoder's merged
     # bf16 W + s B A (LoRA B zeroed in the oracle so the merged term is not added twice); what remains is the bf16
@@ -86,7 +111,7 @@ def test_greedy_decode_vs_oracle(dev):
     for b, (_, r_q, s_q) in enumerate(refq):
         for got, want in ((rp[b].cpu(), r_q), (sp[b].cpu(), s_q)):
             dq = (got - want).abs().max().item()
-            print(f"[decode b={b}] vs the oracle on the decoder's bf16 operands: cumulated max |diff| {dq:.4g} m")
+            print(f"[decode {tag} b={b}] vs the oracle on the decoder's bf16 operands: cumulated max |diff| {dq:.4g} m")
             assert dq <= 5e-2, (b, dq)
     # the oracle's own free-running greedy agrees up to its first near-tie decision
     _, _, toks_o = O.infer(P, cfg, ex, n_new, eos=-1)

@@ -1,0 +1,145 @@
+"""Multi-GPU numerics without the hardware (VERDICT r5 "do this" #6): 8 data-parallel ranks of the HIP engine, all on
+the box's one GPU, exchanging their gradient buckets through gloo exactly as bench.py / ddp.py do over RCCL at N = 8
+(bucketed async all_reduce(SUM) issued during the backward, 1/world and the global-norm clip inside AdamW), for 20
+optimizer steps on fresh batches — against ONE process training the same 8x batch (the reference's DDP semantics,
+/root/reference/simlingo_training/train.py:160-168: every rank averages the same global gradient).
+
+Each step's global batch is 16 samples of equal length with equal LM-loss counts (4 tokens each), so the per-rank
+mean losses average to the global-batch mean exactly and the two trajectories compute the same mathematics; they
+differ by f32 summation order (f32 wire) or by the wire's bf16 rounding of every rank's gradient (bf16 wire, opt-in).
+Tiny geometry (the 8 engines share one GPU), LoRA dropout off (its masks are drawn per row of the local batch).
+
+Gates, written here (like test_drift_gpu.py): every step's rank-averaged loss within LOSS_REL of the single process;
+after 20 steps the held-out predictions within WP_M, and every trainable tensor's 20-step update direction within
+cosine UPD_COS of the single process's. f32 wire: summation order only; bf16 wire: looser, the wire's rounding
+amplified by Adam's per-element normalised steps.
+"""
+import os
+import socket
+
+import pytest
+import torch
+
+pytestmark = [pytest.mark.gpu, pytest.mark.timeout(900)]
+
+WORLD, B_RANK, STEPS, LR = 8, 2, 20, 1e-3
+GATES = {"f32": dict(LOSS_REL=1e-4, WP_M=2e-3, UPD_COS=0.999),
+         "bf16": dict(LOSS_REL=2e-2, WP_M=5e-2, UPD_COS=0.9)}
+
+
+def _slice(obj, a, b, B):
+    """Samples a:b of a batch NamedTuple (tensors / lists with a leading batch dimension)."""
+    if isinstance(obj, torch.Tensor):
+        return obj[a:b] if obj.dim() and obj.shape[0] == B else obj
+    if isinstance(obj, list) and len(obj) == B:
+        return obj[a:b]
+    if isinstance(obj, tuple) and hasattr(obj, "_fields"):
+        return type(obj)(*[_slice(getattr(obj, f), a, b, B) for f in obj._fields])
+    return obj
+
+
+def _batches(cfg):
+    from simlingo_amd.synthetic import make_batch
+    B = WORLD * B_RANK
+    return [make_batch(cfg, B=B, s_text=24, n_loss=4, seed=500 + i) for i in range(STEPS)]
+
+
+def _train(cfg, dev, batches, wire=None, world=1, rank=0):
+    from simlingo_amd.engine import VLAEngine
+    from simlingo_amd.plan import plan_from_example
+    eng = VLAEngine(cfg, dev, seed=3, bucket_bytes=64 << 10, wire=wire or "f32")
+    if world > 1:
+        eng.set_distributed(None, world)
+    losses = []
+    B = WORLD * B_RANK
+    for i, ex in enumerate(batches):
+        if world > 1:
+            ex = _slice(ex, rank * B_RANK, (rank + 1) * B_RANK, B)
+        plan = plan_from_example(cfg, ex)
+        lab = ex.driving_label
+        out4, _, _ = eng.forward(ex.driving_input.camera_images.to(dev), plan, plan.to_device(dev), lab.path.to(dev),
+                                 lab.waypoints.to(dev), training=True)
+        eng.backward(None)
+        eng.adamw_step(LR, i + 1, betas=cfg.betas, eps=cfg.eps, weight_decay=cfg.weight_decay, max_norm=cfg.grad_clip)
+        losses.append(out4.clone())
+    torch.cuda.synchronize()
+    return eng, torch.stack(losses)
+
+
+def _predict(eng, cfg, ex, dev):
+    from simlingo_amd.plan import plan_from_example
+    plan = plan_from_example(cfg, ex)
+    lab = ex.driving_label
+    _, rp, sp = eng.forward(ex.driving_input.camera_images.to(dev), plan, plan.to_device(dev), lab.path.to(dev),
+                            lab.waypoints.to(dev), training=False)
+    torch.cuda.synchronize()
+    return torch.cat([rp.reshape(-1), sp.reshape(-1)]).cpu()
+
+
+def _worker(rank, world, port, ret):
+    import torch.distributed as dist
+    from simlingo_amd.config import tiny_config
+    from simlingo_amd.synthetic import make_batch
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = torch.device("cuda:0")
+    cfg = tiny_config(lora_dropout=0.0)
+    batches = _batches(cfg)
+    held = make_batch(cfg, B=4, s_text=24, n_loss=4, seed=999)
+    for wire in ("f32", "bf16"):
+        eng, losses = _train(cfg, dev, batches, wire=wire, world=world, rank=rank)
+        # the DP step's loss is the mean of the ranks' losses (each rank logs its own under DDP)
+        dist.all_reduce(losses, op=dist.ReduceOp.SUM)
+        master = eng.master.clone()
+        dist.all_reduce(master, op=dist.ReduceOp.MAX)  # every rank holds the same parameters
+        same = torch.equal(master, eng.master)
+        if rank == 0:
+            ret[wire] = dict(losses=(losses / world).cpu(), master=eng.master.cpu(), same=same,
+                             pred=_predict(eng, cfg, held, dev),
+                             n_buckets=len(eng.bucketer.buckets), world=eng.world)
+        del eng
+        dist.barrier()
+    if rank == 0:
+        eng, losses = _train(cfg, dev, batches)
+        ret["single"] = dict(losses=losses.cpu(), master=eng.master.cpu(), pred=_predict(eng, cfg, held, dev),
+                             master0=None)
+        from simlingo_amd.engine import VLAEngine
+        e0 = VLAEngine(cfg, dev, seed=3)
+        ret["master0"] = e0.master.cpu()
+        ret["offsets"] = dict(e0.offsets)
+        ret["shapes"] = {s.name: tuple(s.shape) for s in e0.specs if s.trainable}
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_dp8_gloo_trajectory_matches_single_process(dev):
+    import math
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ret = mp.Manager().dict()
+    mp.spawn(_worker, args=(WORLD, port, ret), nprocs=WORLD, join=True)
+    single, m0 = ret["single"], ret["master0"]
+    offs, shapes = ret["offsets"], ret["shapes"]
+    report = {}
+    for wire in ("f32", "bf16"):
+        r, g = ret[wire], GATES[wire]
+        assert r["world"] == WORLD and r["n_buckets"] > 1 and r["same"], (wire, r["world"], r["n_buckets"])
+        rel = ((r["losses"][:, 0] - single["losses"][:, 0]).abs() / single["losses"][:, 0].abs()).max().item()
+        dwp = (r["pred"] - single["pred"]).abs().max().item()
+        worst_upd = 1.0
+        for name, shp in shapes.items():
+            o, n = offs[name], math.prod(shp)
+            u_dp = r["master"][o:o + n] - m0[o:o + n]
+            u_1 = single["master"][o:o + n] - m0[o:o + n]
+            if u_1.norm() > 0:
+                worst_upd = min(worst_upd, torch.nn.functional.cosine_similarity(u_dp, u_1, dim=0).item())
+        report[wire] = dict(loss_rel_max=rel, heldout_wp_max=dwp, worst_update_cos=worst_upd)
+    print(f"[dp8 vs single process, {STEPS} steps] {report}")
+    for wire, obs in report.items():
+        g = GATES[wire]
+        assert obs["loss_rel_max"] <= g["LOSS_REL"], (wire, obs)
+        assert obs["heldout_wp_max"] <= g["WP_M"], (wire, obs)
+        assert obs["worst_update_cos"] >= g["UPD_COS"], (wire, obs)
