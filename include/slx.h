@@ -384,6 +384,13 @@ int slx_adamw_bf16g(float* p, const void* g_bf16, float* m, float* v, void* p_bf
                     float beta2, float eps, float weight_decay, int step, const float* sumsq, float max_norm,
                     float grad_scale, slx_stream_t s);
 int slx_sumsq_bf16(const void* g_bf16, int64_t n, float* out, int zero_first, slx_stream_t s);
+/* The same sum of squares as per-block partials in `ws` (>= SLX_SUMSQ_PARTS floats) summed in block order: bitwise
+ * reproducible, so data-parallel replicas that hold identical summed gradients compute the identical clip factor and
+ * stay bitwise identical (torch's clip_grad_norm_ reduces in a fixed order too, train.py:206). The engines use these. */
+#define SLX_SUMSQ_PARTS 2048
+int slx_sumsq_ws(const float* g, int64_t n, float* out, int zero_first, float* ws, int64_t ws_floats, slx_stream_t s);
+int slx_sumsq_bf16_ws(const void* g_bf16, int64_t n, float* out, int zero_first, float* ws, int64_t ws_floats,
+                      slx_stream_t s);
 int slx_cast_f32_bf16(const float* src, void* dst, int64_t n, slx_stream_t s);
 
 /* ---- SimLingo-Base (LLaVA-NeXT CLIP encoder + tiny Llama, BASELINE configs[1]) ----------------- */

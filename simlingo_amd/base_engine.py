@@ -440,7 +440,8 @@ class BaseEngine(EngineOps):
             self.m_state = torch.zeros_like(self.master)
             self.v_state = torch.zeros_like(self.master)
             self.sumsq = torch.zeros(1, dtype=F32, device=self.device)
-        K.call("slx_sumsq", K.P(self.grad), self.n_flat, K.P(self.sumsq), 1, K.stream_ptr())
+        ws = self._sumsq_ws()  # fixed-order sum: identical clip factor on every data-parallel replica
+        K.call("slx_sumsq_ws", K.P(self.grad), self.n_flat, K.P(self.sumsq), 1, K.P(ws), ws.numel(), K.stream_ptr())
         hp = ((lr, weight_decay), (vision_lr, weight_decay), (vision_lr, 0.0), (lr, 0.0))
         for (a, b), (lr_k, wd_k) in zip(self.seg_bounds, hp):
             if b <= a:

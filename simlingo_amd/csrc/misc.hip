@@ -886,15 +886,18 @@ int slx_loss_gscale(const float* dtotal, int nl, int nr, int ns, float* gs, slx_
 
 extern "C++" {
 template <typename GT>
-static int sumsq_impl(const GT* g, int64_t n, float* out, int zero_first, slx_stream_t s) {  // out (+)= sum g^2
+static int sumsq_impl(const GT* g, int64_t n, float* out, int zero_first, slx_stream_t s, float* ws = nullptr,
+                      int64_t ws_floats = 0) {  // out (+)= sum g^2
   hipStream_t st = (hipStream_t)s;
   if (zero_first) hipMemsetAsync(out, 0, sizeof(float), st);
   if (!n) return 0;
   long blocks = (n / 4 + 255) / 256;
-  if (blocks > 2048) blocks = 2048;
+  if (blocks > SLX_SUMSQ_PARTS) blocks = SLX_SUMSQ_PARTS;
   if (blocks < 1) blocks = 1;
   const DetMode& dm = det_mode();
-  float* part = dm.on ? dm.ws : nullptr;
+  // ordered partial sums: the caller's workspace (slx_sumsq_ws), else the deterministic mode's
+  float* part = ws ? ws : (dm.on ? dm.ws : nullptr);
+  if (ws) SLX_CHECK_ARG(ws_floats >= blocks, "slx_sumsq_ws: workspace of at least SLX_SUMSQ_PARTS floats");
   hipLaunchKernelGGL(sumsq_kernel<GT>, dim3((unsigned)blocks), dim3(256), 0, st, g, n, out, part);
   SLX_LAUNCH_CHECK("slx_sumsq");
   if (part) return det_reduce(part, (int)blocks, 1, 1, out, 1, st);
@@ -904,6 +907,18 @@ static int sumsq_impl(const GT* g, int64_t n, float* out, int zero_first, slx_st
 
 int slx_sumsq(const float* g, int64_t n, float* out, int zero_first, slx_stream_t s) {
   return sumsq_impl(g, n, out, zero_first, s);
+}
+
+int slx_sumsq_ws(const float* g, int64_t n, float* out, int zero_first, float* ws, int64_t ws_floats, slx_stream_t s) {
+  SLX_CHECK_ARG(ws != nullptr, "slx_sumsq_ws: workspace");
+  return sumsq_impl(g, n, out, zero_first, s, ws, ws_floats);
+}
+
+int slx_sumsq_bf16_ws(const void* g, int64_t n, float* out, int zero_first, float* ws, int64_t ws_floats,
+                      slx_stream_t s) {
+  SLX_CHECK_ARG(((uintptr_t)g & 7) == 0, "slx_sumsq_bf16_ws: 8-B aligned gradients");
+  SLX_CHECK_ARG(ws != nullptr, "slx_sumsq_bf16_ws: workspace");
+  return sumsq_impl((const bf16*)g, n, out, zero_first, s, ws, ws_floats);
 }
 
 int slx_sumsq_bf16(const void* g, int64_t n, float* out, int zero_first, slx_stream_t s) {

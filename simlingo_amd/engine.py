@@ -1006,9 +1006,12 @@ class VLAEngine(EngineOps):
             self.m_state = torch.zeros_like(self.master)
             self.v_state = torch.zeros_like(self.master)
             self.sumsq = torch.zeros(1, dtype=F32, device=self.device)
-        # the summed gradients: the f32 buffer, or (bf16 all-reduce wire) the wire buffer itself, widened in the kernels
+        # the summed gradients: the f32 buffer, or (bf16 all-reduce wire) the wire buffer itself, widened in the kernels;
+        # the sum of squares in a fixed order, so every data-parallel replica computes the same clip factor
         g, g_bf16 = self.bucketer.optimizer_grad()
-        K.call("slx_sumsq_bf16" if g_bf16 else "slx_sumsq", K.P(g), self.n_flat, K.P(self.sumsq), 1, K.stream_ptr())
+        ws = self._sumsq_ws()
+        K.call("slx_sumsq_bf16_ws" if g_bf16 else "slx_sumsq_ws", K.P(g), self.n_flat, K.P(self.sumsq), 1, K.P(ws),
+               ws.numel(), K.stream_ptr())
         K.call("slx_adamw_bf16g" if g_bf16 else "slx_adamw", K.P(self.master), K.P(g), K.P(self.m_state),
                K.P(self.v_state), K.P(self.wbf),
                self.n_flat, float(lr), float(betas[0]), float(betas[1]), float(eps), float(weight_decay), int(step),

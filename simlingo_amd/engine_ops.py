@@ -120,6 +120,12 @@ class EngineOps:
         K.norm_fwd(d)
         return y, d
 
+    def _sumsq_ws(self):
+        """Partials of the ordered gradient sum of squares (slx_sumsq_ws, SLX_SUMSQ_PARTS floats)."""
+        if getattr(self, "_sumsq_part", None) is None:
+            self._sumsq_part = torch.empty(2048, dtype=F32, device=self.device)
+        return self._sumsq_part
+
     def _ws(self, nfloats):
         if getattr(self, "_wsbuf", None) is None or self._wsbuf.numel() < nfloats:
             self._wsbuf = self._e(max(nfloats, 1 << 20), dtype=F32)

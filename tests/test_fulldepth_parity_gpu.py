@@ -27,9 +27,11 @@ pytestmark = [pytest.mark.gpu, pytest.mark.timeout(1200)]
 
 # §8d's bf16 gates
 LOSS_REL_8D, WP_8D, COS_8D = 1e-2, 5e-2, 0.99
-# regression gates: ~3x the maxima the round-6 build showed on these exact inputs (printed by the tests)
-REGRESSION = dict(loss_rel=1e-3, wp=1e-2, cos=0.9995)
-BASE_REGRESSION = dict(loss_rel=1e-3, wp=1e-2, cos=0.9995)
+# regression gates: ~3x the maxima the round-6 build showed on these exact inputs (printed by the tests). Observed
+# (gpurun_out/r6a_tests.log -> DESIGN.md): VLA loss rel 7.3e-4, route 9.2e-3 m, speed 1.06e-2 m, worst gradient cosine
+# 0.99965 (llm.4.lora.k.a); SimLingo-Base loss rel 1.25e-3, route 1.48e-2 m, speed 5.5e-3 m, worst cosine 0.99994
+REGRESSION = dict(loss_rel=2.5e-3, wp=3e-2, cos=0.999)
+BASE_REGRESSION = dict(loss_rel=4e-3, wp=4.5e-2, cos=0.9998)
 
 
 def _grad_stats(eng_G, grads):

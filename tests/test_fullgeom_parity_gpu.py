@@ -89,6 +89,10 @@ def test_full_geometry_step(dev, case, record_property):
     assert max(obs["rel_loss"]) <= 1e-2, obs
     assert obs["route_max"] <= 5e-2 and obs["speed_max"] <= 5e-2, obs
     assert not bad, bad
+    # regression gates at ~3x the maxima observed over these cases (loss rel 3.7e-4, points 3e-3 m, cosine 0.9999)
+    assert max(obs["rel_loss"]) <= 1.2e-3, obs
+    assert max(obs["route_max"], obs["speed_max"]) <= 1e-2, obs
+    assert obs["worst_grad_cos"] >= 0.9997, obs
 
 
 def test_engine_vs_reference_full1_fixture(dev):
