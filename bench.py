@@ -363,6 +363,45 @@ def dropin_line(dl, dev):
     return res
 
 
+def calibration(dev) -> dict:
+    """the bf16 ceiling measured on this box beside the 2.5 PFLOP/s spec. `mfma_loop` = a bare
+    back-to-back v_mfma_f32_32x32x16_bf16 loop on random register operands, one wave per SIMD on every CU (slx_mfma_peak:
+    what the matrix cores sustain at the clock the chip holds under a bf16 load); `gemm_8192` = this library's own bf16
+    GEMM (v3, NT) at M = N = K = 8192 on N(0, 1) operands. HIP events, median of 5."""
+    from simlingo_amd import kernels as K
+
+    def med(fn, reps=5):
+        fn()
+        torch.cuda.synchronize()
+        ts = []
+        for _ in range(reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            fn()
+            e1.record()
+            torch.cuda.synchronize()
+            ts.append(e0.elapsed_time(e1) * 1e-3)
+        return sorted(ts)[len(ts) // 2]
+
+    grid, iters = 256 * 4, 20000
+    out = torch.empty(grid * 256, device=dev)
+    t = med(lambda: K.call("slx_mfma_peak", grid, iters, K.P(out), K.stream_ptr()))
+    mfma = grid * 4 * iters * 4 * 32 * 32 * 16 * 2 / t / 1e12
+    n = 8192
+    g = torch.Generator(device=dev).manual_seed(0)
+    a = torch.randn(n, n, device=dev, generator=g).bfloat16()
+    b = torch.randn(n, n, device=dev, generator=g).bfloat16()
+    c = torch.empty(n, n, device=dev, dtype=torch.bfloat16)
+    tg = med(lambda: K.mm(a, b, c))
+    del a, b, c, out
+    gemm = 2.0 * n ** 3 / tg / 1e12
+    return {"spec_peak_tflops": PEAK_BF16_TFLOPS, "mfma_loop_tflops": round(mfma, 1),
+            "mfma_loop_frac_of_spec": round(mfma / PEAK_BF16_TFLOPS, 4), "gemm_8192_tflops": round(gemm, 1),
+            "gemm_8192_frac_of_spec": round(gemm / PEAK_BF16_TFLOPS, 4),
+            "note": "mfma_loop: bare back-to-back 32x32x16 bf16 MFMAs on random operands, all 1024 SIMDs (the clock "
+                    "the chip holds under bf16 load); gemm_8192: this library's v3 GEMM at 8192^3"}
+
+
 def traffic_record(tag, flop_M):
     """PMC-measured HBM bytes per FC1 launch (profiles/*_{tag}_fc1_traffic.json, newest first)."""
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", f"*{tag}_fc1_traffic.json")), reverse=True):
@@ -491,6 +530,12 @@ def main():
             res["comm_exposed_ms"] = cs.pop("comm_exposed_ms")
             res["comm"] = cs
     if rank == 0 and world == 1 and args.config == "vla" and not args.no_extras:
+        try:
+            res["calibration"] = calibration(dev)
+            res["step_frac_of_mfma_loop"] = round(res["step_mfma_frac"] * PEAK_BF16_TFLOPS
+                                                  / res["calibration"]["mfma_loop_tflops"], 4)
+        except Exception as e:
+            res["calibration"] = {"error": repr(e)[:200]}
         if dl is not None and "error" not in dl:
             try:
                 res["dropin"] = dropin_line(dl, dev)

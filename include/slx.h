@@ -463,14 +463,6 @@ void slx_dec_attn_set_trace(long long* buf);
 /* tests / tools only: 1 = use the split form even for caches of <= 1024 rows (which otherwise run one MFMA
  * workgroup per kv head, no split)                                                                        */
 void slx_dec_attn_force_split(int on);
-/* slx_dec_attn followed by the O projection X[n] += W_o[n, :] . out (the "O GEMV + residual" step), in ONE launch for
- * caches of <= 1024 rows: the O workgroups stream their W_o rows while the attention runs and take the attention
- * output through an in-launch hand-off (sync: slx_dec_sync_ints() zeroed ints per call site, reset by every call;
- * sync[2] != 0 reports a hand-off timeout). Longer caches: the split attention + the O GEMV (two launches).       */
-int slx_dec_sync_ints(void);
-int slx_dec_attn_o(void* cache, int64_t ld, int Hq, int Hkv, const float* cos_tab, const float* sin_tab, int lmax,
-                   float* ws, void* out, const slx_dec_state* st, const void* Wo, int64_t ldwo, int N, int K, float* X,
-                   int* sync, slx_stream_t s);
 /* the attention split over keys WITHOUT an in-launch merge (SLX_DEC_SPLIT_NS workgroups per kv head, default 8, each
  * at most 8 key blocks of 32: lmax <= 256 * ns; partials in ws, sized by slx_dec_attn_ws_floats), then the O GEMV +
  * residual X[n] += W_o[n, :] . out, whose prologue merges the partials (two launches, no counters). out (optional, bf16
@@ -545,6 +537,11 @@ int slx_ce_bwd_f32(const float* logits, int64_t ld, const int* labels, const flo
                    const float* gscale, float* dlogits, int64_t ldd, slx_stream_t s);     /* slx_ce_bwd  */
 int slx_vit_embed_bwd_f32(const float* dx, int N, int T, int D, float* dpos, float* dcls, float* dpatch,
                           slx_stream_t s);                       /* slx_vit_embed_bwd                    */
+
+/* ---- on-box calibration (the bf16 MFMA ceiling measured on the box, reported beside the spec) ------ */
+/* grid workgroups of 4 waves, each wave iters x 4 back-to-back v_mfma_f32_32x32x16_bf16 on random register operands;
+ * FLOPs = grid * 4 * iters * 4 * 32768; out >= grid * 256 floats (the reduced accumulators, so the loop is live)   */
+int slx_mfma_peak(int grid, int iters, float* out, slx_stream_t s);
 
 #ifdef __cplusplus
 }

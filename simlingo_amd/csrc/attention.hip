@@ -95,26 +95,6 @@ struct AttnArgs {
   int tailv;                     // non-causal DMA forms: a short last key / query tile (<= kTailMax rows) on the VALU
 };
 
-// Stage 64 rows x 64 cols (bf16) of a token-major matrix into a swizzled LDS tile (8 KB).
-// Two 16-B chunks per thread; rows >= nrows are zero-filled.
-__device__ __forceinline__ void load64(const bf16* base, long ld, int row0, int nrows, uint4 (&r)[2]) {
-  const int t = threadIdx.x;
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int row = (t >> 3) + 32 * i, c = t & 7;
-    r[i] = (row0 + row < nrows) ? *reinterpret_cast<const uint4*>(base + (long)(row0 + row) * ld + c * 8)
-                                : make_uint4(0u, 0u, 0u, 0u);
-  }
-}
-__device__ __forceinline__ void store64(char* lds, const uint4 (&r)[2]) {
-  const int t = threadIdx.x;
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int row = (t >> 3) + 32 * i, c = t & 7;
-    *reinterpret_cast<uint4*>(lds + sw_off(row, c)) = r[i];
-  }
-}
-
 constexpr float LOG2E = 1.4426950408889634f;
 
 template <int N>
@@ -240,88 +220,6 @@ __device__ __forceinline__ void fwd_tile(const char* Kl, const char* Vl, const b
     }
 }
 
-__global__ __launch_bounds__(256, ATTN_FWD_OCC) void attn_fwd_kernel(AttnArgs a) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * 8192];
-  const BlockCoord bc = attn_block((a.S + 127) / 128, a.Hq, a.Hkv, a.B, a.causal ? 1 : 0, a.tail_first);
-  const int qb = bc.blk, h = bc.h, b = bc.b;
-  const int hk = h / (a.Hq / a.Hkv);
-  const int S = a.S;
-  const int kvlen = a.seqlens ? min(a.seqlens[b], S) : S;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hl = lane >> 5;
-  const int q0 = qb * 128 + w * 32;
-  const int myq = q0 + (lane & 31);
-  const bool active = q0 < S;
-  const float c = a.scale * LOG2E;
-
-  const bf16* kbase = a.k + (long)b * S * a.ldk + hk * 64;
-  const bf16* vbase = a.v + (long)b * S * a.ldv + hk * 64;
-
-  bf16x8 qf[4];
-  {
-    const bf16* qrow = a.q + ((long)b * S + min(myq, S - 1)) * a.ldq + h * 64;
-#pragma unroll
-    for (int kk = 0; kk < 4; ++kk) {
-      bf16x8 z;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) z[j] = (bf16)0.f;
-      qf[kk] = myq < S ? *reinterpret_cast<const bf16x8*>(qrow + 16 * kk + 8 * hl) : z;
-    }
-  }
-  int kend = kvlen;
-  if (a.causal) kend = min(kend, qb * 128 + 128);
-  const int nt = (kend + 63) / 64;
-
-  f32x16 o0, o1, lacc;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) { o0[r] = 0.f; o1[r] = 0.f; lacc[r] = 0.f; }
-  float m = -1e30f;
-
-  uint4 rk[2], rv[2];
-  load64(kbase, a.ldk, 0, S, rk);
-  load64(vbase, a.ldv, 0, S, rv);
-  store64(smem, rk);
-  store64(smem + 8192, rv);
-  __syncthreads();
-
-  for (int t = 0; t < nt; ++t) {
-    const char* Kl = smem + (t & 1) * 16384;
-    const char* Vl = Kl + 8192;
-    if (t + 1 < nt) {
-      load64(kbase, a.ldk, (t + 1) * 64, S, rk);
-      load64(vbase, a.ldv, (t + 1) * 64, S, rv);
-    }
-    if (active) {
-      // boundary tiles (past kvlen, or crossing this wave's causal diagonal) take the masked path
-      const int kfull = a.causal ? min(kvlen, q0 + 1) : kvlen;
-      if ((t + 1) * 64 <= kfull) fwd_tile<false>(Kl, Vl, qf, o0, o1, lacc, m, c, t * 64, kvlen, myq, false, lane);
-      else fwd_tile<true>(Kl, Vl, qf, o0, o1, lacc, m, c, t * 64, kvlen, myq, a.causal, lane);
-    }
-    if (t + 1 < nt) {
-      char* nx = smem + ((t + 1) & 1) * 16384;
-      store64(nx, rk);
-      store64(nx + 8192, rv);
-    }
-    __syncthreads();
-  }
-  if (!active || myq >= S) return;
-  const float lt = lacc[0];
-  const float inv = 1.0f / lt;
-  bf16* orow = a.o + ((long)b * S + myq) * a.ldo + h * 64;
-#pragma unroll
-  for (int g = 0; g < 4; ++g) {
-    const int d = 8 * g + 4 * hl;
-    bf16x4 v0, v1;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      v0[e] = (bf16)(o0[4 * g + e] * inv);
-      v1[e] = (bf16)(o1[4 * g + e] * inv);
-    }
-    *reinterpret_cast<bf16x4*>(orow + d) = v0;
-    *reinterpret_cast<bf16x4*>(orow + 32 + d) = v1;
-  }
-  if (hl == 0 && a.lse) a.lse[((long)b * a.Hq + h) * S + myq] = m + __log2f(lt);
-}
-
 // ---- backward, dK/dV pass: one workgroup = 4 waves = 128 keys of one (b, kv-head); sweeps every q-head of
 // the group x 64-query chunks (Q, dO, lse, delta staged through LDS). S and dP are computed with the key on
 // the lane, so their accumulators are the B operands of dV^T += dO^T P and dK^T += Q^T dS. dK/dV of the
@@ -406,131 +304,6 @@ __device__ __forceinline__ void block_colsum64(char* lds, float* red, const floa
   if (w == 0) atomicAdd(dst + lane, red[lane] + red[64 + lane] + red[128 + lane] + red[192 + lane]);
 }
 
-__global__ __launch_bounds__(256, 2) void attn_bwd_kv_kernel(AttnArgs a) {
-  // LDS: Q chunk x2 (8 KB each) | dO chunk x2 | lse,delta x2
-  __shared__ __attribute__((aligned(16))) char smem[2 * 8192 + 2 * 8192 + 2 * 2 * 64 * 4];
-  char* Qc = smem;
-  char* Dc = smem + 2 * 8192;
-  float* LD = reinterpret_cast<float*>(Dc + 2 * 8192);  // [buf][lse 64 | delta 64]
-
-  const BlockCoord bc = attn_block((a.S + 127) / 128, a.Hkv * a.nsplit, a.Hkv * a.nsplit, a.B, a.causal ? 2 : 0, a.tail_first);
-  const int kblk = bc.blk, hk = bc.h / a.nsplit, sp = bc.h % a.nsplit, b = bc.b;
-  const int G = a.Hq / a.Hkv;
-  const int hg0 = sp * a.hsplit;
-  const int ng = min(G, hg0 + a.hsplit) - hg0;  // q-heads of the group handled here
-  const int S = a.S;
-  const int kvlen = a.seqlens ? min(a.seqlens[b], S) : S;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hl = lane >> 5;
-  const int k0 = kblk * 128;
-  const int kw0 = k0 + 32 * w;  // this wave's first key
-  const int mykey = kw0 + (lane & 31);
-  const float c = a.scale * LOG2E;
-
-  bf16x8 kf[4], vf[4];
-  {
-    const int kr = min(mykey, S - 1);
-    const bf16* kp = a.k + ((long)b * S + kr) * a.ldk + hk * 64;
-    const bf16* vp = a.v + ((long)b * S + kr) * a.ldv + hk * 64;
-#pragma unroll
-    for (int kk = 0; kk < 4; ++kk) {
-      kf[kk] = *reinterpret_cast<const bf16x8*>(kp + 16 * kk + 8 * hl);
-      vf[kk] = *reinterpret_cast<const bf16x8*>(vp + 16 * kk + 8 * hl);
-    }
-  }
-  f32x16 dk0, dk1, dv0, dv1;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) { dk0[r] = dk1[r] = dv0[r] = dv1[r] = 0.f; }
-
-  const int qstart = a.causal ? (k0 / 64) * 64 : 0;
-  const int nch = qstart < S ? (S - qstart + 63) / 64 : 0;
-  const int nit = nch * ng;  // (q-head, chunk) pairs, chunk fastest
-
-  auto stage = [&](int it, uint4 (&rq)[2], uint4 (&rd)[2], float& ld) {
-    const int h = hk * G + hg0 + it / nch, qc = qstart + (it % nch) * 64;
-    load64(a.q + (long)b * S * a.ldq + h * 64, a.ldq, qc, S, rq);
-    load64(a.dout + (long)b * S * a.lddo + h * 64, a.lddo, qc, S, rd);
-    if (tid < 128) {
-      const int qi = qc + (tid & 63);
-      const long base = ((long)b * a.Hq + h) * S;
-      ld = qi < S ? (tid < 64 ? a.lse[base + qi] : a.delta[base + qi]) : 0.f;  // delta is stored negated
-    }
-  };
-  auto commit = [&](int buf, const uint4 (&rq)[2], const uint4 (&rd)[2], float ld) {
-    store64(Qc + buf * 8192, rq);
-    store64(Dc + buf * 8192, rd);
-    if (tid < 128) LD[buf * 128 + tid] = ld;
-  };
-
-  uint4 rq[2], rd[2];
-  float ldv = 0.f;
-  if (nit > 0) {
-    stage(0, rq, rd, ldv);
-    commit(0, rq, rd, ldv);
-  }
-  __syncthreads();
-  for (int it = 0; it < nit; ++it) {
-    const int buf = it & 1;
-    const int qc = qstart + (it % nch) * 64;
-    if (it + 1 < nit) stage(it + 1, rq, rd, ldv);
-    const char* Ql = Qc + buf * 8192;
-    const char* Dl = Dc + buf * 8192;
-    const float* lse_l = LD + buf * 128;
-    // boundary chunks: past S (query tail), this wave's keys past kvlen, or crossing the causal diagonal
-    const bool full = (qc + 64 <= S) && (kw0 + 32 <= kvlen) && (!a.causal || kw0 + 31 <= qc);
-    if (kw0 >= kvlen) {
-      // every key of this wave is padding or past S (e.g. the last key block of InternViT's 1025 tokens): its dK/dV
-      // stay zero, the wave only helps stage
-    } else if (full) bwd_kv_chunk<false>(Ql, Dl, lse_l, lse_l + 64, kf, vf, dk0, dk1, dv0, dv1, c, qc, S, mykey, kvlen, false, lane);
-    else bwd_kv_chunk<true>(Ql, Dl, lse_l, lse_l + 64, kf, vf, dk0, dk1, dv0, dv1, c, qc, S, mykey, kvlen, a.causal, lane);
-    if (it + 1 < nit) commit(buf ^ 1, rq, rd, ldv);
-    __syncthreads();
-  }
-
-  const bool kvalid = mykey < S;
-  float ck0[16], ck1[16], cv0[16], cv1[16];  // the stored bf16 values, for the bias column sums
-  // accumulators: column = key (lane), rows = d
-#pragma unroll
-  for (int g = 0; g < 4; ++g) {
-    const int d = 8 * g + 4 * hl;
-    if (!kvalid) {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) ck0[4 * g + e] = ck1[4 * g + e] = cv0[4 * g + e] = cv1[4 * g + e] = 0.f;
-    } else if (a.dk_acc) {  // f32 partial of this head split; the finalize sums splits, applies RoPE^T, casts
-      const long off = (long)sp * a.B * S * (a.Hkv * 64) + ((long)b * S + mykey) * (a.Hkv * 64) + hk * 64;
-      float* kp = a.dk_acc + off;
-      float* vp = a.dv_acc + off;
-      *reinterpret_cast<float4*>(kp + d) = make_float4(dk0[4 * g] * a.scale, dk0[4 * g + 1] * a.scale, dk0[4 * g + 2] * a.scale, dk0[4 * g + 3] * a.scale);
-      *reinterpret_cast<float4*>(kp + 32 + d) = make_float4(dk1[4 * g] * a.scale, dk1[4 * g + 1] * a.scale, dk1[4 * g + 2] * a.scale, dk1[4 * g + 3] * a.scale);
-      *reinterpret_cast<float4*>(vp + d) = make_float4(dv0[4 * g], dv0[4 * g + 1], dv0[4 * g + 2], dv0[4 * g + 3]);
-      *reinterpret_cast<float4*>(vp + 32 + d) = make_float4(dv1[4 * g], dv1[4 * g + 1], dv1[4 * g + 2], dv1[4 * g + 3]);
-    } else {
-      bf16* kp = a.dk + ((long)b * S + mykey) * a.lddk + hk * 64;
-      bf16* vp = a.dv + ((long)b * S + mykey) * a.lddv + hk * 64;
-      bf16x4 k0v, k1v, v0v, v1v;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        k0v[e] = (bf16)(dk0[4 * g + e] * a.scale);
-        k1v[e] = (bf16)(dk1[4 * g + e] * a.scale);
-        v0v[e] = (bf16)dv0[4 * g + e];
-        v1v[e] = (bf16)dv1[4 * g + e];
-        ck0[4 * g + e] = (float)k0v[e];
-        ck1[4 * g + e] = (float)k1v[e];
-        cv0[4 * g + e] = (float)v0v[e];
-        cv1[4 * g + e] = (float)v1v[e];
-      }
-      *reinterpret_cast<bf16x4*>(kp + d) = k0v;
-      *reinterpret_cast<bf16x4*>(kp + 32 + d) = k1v;
-      *reinterpret_cast<bf16x4*>(vp + d) = v0v;
-      *reinterpret_cast<bf16x4*>(vp + 32 + d) = v1v;
-    }
-  }
-  if (a.dbk) {  // bf16 path only (the host refuses bias sums with the f32 GQA/RoPE finalize)
-    __shared__ float red[256];
-    block_colsum64(smem, red, ck0, ck1, a.dbk + hk * 64, lane, w);
-    block_colsum64(smem, red, cv0, cv1, a.dbv + hk * 64, lane, w);
-  }
-}
-
 // ---- backward, dQ pass (the forward's structure): one workgroup = 4 waves = 128 queries of one (b, h);
 // K/V tiles of 64 keys double-buffered through LDS; per tile S^T = K Q^T and dP^T = V dO^T with the query on
 // the lane, dS^T = P^T (dP^T - delta) in registers, dQ^T += K^T dS^T (K read transposed); it stores -delta for the dK/dV
@@ -576,48 +349,6 @@ __device__ __forceinline__ void bwd_dq_tile(const char* Kl, const char* Vl, cons
       dq1 = mfma32(tr_frag(Kl, kb * 32 + 16 * st, 32, lane), sb, dq1);
     }
 }
-
-// The dQ tile one 32-key half at a time (S, dP, dS and the dQ MFMAs of half kb before half kb + 1), with dP started
-// from a splat of -delta instead of a held vector: half the live S / dP registers, so the DMA-staged dQ pass fits
-// 168 VGPRs and three workgroups per CU (ATTN_DQ_SER, A/B).
-template <bool MASK>
-__device__ __forceinline__ void bwd_dq_tile_ser(const char* Kl, const char* Vl, const bf16x8 (&qf)[4], const bf16x8 (&df)[4],
-                                                f32x16& dq0, f32x16& dq1, float c, float lse, float negdelta, int key0,
-                                                int kvlen, int myq, bool causal, int lane) {
-  const int hl = lane >> 5;
-#pragma unroll
-  for (int kb = 0; kb < 2; ++kb) {
-    f32x16 sv, dp;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) { sv[r] = 0.f; dp[r] = negdelta; }
-#pragma unroll
-    for (int kk = 0; kk < 4; ++kk) {
-      sv = mfma32(row_frag(Kl, kb * 32, kk, lane), qf[kk], sv);
-      dp = mfma32(row_frag(Vl, kb * 32, kk, lane), df[kk], dp);
-    }
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      float pv = __builtin_amdgcn_exp2f(__builtin_fmaf(sv[r], c, -lse));
-      if constexpr (MASK) {
-        const int key = key0 + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
-        const bool ok = (key < kvlen) & (!causal | (key <= myq));
-        pv = ok ? pv : 0.f;
-      }
-      dp[r] = pv * dp[r];
-    }
-#pragma unroll
-    for (int st = 0; st < 2; ++st) {
-      const bf16x8 sb = acc_frag(dp, st);
-      dq0 = mfma32(tr_frag(Kl, kb * 32 + 16 * st, 0, lane), sb, dq0);
-      dq1 = mfma32(tr_frag(Kl, kb * 32 + 16 * st, 32, lane), sb, dq1);
-    }
-  }
-}
-
-#ifndef ATTN_DQ_SER
-#define ATTN_DQ_SER 0
-#endif
-
 // The RoPE table entries of a lane's 16 dQ dims (d = 8 g + 4 hl + e, as float4 per g), issued together: read per
 // element inside `if (a.rcos)`, each load was drained (vmcnt(0)) before the next, 16 round trips per dQ store
 __device__ __forceinline__ void rope_lane_tables(const float* rcos, const float* rsin, long qi, int hl, float4 (&cs)[4],
@@ -629,127 +360,13 @@ __device__ __forceinline__ void rope_lane_tables(const float* rcos, const float*
   }
 }
 
-__global__ __launch_bounds__(256, ATTN_DQ_OCC) void attn_bwd_dq_kernel(AttnArgs a) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * 8192];
-  const BlockCoord bc = attn_block((a.S + 127) / 128, a.Hq, a.Hkv, a.B, a.causal ? 1 : 0, a.tail_first);
-  const int qb = bc.blk, h = bc.h, b = bc.b;
-  const int hk = h / (a.Hq / a.Hkv);
-  const int S = a.S;
-  const int kvlen = a.seqlens ? min(a.seqlens[b], S) : S;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hl = lane >> 5;
-  const int q0 = qb * 128 + w * 32;
-  const int myq = q0 + (lane & 31);
-  const bool active = q0 < S;
-  const float c = a.scale * LOG2E;
-  const bf16* kbase = a.k + (long)b * S * a.ldk + hk * 64;
-  const bf16* vbase = a.v + (long)b * S * a.ldv + hk * 64;
-
-  bf16x8 qf[4], df[4];
-  float lse = 0.f, dlt = 0.f;
-  {
-    const int qr = min(myq, S - 1);
-    const bf16* qrow = a.q + ((long)b * S + qr) * a.ldq + h * 64;
-    const bf16* drow = a.dout + ((long)b * S + qr) * a.lddo + h * 64;
-    const bf16* orow = a.o + ((long)b * S + qr) * a.ldo + h * 64;
-    bf16x8 of[4];
-#pragma unroll
-    for (int kk = 0; kk < 4; ++kk) {
-      qf[kk] = *reinterpret_cast<const bf16x8*>(qrow + 16 * kk + 8 * hl);
-      df[kk] = *reinterpret_cast<const bf16x8*>(drow + 16 * kk + 8 * hl);
-      of[kk] = *reinterpret_cast<const bf16x8*>(orow + 16 * kk + 8 * hl);
-    }
-    const long li = ((long)b * a.Hq + h) * S + qr;
-    lse = a.lse[li];
-    // delta = rowsum(dO * O) of this query (the lane pair l, l^32 holds the two 32-dim halves); written for the
-    // dK/dV pass, which runs after this one
-#pragma unroll
-    for (int kk = 0; kk < 4; ++kk)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) dlt = __builtin_fmaf((float)df[kk][j], (float)of[kk][j], dlt);
-    dlt += __shfl_xor(dlt, 32, 64);
-    if (hl == 0 && active && myq < S) const_cast<float*>(a.delta)[li] = -dlt;  // stored negated (dP chains start there)
-  }
-  f32x16 negd;  // -delta of this lane's query, the dP^T chains' initial accumulator
-#pragma unroll
-  for (int r = 0; r < 16; ++r) negd[r] = -dlt;
-  int kend = kvlen;
-  if (a.causal) kend = min(kend, qb * 128 + 128);
-  const int nt = (kend + 63) / 64;
-  f32x16 dq0, dq1;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) { dq0[r] = 0.f; dq1[r] = 0.f; }
-
-  uint4 rk[2], rv[2];
-  load64(kbase, a.ldk, 0, S, rk);
-  load64(vbase, a.ldv, 0, S, rv);
-  store64(smem, rk);
-  store64(smem + 8192, rv);
-  __syncthreads();
-  for (int t = 0; t < nt; ++t) {
-    const char* Kl = smem + (t & 1) * 16384;
-    const char* Vl = Kl + 8192;
-    if (t + 1 < nt) {
-      load64(kbase, a.ldk, (t + 1) * 64, S, rk);
-      load64(vbase, a.ldv, (t + 1) * 64, S, rv);
-    }
-    if (active) {
-      const int kfull = a.causal ? min(kvlen, q0 + 1) : kvlen;
-      if ((t + 1) * 64 <= kfull) bwd_dq_tile<false>(Kl, Vl, qf, df, dq0, dq1, c, lse, negd, t * 64, kvlen, myq, false, lane);
-      else bwd_dq_tile<true>(Kl, Vl, qf, df, dq0, dq1, c, lse, negd, t * 64, kvlen, myq, a.causal, lane);
-    }
-    if (t + 1 < nt) {
-      char* nx = smem + ((t + 1) & 1) * 16384;
-      store64(nx, rk);
-      store64(nx + 8192, rv);
-    }
-    __syncthreads();
-  }
-  const bool qvalid = active && myq < S;
-  float c0[16], c1[16];  // the stored bf16 values, for the bias column sums
-  // dQ of this query: dims d and d + 32 (a RoPE pair) sit in dq0[r] / dq1[r] of the same lane, so the inverse
-  // rotation and the bf16 store need no exchange (no f32 workspace, no finalize launch)
-  const long qi = qvalid ? myq : 0;  // rows past S (no store) index row 0 of dq and of the RoPE tables
-  bf16* qrow = a.dq + ((long)b * S + qi) * a.lddq + h * 64;
-  float4 rtc[4], rts[4];
-  if (a.rcos) rope_lane_tables(a.rcos, a.rsin, qi, hl, rtc, rts);
-#pragma unroll
-  for (int g = 0; g < 4; ++g) {
-    const int d = 8 * g + 4 * hl;
-    bf16x4 v0, v1;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      float x0 = dq0[4 * g + e] * a.scale, x1 = dq1[4 * g + e] * a.scale;
-      if (a.rcos) {
-        const float cs = reinterpret_cast<const float*>(&rtc[g])[e], sn = reinterpret_cast<const float*>(&rts[g])[e];
-        const float y0 = x0 * cs + x1 * sn, y1 = x1 * cs - x0 * sn;  // RoPE^T (rope_pair, inverse)
-        x0 = y0;
-        x1 = y1;
-      }
-      v0[e] = (bf16)x0;
-      v1[e] = (bf16)x1;
-      c0[4 * g + e] = qvalid ? (float)v0[e] : 0.f;
-      c1[4 * g + e] = qvalid ? (float)v1[e] : 0.f;
-    }
-    if (qvalid) {
-      *reinterpret_cast<bf16x4*>(qrow + d) = v0;
-      *reinterpret_cast<bf16x4*>(qrow + 32 + d) = v1;
-    }
-  }
-  if (a.dbq) {
-    __shared__ float red[256];
-    block_colsum64(smem, red, c0, c1, a.dbq + h * 64, lane, w);
-  }
-}
-
-// ---- LDS-DMA staged forms (round 4) --------------------------------------------------------------------------------
-// The kernels above stage every K/V (or Q/dO) tile through registers: global loads issued one tile ahead, then
-// ds_write_b128 into the other half of a 2-slot LDS ring, one barrier per tile. PMC (profiles/round3_final_pmc.txt):
-// the ViT backward passes wait 31-37 % of their wave cycles (s_waitcnt / barrier) at MFMA busy 0.31; with the softmax
-// removed the forward structure alone ran at ~860 TF. Here tiles arrive by LDS-DMA (buffer_load_dwordx4 ... lds, the
-// v3 GEMM's staging): a ring of NSLOT slots, each tile issued NSLOT - 1 tiles ahead right after the barrier that frees
-// its slot, a counted vmcnt before that barrier (every wave issues the same number of pieces per tile; tiles past the
-// end are all-sentinel pieces that land zeros in a slot nobody reads), no staging registers, no ds_write. The compute
-// bodies (fwd_tile, bwd_dq_tile, bwd_kv_chunk) are the register-staged kernels' own, so the outputs are identical.
+// ---- the kernels: tiles staged by LDS-DMA (round 4) ----------------------------------------------------------------
+// Tiles arrive by LDS-DMA (buffer_load_dwordx4 ... lds, the v3 GEMM's staging): a ring of NSLOT slots, each tile
+// issued NSLOT - 1 tiles ahead right after the barrier that frees its slot, a counted vmcnt before that barrier (every
+// wave issues the same number of pieces per tile; tiles past the end are all-sentinel pieces that land zeros in a slot
+// nobody reads), no staging registers, no ds_write. (The round-1..3 register-staged forms - global loads one tile
+// ahead, ds_write_b128 into a 2-slot ring - and the round-4 8-wave ping-pong forms, 1.5x slower on the backward, were
+// retired in round 6; the compute bodies fwd_tile, bwd_dq_tile and bwd_kv_chunk are theirs.)
 constexpr unsigned kAttnSent = 0x7FFFFFF0u;  // past every descriptor: the DMA lands zeros
 
 __device__ __forceinline__ int sw_xor(int row) { return (((row >> 1) & 1) << 2) | ((row >> 2) & 3); }  // sw_off's swizzle
@@ -869,7 +486,8 @@ __device__ __forceinline__ void tail_axpy(const bf16* row, float w, f32x16& acc0
 #endif
 #endif
 
-// forward: attn_fwd_kernel with the K/V tiles of the (b, kv-head) streamed through an NSLOT ring (16 KiB per slot)
+// forward: one workgroup = 4 waves = 128 queries of one (b, h); the K/V tiles of the (b, kv-head) streamed through an
+// NSLOT ring (16 KiB per slot), fwd_tile per 64-key tile
 __global__ __launch_bounds__(256, ATTN_FWD_OCC) void attn_fwd_dma_kernel(AttnArgs a) {
   constexpr int NS = ATTN_NSLOT;
   __shared__ __attribute__((aligned(1024))) char smem[NS * 16384];
@@ -972,7 +590,7 @@ __global__ __launch_bounds__(256, ATTN_FWD_OCC) void attn_fwd_dma_kernel(AttnArg
   if (hl == 0 && a.lse) a.lse[((long)b * a.Hq + h) * S + myq] = m + __log2f(lt);
 }
 
-// dQ pass: attn_bwd_dq_kernel with the K/V tiles through the NSLOT ring
+// dQ pass (the forward's shape): 128 queries of one (b, h) per workgroup, the K/V tiles through the NSLOT ring
 __global__ __launch_bounds__(256, ATTN_DQ_OCC) void attn_bwd_dq_dma_kernel(AttnArgs a) {
   constexpr int NS = ATTN_NSLOT;
   __shared__ __attribute__((aligned(1024))) char smem[NS * 16384];
@@ -1049,13 +667,8 @@ __global__ __launch_bounds__(256, ATTN_DQ_OCC) void attn_bwd_dq_dma_kernel(AttnA
     const char* Vl = Kl + 8192;
     if (active && !(a.causal && t * 64 > q0 + 31)) {
       const int kfull = a.causal ? min(kvlen, q0 + 1) : kvlen;
-#if ATTN_DQ_SER
-      if ((t + 1) * 64 <= kfull) bwd_dq_tile_ser<false>(Kl, Vl, qf, df, dq0, dq1, c, lse, -dlt, t * 64, kvlen, myq, false, lane);
-      else bwd_dq_tile_ser<true>(Kl, Vl, qf, df, dq0, dq1, c, lse, -dlt, t * 64, kvlen, myq, a.causal, lane);
-#else
       if ((t + 1) * 64 <= kfull) bwd_dq_tile<false>(Kl, Vl, qf, df, dq0, dq1, c, lse, negd, t * 64, kvlen, myq, false, lane);
       else bwd_dq_tile<true>(Kl, Vl, qf, df, dq0, dq1, c, lse, negd, t * 64, kvlen, myq, a.causal, lane);
-#endif
     }
   }
   wait_vmcnt<0>();
@@ -1104,242 +717,7 @@ __global__ __launch_bounds__(256, ATTN_DQ_OCC) void attn_bwd_dq_dma_kernel(AttnA
   }
 }
 
-// ---- ping-pong dQ pass (round 4) --------------------------------------------------------------------------------
-// 8 waves per workgroup: group A (waves 0-3) and group B (waves 4-7) hold the SAME 128 queries (32 per wave, wave
-// w & 3) and split the key tiles by parity (A: even, B: odd). Each wave alternates an MFMA phase (S = K Q^T and
-// dP = V dO^T - delta of its current tile, 16 MFMAs, plus dQ^T += K^T dS^T of its previous tile, 8 MFMAs) and a VALU
-// phase (p = exp2(S c - lse), dS = p dP, the bf16 dS^T fragments), and the two groups run one phase apart, so every
-// SIMD holds one wave in its matrix phase beside one in its VALU phase (MI355X_MICROARCH.md 'Two waves per SIMD': the
-// matrix pipe and the VALU issue of a SIMD run two waves' complementary segments concurrently). One s_barrier per
-// phase for the 8 waves; K/V tiles arrive by LDS-DMA into a PP_NSL-slot ring, tile ph + PP_D issued at the start of
-// phase ph (tile t is read in phases t and t + 2). At the end group B hands its partial dQ to group A through LDS.
-// Same arithmetic per (query, key) as attn_bwd_dq_kernel; the dQ sum is split in two halves (even / odd key tiles)
-// added once, so the output differs from the single-chain kernels by f32 rounding only.
-#ifndef PP_NSL
-#define PP_NSL 5
-#endif
-constexpr int PP_D = PP_NSL - 3;  // DMA distance in tiles (the slot of tile ph + D held tile ph + D - NSL <= ph - 3)
-
-template <bool MASK>
-__device__ __forceinline__ void pp_sdp(const char* Kl, const char* Vl, const bf16x8 (&qf)[4], const bf16x8 (&df)[4],
-                                       const f32x16& negd, f32x16 (&s)[2], f32x16 (&dp)[2], int lane) {
-#pragma unroll
-  for (int kb = 0; kb < 2; ++kb) {
-#pragma unroll
-    for (int r = 0; r < 16; ++r) s[kb][r] = 0.f;
-    s[kb] = mfma32(row_frag(Kl, kb * 32, 0, lane), qf[0], s[kb]);
-    dp[kb] = mfma32(row_frag(Vl, kb * 32, 0, lane), df[0], negd);
-#pragma unroll
-    for (int kk = 1; kk < 4; ++kk) {
-      s[kb] = mfma32(row_frag(Kl, kb * 32, kk, lane), qf[kk], s[kb]);
-      dp[kb] = mfma32(row_frag(Vl, kb * 32, kk, lane), df[kk], dp[kb]);
-    }
-  }
-}
-
-template <bool MASK>
-__device__ __forceinline__ void pp_ds(const f32x16 (&s)[2], const f32x16 (&dp)[2], bf16x8 (&dsb)[2][2], float c,
-                                      float lse, int key0, int kvlen, int myq, bool causal, int lane) {
-  const int hl = lane >> 5;
-#pragma unroll
-  for (int kb = 0; kb < 2; ++kb) {
-    f32x16 ds;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[kb][r], c, -lse));
-      if constexpr (MASK) {
-        const int key = key0 + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
-        const bool ok = (key < kvlen) & (!causal | (key <= myq));
-        p = ok ? p : 0.f;
-      }
-      ds[r] = p * dp[kb][r];
-    }
-    dsb[kb][0] = acc_frag(ds, 0);
-    dsb[kb][1] = acc_frag(ds, 1);
-  }
-}
-
-__device__ __forceinline__ void pp_dq(const char* Kl, const bf16x8 (&dsb)[2][2], f32x16& dq0, f32x16& dq1, int lane) {
-#pragma unroll
-  for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-    for (int st = 0; st < 2; ++st) {
-      dq0 = mfma32(tr_frag(Kl, kb * 32 + 16 * st, 0, lane), dsb[kb][st], dq0);
-      dq1 = mfma32(tr_frag(Kl, kb * 32 + 16 * st, 32, lane), dsb[kb][st], dq1);
-    }
-}
-
-__global__ __launch_bounds__(512, 1) void attn_bwd_dq_pp_kernel(AttnArgs a) {
-  constexpr int NS = PP_NSL, D = PP_D;
-  __shared__ __attribute__((aligned(1024))) char smem[NS * 16384];
-  const BlockCoord bc = attn_block((a.S + 127) / 128, a.Hq, a.Hkv, a.B, a.causal ? 1 : 0, a.tail_first);
-  const int qb = bc.blk, h = bc.h, b = bc.b;
-  const int hk = h / (a.Hq / a.Hkv);
-  const int S = a.S;
-  const int kvlen = a.seqlens ? min(a.seqlens[b], S) : S;
-  const int tid = threadIdx.x, lane = tid & 63, hl = lane >> 5;
-  const int w = tid >> 6;
-  const int wu = __builtin_amdgcn_readfirstlane(w);
-  const int grp = wu >> 2;  // 0 = A (even key tiles), 1 = B (odd key tiles)
-  const int q0 = qb * 128 + (w & 3) * 32;
-  const int myq = q0 + (lane & 31);
-  const bool active = q0 < S;
-  const float c = a.scale * LOG2E;
-  const bf16* kbase = a.k + (long)b * S * a.ldk + hk * 64;
-  const bf16* vbase = a.v + (long)b * S * a.ldv + hk * 64;
-  const __amdgpu_buffer_rsrc_t rk = slice_rsrc(kbase, a.ldk, S, 2), rv = slice_rsrc(vbase, a.ldv, S, 2);
-
-  bf16x8 qf[4], df[4];
-  float lse = 0.f, dlt = 0.f;
-  {
-    const int qr = min(myq, S - 1);
-    const bf16* qrow = a.q + ((long)b * S + qr) * a.ldq + h * 64;
-    const bf16* drow = a.dout + ((long)b * S + qr) * a.lddo + h * 64;
-    const bf16* orow = a.o + ((long)b * S + qr) * a.ldo + h * 64;
-    bf16x8 of[4];
-#pragma unroll
-    for (int kk = 0; kk < 4; ++kk) {
-      qf[kk] = *reinterpret_cast<const bf16x8*>(qrow + 16 * kk + 8 * hl);
-      df[kk] = *reinterpret_cast<const bf16x8*>(drow + 16 * kk + 8 * hl);
-      of[kk] = *reinterpret_cast<const bf16x8*>(orow + 16 * kk + 8 * hl);
-    }
-    const long li = ((long)b * a.Hq + h) * S + qr;
-    lse = a.lse[li];
-#pragma unroll
-    for (int kk = 0; kk < 4; ++kk)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) dlt = __builtin_fmaf((float)df[kk][j], (float)of[kk][j], dlt);
-    dlt += __shfl_xor(dlt, 32, 64);
-    if (grp == 0 && hl == 0 && active && myq < S) const_cast<float*>(a.delta)[li] = -dlt;
-  }
-  f32x16 negd;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) negd[r] = -dlt;
-  int kend = kvlen;
-  if (a.causal) kend = min(kend, qb * 128 + 128);
-  const int nt = (kend + 63) / 64;
-  const int ng = grp == 0 ? (nt + 1) / 2 : nt / 2;  // this group's tiles: grp, grp + 2, ...
-  // per-phase DMA: 16 pieces per tile, two per wave (waves 0-3: K pieces 0-7, waves 4-7: V pieces 0-7)
-  int lo[2], lr[2];
-  dma_lane_offsets(grp ? a.ldv : a.ldk, wu & 3, lane, lo, lr);
-  auto issue = [&](int t) {
-    char* slot = smem + (t % NS) * 16384 + grp * 8192;
-    const int r0 = t < nt ? t * 64 : S;
-    dma_tile64(grp ? rv : rk, slot, grp ? a.ldv : a.ldk, r0, S, wu & 3, lo, lr);
-  };
-  f32x16 dq0, dq1, s[2], dp[2];
-  bf16x8 dsb[2][2];
-#pragma unroll
-  for (int r = 0; r < 16; ++r) { dq0[r] = 0.f; dq1[r] = 0.f; }
-  drain_known_vm();
-#pragma unroll
-  for (int j = 0; j < D; ++j) issue(j);
-  // phases: group g's tile j (key tile 2j + g) has its MFMA phase at ph = 2j + g + 2j... (local phase 2j), its VALU
-  // phase one later, and its dQ MFMAs in the next MFMA phase (local 2j + 2); B runs one phase behind A
-  const int nph = max(2 * ((nt + 1) / 2) + 1, 2 * (nt / 2) + 2);
-  for (int ph = 0; ph < nph; ++ph) {
-    wait_vmcnt<2 * (D - 1)>();  // this wave's pieces of tile ph landed (tiles ph+1 .. ph+D-1 may still fly)
-    __syncthreads();             // every wave's pieces landed; phase ph - 1 finished everywhere (frees tile ph-3's slot)
-    issue(ph + D);
-    const int loc = ph - grp;
-    if (loc < 0 || !active) continue;
-    const int j = loc >> 1;
-    if ((loc & 1) == 0) {  // MFMA phase: dQ of the previous tile, then S / dP of tile j
-      if (j >= 1) {
-        const int tp = 2 * (j - 1) + grp;
-        if (!(a.causal && tp * 64 > q0 + 31)) pp_dq(smem + (tp % NS) * 16384, dsb, dq0, dq1, lane);
-      }
-      if (j < ng) {
-        const int t = 2 * j + grp;
-        if (!(a.causal && t * 64 > q0 + 31)) {
-          const char* Kl = smem + (t % NS) * 16384;
-          pp_sdp<false>(Kl, Kl + 8192, qf, df, negd, s, dp, lane);
-        }
-      }
-    } else if (j < ng) {  // VALU phase of tile j
-      const int t = 2 * j + grp;
-      if (!(a.causal && t * 64 > q0 + 31)) {
-        const int kfull = a.causal ? min(kvlen, q0 + 1) : kvlen;
-        if ((t + 1) * 64 <= kfull) pp_ds<false>(s, dp, dsb, c, lse, t * 64, kvlen, myq, false, lane);
-        else pp_ds<true>(s, dp, dsb, c, lse, t * 64, kvlen, myq, a.causal, lane);
-      }
-    }
-  }
-  wait_vmcnt<0>();
-  __syncthreads();
-  // group B's partial dQ -> group A through LDS ([4 waves][2][16 regs][64 lanes] f32 = 32 KiB)
-  float* xch = reinterpret_cast<float*>(smem);
-  if (grp == 1) {
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      xch[(((w & 3) * 2 + 0) * 16 + r) * 64 + lane] = dq0[r];
-      xch[(((w & 3) * 2 + 1) * 16 + r) * 64 + lane] = dq1[r];
-    }
-  }
-  __syncthreads();
-  const bool qvalid = grp == 0 && active && myq < S;
-  float c0[16], c1[16];
-  if (grp == 0) {
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      dq0[r] += xch[(((w & 3) * 2 + 0) * 16 + r) * 64 + lane];
-      dq1[r] += xch[(((w & 3) * 2 + 1) * 16 + r) * 64 + lane];
-    }
-    const long qi = qvalid ? myq : 0;
-    bf16* qrow = a.dq + ((long)b * S + qi) * a.lddq + h * 64;
-    float4 rtc[4], rts[4];
-    if (a.rcos) rope_lane_tables(a.rcos, a.rsin, qi, hl, rtc, rts);
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int d = 8 * g + 4 * hl;
-      bf16x4 v0, v1;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        float x0 = dq0[4 * g + e] * a.scale, x1 = dq1[4 * g + e] * a.scale;
-        if (a.rcos) {
-          const float cs = reinterpret_cast<const float*>(&rtc[g])[e], sn = reinterpret_cast<const float*>(&rts[g])[e];
-          const float y0 = x0 * cs + x1 * sn, y1 = x1 * cs - x0 * sn;
-          x0 = y0;
-          x1 = y1;
-        }
-        v0[e] = (bf16)x0;
-        v1[e] = (bf16)x1;
-        c0[4 * g + e] = qvalid ? (float)v0[e] : 0.f;
-        c1[4 * g + e] = qvalid ? (float)v1[e] : 0.f;
-      }
-      if (qvalid) {
-        *reinterpret_cast<bf16x4*>(qrow + d) = v0;
-        *reinterpret_cast<bf16x4*>(qrow + 32 + d) = v1;
-      }
-    }
-  }
-  if (a.dbq) {  // bias column sums over group A's 128 rows (block_colsum64's scheme; group B only joins the barriers)
-    __shared__ float red[256];
-    __syncthreads();  // the exchange area is read
-    float* tl = reinterpret_cast<float*>(smem) + (w & 3) * 2048;
-    const int q = lane & 31;
-    if (grp == 0) {
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int c4 = 2 * g + hl;
-        *reinterpret_cast<float4*>(tl + q * 64 + ((c4 ^ (q & 15)) << 2)) =
-            make_float4(c0[4 * g], c0[4 * g + 1], c0[4 * g + 2], c0[4 * g + 3]);
-        *reinterpret_cast<float4*>(tl + q * 64 + (((8 + c4) ^ (q & 15)) << 2)) =
-            make_float4(c1[4 * g], c1[4 * g + 1], c1[4 * g + 2], c1[4 * g + 3]);
-      }
-      __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      float sum = 0.f;
-      const int c4 = lane >> 2, e = lane & 3;
-#pragma unroll
-      for (int r = 0; r < 32; ++r) sum += tl[r * 64 + ((c4 ^ (r & 15)) << 2) + e];
-      red[w * 64 + lane] = sum;
-    }
-    __syncthreads();
-    if (w == 0) atomicAdd(a.dbq + h * 64 + lane, red[lane] + red[64 + lane] + red[128 + lane] + red[192 + lane]);
-  }
-}
-
-// dK/dV pass: attn_bwd_kv_kernel with each (q-head, 64-query chunk) stage - Q tile, dO tile, lse[64], -delta[64] -
+// dK/dV pass: 128 keys of one (b, kv-head) per workgroup, sweeping the group's q-heads; each (q-head, 64-query chunk) stage - Q tile, dO tile, lse[64], -delta[64] -
 // through the NSLOT ring (16.5 KiB per slot). Per wave and stage 5 DMA instructions: Q and dO pieces (2 + 2) and one
 // 4-B row piece (wave 0: lse, wave 1: -delta, waves 2-3: a sentinel piece into the slot's scratch row).
 constexpr int KV_SLOT = 16384 + 4 * 256;
@@ -1499,436 +877,6 @@ __global__ __launch_bounds__(256, ATTN_KV_OCC) void attn_bwd_kv_dma_kernel(AttnA
   }
 }
 
-// bf16 fragments packed into the low 8 dwords of the f32 accumulator they were computed from (no separate fragment
-// registers: P and dS of a stage live in the registers of its S and dP accumulators until the next MFMA phase)
-__device__ __forceinline__ void pack_frags(f32x16& x, const bf16x8& f0, const bf16x8& f1) {
-  const uint4 u0 = __builtin_bit_cast(uint4, f0), u1 = __builtin_bit_cast(uint4, f1);
-  x[0] = __uint_as_float(u0.x); x[1] = __uint_as_float(u0.y); x[2] = __uint_as_float(u0.z); x[3] = __uint_as_float(u0.w);
-  x[4] = __uint_as_float(u1.x); x[5] = __uint_as_float(u1.y); x[6] = __uint_as_float(u1.z); x[7] = __uint_as_float(u1.w);
-}
-__device__ __forceinline__ bf16x8 packed_frag(const f32x16& x, int st) {
-  const uint4 u = make_uint4(__float_as_uint(x[4 * st]), __float_as_uint(x[4 * st + 1]), __float_as_uint(x[4 * st + 2]),
-                             __float_as_uint(x[4 * st + 3]));
-  return __builtin_bit_cast(bf16x8, u);
-}
-
-// ---- ping-pong forward (round 4) ------------------------------------------------------------------------------
-// attn_fwd_kernel's work in 8 waves: groups A / B hold the same 128 queries and split the key tiles by parity. MFMA
-// phase: O^T += V^T P^T (and the row sums) of the previous tile, then S^T = K Q^T of the current one; VALU phase: the
-// max, the lazy rescale of O / l, p = exp2(s c - m) packed to bf16 in S's registers. Each group keeps its own (m, l,
-// O); group B's are merged into A's through LDS at the end (O = O_A 2^(m_A - m) + O_B 2^(m_B - m), same for l).
-__global__ __launch_bounds__(512, 1) void attn_fwd_pp_kernel(AttnArgs a) {
-  constexpr int NS = PP_NSL, D = PP_D;
-  __shared__ __attribute__((aligned(1024))) char smem[NS * 16384];
-  const BlockCoord bc = attn_block((a.S + 127) / 128, a.Hq, a.Hkv, a.B, a.causal ? 1 : 0, a.tail_first);
-  const int qb = bc.blk, h = bc.h, b = bc.b;
-  const int hk = h / (a.Hq / a.Hkv);
-  const int S = a.S;
-  const int kvlen = a.seqlens ? min(a.seqlens[b], S) : S;
-  const int tid = threadIdx.x, lane = tid & 63, hl = lane >> 5;
-  const int w = tid >> 6;
-  const int wu = __builtin_amdgcn_readfirstlane(w);
-  const int grp = wu >> 2;
-  const int q0 = qb * 128 + (w & 3) * 32;
-  const int myq = q0 + (lane & 31);
-  const bool active = q0 < S;
-  const float c = a.scale * LOG2E;
-  const bf16* kbase = a.k + (long)b * S * a.ldk + hk * 64;
-  const bf16* vbase = a.v + (long)b * S * a.ldv + hk * 64;
-  const __amdgpu_buffer_rsrc_t rk = slice_rsrc(kbase, a.ldk, S, 2), rv = slice_rsrc(vbase, a.ldv, S, 2);
-  bf16x8 qf[4];
-  {
-    const bf16* qrow = a.q + ((long)b * S + min(myq, S - 1)) * a.ldq + h * 64;
-#pragma unroll
-    for (int kk = 0; kk < 4; ++kk) {
-      bf16x8 z;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) z[j] = (bf16)0.f;
-      qf[kk] = myq < S ? *reinterpret_cast<const bf16x8*>(qrow + 16 * kk + 8 * hl) : z;
-    }
-  }
-  int kend = kvlen;
-  if (a.causal) kend = min(kend, qb * 128 + 128);
-  const int nt = (kend + 63) / 64;
-  const int ng = grp == 0 ? (nt + 1) / 2 : nt / 2;
-  int lo[2], lr[2];
-  dma_lane_offsets(grp ? a.ldv : a.ldk, wu & 3, lane, lo, lr);
-  auto issue = [&](int t) {
-    char* slot = smem + (t % NS) * 16384 + grp * 8192;
-    const int r0 = t < nt ? t * 64 : S;
-    dma_tile64(grp ? rv : rk, slot, grp ? a.ldv : a.ldk, r0, S, wu & 3, lo, lr);
-  };
-  f32x16 o0, o1, lacc, s2[2];
-#pragma unroll
-  for (int r = 0; r < 16; ++r) { o0[r] = 0.f; o1[r] = 0.f; lacc[r] = 0.f; }
-  float m = -1e30f;
-  bf16x8 ones;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) ones[j] = (bf16)1.0f;
-  bool prev_on = false;
-  int prev_t = 0;
-  drain_known_vm();
-#pragma unroll
-  for (int j = 0; j < D; ++j) issue(j);
-  const int nph = max(2 * ((nt + 1) / 2) + 1, 2 * (nt / 2) + 2);
-  for (int ph = 0; ph < nph; ++ph) {
-    wait_vmcnt<2 * (D - 1)>();
-    __syncthreads();
-    issue(ph + D);
-    const int loc = ph - grp;
-    if (loc < 0 || !active) continue;
-    const int j = loc >> 1;
-    if ((loc & 1) == 0) {  // MFMA phase: P V (and row sums) of the previous tile, S of this one
-      if (j >= 1 && prev_on) {
-        const char* Vl = smem + (prev_t % NS) * 16384 + 8192;
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-          for (int st = 0; st < 2; ++st) {
-            const bf16x8 pb = packed_frag(s2[kb], st);
-            o0 = mfma32(tr_frag(Vl, kb * 32 + 16 * st, 0, lane), pb, o0);
-            o1 = mfma32(tr_frag(Vl, kb * 32 + 16 * st, 32, lane), pb, o1);
-            lacc = mfma32(ones, pb, lacc);
-          }
-      }
-      prev_on = false;
-      if (j < ng) {
-        const int t = 2 * j + grp;
-        if (!(a.causal && t * 64 > q0 + 31)) {
-          const char* Kl = smem + (t % NS) * 16384;
-#pragma unroll
-          for (int kb = 0; kb < 2; ++kb) {
-#pragma unroll
-            for (int r = 0; r < 16; ++r) s2[kb][r] = 0.f;
-#pragma unroll
-            for (int kk = 0; kk < 4; ++kk) s2[kb] = mfma32(row_frag(Kl, kb * 32, kk, lane), qf[kk], s2[kb]);
-          }
-          prev_on = true;
-          prev_t = t;
-        }
-      }
-    } else if (j < ng && prev_on) {  // VALU phase: softmax of tile j
-      const int t = prev_t, key0 = t * 64;
-      const int kfull = a.causal ? min(kvlen, q0 + 1) : kvlen;
-      if ((t + 1) * 64 > kfull) {
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int key = key0 + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
-            const bool ok = (key < kvlen) & (!a.causal | (key <= myq));
-            s2[kb][r] = ok ? s2[kb][r] : MASKED;
-          }
-      }
-      float mx = s2[0][0];
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s2[kb][r]);
-      mx = half_swap_max(mx) * c;
-      if (__builtin_amdgcn_ballot_w64(mx > m + LAZY)) {
-        const float mnew = fmaxf(m, mx);
-        const float alpha = __builtin_amdgcn_exp2f(m - mnew);
-        m = mnew;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) { o0[r] *= alpha; o1[r] *= alpha; lacc[r] *= alpha; }
-      }
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb) {
-        f32x16 p;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) p[r] = __builtin_amdgcn_exp2f(__builtin_fmaf(s2[kb][r], c, -m));
-        pack_frags(s2[kb], acc_frag(p, 0), acc_frag(p, 1));
-      }
-    }
-  }
-  wait_vmcnt<0>();
-  __syncthreads();
-  // merge group B's (m, l, O) into group A's: [4 waves][o0 16 | o1 16 | l 16 | m][64] f32
-  float* xch = reinterpret_cast<float*>(smem);
-  float* xw = xch + (w & 3) * 49 * 64 + lane;
-  if (grp == 1) {
-#pragma unroll
-    for (int r = 0; r < 16; ++r) { xw[r * 64] = o0[r]; xw[(16 + r) * 64] = o1[r]; xw[(32 + r) * 64] = lacc[r]; }
-    xw[48 * 64] = m;
-  }
-  __syncthreads();
-  if (grp == 1 || !active || myq >= S) return;
-  const float mb = xw[48 * 64];
-  const float mm = fmaxf(m, mb);
-  const float fa = __builtin_amdgcn_exp2f(m - mm), fb = __builtin_amdgcn_exp2f(mb - mm);
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    o0[r] = o0[r] * fa + xw[r * 64] * fb;
-    o1[r] = o1[r] * fa + xw[(16 + r) * 64] * fb;
-  }
-  const float lt = lacc[0] * fa + xw[32 * 64] * fb;
-  const float inv = 1.0f / lt;
-  bf16* orow = a.o + ((long)b * S + myq) * a.ldo + h * 64;
-#pragma unroll
-  for (int g = 0; g < 4; ++g) {
-    const int d = 8 * g + 4 * hl;
-    bf16x4 v0, v1;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      v0[e] = (bf16)(o0[4 * g + e] * inv);
-      v1[e] = (bf16)(o1[4 * g + e] * inv);
-    }
-    *reinterpret_cast<bf16x4*>(orow + d) = v0;
-    *reinterpret_cast<bf16x4*>(orow + 32 + d) = v1;
-  }
-  if (hl == 0 && a.lse) a.lse[((long)b * a.Hq + h) * S + myq] = mm + __log2f(lt);
-}
-
-// ---- ping-pong dK/dV pass (round 4) ------------------------------------------------------------------------------
-// attn_bwd_kv_dma_kernel's work in 8 waves: groups A (waves 0-3) and B (4-7) hold the SAME 128 keys (32 per wave,
-// w & 3) and split the (q-head, 64-query chunk) stages by parity (A even, B odd). Per stage a wave runs an MFMA phase
-// (dV^T += dO^T P and dK^T += Q^T dS of its previous stage, 16 MFMAs, then S^T = Q K^T and dP^T = dO V^T - delta of
-// the current stage, 16 MFMAs) and a VALU phase (p, dS and their bf16 fragments), the groups one phase apart (see
-// attn_bwd_dq_pp_kernel). A stage's slot is read in phases it (S / dP), it + 1 (lse, delta) and it + 2 (dV / dK);
-// stage it + PP_D is issued at the start of phase it. Group B's partial dK / dV reach group A through LDS at the end.
-template <bool MASK>
-__device__ __forceinline__ void ppkv_valu(const float* lse_l, f32x16 (&sp)[2], f32x16 (&dp)[2], float c, int qc, int S,
-                                          int mykey, int kvlen, bool causal, int lane) {
-  const int hl = lane >> 5;
-#pragma unroll
-  for (int qa = 0; qa < 2; ++qa) {
-    f32x16 p16, d16;
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int ql = qa * 32 + 8 * g + 4 * hl;
-      const f32x4 L4 = *reinterpret_cast<const f32x4*>(lse_l + ql);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int r = 4 * g + e;
-        float p = __builtin_amdgcn_exp2f(__builtin_fmaf(sp[qa][r], c, -L4[e]));
-        if constexpr (MASK) {
-          const int q = qc + ql + e;
-          const bool ok = (q < S) & (mykey < kvlen) & (!causal | (mykey <= q));
-          p = ok ? p : 0.f;
-        }
-        p16[r] = p;
-        d16[r] = p * dp[qa][r];
-      }
-    }
-    pack_frags(sp[qa], acc_frag(p16, 0), acc_frag(p16, 1));
-    pack_frags(dp[qa], acc_frag(d16, 0), acc_frag(d16, 1));
-  }
-}
-
-__global__ __launch_bounds__(512, 1) void attn_bwd_kv_pp_kernel(AttnArgs a) {
-  constexpr int NS = PP_NSL, D = PP_D;
-  __shared__ __attribute__((aligned(1024))) char smem[NS * KV_SLOT > 65536 ? NS * KV_SLOT : 65536];
-  const BlockCoord bc = attn_block((a.S + 127) / 128, a.Hkv * a.nsplit, a.Hkv * a.nsplit, a.B, a.causal ? 2 : 0, a.tail_first);
-  const int kblk = bc.blk, hk = bc.h / a.nsplit, sp_ = bc.h % a.nsplit, b = bc.b;
-  const int G = a.Hq / a.Hkv;
-  const int hg0 = sp_ * a.hsplit;
-  const int ng = min(G, hg0 + a.hsplit) - hg0;
-  const int S = a.S;
-  const int kvlen = a.seqlens ? min(a.seqlens[b], S) : S;
-  const int tid = threadIdx.x, lane = tid & 63, hl = lane >> 5;
-  const int w = tid >> 6;
-  const int wu = __builtin_amdgcn_readfirstlane(w);
-  const int grp = wu >> 2;
-  const int k0 = kblk * 128;
-  const int kw0 = k0 + 32 * (w & 3);
-  const int mykey = kw0 + (lane & 31);
-  const float c = a.scale * LOG2E;
-
-  bf16x8 kf[4], vf[4];
-  {
-    const int kr = min(mykey, S - 1);
-    const bf16* kp = a.k + ((long)b * S + kr) * a.ldk + hk * 64;
-    const bf16* vp = a.v + ((long)b * S + kr) * a.ldv + hk * 64;
-#pragma unroll
-    for (int kk = 0; kk < 4; ++kk) {
-      kf[kk] = *reinterpret_cast<const bf16x8*>(kp + 16 * kk + 8 * hl);
-      vf[kk] = *reinterpret_cast<const bf16x8*>(vp + 16 * kk + 8 * hl);
-    }
-  }
-  f32x16 dk0, dk1, dv0, dv1;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) { dk0[r] = dk1[r] = dv0[r] = dv1[r] = 0.f; }
-
-  const int qstart = a.causal ? (k0 / 64) * 64 : 0;
-  const int nch = qstart < S ? (S - qstart + 63) / 64 : 0;
-  const int nit = nch * ng;
-  // per stage 16 + 16 + 1 DMA pieces: waves 0-3 the Q tile (2 each), waves 4-7 the dO tile (2 each); the lse row by
-  // wave 0 and the -delta row by wave 4 (the other waves issue a sentinel row piece into the slot's scratch rows, so
-  // every wave issues 3 pieces per stage)
-  int lo[2], lr[2];
-  dma_lane_offsets(grp ? a.lddo : a.ldq, wu & 3, lane, lo, lr);
-  auto issue = [&](int it) {
-    char* slot = smem + (it % NS) * KV_SLOT;
-    const bool real = it < nit;
-    const int h = hk * G + hg0 + (real ? it / nch : 0), qc = real ? qstart + (it % nch) * 64 : S;
-    const bf16* src = grp ? a.dout + (long)b * S * a.lddo + h * 64 : a.q + (long)b * S * a.ldq + h * 64;
-    const long ld = grp ? a.lddo : a.ldq;
-    dma_tile64(slice_rsrc(src, ld, S, 2), slot + grp * 8192, ld, qc, S, wu & 3, lo, lr);
-    const long base = ((long)b * a.Hq + h) * S;
-    const int rowp = (wu & 3) == 0 ? grp : 2 + (wu & 1);  // waves 0 / 4: the lse / delta rows; others: scratch rows
-    const float* fsrc = grp ? a.delta + base : a.lse + base;
-    dma_row64_f32(__builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(fsrc), (short)0, S * 4, 0x00020000),
-                  slot + 16384 + 256 * rowp, qc, (wu & 3) == 0 ? S : 0, lane);
-  };
-
-  f32x16 spa[2], dpa[2];
-  int prev_qc = 0;
-  bool prev_on = false;
-  drain_known_vm();
-#pragma unroll
-  for (int j = 0; j < D; ++j) issue(j);
-  const int nph = max(2 * ((nit + 1) / 2) + 1, 2 * (nit / 2) + 2);
-  for (int ph = 0; ph < nph; ++ph) {
-    wait_vmcnt<3 * (D - 1)>();
-    __syncthreads();
-    issue(ph + D);
-    const int loc = ph - grp;
-    if (loc < 0 || kw0 >= kvlen) continue;
-    const int j = loc >> 1;
-    const int my_n = grp == 0 ? (nit + 1) / 2 : nit / 2;
-    if ((loc & 1) == 0) {  // MFMA phase: dV / dK of the previous stage, S / dP of this one
-      if (j >= 1 && prev_on) {
-        const int itp = 2 * (j - 1) + grp;
-        const char* slot = smem + (itp % NS) * KV_SLOT;
-#pragma unroll
-        for (int qa = 0; qa < 2; ++qa)
-#pragma unroll
-          for (int st = 0; st < 2; ++st) {
-            const bf16x8 pbf = packed_frag(spa[qa], st), sbf = packed_frag(dpa[qa], st);
-            dv0 = mfma32(tr_frag(slot + 8192, qa * 32 + 16 * st, 0, lane), pbf, dv0);
-            dv1 = mfma32(tr_frag(slot + 8192, qa * 32 + 16 * st, 32, lane), pbf, dv1);
-            dk0 = mfma32(tr_frag(slot, qa * 32 + 16 * st, 0, lane), sbf, dk0);
-            dk1 = mfma32(tr_frag(slot, qa * 32 + 16 * st, 32, lane), sbf, dk1);
-          }
-      }
-      prev_on = false;
-      if (j < my_n) {
-        const int it = 2 * j + grp;
-        const int qc = qstart + (it % nch) * 64;
-        if (!(a.causal && kw0 > qc + 63)) {
-          const char* slot = smem + (it % NS) * KV_SLOT;
-          const float* ld_ = reinterpret_cast<const float*>(slot + 16384);
-#pragma unroll
-          for (int qa = 0; qa < 2; ++qa) {
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {  // dP^T starts from -delta (stored negated) of each register's query
-              const f32x4 D4 = *reinterpret_cast<const f32x4*>(ld_ + 64 + qa * 32 + 8 * g + 4 * hl);
-#pragma unroll
-              for (int e = 0; e < 4; ++e) { spa[qa][4 * g + e] = 0.f; dpa[qa][4 * g + e] = D4[e]; }
-            }
-#pragma unroll
-            for (int kk = 0; kk < 4; ++kk) {
-              spa[qa] = mfma32(row_frag(slot, qa * 32, kk, lane), kf[kk], spa[qa]);
-              dpa[qa] = mfma32(row_frag(slot + 8192, qa * 32, kk, lane), vf[kk], dpa[qa]);
-            }
-          }
-          prev_on = true;
-          prev_qc = qc;
-        }
-      }
-    } else if (j < my_n && prev_on) {  // VALU phase of stage j (prev_on: its S / dP ran)
-      const int it = 2 * j + grp;
-      const char* slot = smem + (it % NS) * KV_SLOT;
-      const float* lse_l = reinterpret_cast<const float*>(slot + 16384);
-      const int qc = prev_qc;
-      const bool full = (qc + 64 <= S) && (kw0 + 32 <= kvlen) && (!a.causal || kw0 + 31 <= qc);
-      if (full) ppkv_valu<false>(lse_l, spa, dpa, c, qc, S, mykey, kvlen, false, lane);
-      else ppkv_valu<true>(lse_l, spa, dpa, c, qc, S, mykey, kvlen, a.causal, lane);
-    }
-  }
-  wait_vmcnt<0>();
-  __syncthreads();
-  // group B's partial dK / dV -> group A: [4 waves][4 accumulators][16][64] f32 = 64 KiB
-  float* xch = reinterpret_cast<float*>(smem);
-  if (grp == 1) {
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      float* xw = xch + ((w & 3) * 4) * 1024 + r * 64 + lane;
-      xw[0] = dk0[r];
-      xw[1024] = dk1[r];
-      xw[2048] = dv0[r];
-      xw[3072] = dv1[r];
-    }
-  }
-  __syncthreads();
-  const bool kvalid = grp == 0 && mykey < S;
-  float ck0[16], ck1[16], cv0[16], cv1[16];
-#pragma unroll
-  for (int r = 0; r < 16; ++r) ck0[r] = ck1[r] = cv0[r] = cv1[r] = 0.f;
-  if (grp == 0) {
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const float* xw = xch + ((w & 3) * 4) * 1024 + r * 64 + lane;
-      dk0[r] += xw[0];
-      dk1[r] += xw[1024];
-      dv0[r] += xw[2048];
-      dv1[r] += xw[3072];
-    }
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int d = 8 * g + 4 * hl;
-      if (!kvalid) {
-      } else if (a.dk_acc) {
-        const long off = (long)sp_ * a.B * S * (a.Hkv * 64) + ((long)b * S + mykey) * (a.Hkv * 64) + hk * 64;
-        float* kp = a.dk_acc + off;
-        float* vp = a.dv_acc + off;
-        *reinterpret_cast<float4*>(kp + d) = make_float4(dk0[4 * g] * a.scale, dk0[4 * g + 1] * a.scale, dk0[4 * g + 2] * a.scale, dk0[4 * g + 3] * a.scale);
-        *reinterpret_cast<float4*>(kp + 32 + d) = make_float4(dk1[4 * g] * a.scale, dk1[4 * g + 1] * a.scale, dk1[4 * g + 2] * a.scale, dk1[4 * g + 3] * a.scale);
-        *reinterpret_cast<float4*>(vp + d) = make_float4(dv0[4 * g], dv0[4 * g + 1], dv0[4 * g + 2], dv0[4 * g + 3]);
-        *reinterpret_cast<float4*>(vp + 32 + d) = make_float4(dv1[4 * g], dv1[4 * g + 1], dv1[4 * g + 2], dv1[4 * g + 3]);
-      } else {
-        bf16* kp = a.dk + ((long)b * S + mykey) * a.lddk + hk * 64;
-        bf16* vp = a.dv + ((long)b * S + mykey) * a.lddv + hk * 64;
-        bf16x4 k0v, k1v, v0v, v1v;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          k0v[e] = (bf16)(dk0[4 * g + e] * a.scale);
-          k1v[e] = (bf16)(dk1[4 * g + e] * a.scale);
-          v0v[e] = (bf16)dv0[4 * g + e];
-          v1v[e] = (bf16)dv1[4 * g + e];
-          ck0[4 * g + e] = (float)k0v[e];
-          ck1[4 * g + e] = (float)k1v[e];
-          cv0[4 * g + e] = (float)v0v[e];
-          cv1[4 * g + e] = (float)v1v[e];
-        }
-        *reinterpret_cast<bf16x4*>(kp + d) = k0v;
-        *reinterpret_cast<bf16x4*>(kp + 32 + d) = k1v;
-        *reinterpret_cast<bf16x4*>(vp + d) = v0v;
-        *reinterpret_cast<bf16x4*>(vp + 32 + d) = v1v;
-      }
-    }
-  }
-  if (a.dbk) {  // bias column sums over group A's 128 keys; group B joins the barriers only
-    __shared__ float red[256];
-    for (int pass = 0; pass < 2; ++pass) {
-      const float (&v0)[16] = pass ? cv0 : ck0;
-      const float (&v1)[16] = pass ? cv1 : ck1;
-      __syncthreads();
-      float* tl = reinterpret_cast<float*>(smem) + (w & 3) * 2048;
-      const int q = lane & 31;
-      if (grp == 0) {
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int c4 = 2 * g + hl;
-          *reinterpret_cast<float4*>(tl + q * 64 + ((c4 ^ (q & 15)) << 2)) =
-              make_float4(v0[4 * g], v0[4 * g + 1], v0[4 * g + 2], v0[4 * g + 3]);
-          *reinterpret_cast<float4*>(tl + q * 64 + (((8 + c4) ^ (q & 15)) << 2)) =
-              make_float4(v1[4 * g], v1[4 * g + 1], v1[4 * g + 2], v1[4 * g + 3]);
-        }
-        __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        float sum = 0.f;
-        const int c4 = lane >> 2, e = lane & 3;
-#pragma unroll
-        for (int r = 0; r < 32; ++r) sum += tl[r * 64 + ((c4 ^ (r & 15)) << 2) + e];
-        red[w * 64 + lane] = sum;
-      }
-      __syncthreads();
-      if (w == 0) atomicAdd((pass ? a.dbv : a.dbk) + hk * 64 + lane, red[lane] + red[64 + lane] + red[128 + lane] + red[192 + lane]);
-    }
-  }
-}
-
 __device__ __forceinline__ void rope_pair(float& x0, float& x1, float cs, float sn, bool inverse) {
   const float a = x0, b = x1;
   if (!inverse) { x0 = a * cs - b * sn; x1 = b * cs + a * sn; }
@@ -2035,8 +983,6 @@ struct DecMfmaArgs {
 
 constexpr int kDecKeys = 1024;
 
-// PUBLISH: the output rows are handed to the O-projection workgroups of the same launch (agent-scope stores).
-template <bool PUBLISH>
 __device__ __forceinline__ void dec_attn_mfma_body(const DecMfmaArgs& a, int g, char* smem) {
   char* Vl = smem;                          // [kDecKeys][64] bf16, swizzled (128 KB); reused for the O^T partials
   char* Ql = smem + kDecKeys * 128;         // [32][64] bf16 rotated q heads (rows >= G zero), swizzled
@@ -2191,119 +1137,14 @@ __device__ __forceinline__ void dec_attn_mfma_body(const DecMfmaArgs& a, int g, 
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc += op[(i * G + hh) * 64 + d];
     const bf16 o = (bf16)(acc / Lh[hh]);
-    if constexpr (PUBLISH)
-      __hip_atomic_store(reinterpret_cast<unsigned short*>(a.out) + (g * G + hh) * 64 + d, __builtin_bit_cast(unsigned short, o),
-                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else
-      a.out[(g * G + hh) * 64 + d] = o;
+    a.out[(g * G + hh) * 64 + d] = o;
   }
 }
 
 __global__ __launch_bounds__(1024) void dec_attn_mfma_kernel(DecMfmaArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   if (a.st[2]) return;
-  dec_attn_mfma_body<false>(a, blockIdx.x, smem);
-}
-
-// Attention + O projection in one launch: workgroups [0, Hkv) run the attention above and publish their rows of the
-// attention output; workgroups [Hkv, Hkv + nO) own 16 rows of W_o each (one per wave), load their weight rows at
-// launch (the weight latency overlaps the attention), wait for the Hkv publications on a counter, then read the output
-// row and add W_o rows . out into the f32 residual. Every workgroup of this launch is resident at once (2 + 56 of 1024
-// threads on 256 CUs), and the wait is bounded, so a lost publication cannot hang the queue (the row is then skipped
-// and the error counter set). Hand-off: agent-scope stores, vmcnt(0), workgroup barrier, one agent-scope add; the
-// waiters poll with agent-scope loads and s_sleep, then load the published bytes with agent-scope loads
-// (MI355X_MICROARCH.md, inter-workgroup visibility, table row 1). sync[0] counts arrivals, sync[1] finished O
-// workgroups (the last one resets both), sync[2] is a sticky timeout flag.
-struct DecOArgs {
-  const bf16* W; long ldw; int N; int K;  // W_o [N][K] bf16 (LoRA merged)
-  float* X;                               // residual row, X[n] += (W_o out)[n]
-  int* sync;
-};
-
-__global__ __launch_bounds__(1024) void dec_attn_o_kernel(DecMfmaArgs a, DecOArgs o) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  if (a.st[2]) return;
-  const int nA = a.Hkv;
-  if ((int)blockIdx.x < nA) {
-    dec_attn_mfma_body<true>(a, blockIdx.x, smem);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) __hip_atomic_fetch_add(o.sync, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return;
-  }
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int n = ((int)blockIdx.x - nA) * 16 + w;
-  const int nch = o.K >> 3;
-  uint4 wv[2];
-#pragma unroll
-  for (int c = 0; c < 2; ++c) {
-    const int ch = lane + 64 * c;
-    wv[c] = (n < o.N && ch < nch) ? *reinterpret_cast<const uint4*>(o.W + (long)n * o.ldw + 8 * ch) : make_uint4(0u, 0u, 0u, 0u);
-  }
-  __shared__ int ok_s;
-  if (tid == 0) {
-    int ok = 0;
-    for (int it = 0; it < (1 << 20); ++it) {  // bounded: ~1 s at most, far beyond a healthy attention (~10 us)
-      if (__hip_atomic_load(o.sync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= nA) { ok = 1; break; }
-      __builtin_amdgcn_s_sleep(1);
-    }
-    if (!ok) __hip_atomic_store(o.sync + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    ok_s = ok;
-  }
-  __syncthreads();
-  bf16* xs = reinterpret_cast<bf16*>(smem);
-  if (ok_s) {
-    for (int c = tid; c < nch; c += 1024) {  // the attention output row: agent-scope 4-B loads
-      const unsigned* src = reinterpret_cast<const unsigned*>(a.out + 8 * c);
-      uint4 v;
-      v.x = __hip_atomic_load(const_cast<unsigned*>(src), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      v.y = __hip_atomic_load(const_cast<unsigned*>(src + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      v.z = __hip_atomic_load(const_cast<unsigned*>(src + 2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      v.w = __hip_atomic_load(const_cast<unsigned*>(src + 3), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      *reinterpret_cast<uint4*>(xs + 8 * c) = v;
-    }
-  }
-  __syncthreads();
-  if (ok_s && n < o.N) {
-    float acc = 0.f;
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      const int ch = lane + 64 * c;
-      if (ch < nch) {
-        const bf16x8 wb = __builtin_bit_cast(bf16x8, wv[c]);
-        const bf16x8 x = *reinterpret_cast<const bf16x8*>(xs + 8 * ch);
-        float sc = 0.f;  // the summation order of dec_gemv_kernel's dot8 (so both O paths round alike)
-#pragma unroll
-        for (int e = 0; e < 8; ++e) sc = __builtin_fmaf((float)wb[e], (float)x[e], sc);
-        acc += sc;
-      }
-    }
-    acc = warp_sum(acc);
-    if (lane == 0) o.X[n] += acc;
-  }
-  __syncthreads();
-  if (tid == 0) {  // the last O workgroup resets the counters for this layer's next step
-    const int nO = (int)gridDim.x - nA;
-    if (__hip_atomic_fetch_add(o.sync + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nO - 1) {
-      __hip_atomic_store(o.sync, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(o.sync + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-}
-
-int dec_attn_o_launch(void* cache, long ld, int Hq, int Hkv, const float* cos_tab, const float* sin_tab, void* out,
-                      const void* st, const void* Wo, long ldwo, int N, int K, float* X, int* sync, hipStream_t s) {
-  constexpr int LDS = kDecKeys * 128 + 32 * 128 + (64 + 16 * 32 + 32 + 32) * 4;
-  static bool attr = false;
-  if (!attr) {
-    hipFuncSetAttribute((const void*)dec_attn_o_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
-    attr = true;
-  }
-  DecMfmaArgs a{(bf16*)cache, ld, Hq, Hkv, cos_tab, sin_tab, (bf16*)out, (const int*)st, 0.125f};
-  DecOArgs o{(const bf16*)Wo, ldwo, N, K, X, sync};
-  hipLaunchKernelGGL(dec_attn_o_kernel, dim3(Hkv + (N + 15) / 16), dim3(1024), LDS, s, a, o);
-  SLX_LAUNCH_CHECK("slx_dec_attn_o");
-  return 0;
+  dec_attn_mfma_body(a, blockIdx.x, smem);
 }
 
 // ---- decode attention split over keys, merged by the O GEMV (slx_dec_attn_o_split) ----------------------------------
@@ -2527,32 +1368,13 @@ static int fill_common(AttnArgs& a, const slx_attn_desc* d) {
   return 0;
 }
 
-// SLX_ATTN_DMA: 1 (default) = the LDS-DMA staged kernels, 0 = the register-staged ones (A/B; identical outputs)
-#ifndef ATTN_DMA_DEFAULT
-#define ATTN_DMA_DEFAULT 1
-#endif
-// SLX_ATTN_PP: 1 = the ping-pong (8-wave, MFMA / VALU phase-alternating) dQ pass
-#ifndef ATTN_PP_DEFAULT
-#define ATTN_PP_DEFAULT 0
-#endif
-static bool attn_pp() {
-  static const bool on = [] { const char* e = getenv("SLX_ATTN_PP"); return e ? atoi(e) != 0 : ATTN_PP_DEFAULT != 0; }();
-  return on;
-}
-static bool attn_dma() {
-  static const bool on = [] { const char* e = getenv("SLX_ATTN_DMA"); return e ? atoi(e) != 0 : ATTN_DMA_DEFAULT != 0; }();
-  return on;
-}
-
 extern "C" int slx_attn_fwd(const slx_attn_desc* d, slx_stream_t stream) {
   AttnArgs a;
   int rc = fill_common(a, d);
   if (rc) return rc;
   if (a.B == 0 || a.S == 0) return 0;
   dim3 grid(((a.S + 127) / 128) * a.Hq * a.B);
-  if (attn_pp()) hipLaunchKernelGGL(attn_fwd_pp_kernel, grid, dim3(512), 0, (hipStream_t)stream, a);
-  else if (attn_dma()) hipLaunchKernelGGL(attn_fwd_dma_kernel, grid, dim3(256), 0, (hipStream_t)stream, a);
-  else hipLaunchKernelGGL(attn_fwd_kernel, grid, dim3(256), 0, (hipStream_t)stream, a);
+  hipLaunchKernelGGL(attn_fwd_dma_kernel, grid, dim3(256), 0, (hipStream_t)stream, a);
   SLX_LAUNCH_CHECK("slx_attn_fwd");
   return 0;
 }
@@ -2581,9 +1403,7 @@ extern "C" int slx_attn_bwd(const slx_attn_desc* d, const slx_attn_bwd_desc* g, 
   const long ntok = (long)a.B * a.S;
   const int nblk = (a.S + 127) / 128;
   // dQ pass first: it computes delta = rowsum(dO * O) per query in its prologue and stores it for the dK/dV pass
-  if (attn_pp()) hipLaunchKernelGGL(attn_bwd_dq_pp_kernel, dim3(nblk * a.Hq * a.B), dim3(512), 0, st, a);
-  else if (attn_dma()) hipLaunchKernelGGL(attn_bwd_dq_dma_kernel, dim3(nblk * a.Hq * a.B), dim3(256), 0, st, a);
-  else hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3(nblk * a.Hq * a.B), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(attn_bwd_dq_dma_kernel, dim3(nblk * a.Hq * a.B), dim3(256), 0, st, a);
   SLX_LAUNCH_CHECK("slx_attn_bwd(dq)");
   {  // split a GQA group's q-heads over workgroups: one q-head per workgroup (Qwen2: 7 x 112 = 784 workgroups; with the
      // heaviest-first order +0.25 % on the step over the 4-way split that just fills the chip,
@@ -2596,9 +1416,7 @@ extern "C" int slx_attn_bwd(const slx_attn_desc* d, const slx_attn_bwd_desc* g, 
     a.hsplit = (G + ns - 1) / ns;
     a.nsplit = (G + a.hsplit - 1) / a.hsplit;
   }
-  if (attn_pp()) hipLaunchKernelGGL(attn_bwd_kv_pp_kernel, dim3(nblk * a.Hkv * a.nsplit * a.B), dim3(512), 0, st, a);
-  else if (attn_dma()) hipLaunchKernelGGL(attn_bwd_kv_dma_kernel, dim3(nblk * a.Hkv * a.nsplit * a.B), dim3(256), 0, st, a);
-  else hipLaunchKernelGGL(attn_bwd_kv_kernel, dim3(nblk * a.Hkv * a.nsplit * a.B), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(attn_bwd_kv_dma_kernel, dim3(nblk * a.Hkv * a.nsplit * a.B), dim3(256), 0, st, a);
   SLX_LAUNCH_CHECK("slx_attn_bwd(dk/dv)");
   // finalize: f32 -> bf16, summing head-split partials and applying the RoPE transpose where asked
   auto rope_args = [&](const float* src, int heads, bf16* dst, long ld, bool rope, int nsplit) {

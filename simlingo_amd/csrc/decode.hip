@@ -27,8 +27,6 @@ int dec_attn_split_launch(void* cache, long ld, int Hq, int Hkv, const float* co
                           float* ws, int ns, const void* st, hipStream_t s);
 int dec_attn_mfma_launch(void* cache, long ld, int Hq, int Hkv, const float* cos_tab, const float* sin_tab, void* out,
                          const void* st, hipStream_t s);
-int dec_attn_o_launch(void* cache, long ld, int Hq, int Hkv, const float* cos_tab, const float* sin_tab, void* out,
-                      const void* st, const void* Wo, long ldwo, int N, int K, float* X, int* sync, hipStream_t s);
 static long long* g_dec_trace = nullptr;  // tools only (slx_dec_attn_set_trace)
 static int g_dec_force_split = 0;         // tests / tools only (slx_dec_attn_force_split)
 
@@ -661,27 +659,6 @@ int slx_dec_attn_o_split(void* cache, int64_t ld, int Hq, int Hkv, const float* 
                      (size_t)K * 2, (hipStream_t)s, a);
   SLX_LAUNCH_CHECK("slx_dec_attn_o_split(O GEMV)");
   return 0;
-}
-
-int slx_dec_sync_ints(void) { return 4; }
-
-int slx_dec_attn_o(void* cache, int64_t ld, int Hq, int Hkv, const float* cos_tab, const float* sin_tab, int lmax,
-                   float* ws, void* out, const slx_dec_state* st, const void* Wo, int64_t ldwo, int N, int K, float* X,
-                   int* sync, slx_stream_t s) {
-  SLX_CHECK_ARG(cache && cos_tab && sin_tab && ws && out && st && Wo && X && sync, "slx_dec_attn_o: null argument");
-  SLX_CHECK_ARG(K == Hq * 64 && K % 8 == 0 && K <= 1024 && ldwo % 8 == 0 && ((uintptr_t)Wo & 15) == 0 &&
-                ((uintptr_t)out & 15) == 0, "slx_dec_attn_o: K == Hq * 64 <= 1024, 16-B aligned W_o rows and out");
-  SLX_CHECK_ARG(Hkv > 0 && Hq % Hkv == 0 && Hq / Hkv <= 32 && ld % 8 == 0 && ((uintptr_t)cache & 15) == 0,
-                "slx_dec_attn_o: Hq/Hkv <= 32, 16-B aligned cache rows");
-  if (lmax <= 1024 && !g_dec_trace && !g_dec_force_split)
-    return dec_attn_o_launch(cache, ld, Hq, Hkv, cos_tab, sin_tab, out, st, Wo, ldwo, N, K, X, sync, (hipStream_t)s);
-  // long caches: the split attention, then the O GEMV as its own launch
-  int rc = slx_dec_attn(cache, ld, Hq, Hkv, cos_tab, sin_tab, lmax, ws, out, st, s);
-  if (rc) return rc;
-  slx_dec_gemv_desc d;
-  memset(&d, 0, sizeof(d));
-  d.mode = SLX_DEC_RESID; d.W = Wo; d.ldw = ldwo; d.N = N; d.K = K; d.xb = out; d.resid = X; d.state = st;
-  return slx_dec_gemv(&d, s);
 }
 
 }  // extern "C"

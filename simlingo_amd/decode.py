@@ -34,9 +34,6 @@ import torch
 from . import kernels as K
 
 BF16, F32 = torch.bfloat16, torch.float32
-# attention + O projection as one launch (slx_dec_attn_o) instead of slx_dec_attn + the O GEMV: off by default, it
-# measured 35 us per token SLOWER (tools/fuse_o_ab.sh, profiles/round2_s3_fuse_o_ab.txt); SLX_DEC_FUSE_O=1 turns it on
-FUSE_O = os.environ.get("SLX_DEC_FUSE_O", "0") == "1"
 # the attention split over keys (Hkv x 8 workgroups) with its partials merged by the O GEMV's prologue
 # (slx_dec_attn_o_split) instead of one MFMA workgroup per kv head + the O GEMV: 0.71 vs 0.80 ms per token in
 # alternating bench_infer runs (tools/ab/r4_dec_ab.sh, profiles/round4_knobs_ab.txt); SLX_DEC_SPLIT_O=0 restores the old pair
@@ -58,10 +55,7 @@ K.register("slx_dec_gemv", [ctypes.POINTER(DecGemvDesc), K.c_vp])
 K.register("slx_dec_attn_nsplit", [K.c_int])
 K.register("slx_dec_attn_ws_floats", [K.c_int, K.c_int, K.c_int])
 K.register("slx_dec_attn", [K.c_vp, K.c_i64, K.c_int, K.c_int, K.c_vp, K.c_vp, K.c_int, K.c_vp, K.c_vp, K.c_vp, K.c_vp])
-K.register("slx_dec_sync_ints", [])
 K.register("slx_dec_attn_o_split_ok", [K.c_int])
-K.register("slx_dec_attn_o", [K.c_vp, K.c_i64, K.c_int, K.c_int, K.c_vp, K.c_vp, K.c_int, K.c_vp, K.c_vp, K.c_vp, K.c_vp,
-                              K.c_i64, K.c_int, K.c_int, K.c_vp, K.c_vp, K.c_vp])
 K.register("slx_dec_attn_o_split", [K.c_vp, K.c_i64, K.c_int, K.c_int, K.c_vp, K.c_vp, K.c_int, K.c_vp, K.c_vp, K.c_vp,
                                     K.c_vp, K.c_i64, K.c_int, K.c_int, K.c_vp, K.c_vp])
 
@@ -107,9 +101,6 @@ class GreedyDecoder:
         self.attn_ws = torch.zeros(max(nws, 1), dtype=F32, device=dev)
         # the split path's cache-length limit depends on SLX_DEC_SPLIT_NS (C side); past it, attention + O GEMV
         self.split_ok = bool(K.lib().slx_dec_attn_o_split_ok(self.max_len))
-        # attention + O projection hand-off counters, one 128-B line per layer (slx_dec_attn_o resets them per call)
-        assert K.lib().slx_dec_sync_ints() <= 32
-        self.sync = torch.zeros(cfg.llm_layers, 32, dtype=torch.int32, device=dev)
         self._build_step_descs()
         self.graph = None
         if use_graph:
@@ -183,12 +174,6 @@ class GreedyDecoder:
                                                  K.P(self.cos), K.P(self.sin), self.max_len, K.P(self.attn_ws), None,
                                                  K.P(self.state), K.P(wo), wo.stride(0), cfg.llm_dim, self.qn,
                                                  K.P(self.X), s), "slx_dec_attn_o_split")
-            elif FUSE_O:  # attention + O projection (+ residual): one launch for caches of <= 1024 rows
-                wo = self.Wm[i]["o_w"]
-                K.check(lib.slx_dec_attn_o(K.P(cache), cache.stride(0), cfg.llm_heads, cfg.llm_kv_heads, K.P(self.cos),
-                                           K.P(self.sin), self.max_len, K.P(self.attn_ws), K.P(self.obuf),
-                                           K.P(self.state), K.P(wo), wo.stride(0), cfg.llm_dim, self.qn, K.P(self.X),
-                                           K.P(self.sync[i]), s), "slx_dec_attn_o")
             else:
                 K.check(lib.slx_dec_attn(K.P(cache), cache.stride(0), cfg.llm_heads, cfg.llm_kv_heads, K.P(self.cos),
                                          K.P(self.sin), self.max_len, K.P(self.attn_ws), K.P(self.obuf),
@@ -277,11 +262,6 @@ class GreedyDecoder:
                 break
         self._begin()  # records the last token (no-op after EOS)
         ev[2].record()
-        if FUSE_O and int(self.sync[:, 2].max().item()):
-            # a fused attention + O launch timed out waiting for its attention workgroups and skipped its O rows:
-            # the residual stream, hence every later token, is wrong (dec_attn_o_kernel, attention.hip)
-            self.sync[:, 2].zero_()
-            raise RuntimeError("slx_dec_attn_o: attention hand-off timed out; generated tokens are invalid")
         n = int(self.state[1].item())
         self.last_timing = {"prefill_ms": ev[0].elapsed_time(ev[1]), "decode_ms": ev[1].elapsed_time(ev[2]),
                             "decode_steps": done_steps}

@@ -370,6 +370,7 @@ for _n, _a in {
     "slx_set_deterministic": [_i, _vp, _I],
     "slx_sumsq_bf16": [_vp, _I, _vp, _i, _vp],
     "slx_sumsq_ws": [_vp, _I, _vp, _i, _vp, _I, _vp],
+    "slx_mfma_peak": [_i, _i, _vp, _vp],
     "slx_sumsq_bf16_ws": [_vp, _I, _vp, _i, _vp, _I, _vp],
     "slx_adamw_bf16g": [_vp, _vp, _vp, _vp, _vp, _I, _f, _f, _f, _f, _f, _i, _vp, _f, _f, _vp],
     "slx_get_deterministic": [],

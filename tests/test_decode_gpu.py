@@ -223,46 +223,6 @@ def test_dec_attn_forms_vs_torch(dev, pos):
             _check_rotated_k(krow, rope(orig[None])[0], orig)
 
 
-@pytest.mark.parametrize("pos,split", [(300, 0), (1000, 0), (300, 1)])
-def test_dec_attn_o_fused_equals_separate(dev, pos, split):
-    """slx_dec_attn_o (attention + O projection + residual in one launch, the O workgroups taking the attention
-    output through an in-launch hand-off) vs slx_dec_attn followed by the O GEMV: bit-identical residual row, and
-    the hand-off counters back at zero with no timeout flagged; split=1 exercises the long-cache fallback."""
-    import ctypes
-    from simlingo_amd import decode as D
-    from simlingo_amd import kernels as K
-    K.register("slx_dec_attn_force_split", [ctypes.c_int])
-    Hq, Hkv, lmax, d = 14, 2, 1024, 896
-    ld = (Hq + 2 * Hkv) * 64
-    gen = torch.Generator(device=dev).manual_seed(pos + 7)
-    cache0 = torch.randn(lmax, ld, device=dev, generator=gen).bfloat16()
-    Wo = (torch.randn(d, Hq * 64, device=dev, generator=gen) * 0.03).bfloat16()
-    X0 = torch.randn(d, device=dev, generator=gen)
-    cos, sin = K.rope_tables(lmax, 1e6, dev)
-    st = torch.tensor([pos, 0, 0, 100, -1, 0, 0, 0], dtype=torch.int32, device=dev)
-    lib = K.lib()
-    ws = torch.zeros(lib.slx_dec_attn_ws_floats(Hq, Hkv, lmax), device=dev)
-    lib.slx_dec_attn_force_split(split)
-    try:
-        c1, X1, o1 = cache0.clone(), X0.clone(), torch.empty(Hq * 64, dtype=torch.bfloat16, device=dev)
-        K.check(lib.slx_dec_attn(K.P(c1), ld, Hq, Hkv, K.P(cos), K.P(sin), lmax, K.P(ws), K.P(o1), K.P(st),
-                                 K.stream_ptr()), "slx_dec_attn")
-        desc = D._gemv_desc(D.DEC_RESID, Wo, d, Hq * 64, xb=o1, resid=X1, state=st)
-        K.check(lib.slx_dec_gemv(ctypes.byref(desc), K.stream_ptr()), "slx_dec_gemv")
-        sync = torch.zeros(32, dtype=torch.int32, device=dev)
-        for rep in range(2):  # the second call checks that the counters were reset
-            c2, X2, o2 = cache0.clone(), X0.clone(), torch.empty(Hq * 64, dtype=torch.bfloat16, device=dev)
-            K.check(lib.slx_dec_attn_o(K.P(c2), ld, Hq, Hkv, K.P(cos), K.P(sin), lmax, K.P(ws), K.P(o2), K.P(st),
-                                       K.P(Wo), Wo.stride(0), d, Hq * 64, K.P(X2), K.P(sync), K.stream_ptr()),
-                    "slx_dec_attn_o")
-            torch.cuda.synchronize()
-            assert torch.equal(o1, o2) and torch.equal(c1, c2), rep
-            assert torch.equal(X1, X2), (rep, (X1 - X2).abs().max().item())
-            assert sync[:3].tolist() == [0, 0, 0], sync[:3].tolist()
-    finally:
-        lib.slx_dec_attn_force_split(0)
-
-
 @pytest.mark.parametrize("pos", [0, 31, 32, 300, 1000, 1023])
 def test_dec_attn_o_split_vs_torch(dev, pos):
     """slx_dec_attn_o_split (the attention split over 8 workgroups per kv head, partials merged in the O GEMV's

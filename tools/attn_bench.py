@@ -54,7 +54,7 @@ for name in args or list(SHAPES):
     tb = timeit(lambda: K.attn_bwd(q, k, v, o, lse, dout, dqkv[:, :Hq * 64], dqkv[:, Hq * 64:(Hq + Hkv) * 64],
                                    dqkv[:, (Hq + Hkv) * 64:], ws, **kw))
     print(f"{name}: fwd {tf * 1e3:7.1f} us {fl / tf / 1e9:6.0f} TF | bwd {tb * 1e3:7.1f} us {2.5 * fl / tb / 1e9:6.0f} TF"
-          f" [SLX_ATTN_DMA={os.environ.get('SLX_ATTN_DMA', '1')}]", flush=True)
+          "", flush=True)
     if save:
         outs[name] = {"o": o.cpu(), "lse": lse.cpu(), "dqkv": dqkv.cpu()}
 if save:

@@ -1,5 +1,5 @@
 # Round 4 step-level A/B: alternating bench processes on one box (N=1, config 3, --no-extras, no CPU baseline).
-# usage: bash tools/step_ab.sh "ENV_A" "ENV_B" [pairs]   e.g. "SLX_ATTN_DMA=0" "SLX_ATTN_DMA=1"
+# usage: bash tools/step_ab.sh "ENV_A" "ENV_B" [pairs]   e.g. "SLX_GEMM_FE=0" "SLX_GEMM_FE=1"
 set -e
 cd $GRAFT_REPO_ROOT
 A="$1"; B="$2"; N="${3:-2}"
