@@ -72,6 +72,7 @@ class GradBucketer:
         self.group_bucket = {g: bk for bk in self.buckets for g in bk.groups}
         self.pg = None
         self.world = 1
+        self._clean = False  # True between a completed wait() and the next step's first issue (wait is idempotent)
 
     def set_distributed(self, pg=None, world: int = 1):
         self.pg = pg
@@ -92,6 +93,7 @@ class GradBucketer:
                 src = self.wire_buf[bk.start:bk.end]
                 src.copy_(self.flat[bk.start:bk.end])
             bk.handle = dist.all_reduce(src, group=self.pg, async_op=True)
+            self._clean = False
             if self.trace_on:
                 self.trace.append(("issue", self.buckets.index(bk), time.perf_counter()))
             if self.timing:
@@ -159,6 +161,8 @@ class GradBucketer:
     def wait(self):
         """Wait for this step's exchange. At world > 1 every bucket must have been issued by the backward: a bucket
         left out would hand the optimizer a stale summed slice (bf16 wire) or an un-summed local one (f32)."""
+        if self.world > 1 and self._clean:
+            return  # this step's exchange was already waited for
         if self.world > 1:
             missing = [i for i, bk in enumerate(self.buckets) if bk.handle is None]
             if missing:
@@ -178,6 +182,7 @@ class GradBucketer:
             bk._seen = False
         if self.timing and waited and self.steps and "wait" not in self.steps[-1]:
             self.steps[-1]["wait"] = self._stamp()
+        self._clean = self.world > 1
 
     def optimizer_grad(self):
         """(gradient buffer, is_bf16) the optimizer reads after wait(): the summed bf16 wire buffer when the exchange

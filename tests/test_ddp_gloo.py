@@ -203,3 +203,35 @@ def test_wait_refuses_unexchanged_buckets():
         bk.wait()
     bk.set_distributed(None, 1)
     bk.wait()  # single process: nothing to exchange
+
+
+def test_wait_is_idempotent_after_an_exchange():
+    """wait() twice in one step (the optimizer's own wait after an explicit one) is a no-op the second time; a new
+    step's partial exchange is refused again."""
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ret = mp.Manager().dict()
+    mp.spawn(_idem_worker, args=(port, ret), nprocs=1, join=True)
+    assert ret["ok"], dict(ret)
+
+
+def _idem_worker(rank, port, ret):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    g = torch.ones(4096)
+    bk = GradBucketer(g, {"a": (0, 2048), "b": (2048, 4096)}, bucket_bytes=1024)
+    bk.set_distributed(None, 2)  # issue as at N = 2; the group has one rank
+    bk.group_done("a")
+    bk.group_done("b")
+    bk.wait()
+    bk.wait()
+    bk.group_done("a")  # next step: only one bucket issued
+    try:
+        bk.wait()
+        ret["ok"] = False
+    except RuntimeError:
+        ret["ok"] = True
+    dist.destroy_process_group()

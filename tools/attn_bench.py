@@ -9,7 +9,11 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from simlingo_amd import kernels as K  # noqa: E402
 
 dev = torch.device("cuda")
-SHAPES = {"vit": dict(B=16, S=1025, Hq=16, Hkv=16, causal=False), "llm": dict(B=8, S=798, Hq=14, Hkv=2, causal=True)}
+SHAPES = {"vit": dict(B=16, S=1025, Hq=16, Hkv=16, causal=False), "llm": dict(B=8, S=798, Hq=14, Hkv=2, causal=True),
+          # the InternViT shape without its class token: what the 1025th row's tail blocks cost
+          "vit1024": dict(B=16, S=1024, Hq=16, Hkv=16, causal=False),
+          # Qwen2 without the GQA sharing (7 times the K/V heads): what the grouped K/V costs or saves
+          "llm_mha": dict(B=8, S=798, Hq=14, Hkv=14, causal=True)}
 
 
 def timeit(fn, n=10):
