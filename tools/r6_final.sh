@@ -1,11 +1,11 @@
-# Round-5 final GPU check on the current build: the -m gpu suite, smoke(), the default bench line (CPU baseline
+# Round-6 final GPU check on the current build: the -m gpu suite, smoke(), the default bench line (CPU baseline
 # included), the rocprofv3 --kernel-trace --stats CSV + steady-step tables of the bench command, HBM-traffic records of
 # the three roofline kernels (separate FETCH_SIZE / WRITE_SIZE passes), and the decode profile.
 set -e
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-TAG=${1:-r5final}
-timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread > gpurun_out/${TAG}_tests.log 2>&1 || { tail -40 gpurun_out/${TAG}_tests.log; exit 1; }
+TAG=${1:-r6final}
+timeout -k 10 1500 python3 -u -m pytest tests -m gpu -x -q --timeout 1200 --timeout-method thread > gpurun_out/${TAG}_tests.log 2>&1 || { tail -40 gpurun_out/${TAG}_tests.log; exit 1; }
 tail -1 gpurun_out/${TAG}_tests.log
 timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${TAG}_smoke.log 2>&1 || { tail -20 gpurun_out/${TAG}_smoke.log; exit 1; }
 tail -1 gpurun_out/${TAG}_smoke.log
@@ -24,3 +24,4 @@ for c in vla_pair vla base; do
   rm -rf gpurun_out/pmc_${c}_f gpurun_out/pmc_${c}_w
 done
 bash tools/dec_prof.sh ${TAG}_dec
+bash tools/attn_pmc_dispatch.sh > /dev/null && cp gpurun_out/attn_pmc_dispatch.jsonl gpurun_out/${TAG}_attn_pmc_dispatch.jsonl
