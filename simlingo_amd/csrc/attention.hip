@@ -93,6 +93,10 @@ struct AttnArgs {
   const float* rcos; const float* rsin;
   int tail_first;                // non-causal: each XCD's partial last row blocks dispatched first (SLX_ATTN_TAIL_FIRST)
   int tailv;                     // non-causal DMA forms: a short last key / query tile (<= kTailMax rows) on the VALU
+  // non-causal: the rows past the last whole 128-row block (S % 128 <= kTailQ, InternViT's 1025th token) folded into
+  // that block's workgroup instead of a workgroup of their own (the forward / dQ passes: queries; dK/dV: keys)
+  int qtail, nqb;                // query blocks launched (S / 128 with a folded tail, else ceil(S / 128))
+  int ktail, nkb;                // key blocks launched (dK/dV pass)
 };
 
 constexpr float LOG2E = 1.4426950408889634f;
@@ -480,6 +484,111 @@ __device__ __forceinline__ void tail_axpy(const bf16* row, float w, f32x16& acc0
   }
 }
 
+// ---- the row tail folded into the last whole block (round 6) ------------------------------------------------------
+// InternViT's T = 1025 = 8 * 128 + 1: with ceil(T / 128) blocks, 256 of the 2304 workgroups of each pass carry ONE
+// query (forward / dQ) or ONE key (dK/dV) through the whole sweep, half a round of slots on the 512-slot chip
+// (isolated: forward 121.7 us at T = 1025 against 90.1 at T = 1024, backward 325.7 against 274.0; profiles/
+// round6_attn_tail.txt). Here the last whole block's workgroup takes those rows (<= kTailQ) along: per 64-row tile
+// the 4 waves split the tile's 64 rows 16 each, a lane = (row 16w + l / 4, dim quarter l & 3) forms its quarter of
+// the tail row's dot products (two 16-B LDS reads against the tail row staged in LDS, a quad sum), and the weighted
+// column sums over the wave's 16 rows run with lane = dim (16 readlanes + 16 LDS reads). The forward keeps one
+// online-softmax state (m, l, o) per wave, merged across the 4 waves at the end; the dQ / dK-dV sums are plain sums
+// over the waves. Same bf16 operands, f32 products, p / dS rounded to bf16 where the MFMA forms round them.
+constexpr int kTailQ = 2;
+
+__device__ __forceinline__ float wave_sum64(float x) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) x += __shfl_xor(x, o, 64);
+  return x;
+}
+__device__ __forceinline__ float rdlane(float x, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), l));
+}
+// dims [16 qd, 16 qd + 16) of row `row` of an sw_off tile . the same dims of a 64-dim bf16 row in LDS, summed over the
+// lane's quad (lanes 4i .. 4i + 3 hold the four quarters of row i): every lane of the quad gets the full dot product
+__device__ __forceinline__ float quarter_dot(const char* tile, int row, int qd, const bf16* v) {
+  const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(tile + sw_off(row, 2 * qd));
+  const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(tile + sw_off(row, 2 * qd + 1));
+  const bf16x8 b0 = *reinterpret_cast<const bf16x8*>(v + 16 * qd);
+  const bf16x8 b1 = *reinterpret_cast<const bf16x8*>(v + 16 * qd + 8);
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s = __builtin_fmaf((float)a0[j], (float)b0[j], s);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s = __builtin_fmaf((float)a1[j], (float)b1[j], s);
+  s += __shfl_xor(s, 1, 64);
+  return s + __shfl_xor(s, 2, 64);
+}
+// acc + sum over kk < 16 of wv(lane 4 kk) * tile[r0 + kk][lane]  (lane = dim)
+__device__ __forceinline__ float col_axpy16(const char* tile, int r0, float wv, int lane, float acc) {
+#pragma unroll
+  for (int kk = 0; kk < 16; ++kk)
+    acc = __builtin_fmaf(rdlane(wv, 4 * kk), (float)*reinterpret_cast<const bf16*>(tile + sw_elem(r0 + kk, lane)), acc);
+  return acc;
+}
+
+// forward: the tail query rows (tq: q_j at rows 2j of a pair-staged buffer) against one K/V tile, this wave's 16 keys
+__device__ __forceinline__ void fwd_qtail_tile(const char* Kl, const char* Vl, const bf16* tq, int nq, int key0, int klim,
+                                               float c, int w, int lane, float (&tm)[kTailQ], float (&tl)[kTailQ],
+                                               float (&to)[kTailQ]) {
+  const int kr = 16 * w + (lane >> 2), qd = lane & 3;
+  const bool kok = key0 + kr < klim;
+#pragma unroll
+  for (int j = 0; j < kTailQ; ++j) {
+    if (j < nq) {
+      const float s = kok ? quarter_dot(Kl, kr, qd, tq + 2 * j * 64) * c : -INFINITY;
+      float mx = s;
+#pragma unroll
+      for (int o = 4; o < 64; o <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+      const float mnew = fmaxf(tm[j], mx);
+      const float alpha = __builtin_amdgcn_exp2f(tm[j] - mnew);
+      const float p = kok ? (float)(bf16)__builtin_amdgcn_exp2f(s - mnew) : 0.f;
+      float ps = p;
+#pragma unroll
+      for (int o = 4; o < 64; o <<= 1) ps += __shfl_xor(ps, o, 64);
+      tl[j] = tl[j] * alpha + ps;
+      to[j] = col_axpy16(Vl, 16 * w, p, lane, to[j] * alpha);
+      tm[j] = mnew;
+    }
+  }
+}
+
+// dQ pass: the tail queries (tq pairs: q_j, dO_j; ts[2j] = lse_j, ts[2j + 1] = delta_j) against one K/V tile
+__device__ __forceinline__ void dq_qtail_tile(const char* Kl, const char* Vl, const bf16* tq, const float* ts, int nq,
+                                              int key0, int klim, float c, int w, int lane, float (&tdq)[kTailQ]) {
+  const int kr = 16 * w + (lane >> 2), qd = lane & 3;
+  const bool kok = key0 + kr < klim;
+#pragma unroll
+  for (int j = 0; j < kTailQ; ++j) {
+    if (j < nq) {
+      const float sv = quarter_dot(Kl, kr, qd, tq + 2 * j * 64);
+      const float dpv = quarter_dot(Vl, kr, qd, tq + (2 * j + 1) * 64);
+      const float pv = __builtin_amdgcn_exp2f(__builtin_fmaf(sv, c, -ts[2 * j]));
+      const float ds = kok ? (float)(bf16)(pv * (dpv - ts[2 * j + 1])) : 0.f;
+      tdq[j] = col_axpy16(Kl, 16 * w, ds, lane, tdq[j]);
+    }
+  }
+}
+
+// dK/dV pass: the tail keys (tk pairs: k_j, v_j) against one (q-head, 64-query chunk) stage, this wave's 16 queries
+__device__ __forceinline__ void kv_ktail_stage(const char* Ql, const char* Dl, const float* lse_l, const float* nd_l,
+                                               const bf16* tk, int nk, int qc, int S, float c, int w, int lane,
+                                               float (&tdk)[kTailQ], float (&tdv)[kTailQ]) {
+  const int qr = 16 * w + (lane >> 2), qd = lane & 3;
+  const bool qok = qc + qr < S;
+#pragma unroll
+  for (int j = 0; j < kTailQ; ++j) {
+    if (j < nk) {
+      const float sv = quarter_dot(Ql, qr, qd, tk + 2 * j * 64);
+      const float dpv = quarter_dot(Dl, qr, qd, tk + (2 * j + 1) * 64);
+      const float pv = qok ? __builtin_amdgcn_exp2f(__builtin_fmaf(sv, c, -lse_l[qr])) : 0.f;
+      const float pb = (float)(bf16)pv, sb = (float)(bf16)(pv * (dpv + nd_l[qr]));  // nd_l: -delta
+      tdv[j] = col_axpy16(Dl, 16 * w, pb, lane, tdv[j]);
+      tdk[j] = col_axpy16(Ql, 16 * w, sb, lane, tdk[j]);
+    }
+  }
+}
+
 #ifndef ATTN_NSLOT
 #ifndef ATTN_NSLOT
 #define ATTN_NSLOT 2  // one tile ahead: fastest of 2 / 3 / 4 slots on both shapes (profiles/round4_attn_dma_ab.txt)
@@ -491,7 +600,7 @@ __device__ __forceinline__ void tail_axpy(const bf16* row, float w, f32x16& acc0
 __global__ __launch_bounds__(256, ATTN_FWD_OCC) void attn_fwd_dma_kernel(AttnArgs a) {
   constexpr int NS = ATTN_NSLOT;
   __shared__ __attribute__((aligned(1024))) char smem[NS * 16384];
-  const BlockCoord bc = attn_block((a.S + 127) / 128, a.Hq, a.Hkv, a.B, a.causal ? 1 : 0, a.tail_first);
+  const BlockCoord bc = attn_block(a.nqb, a.Hq, a.Hkv, a.B, a.causal ? 1 : 0, a.tail_first);
   const int qb = bc.blk, h = bc.h, b = bc.b;
   const int hk = h / (a.Hq / a.Hkv);
   const int S = a.S;
@@ -506,6 +615,16 @@ __global__ __launch_bounds__(256, ATTN_FWD_OCC) void attn_fwd_dma_kernel(AttnArg
   const bf16* kbase = a.k + (long)b * S * a.ldk + hk * 64;
   const bf16* vbase = a.v + (long)b * S * a.ldv + hk * 64;
   const __amdgpu_buffer_rsrc_t rk = slice_rsrc(kbase, a.ldk, S, 2), rv = slice_rsrc(vbase, a.ldv, S, 2);
+  // the folded query tail (workgroup-uniform): rows a.nqb * 128 .. + nq - 1 ride with the last whole block
+  const int nq = (a.qtail && qb == a.nqb - 1) ? a.qtail : 0;
+  __shared__ __attribute__((aligned(16))) bf16 tqrows[2 * kTailQ * 64];
+  {
+    const bf16* tqa = a.q + ((long)b * S + a.nqb * 128) * a.ldq + h * 64;
+    tail_stage(tqrows, tqa, a.ldq, tqa, a.ldq, nq);
+  }
+  float tm[kTailQ], tl[kTailQ], to[kTailQ];
+#pragma unroll
+  for (int j = 0; j < kTailQ; ++j) { tm[j] = -1e30f; tl[j] = 0.f; to[j] = 0.f; }
 
   bf16x8 qf[4];
   {
@@ -554,6 +673,7 @@ __global__ __launch_bounds__(256, ATTN_FWD_OCC) void attn_fwd_dma_kernel(AttnArg
       if ((t + 1) * 64 <= kfull) fwd_tile<false>(Kl, Vl, qf, o0, o1, lacc, m, c, t * 64, kvlen, myq, false, lane);
       else fwd_tile<true>(Kl, Vl, qf, o0, o1, lacc, m, c, t * 64, kvlen, myq, a.causal, lane);
     }
+    if (nq) fwd_qtail_tile(Kl, Vl, tqrows, nq, t * 64, kend - ntail, c, w, lane, tm, tl, to);
   }
   wait_vmcnt<0>();  // the trailing sentinel pieces have landed before the workgroup's LDS is released
   if (active) {
@@ -569,6 +689,50 @@ __global__ __launch_bounds__(256, ATTN_FWD_OCC) void attn_fwd_dma_kernel(AttnArg
       const float pb = (float)(bf16)__builtin_amdgcn_exp2f(sc - m);
       lacc[0] += pb;
       tail_axpy(trows + (2 * j + 1) * 64, pb, o0, o1, hl);
+    }
+  }
+  if (nq) {  // the folded tail queries: the short key tail (wave 0, lane = dim), then the 4 waves' states merged
+    __shared__ float tqred[kTailQ][4][66];
+    if (w == 0) {
+#pragma unroll
+      for (int j = 0; j < kTailQ; ++j) {
+        if (j >= nq) continue;
+        const float qv = (float)tqrows[2 * j * 64 + lane];
+        for (int jj = 0; jj < ntail; ++jj) {
+          const float sc = wave_sum64(qv * (float)trows[2 * jj * 64 + lane]) * c;
+          const float mnew = fmaxf(tm[j], sc);
+          const float alpha = __builtin_amdgcn_exp2f(tm[j] - mnew);
+          const float pb = (float)(bf16)__builtin_amdgcn_exp2f(sc - mnew);
+          tl[j] = tl[j] * alpha + pb;
+          to[j] = __builtin_fmaf(pb, (float)trows[(2 * jj + 1) * 64 + lane], to[j] * alpha);
+          tm[j] = mnew;
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < kTailQ; ++j) {
+      if (j < nq) {
+        tqred[j][w][lane] = to[j];
+        if (lane == 0) { tqred[j][w][64] = tm[j]; tqred[j][w][65] = tl[j]; }
+      }
+    }
+    __syncthreads();
+    if (w == 0) {
+      for (int j = 0; j < nq; ++j) {
+        float M = tqred[j][0][64];
+#pragma unroll
+        for (int ww = 1; ww < 4; ++ww) M = fmaxf(M, tqred[j][ww][64]);
+        float L = 0.f, O = 0.f;
+#pragma unroll
+        for (int ww = 0; ww < 4; ++ww) {
+          const float f = __builtin_amdgcn_exp2f(tqred[j][ww][64] - M);
+          L = __builtin_fmaf(tqred[j][ww][65], f, L);
+          O = __builtin_fmaf(tqred[j][ww][lane], f, O);
+        }
+        const long row = a.nqb * 128 + j;
+        a.o[((long)b * S + row) * a.ldo + h * 64 + lane] = (bf16)(O / L);
+        if (lane == 0 && a.lse) a.lse[((long)b * a.Hq + h) * S + row] = M + __log2f(L);
+      }
     }
   }
   if (!active || myq >= S) return;
@@ -594,7 +758,7 @@ __global__ __launch_bounds__(256, ATTN_FWD_OCC) void attn_fwd_dma_kernel(AttnArg
 __global__ __launch_bounds__(256, ATTN_DQ_OCC) void attn_bwd_dq_dma_kernel(AttnArgs a) {
   constexpr int NS = ATTN_NSLOT;
   __shared__ __attribute__((aligned(1024))) char smem[NS * 16384];
-  const BlockCoord bc = attn_block((a.S + 127) / 128, a.Hq, a.Hkv, a.B, a.causal ? 1 : 0, a.tail_first);
+  const BlockCoord bc = attn_block(a.nqb, a.Hq, a.Hkv, a.B, a.causal ? 1 : 0, a.tail_first);
   const int qb = bc.blk, h = bc.h, b = bc.b;
   const int hk = h / (a.Hq / a.Hkv);
   const int S = a.S;
@@ -609,6 +773,30 @@ __global__ __launch_bounds__(256, ATTN_DQ_OCC) void attn_bwd_dq_dma_kernel(AttnA
   const bf16* kbase = a.k + (long)b * S * a.ldk + hk * 64;
   const bf16* vbase = a.v + (long)b * S * a.ldv + hk * 64;
   const __amdgpu_buffer_rsrc_t rk = slice_rsrc(kbase, a.ldk, S, 2), rv = slice_rsrc(vbase, a.ldv, S, 2);
+  // the folded query tail (workgroup-uniform): q / dO rows staged in LDS, lse and delta per row in tqst (delta from
+  // dO . O by wave 0, stored negated for the dK/dV pass like every other row's)
+  const int nq = (a.qtail && qb == a.nqb - 1) ? a.qtail : 0;
+  __shared__ __attribute__((aligned(16))) bf16 tqrows[2 * kTailQ * 64];
+  __shared__ float tqst[2 * kTailQ];
+  {
+    const long r0 = (long)b * S + a.nqb * 128;
+    tail_stage(tqrows, a.q + r0 * a.ldq + h * 64, a.ldq, a.dout + r0 * a.lddo + h * 64, a.lddo, nq);
+    if (w == 0) {
+      for (int j = 0; j < nq; ++j) {
+        const float dv = (float)a.dout[(r0 + j) * a.lddo + h * 64 + lane], ov = (float)a.o[(r0 + j) * a.ldo + h * 64 + lane];
+        const float dl = wave_sum64(dv * ov);
+        const long li = ((long)b * a.Hq + h) * S + a.nqb * 128 + j;
+        if (lane == 0) {
+          tqst[2 * j] = a.lse[li];
+          tqst[2 * j + 1] = dl;
+          const_cast<float*>(a.delta)[li] = -dl;
+        }
+      }
+    }
+  }
+  float tdq[kTailQ];
+#pragma unroll
+  for (int j = 0; j < kTailQ; ++j) tdq[j] = 0.f;
 
   bf16x8 qf[4], df[4];
   float lse = 0.f, dlt = 0.f;
@@ -670,6 +858,7 @@ __global__ __launch_bounds__(256, ATTN_DQ_OCC) void attn_bwd_dq_dma_kernel(AttnA
       if ((t + 1) * 64 <= kfull) bwd_dq_tile<false>(Kl, Vl, qf, df, dq0, dq1, c, lse, negd, t * 64, kvlen, myq, false, lane);
       else bwd_dq_tile<true>(Kl, Vl, qf, df, dq0, dq1, c, lse, negd, t * 64, kvlen, myq, a.causal, lane);
     }
+    if (nq) dq_qtail_tile(Kl, Vl, tqrows, tqst, nq, t * 64, kend - ntail, c, w, lane, tdq);
   }
   wait_vmcnt<0>();
   if (active) {
@@ -679,6 +868,35 @@ __global__ __launch_bounds__(256, ATTN_DQ_OCC) void attn_bwd_dq_dma_kernel(AttnA
       const float dpv = tail_dot(trows + (2 * j + 1) * 64, df, hl);
       const float pv = __builtin_amdgcn_exp2f(__builtin_fmaf(sv, c, -lse));
       tail_axpy(krow, (float)(bf16)(pv * (dpv - dlt)), dq0, dq1, hl);
+    }
+  }
+  if (nq) {  // the folded tail queries: the short key tail (wave 0, lane = dim), the 4 waves' sums, the dQ rows
+    __shared__ float tqred[kTailQ][4][64];
+    if (w == 0) {
+#pragma unroll
+      for (int j = 0; j < kTailQ; ++j) {
+        if (j >= nq) continue;
+        const float qv = (float)tqrows[2 * j * 64 + lane], dov = (float)tqrows[(2 * j + 1) * 64 + lane];
+        for (int jj = 0; jj < ntail; ++jj) {
+          const float kv = (float)trows[2 * jj * 64 + lane];
+          const float sv = wave_sum64(qv * kv);
+          const float dpv = wave_sum64(dov * (float)trows[(2 * jj + 1) * 64 + lane]);
+          const float pv = __builtin_amdgcn_exp2f(__builtin_fmaf(sv, c, -tqst[2 * j]));
+          tdq[j] = __builtin_fmaf((float)(bf16)(pv * (dpv - tqst[2 * j + 1])), kv, tdq[j]);
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < kTailQ; ++j)
+      if (j < nq) tqred[j][w][lane] = tdq[j];
+    __syncthreads();
+    if (w == 0) {
+      for (int j = 0; j < nq; ++j) {
+        const float x = ((tqred[j][0][lane] + tqred[j][1][lane]) + (tqred[j][2][lane] + tqred[j][3][lane])) * a.scale;
+        const bf16 xb = (bf16)x;
+        a.dq[((long)b * S + a.nqb * 128 + j) * a.lddq + h * 64 + lane] = xb;
+        if (a.dbq) atomicAdd(a.dbq + h * 64 + lane, (float)xb);
+      }
     }
   }
   __syncthreads();  // the ring is free for the bias column sums' LDS tiles
@@ -727,7 +945,7 @@ constexpr int KV_SLOT = 16384 + 4 * 256;
 __global__ __launch_bounds__(256, ATTN_KV_OCC) void attn_bwd_kv_dma_kernel(AttnArgs a) {
   constexpr int NS = ATTN_NSLOT;
   __shared__ __attribute__((aligned(1024))) char smem[NS * KV_SLOT];
-  const BlockCoord bc = attn_block((a.S + 127) / 128, a.Hkv * a.nsplit, a.Hkv * a.nsplit, a.B, a.causal ? 2 : 0, a.tail_first);
+  const BlockCoord bc = attn_block(a.nkb, a.Hkv * a.nsplit, a.Hkv * a.nsplit, a.B, a.causal ? 2 : 0, a.tail_first);
   const int kblk = bc.blk, hk = bc.h / a.nsplit, sp = bc.h % a.nsplit, b = bc.b;
   const int G = a.Hq / a.Hkv;
   const int hg0 = sp * a.hsplit;
@@ -769,6 +987,17 @@ __global__ __launch_bounds__(256, ATTN_KV_OCC) void attn_bwd_kv_dma_kernel(AttnA
     if (nch == 0) __syncthreads();
   }
   const int nit = nch * ng;
+  // the folded key tail (workgroup-uniform): keys a.nkb * 128 .. + nk - 1 ride with the last whole key block (k / v
+  // rows staged in LDS; a key past kvlen contributes nothing)
+  const int nk = (a.ktail && kblk == a.nkb - 1 && a.nkb * 128 < kvlen) ? min(a.ktail, kvlen - a.nkb * 128) : 0;
+  __shared__ __attribute__((aligned(16))) bf16 tkrows[2 * kTailQ * 64];
+  {
+    const long r0 = (long)b * S + a.nkb * 128;
+    tail_stage(tkrows, a.k + r0 * a.ldk + hk * 64, a.ldk, a.v + r0 * a.ldv + hk * 64, a.ldv, nk);
+  }
+  float tdk[kTailQ], tdv[kTailQ];
+#pragma unroll
+  for (int j = 0; j < kTailQ; ++j) { tdk[j] = 0.f; tdv[j] = 0.f; }
   int qo[2], qr_[2], doo[2], dr_[2];
   dma_lane_offsets(a.ldq, wu, lane, qo, qr_);
   dma_lane_offsets(a.lddo, wu, lane, doo, dr_);
@@ -814,6 +1043,7 @@ __global__ __launch_bounds__(256, ATTN_KV_OCC) void attn_bwd_kv_dma_kernel(AttnA
     if (kw0 >= kvlen || (a.causal && kw0 > qc + 63)) {  // padding keys, or every key of the wave above the chunk
     } else if (full) bwd_kv_chunk<false>(Ql, Dl, lse_l, lse_l + 64, kf, vf, dk0, dk1, dv0, dv1, c, qc, S, mykey, kvlen, false, lane);
     else bwd_kv_chunk<true>(Ql, Dl, lse_l, lse_l + 64, kf, vf, dk0, dk1, dv0, dv1, c, qc, S, mykey, kvlen, a.causal, lane);
+    if (nk) kv_ktail_stage(Ql, Dl, lse_l, lse_l + 64, tkrows, nk, qc, S, c, w, lane, tdk, tdv);
     issue(it + NS - 1);  // into slot (it - 1) % NS: every wave finished stage it - 1 before this iteration's barrier
   }
   wait_vmcnt<0>();
@@ -829,6 +1059,44 @@ __global__ __launch_bounds__(256, ATTN_KV_OCC) void attn_bwd_kv_dma_kernel(AttnA
       pv = mykey < kvlen ? pv : 0.f;
       tail_axpy(drow, (float)(bf16)pv, dv0, dv1, hl);
       tail_axpy(qrow, (float)(bf16)(pv * (dpv + a.delta[li])), dk0, dk1, hl);  // a.delta holds -delta
+    }
+  }
+  if (nk) {  // the folded tail keys: the short query tail (wave 0, lane = dim), the 4 waves' sums, the dK / dV rows
+    __shared__ float tkred[2][kTailQ][4][64];
+    if (w == 0) {
+      const int h = hk * G + hg0;
+#pragma unroll
+      for (int j = 0; j < kTailQ; ++j) {
+        if (j >= nk) continue;
+        const float kv = (float)tkrows[2 * j * 64 + lane], vv = (float)tkrows[(2 * j + 1) * 64 + lane];
+        for (int jq = 0; jq < qtail; ++jq) {
+          const long li = ((long)b * a.Hq + h) * S + S - qtail + jq;
+          const float qv = (float)trows[2 * jq * 64 + lane], dov = (float)trows[(2 * jq + 1) * 64 + lane];
+          const float sv = wave_sum64(qv * kv), dpv = wave_sum64(dov * vv);
+          const float pv = __builtin_amdgcn_exp2f(__builtin_fmaf(sv, c, -a.lse[li]));
+          tdv[j] = __builtin_fmaf((float)(bf16)pv, dov, tdv[j]);
+          tdk[j] = __builtin_fmaf((float)(bf16)(pv * (dpv + a.delta[li])), qv, tdk[j]);
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < kTailQ; ++j) {
+      if (j < nk) { tkred[0][j][w][lane] = tdk[j]; tkred[1][j][w][lane] = tdv[j]; }
+    }
+    __syncthreads();
+    if (w == 0) {
+      for (int j = 0; j < nk; ++j) {
+        const bf16 kx = (bf16)(((tkred[0][j][0][lane] + tkred[0][j][1][lane]) + (tkred[0][j][2][lane] + tkred[0][j][3][lane]))
+                               * a.scale);
+        const bf16 vx = (bf16)((tkred[1][j][0][lane] + tkred[1][j][1][lane]) + (tkred[1][j][2][lane] + tkred[1][j][3][lane]));
+        const long row = (long)b * S + a.nkb * 128 + j;
+        a.dk[row * a.lddk + hk * 64 + lane] = kx;
+        a.dv[row * a.lddv + hk * 64 + lane] = vx;
+        if (a.dbk) {
+          atomicAdd(a.dbk + hk * 64 + lane, (float)kx);
+          atomicAdd(a.dbv + hk * 64 + lane, (float)vx);
+        }
+      }
     }
   }
   __syncthreads();  // ring free for the bias column sums' LDS tiles
@@ -1365,7 +1633,16 @@ static int fill_common(AttnArgs& a, const slx_attn_desc* d) {
   a.tail_first = (!d->causal && d->S % 128 != 0) ? tf : 0;
   static const int tv = [] { const char* e = getenv("SLX_ATTN_TAILV"); return e ? atoi(e) : 1; }();
   a.tailv = tv;
+  a.nqb = a.nkb = (d->S + 127) / 128;
   return 0;
+}
+
+// the row tail (S % 128 <= kTailQ) folded into the last whole block: non-causal, at least one whole block
+// (SLX_ATTN_QTAIL=0 launches the tail rows' own workgroups as before, A/B)
+static int row_tail(const AttnArgs& a) {
+  static const int on = [] { const char* e = getenv("SLX_ATTN_QTAIL"); return e ? atoi(e) : 1; }();
+  const int r = a.S % 128;
+  return (on && !a.causal && a.tailv && a.S >= 128 && r > 0 && r <= kTailQ) ? r : 0;
 }
 
 extern "C" int slx_attn_fwd(const slx_attn_desc* d, slx_stream_t stream) {
@@ -1373,7 +1650,9 @@ extern "C" int slx_attn_fwd(const slx_attn_desc* d, slx_stream_t stream) {
   int rc = fill_common(a, d);
   if (rc) return rc;
   if (a.B == 0 || a.S == 0) return 0;
-  dim3 grid(((a.S + 127) / 128) * a.Hq * a.B);
+  a.qtail = row_tail(a);
+  a.nqb = a.qtail ? a.S / 128 : (a.S + 127) / 128;
+  dim3 grid(a.nqb * a.Hq * a.B);
   hipLaunchKernelGGL(attn_fwd_dma_kernel, grid, dim3(256), 0, (hipStream_t)stream, a);
   SLX_LAUNCH_CHECK("slx_attn_fwd");
   return 0;
@@ -1401,9 +1680,14 @@ extern "C" int slx_attn_bwd(const slx_attn_desc* d, const slx_attn_bwd_desc* g, 
   SLX_CHECK_ARG((a.dbk == nullptr) == (a.dbv == nullptr), "slx_attn_bwd: dbias_k and dbias_v go together");
   SLX_CHECK_ARG(!a.dbk || !f32kv, "slx_attn_bwd: dk/dv bias sums need the bf16 dK/dV path (no GQA, no RoPE)");
   const long ntok = (long)a.B * a.S;
-  const int nblk = (a.S + 127) / 128;
+  // the folded row tails: queries in the dQ pass (its dQ store has no RoPE^T for them), keys in the dK/dV pass (bf16
+  // dK / dV written directly: no GQA, no RoPE)
+  a.qtail = a.rcos ? 0 : row_tail(a);
+  a.nqb = a.qtail ? a.S / 128 : (a.S + 127) / 128;
+  a.ktail = f32kv ? 0 : row_tail(a);
+  a.nkb = a.ktail ? a.S / 128 : (a.S + 127) / 128;
   // dQ pass first: it computes delta = rowsum(dO * O) per query in its prologue and stores it for the dK/dV pass
-  hipLaunchKernelGGL(attn_bwd_dq_dma_kernel, dim3(nblk * a.Hq * a.B), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(attn_bwd_dq_dma_kernel, dim3(a.nqb * a.Hq * a.B), dim3(256), 0, st, a);
   SLX_LAUNCH_CHECK("slx_attn_bwd(dq)");
   {  // split a GQA group's q-heads over workgroups: one q-head per workgroup (Qwen2: 7 x 112 = 784 workgroups; with the
      // heaviest-first order +0.25 % on the step over the 4-way split that just fills the chip,
@@ -1416,7 +1700,7 @@ extern "C" int slx_attn_bwd(const slx_attn_desc* d, const slx_attn_bwd_desc* g, 
     a.hsplit = (G + ns - 1) / ns;
     a.nsplit = (G + a.hsplit - 1) / a.hsplit;
   }
-  hipLaunchKernelGGL(attn_bwd_kv_dma_kernel, dim3(nblk * a.Hkv * a.nsplit * a.B), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(attn_bwd_kv_dma_kernel, dim3(a.nkb * a.Hkv * a.nsplit * a.B), dim3(256), 0, st, a);
   SLX_LAUNCH_CHECK("slx_attn_bwd(dk/dv)");
   // finalize: f32 -> bf16, summing head-split partials and applying the RoPE transpose where asked
   auto rope_args = [&](const float* src, int heads, bf16* dst, long ld, bool rope, int nsplit) {

@@ -32,6 +32,12 @@ def ref_attn(q, k, v, B, S, Hq, Hkv, causal, lens):
 CASES = [
     # B, S, Hq, Hkv, causal, lens
     (2, 1025, 2, 2, False, None),
+    # the row tail folded into the last whole block (S % 128 in 1..2): 129 = 1 block + 1, 258 = 2 blocks + 2; 1027
+    # (3 rows: not folded) and 1024 (no tail) keep the plain layout
+    (2, 129, 2, 2, False, None),
+    (1, 258, 3, 3, False, None),
+    (1, 1027, 2, 2, False, None),
+    (1, 1024, 1, 1, False, None),
     (3, 200, 4, 4, False, None),
     (2, 150, 14, 2, True, [150, 97]),
     (1, 64, 2, 1, True, None),
