@@ -504,6 +504,11 @@ __device__ __forceinline__ float wave_sum64(float x) {
 __device__ __forceinline__ float rdlane(float x, int l) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), l));
 }
+// x + x of the lane (l ^ 1), then (l ^ 2): DPP quad permutations, no LDS round trip (a __shfl_xor is a ds_bpermute)
+__device__ __forceinline__ float quad_sum(float x) {
+  x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0xB1, 0xF, 0xF, true));  // quad_perm [1, 0, 3, 2]
+  return x + __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x4E, 0xF, 0xF, true));  // [2, 3, 0, 1]
+}
 // dims [16 qd, 16 qd + 16) of row `row` of an sw_off tile . the same dims of a 64-dim bf16 row in LDS, summed over the
 // lane's quad (lanes 4i .. 4i + 3 hold the four quarters of row i): every lane of the quad gets the full dot product
 __device__ __forceinline__ float quarter_dot(const char* tile, int row, int qd, const bf16* v) {
@@ -516,8 +521,7 @@ __device__ __forceinline__ float quarter_dot(const char* tile, int row, int qd, 
   for (int j = 0; j < 8; ++j) s = __builtin_fmaf((float)a0[j], (float)b0[j], s);
 #pragma unroll
   for (int j = 0; j < 8; ++j) s = __builtin_fmaf((float)a1[j], (float)b1[j], s);
-  s += __shfl_xor(s, 1, 64);
-  return s + __shfl_xor(s, 2, 64);
+  return quad_sum(s);
 }
 // acc + sum over kk < 16 of wv(lane 4 kk) * tile[r0 + kk][lane]  (lane = dim)
 __device__ __forceinline__ float col_axpy16(const char* tile, int r0, float wv, int lane, float acc) {
@@ -527,7 +531,10 @@ __device__ __forceinline__ float col_axpy16(const char* tile, int r0, float wv, 
   return acc;
 }
 
-// forward: the tail query rows (tq: q_j at rows 2j of a pair-staged buffer) against one K/V tile, this wave's 16 keys
+// forward: the tail query rows (tq: q_j at rows 2j of a pair-staged buffer) against one K/V tile, this wave's 16 keys.
+// The wave's running max tm moves only when a score exceeds it by LAZY (ballot; a wave reduction then), as in fwd_tile,
+// so the common tile needs no cross-lane reduction: each key's lanes hold p, lane-private partial sums tl (one lane per
+// key counts) are reduced once at the end, and O accumulates with lane = dim.
 __device__ __forceinline__ void fwd_qtail_tile(const char* Kl, const char* Vl, const bf16* tq, int nq, int key0, int klim,
                                                float c, int w, int lane, float (&tm)[kTailQ], float (&tl)[kTailQ],
                                                float (&to)[kTailQ]) {
@@ -537,18 +544,19 @@ __device__ __forceinline__ void fwd_qtail_tile(const char* Kl, const char* Vl, c
   for (int j = 0; j < kTailQ; ++j) {
     if (j < nq) {
       const float s = kok ? quarter_dot(Kl, kr, qd, tq + 2 * j * 64) * c : -INFINITY;
-      float mx = s;
+      if (__builtin_amdgcn_ballot_w64(s > tm[j] + LAZY)) {
+        float mx = s;
 #pragma unroll
-      for (int o = 4; o < 64; o <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
-      const float mnew = fmaxf(tm[j], mx);
-      const float alpha = __builtin_amdgcn_exp2f(tm[j] - mnew);
-      const float p = kok ? (float)(bf16)__builtin_amdgcn_exp2f(s - mnew) : 0.f;
-      float ps = p;
-#pragma unroll
-      for (int o = 4; o < 64; o <<= 1) ps += __shfl_xor(ps, o, 64);
-      tl[j] = tl[j] * alpha + ps;
-      to[j] = col_axpy16(Vl, 16 * w, p, lane, to[j] * alpha);
-      tm[j] = mnew;
+        for (int o = 4; o < 64; o <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+        const float mnew = fmaxf(tm[j], mx);
+        const float alpha = __builtin_amdgcn_exp2f(tm[j] - mnew);
+        tl[j] *= alpha;
+        to[j] *= alpha;
+        tm[j] = mnew;
+      }
+      const float p = kok ? (float)(bf16)__builtin_amdgcn_exp2f(s - tm[j]) : 0.f;
+      tl[j] += qd == 0 ? p : 0.f;
+      to[j] = col_axpy16(Vl, 16 * w, p, lane, to[j]);
     }
   }
 }
@@ -693,6 +701,8 @@ __global__ __launch_bounds__(256, ATTN_FWD_OCC) void attn_fwd_dma_kernel(AttnArg
   }
   if (nq) {  // the folded tail queries: the short key tail (wave 0, lane = dim), then the 4 waves' states merged
     __shared__ float tqred[kTailQ][4][66];
+#pragma unroll
+    for (int j = 0; j < kTailQ; ++j) tl[j] = wave_sum64(tl[j]);  // the lane-private partial sums of fwd_qtail_tile
     if (w == 0) {
 #pragma unroll
       for (int j = 0; j < kTailQ; ++j) {
