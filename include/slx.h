@@ -224,6 +224,9 @@ typedef struct {
   void* t; int64_t ldt;               /* bf16 [M, >= 32*nsites] */
   float p; int64_t ldmask;
   const uint32_t* bits[4]; int64_t ldbits;  /* keep bits per site (p > 0), ldbits >= Kin/32 words per row */
+  int gen_bits;  /* p > 0: 0 = read the keep bits (slx_dropout_bits wrote them); 1 = GENERATE them from seed[j] /
+                  * ldmask while x is read (drop_keep, the same hash as slx_dropout_bits) and write them to bits[j] for
+                  * the backward (round 6: no separate keep-bit launch)                                           */
 } slx_lora_down_desc;
 int slx_lora_down(const slx_lora_down_desc* d, slx_stream_t stream);
 /* A [32, Kin] bf16 (row stride lda, the peft lora_A.weight layout) -> Af, a packed fragment order (Kin % 32 == 0):
@@ -320,6 +323,8 @@ typedef struct slx_swiglu_lora_down_desc {
   void* t; int64_t ldt;
   float* ws; int64_t ws_floats;
   int64_t M; int F;
+  uint64_t seed; int gen_bits;  /* p > 0 and gen_bits: the keep bits are generated here (seed, ldmask = F) and
+                                 * written to bits, as slx_lora_down's gen_bits                              */
 } slx_swiglu_lora_down_desc;
 int slx_swiglu_lora_down(const slx_swiglu_lora_down_desc* d, slx_stream_t stream);
 int64_t slx_swiglu_lora_down_ws_floats(int64_t M, int F);

@@ -26,7 +26,17 @@ struct LoraDownArgs {
   float p;
   uint32_t thr;
   long ldmask;
+  uint32_t s1[4];  // gen: drop_seed_mix(seed) per site
+  int gen;         // generate the keep bits (and write them to bits[s]) instead of reading them
 };
+
+// keep word of 32 consecutive mask indices i0 .. i0 + 31 (i0 even): bit c = drop_keep(s1, i0 + c, thr), 16 pair hashes
+__device__ __forceinline__ uint32_t keep_word(uint32_t s1, unsigned long long i0, uint32_t thr) {
+  uint32_t wd = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) wd |= drop_keep8(s1, i0 + 8 * q, thr) << (8 * q);
+  return wd;
+}
 
 // Block = 32 rows x every site, 8 waves; wave w takes the step pairs (64 k = one 128-B line per row) w, w+8, ...
 // Per pair: x [32 x 64] is read with coalesced 16-B loads (8 rows x 128 B per instruction), scaled to
@@ -69,6 +79,20 @@ __global__ __launch_bounds__(512) void lora_down_kernel(LoraDownArgs a) {
                                        : make_uint4(0u, 0u, 0u, 0u);
     }
     const int gm = m0 + r;
+    if (drop && a.gen) {  // keep words generated here: lane half h hashes word 2 pi + h of its row, the halves swap
+      const int st = 2 * pi + h;
+      const bool ok = st < nk && gm < a.M;
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        const uint32_t wd = ok ? keep_word(a.s1[s], (unsigned long long)gm * a.ldmask + 32 * st, a.thr) : 0u;
+        if (ok) const_cast<uint32_t*>(a.bits[s])[(long)gm * a.ldbits + st] = wd;  // for the backward's consumers
+        const auto sw = __builtin_amdgcn_permlane32_swap(wd, wd, false, false);
+        const uint32_t other = sw[0] ^ sw[1] ^ wd;  // one of the pair is the lane's own word
+        R.kw[s][0] = h ? other : wd;
+        R.kw[s][1] = h ? wd : other;
+      }
+      return;
+    }
 #pragma unroll
     for (int ss = 0; ss < 2; ++ss) {
       const int st = 2 * pi + ss;
@@ -1009,6 +1033,7 @@ struct SldArgs {
   bf16* t; long ldt;
   float* part;                    // [F / 256][M][32] f32 partials
   int M, F;
+  uint32_t s1, thr; int gen;      // gen: the keep bits generated here (mask index m * F + n) and written to bits
 };
 
 template <bool DROP>  // as lora_swiglu_bwd_kernel's
@@ -1025,7 +1050,18 @@ __global__ __launch_bounds__(256) void swiglu_lora_down_kernel(SldArgs a) {
     const int m = min(m0 + row, a.M - 1);
     gg[i] = *reinterpret_cast<const uint4*>(a.gu + (long)m * a.ldgu + n);
     uu[i] = *reinterpret_cast<const uint4*>(a.gu + (long)m * a.ldgu + a.F + n);
-    kb[i] = DROP ? (a.bits[(long)m * a.ldbits + (n >> 5)] >> (n & 31)) & 0xFFu : 0xFFu;
+    if (!DROP || a.gen) kb[i] = 0xFFu;
+    else kb[i] = (a.bits[(long)m * a.ldbits + (n >> 5)] >> (n & 31)) & 0xFFu;
+  }
+  if (DROP && a.gen) {  // the 8 keep bits of each piece hashed while its loads fly; byte (n / 8) % 4 of its word stored
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = tid + 256 * i, row = c >> 5, n = n0 + 8 * (c & 31);
+      kb[i] = drop_keep8(a.s1, (unsigned long long)(m0 + row) * a.F + n, a.thr);
+      if (m0 + row < a.M)
+        reinterpret_cast<uint8_t*>(const_cast<uint32_t*>(a.bits))[((long)(m0 + row) * a.ldbits + (n >> 5)) * 4 + ((n >> 3) & 3)] =
+            (uint8_t)kb[i];
+    }
   }
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -1093,6 +1129,12 @@ extern "C" int slx_lora_down(const slx_lora_down_desc* d, slx_stream_t stream) {
   }
   a.ldbits = d->ldbits;
   a.t = (bf16*)d->t; a.ldt = d->ldt; a.p = d->p; a.ldmask = d->ldmask;
+  a.gen = d->gen_bits && d->p > 0.f;
+  if (a.gen) {
+    SLX_CHECK_ARG(d->ldmask % 2 == 0, "slx_lora_down: gen_bits needs an even ldmask");
+    a.thr = (uint32_t)(d->p * 65536.0f + 0.5f);  // slx_dropout_bits' threshold
+    for (int i = 0; i < d->nsites; ++i) a.s1[i] = drop_seed_mix(d->seed[i]);
+  }
   dim3 grid((unsigned)((d->M + 31) / 32));
   hipStream_t st = (hipStream_t)stream;
   switch (d->nsites) {
@@ -1422,6 +1464,9 @@ extern "C" int slx_swiglu_lora_down(const slx_swiglu_lora_down_desc* d, slx_stre
   a.t = (bf16*)d->t; a.ldt = d->ldt;
   a.part = d->ws;
   a.M = (int)d->M; a.F = d->F;
+  a.gen = d->gen_bits && d->p > 0.f;
+  a.s1 = drop_seed_mix(d->seed);
+  a.thr = (uint32_t)(d->p * 65536.0f + 0.5f);  // slx_dropout_bits' threshold
   hipStream_t st = (hipStream_t)stream;
   const dim3 grid((unsigned)(d->F / 256), (unsigned)((d->M + 31) / 32));
   if (a.bits) hipLaunchKernelGGL(swiglu_lora_down_kernel<true>, grid, dim3(256), 0, st, a);

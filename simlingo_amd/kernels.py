@@ -275,7 +275,7 @@ class LoraDownDesc(ctypes.Structure):
     _fields_ = [
         ("x", c_vp), ("ldx", c_i64), ("M", c_i64), ("Kin", c_int), ("r", c_int), ("nsites", c_int),
         ("A", c_vp * 4), ("seed", ctypes.c_uint64 * 4), ("t", c_vp), ("ldt", c_i64), ("p", c_float), ("ldmask", c_i64),
-        ("bits", c_vp * 4), ("ldbits", c_i64),
+        ("bits", c_vp * 4), ("ldbits", c_i64), ("gen_bits", c_int),
     ]
 
 
@@ -587,9 +587,10 @@ def lora_pack_a(a, layout=0, out=None):
     return out
 
 
-def lora_down(x, As, t, seeds, p=0.0, ldmask=None, bits=None, packed=False):
+def lora_down(x, As, t, seeds, p=0.0, ldmask=None, bits=None, packed=False, gen=False):
     """t[:, 32j:32j+32] = drop_j(x) As[j]^T for the sites sharing x (one launch); p > 0: bits[j] (int32
-    [M, >= kin/32]) holds site j's keep mask (dropout_bits); seeds are not used by the kernel.
+    [M, >= kin/32]) holds site j's keep mask (dropout_bits), or with gen=True the kernel generates it from seeds[j]
+    (the same drop_keep hash) and writes it there for the backward.
     packed=True: As[j] are already in slx_lora_pack_a's fragment order (flat, 32 * kin elements); else the [32, kin]
     matrices are packed here first (one extra launch per site)."""
     assert x.dtype == torch.bfloat16 and t.dtype == torch.bfloat16 and 1 <= len(As) <= 4
@@ -610,6 +611,7 @@ def lora_down(x, As, t, seeds, p=0.0, ldmask=None, bits=None, packed=False):
             d.bits[j] = bits[j].data_ptr()
             d.ldbits = bits[j].stride(0)
     d.t, d.ldt, d.p, d.ldmask = P(t).value, t.stride(0), float(p), kin if ldmask is None else ldmask
+    d.gen_bits = int(bool(gen))
     check(lib().slx_lora_down(ctypes.byref(d), stream_ptr()), "slx_lora_down")
 
 
@@ -744,17 +746,18 @@ def lora_swiglu_bwd_grads(dt, at, resid, gu, dgu, bits, p, tg, tu, dA_down, dB_g
 class SwigluLoraDownDesc(ctypes.Structure):
     _fields_ = [("gu", c_vp), ("ldgu", c_i64), ("act", c_vp), ("ldact", c_i64), ("A", c_vp), ("lda", c_i64),
                 ("bits", c_vp), ("ldbits", c_i64), ("p", c_float), ("t", c_vp), ("ldt", c_i64), ("ws", c_vp),
-                ("ws_floats", c_i64), ("M", c_i64), ("F", c_int)]
+                ("ws_floats", c_i64), ("M", c_i64), ("F", c_int), ("seed", ctypes.c_uint64), ("gen_bits", c_int)]
 
 
 register("slx_swiglu_lora_down", [ctypes.POINTER(SwigluLoraDownDesc), c_vp])
 register("slx_swiglu_lora_down_ws_floats", [c_i64, c_int], restype=c_i64)
 
 
-def swiglu_lora_down(gu, act, A, t, bits, p, ws):
+def swiglu_lora_down(gu, act, A, t, bits, p, ws, seed=None):
     """slx_swiglu_lora_down: act = bf16(silu(g) u) from gu bf16 [M, 2F], t = drop(act) A^T (bf16 [M, 32] view).
     A bf16 [>= 32, F] rows (lora_A), bits int32 [M, >= F/32] keep bits (p > 0), ws f32 scratch of
-    slx_swiglu_lora_down_ws_floats(M, F) floats (engine-owned, reused)."""
+    slx_swiglu_lora_down_ws_floats(M, F) floats (engine-owned, reused). seed given (p > 0): the kernel generates the keep
+    bits (the site seed's drop_keep hash, mask index m * F + n) and writes them to bits instead of reading them."""
     M, F = act.shape
     for x in (gu, act, A, t):
         assert x.dtype == torch.bfloat16 and x.is_cuda and x.stride(1) == 1
@@ -768,6 +771,8 @@ def swiglu_lora_down(gu, act, A, t, bits, p, ws):
         assert bits is not None and bits.dtype == torch.int32 and bits.shape[0] == M and bits.shape[1] * 32 >= F
         d.bits, d.ldbits = bits.data_ptr(), bits.stride(0)
     d.p, d.t, d.ldt, d.ws, d.ws_floats, d.M, d.F = float(p), t.data_ptr(), t.stride(0), ws.data_ptr(), ws.numel(), M, F
+    if seed is not None:
+        d.seed, d.gen_bits = int(seed) & ((1 << 64) - 1), 1
     check(lib().slx_swiglu_lora_down(ctypes.byref(d), stream_ptr()), "slx_swiglu_lora_down")
 
 

@@ -306,3 +306,50 @@ def test_swiglu_lora_down(dev, M, F, p):
     mask = torch.from_numpy(keep_scale(123, M, F, F, p)).to(dev) if p > 0 else 1.0
     xd = (act.float() * mask).bfloat16().float()
     torch.testing.assert_close(t[:, 8:40].float(), xd @ A.float().t(), atol=3e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("M,kin,nsites", [(300, 256, 3), (6384 // 8 + 5, 896, 2), (1, 128, 4), (6384, 4864, 1)])
+def test_lora_down_generates_keep_bits(dev, M, kin, nsites):
+    """gen_bits (round 6, the engine's default): slx_lora_down hashes each site's keep mask itself while it reads x and
+    writes the bits for the backward - bit-identical to slx_dropout_bits / the host mirror, and t bit-identical to the
+    read-the-bits launch (the same masked operand, the same MFMAs)."""
+    from simlingo_amd.dropmask import keep_bits
+    g = torch.Generator(device=dev).manual_seed(12)
+    x = torch.randn(M, kin + 64, device=dev, generator=g).bfloat16()[:, :kin]
+    As = [(torch.randn(32, kin, device=dev, generator=g) * 0.1).bfloat16() for _ in range(nsites)]
+    seeds = [987654 + 31 * j for j in range(nsites)]
+    p = 0.1
+    ref_bits = [torch.zeros(M, kin // 32, device=dev, dtype=torch.int32) for _ in range(nsites)]
+    K.dropout_bits([(seeds[j], ref_bits[j], kin, kin) for j in range(nsites)], M, p)
+    t_ref = torch.zeros(M, 32 * nsites, device=dev).bfloat16()
+    K.lora_down(x, As, t_ref, seeds, p=p, bits=ref_bits)
+    bits = [torch.full((M, kin // 32), -1, device=dev, dtype=torch.int32) for _ in range(nsites)]
+    t = torch.zeros(M, 32 * nsites, device=dev).bfloat16()
+    K.lora_down(x, As, t, seeds, p=p, bits=bits, gen=True)
+    torch.cuda.synchronize()
+    for j in range(nsites):
+        assert torch.equal(bits[j], ref_bits[j]), j
+        want = torch.from_numpy(keep_bits(seeds[j], M, kin, kin, p).view("int32")).to(dev)
+        assert torch.equal(bits[j], want), j
+    assert torch.equal(t, t_ref)
+
+
+@pytest.mark.parametrize("M,F", [(6384, 4864), (77, 256)])
+def test_swiglu_lora_down_generates_keep_bits(dev, M, F):
+    """slx_swiglu_lora_down with a seed: the down site's keep bits hashed in the pass (mask index m * F + n) and stored
+    bytewise - equal to the host mirror - and act / t bit-identical to the launch that reads those bits."""
+    from simlingo_amd.dropmask import keep_bits
+    g = torch.Generator(device=dev).manual_seed(43)
+    gu = torch.randn(M, 2 * F, device=dev, generator=g).bfloat16()
+    A = (torch.randn(32, F, device=dev, generator=g) * 0.05).bfloat16()
+    p, seed = 0.1, 4242
+    want = torch.from_numpy(keep_bits(seed, M, F, F, p).view("int32")).to(dev)
+    ws = torch.zeros(K.lib().slx_swiglu_lora_down_ws_floats(M, F), device=dev)
+    act_r, t_r = torch.empty(M, F, device=dev, dtype=torch.bfloat16), torch.zeros(M, 32, device=dev, dtype=torch.bfloat16)
+    K.swiglu_lora_down(gu, act_r, A, t_r, want.clone(), p, ws)
+    bits = torch.full((M, F // 32), -1, device=dev, dtype=torch.int32)
+    act, t = torch.empty(M, F, device=dev, dtype=torch.bfloat16), torch.zeros(M, 32, device=dev, dtype=torch.bfloat16)
+    K.swiglu_lora_down(gu, act, A, t, bits, p, ws, seed=seed)
+    torch.cuda.synchronize()
+    assert torch.equal(bits, want)
+    assert torch.equal(act, act_r) and torch.equal(t, t_r)
