@@ -556,14 +556,17 @@ __global__ void pack_scaled_kernel(const long long* tab, int n) {
   const long rows = t[4], cols = t[5];
   const float sc = __int_as_float((int)t[6]);
   const int mode = (int)t[7];
-  for (long i = (long)blockIdx.y * blockDim.x + threadIdx.x; i < rows * cols; i += (long)gridDim.y * blockDim.x) {
-    const long r = i / cols, c = i % cols;
-    const float v = src[r * lds + c] * sc;
-    if (mode == 1) reinterpret_cast<float*>(t[2])[r * ldd + c] = v;
+  // 32-bit index arithmetic (an entry is at most 4864 x 32 elements): the 64-bit division per element this loop used
+  // to do was most of the launch's time (engine._build_lora_cat refuses an entry of 2^31 elements or more)
+  const int nel = (int)(rows * cols), ncol = (int)cols;
+  for (int i = blockIdx.y * blockDim.x + threadIdx.x; i < nel; i += gridDim.y * blockDim.x) {
+    const int r = i / ncol, c = i - r * ncol;
+    const float v = src[(long)r * lds + c] * sc;
+    if (mode == 1) reinterpret_cast<float*>(t[2])[(long)r * ldd + c] = v;
     else if (mode == 2) reinterpret_cast<bf16*>(t[2])[lora_frag_index((int)r, (int)c)] = (bf16)v;
     else if (mode == 3) reinterpret_cast<bf16*>(t[2])[lora_dxfrag_index((int)r, (int)c)] = (bf16)v;
-    else if (mode == 4) reinterpret_cast<bf16*>(t[2])[c * ldd + r] = (bf16)v;
-    else reinterpret_cast<bf16*>(t[2])[r * ldd + c] = (bf16)v;
+    else if (mode == 4) reinterpret_cast<bf16*>(t[2])[(long)c * ldd + r] = (bf16)v;
+    else reinterpret_cast<bf16*>(t[2])[(long)r * ldd + c] = (bf16)v;
   }
 }
 
