@@ -362,6 +362,167 @@ __global__ __launch_bounds__(256) void norm_bwd_wave_kernel(NormArgs a) {
   }
 }
 
+// The same backward for the InternViT / CLIP rows (D = 1024, accumulating dx, no pixel shuffle, no bf16 dx copy) with
+// every load and store unconditional. In norm_bwd_wave_kernel the per-column `col < D` guards, the runtime
+// accumulate / pixel-shuffle choices and the guarded next-row prefetch put each load inside a branch; hipcc then waited
+// for each column chunk's dy before issuing the next chunk's loads (4 round trips per row) and drained vmcnt(0) behind
+// the prefetch. Here:
+//  * the next row's loads are issued for a clamped row index (a wave's last row re-reads itself), and the loop is a
+//    two-row ping-pong (A / B register sets, the first row peeled) so no loop-carried copy of in-flight registers forces
+//    a drain at the loop head, and the loop is entered with the same loads-then-stores pattern it repeats;
+//  * gamma and the layer scale come from LDS (staged once), so no global load of them is queued behind a row's stream;
+//  * dy stays in its bf16 registers until it is used; the row sums are DPP row sums + 4 readlanes.
+__device__ __forceinline__ float wave_sum_dpp(float x) {
+  x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0xB1, 0xF, 0xF, true));   // quad_perm [1, 0, 3, 2]
+  x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x4E, 0xF, 0xF, true));   // quad_perm [2, 3, 0, 1]
+  x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x124, 0xF, 0xF, true));  // row_ror:4
+  x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x128, 0xF, 0xF, true));  // row_ror:8
+  const auto rl = [&](int l) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), l)); };
+  return (rl(0) + rl(16)) + (rl(32) + rl(48));
+}
+
+template <bool RMS, bool LS, bool DYB>
+__global__ __launch_bounds__(256) void norm_bwd_wave1024_kernel(NormArgs a) {
+  constexpr int D = 1024;
+  constexpr int NACC = LS ? 4 : 2;
+  __shared__ __attribute__((aligned(16))) float cs[4][NACC][D];
+  __shared__ __attribute__((aligned(16))) float gl[LS ? 2 : 1][D];  // gamma | layer scale
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  *reinterpret_cast<float4*>(&gl[0][threadIdx.x * 4]) = *reinterpret_cast<const float4*>(a.gamma + threadIdx.x * 4);
+  if constexpr (LS) *reinterpret_cast<float4*>(&gl[LS ? 1 : 0][threadIdx.x * 4]) = *reinterpret_cast<const float4*>(a.ls + threadIdx.x * 4);
+#pragma unroll
+  for (int q = 0; q < NACC; ++q)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) *reinterpret_cast<float4*>(&cs[w][q][(lane + 64 * i) * 4]) = make_float4(0.f, 0.f, 0.f, 0.f);
+  __syncthreads();
+  auto acc4 = [&](int q, int col, const float (&v)[4]) {
+    float4* p = reinterpret_cast<float4*>(&cs[w][q][col]);
+    float4 c = *p;
+    c.x += v[0]; c.y += v[1]; c.z += v[2]; c.w += v[3];
+    *p = c;
+  };
+  struct RowIn {
+    float mu, rs;
+    float4 t[4], dxo[4], df[4];
+    bf16x4 db[4], lyv[4];
+  };
+  auto load_row = [&](long row, RowIn& r) {
+    r.mu = RMS ? 0.f : a.mean[row];
+    r.rs = a.rstd[row];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int col = (lane + 64 * i) * 4;
+      r.dxo[i] = ldnt_f4(a.dx + row * a.lddx + col);
+      if constexpr (LS) r.lyv[i] = ldnt_b4(a.lsy + row * a.ldlsy + col);
+      r.t[i] = ldnt_f4(a.x + row * a.ldx + col);
+      if constexpr (DYB) r.db[i] = ldnt_b4(reinterpret_cast<const bf16*>(a.dy) + row * a.lddy + col);
+      else r.df[i] = ldnt_f4(a.dy + row * a.lddy + col);
+    }
+  };
+  auto dy4 = [&](const RowIn& r, int i, float (&dv)[4]) {
+    if constexpr (DYB) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) dv[e] = (float)r.db[i][e];
+    } else {
+      dv[0] = r.df[i].x; dv[1] = r.df[i].y; dv[2] = r.df[i].z; dv[3] = r.df[i].w;
+    }
+  };
+  auto process = [&](const RowIn& cur, long row) {
+    const float mu = cur.mu, rs = cur.rs;
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int col = (lane + 64 * i) * 4;
+      const float4 t = cur.t[i], g = *reinterpret_cast<const float4*>(&gl[0][col]);
+      const float tv[4] = {t.x, t.y, t.z, t.w}, gv[4] = {g.x, g.y, g.z, g.w};
+      float dv[4], ag[4];
+      dy4(cur, i, dv);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float xh = (tv[e] - mu) * rs;
+        const float gd = dv[e] * gv[e];
+        s1 += gd;
+        s2 += gd * xh;
+        ag[e] = dv[e] * (RMS ? (float)(bf16)xh : xh);
+      }
+      acc4(0, col, ag);
+      acc4(1, col, dv);
+    }
+    const float m1 = RMS ? 0.f : wave_sum_dpp(s1) / D;
+    const float m2 = wave_sum_dpp(s2) / D;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int col = (lane + 64 * i) * 4;
+      float ov[4];
+      {
+        const float4 t = cur.t[i], g = *reinterpret_cast<const float4*>(&gl[0][col]);
+        const float tv[4] = {t.x, t.y, t.z, t.w}, gv[4] = {g.x, g.y, g.z, g.w};
+        float dv[4];
+        dy4(cur, i, dv);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float xh = (tv[e] - mu) * rs;
+          const float gd = __fmul_rn(dv[e], gv[e]);  // a rounded product, as norm_bwd_wave_kernel keeps it
+          ov[e] = rs * (gd - m1 - xh * m2);
+        }
+      }
+      ov[0] += cur.dxo[i].x; ov[1] += cur.dxo[i].y; ov[2] += cur.dxo[i].z; ov[3] += cur.dxo[i].w;
+      *reinterpret_cast<float4*>(a.dx + row * a.lddx + col) = make_float4(ov[0], ov[1], ov[2], ov[3]);
+      if constexpr (LS) {
+        const float4 l4 = *reinterpret_cast<const float4*>(&gl[LS ? 1 : 0][col]);
+        const bf16x4 yy = cur.lyv[i];
+        const float lv[4] = {l4.x, l4.y, l4.z, l4.w};
+        bf16x4 go;
+        float al[4], aq[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float gv = ov[e] * lv[e];
+          go[e] = (bf16)gv;
+          al[e] = ov[e] * (float)yy[e];
+          aq[e] = gv;
+        }
+        acc4(LS ? 2 : 0, col, al);
+        acc4(LS ? 3 : 0, col, aq);
+        *reinterpret_cast<bf16x4*>(a.lsg + row * a.ldlsg + col) = go;
+      }
+    }
+  };
+  // host guarantees rows >= 16 * gridDim.x: every wave owns at least its first row
+  const long stride = (long)gridDim.x * 4;
+  const auto clamp = [&](long r) { return r < a.rows ? r : a.rows - 1; };
+  long row = (long)blockIdx.x * 4 + w;
+  // sched_barrier after each prefetch: without it the scheduler hoists the current row's first arithmetic above the
+  // next row's loads, which then wait for the current row's data (the overlap this loop exists for is lost)
+  RowIn A, B;
+  load_row(row, B);
+  load_row(clamp(row + stride), A);
+  __builtin_amdgcn_sched_barrier(0);
+  process(B, row);
+  row += stride;
+  while (row < a.rows) {  // A holds `row`
+    load_row(clamp(row + stride), B);
+    __builtin_amdgcn_sched_barrier(0);
+    process(A, row);
+    row += stride;
+    if (row >= a.rows) break;
+    load_row(clamp(row + stride), A);
+    __builtin_amdgcn_sched_barrier(0);
+    process(B, row);
+    row += stride;
+  }
+  __syncthreads();  // 4 waves' column partials summed through LDS, then contiguous f32 atomics
+  for (int c = threadIdx.x; c < D; c += 256) {
+    if (a.dgamma) norm_param_out(a, 0, a.dgamma, c, cs[0][0][c] + cs[1][0][c] + cs[2][0][c] + cs[3][0][c]);
+    if (a.dbeta) norm_param_out(a, 1, a.dbeta, c, cs[0][1][c] + cs[1][1][c] + cs[2][1][c] + cs[3][1][c]);
+    if constexpr (LS) {
+      norm_param_out(a, 2, a.dls, c,
+                     cs[0][LS ? 2 : 0][c] + cs[1][LS ? 2 : 0][c] + cs[2][LS ? 2 : 0][c] + cs[3][LS ? 2 : 0][c]);
+      norm_param_out(a, 3, a.dlsb, c,
+                     cs[0][LS ? 3 : 0][c] + cs[1][LS ? 3 : 0][c] + cs[2][LS ? 3 : 0][c] + cs[3][LS ? 3 : 0][c]);
+    }
+  }
+}
+
 // One row at a time per wave, column sums in registers: the form for few rows per wave (Qwen2 RMSNorm, 6384 rows),
 // where norm_bwd_wave_kernel's second row in flight does not pay for its LDS accumulators.
 template <bool RMS, bool LS, bool DYB>
@@ -586,6 +747,15 @@ using namespace slx;
 
 static constexpr int kBwdBlocks = 512;
 
+// SLX_NORM_W1024=0: the D = 1024 LayerNorm backward through norm_bwd_wave_kernel instead (A/B)
+static bool norm_w1024() {
+  static const bool on = [] {
+    const char* e = getenv("SLX_NORM_W1024");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 template <bool RMS>
 static int norm_fwd(NormArgs& a, hipStream_t st) {
   SLX_CHECK_ARG(a.D % 4 == 0 && a.D <= 4096, "norm fwd: D=%d must be a multiple of 4 and <= 4096", a.D);
@@ -614,7 +784,16 @@ static int norm_bwd(NormArgs& a, float* dgamma, float* dbeta, int accumulate, hi
     if (dbeta) hipMemsetAsync(dbeta, 0, a.D * sizeof(float), st);
   }
   const bool two_rows = a.rows >= 16 * nblk;  // >= 4 rows per wave: two rows in flight per wave pay off
-  if (a.D <= 1024 && a.ls && two_rows) {
+  if (a.D == 1024 && two_rows && !a.ps && a.dx_accumulate && !a.dxb && norm_w1024()) {
+    // (InternViT / CLIP layers) branch-free form
+    if (a.ls) {
+      if (a.dy_bf16) hipLaunchKernelGGL((norm_bwd_wave1024_kernel<RMS, true, true>), dim3(nblk), dim3(256), 0, st, a);
+      else hipLaunchKernelGGL((norm_bwd_wave1024_kernel<RMS, true, false>), dim3(nblk), dim3(256), 0, st, a);
+    } else {
+      if (a.dy_bf16) hipLaunchKernelGGL((norm_bwd_wave1024_kernel<RMS, false, true>), dim3(nblk), dim3(256), 0, st, a);
+      else hipLaunchKernelGGL((norm_bwd_wave1024_kernel<RMS, false, false>), dim3(nblk), dim3(256), 0, st, a);
+    }
+  } else if (a.D <= 1024 && a.ls && two_rows) {
     if (a.dy_bf16) hipLaunchKernelGGL((norm_bwd_wave_kernel<RMS, true, true>), dim3(nblk), dim3(256), 0, st, a);
     else hipLaunchKernelGGL((norm_bwd_wave_kernel<RMS, true, false>), dim3(nblk), dim3(256), 0, st, a);
   } else if (a.D <= 1024 && a.ls) {

@@ -176,3 +176,43 @@ def test_norm_bwd_bf16_dy(dev, rms, fused_ls):
     assert torch.equal(dx_f, dx_b) and torch.equal(g_f, g_b)
     for a, b in ((gm_f, gm_b), (bt_f, bt_b), (dls_f, dls_b), (db_f, db_b)):  # cross-block sums: order may differ
         torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("dy_bf16,fused_ls", [(True, True), (False, True), (True, False)])
+def test_layernorm_bwd_1024_many_rows_vs_torch(dev, dy_bf16, fused_ls):
+    """The InternViT / CLIP LayerNorm backward at the step's row count (16400 rows of 1024: the branch-free
+    norm_bwd_wave1024_kernel, two rows in flight per wave, odd rows per wave included) against a float64 reference of
+    the same inputs: dx accumulated onto its input, dgamma / dbeta, and the fused layer-scale branch (g = bf16(dx * ls),
+    dls = sum dx * y, dbias = sum dx * ls)."""
+    M, D = 16400, 1024
+    gen = torch.Generator(device=dev).manual_seed(13)
+    x = torch.randn(M, D, device=dev, generator=gen) * 1.5 + 0.25
+    gamma, beta = torch.rand(D, device=dev, generator=gen) + 0.5, torch.randn(D, device=dev, generator=gen)
+    y = torch.empty(M, D, device=dev, dtype=torch.bfloat16)
+    mean, rstd = torch.empty(M, device=dev), torch.empty(M, device=dev)
+    d = K.norm_desc(x, gamma, beta, y, mean, rstd, M, D, 1e-6)
+    K.norm_fwd(d)
+    dy = torch.randn(M, D, device=dev, generator=gen)
+    if dy_bf16:
+        dy = dy.bfloat16()
+    dx0 = torch.randn(M, D, device=dev, generator=gen)
+    ls = torch.rand(D, device=dev, generator=gen) * 0.2
+    yb = torch.randn(M, D, device=dev, generator=gen).bfloat16()
+    dx = dx0.clone()
+    dgm, dbt = torch.zeros(D, device=dev), torch.zeros(D, device=dev)
+    g = torch.empty(M, D, device=dev, dtype=torch.bfloat16)
+    dls, dbias = torch.zeros(D, device=dev), torch.zeros(D, device=dev)
+    K.norm_bwd(d, dy, dx, dx_accumulate=True, dgamma=dgm, dbeta=dbt, ws=torch.empty(K.norm_ws_floats(D), device=dev),
+               param_accumulate=True, ls_branch=(ls, yb, g, dls, dbias) if fused_ls else None)
+    torch.cuda.synchronize()
+    xd, dyd = x.double(), dy.double()
+    xh = (xd - mean.double()[:, None]) * rstd.double()[:, None]
+    gd = dyd * gamma.double()
+    ref = rstd.double()[:, None] * (gd - gd.mean(1, keepdim=True) - xh * (gd * xh).mean(1, keepdim=True)) + dx0.double()
+    torch.testing.assert_close(dx.double(), ref, rtol=1e-5, atol=2e-5)
+    torch.testing.assert_close(dgm.double(), (dyd * xh).sum(0), rtol=1e-4, atol=5e-3)
+    torch.testing.assert_close(dbt.double(), dyd.sum(0), rtol=1e-4, atol=5e-3)
+    if fused_ls:
+        assert torch.equal(g, (dx * ls).bfloat16())
+        torch.testing.assert_close(dls.double(), (dx.double() * yb.double()).sum(0), rtol=1e-4, atol=5e-3)
+        torch.testing.assert_close(dbias.double(), (dx.double() * ls.double()).sum(0), rtol=1e-4, atol=5e-3)
