@@ -537,44 +537,42 @@ __global__ __launch_bounds__(256) void norm_bwd_row_kernel(NormArgs a) {
     const float rs = a.rstd[row];
     float xh[16], gd[16];
     float s1 = 0.f, s2 = 0.f;
-    // the row's accumulate input (dx) and layer-scale branch rows are loaded with x / dy, so a row costs one memory
-    // round trip instead of two
-    float4 dxo[4];
-    bf16x4 lyv[4];
+    // every load of the row issued together and unconditionally (columns past D read column 0, a non-accumulating
+    // call reads the dx row it is about to overwrite; both are zeroed by a select): a load inside a branch, or a bf16
+    // dy widened right after its load, made hipcc wait for each column chunk before issuing the next one's loads
+    float4 dxo[4], tt[4], gg[4], df[4], lsv[4];
+    bf16x4 db[4], lyv[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int col = (lane + 64 * i) * 4;
-      dxo[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (col < a.D && a.dx_accumulate) {
-        const float* dsrc = a.ps ? a.dx + ps_src_row(row, col / a.C, a.G, a.tok_per_img) * a.lddx + (col % a.C)
-                                 : a.dx + row * a.lddx + col;
-        dxo[i] = ldnt_f4(dsrc);
-      }
+      const int cl = col < a.D ? col : 0;
+      const long xr = a.ps ? ps_src_row(row, cl / a.C, a.G, a.tok_per_img) : row;
+      const int xc = a.ps ? cl % a.C : cl;
+      dxo[i] = ldnt_f4(a.dx + xr * a.lddx + xc);
       if constexpr (LS) {
-        if (col < a.D) lyv[i] = *reinterpret_cast<const bf16x4*>(a.lsy + row * a.ldlsy + col);
+        lyv[i] = *reinterpret_cast<const bf16x4*>(a.lsy + row * a.ldlsy + cl);
+        lsv[i] = *reinterpret_cast<const float4*>(a.ls + cl);
       }
+      tt[i] = ldnt_f4(a.x + xr * a.ldx + xc);
+      if constexpr (DYB) db[i] = ldnt_b4(reinterpret_cast<const bf16*>(a.dy) + row * a.lddy + cl);
+      else df[i] = ldnt_f4(a.dy + row * a.lddy + cl);
+      gg[i] = *reinterpret_cast<const float4*>(a.gamma + cl);
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int col = (lane + 64 * i) * 4;
-      float4 t = make_float4(0.f, 0.f, 0.f, 0.f), d = make_float4(0.f, 0.f, 0.f, 0.f), g = t;
-      if (col < a.D) {
-        const float* src = a.ps ? a.x + ps_src_row(row, col / a.C, a.G, a.tok_per_img) * a.ldx + (col % a.C)
-                                : a.x + row * a.ldx + col;
-        t = ldnt_f4(src);
-        if constexpr (DYB) {
-          const bf16x4 b = ldnt_b4(reinterpret_cast<const bf16*>(a.dy) + row * a.lddy + col);
-          d = make_float4((float)b[0], (float)b[1], (float)b[2], (float)b[3]);
-        } else {
-          d = ldnt_f4(a.dy + row * a.lddy + col);
-        }
-        g = *reinterpret_cast<const float4*>(a.gamma + col);
-      }
+      const bool ok = col < a.D;
+      const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+      const float4 t = ok ? tt[i] : z, g = ok ? gg[i] : z;
+      float4 d = df[i];
+      if constexpr (DYB) d = make_float4((float)db[i][0], (float)db[i][1], (float)db[i][2], (float)db[i][3]);
+      if (!ok) d = z;
+      if (!(ok && a.dx_accumulate)) dxo[i] = z;
       const float tv[4] = {t.x, t.y, t.z, t.w}, dv[4] = {d.x, d.y, d.z, d.w}, gv[4] = {g.x, g.y, g.z, g.w};
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int k = 4 * i + e;
-        xh[k] = col < a.D ? (tv[e] - mu) * rs : 0.f;
+        xh[k] = ok ? (tv[e] - mu) * rs : 0.f;
         gd[k] = dv[e] * gv[e];
         s1 += gd[k];
         s2 += gd[k] * xh[k];
@@ -604,7 +602,7 @@ __global__ __launch_bounds__(256) void norm_bwd_row_kernel(NormArgs a) {
         *reinterpret_cast<bf16x4*>(a.dxb + row * a.lddxb + col) = ob;
       }
       if constexpr (LS) {  // slx_ls_branch_bwd's per-element work on the row just produced (colsum_kernel<2>)
-        const float4 l4 = *reinterpret_cast<const float4*>(a.ls + col);
+        const float4 l4 = lsv[i];
         const bf16x4 yy = lyv[i];
         const float lv[4] = {l4.x, l4.y, l4.z, l4.w};
         bf16x4 go;
