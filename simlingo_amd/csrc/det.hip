@@ -25,8 +25,29 @@ __global__ __launch_bounds__(256) void det_reduce_kernel(const float* __restrict
   out[i] = accumulate ? out[i] + s : s;
 }
 
+// one output (the clip's gradient sum of squares over 2048 partials): 256 threads each sum a strided subset in a fixed
+// order, then a fixed LDS tree (one serial thread over 2048 dependent loads took 125 us)
+__global__ __launch_bounds__(256) void det_sum1_kernel(const float* __restrict__ part, int nparts, long stride,
+                                                       float* __restrict__ out, int accumulate) {
+  __shared__ float sh[256];
+  float s = 0.f;
+  for (int p = threadIdx.x; p < nparts; p += 256) s += part[(long)p * stride];
+  sh[threadIdx.x] = s;
+  __syncthreads();
+  for (int h = 128; h > 0; h >>= 1) {
+    if (threadIdx.x < h) sh[threadIdx.x] += sh[threadIdx.x + h];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[0] = accumulate ? out[0] + sh[0] : sh[0];
+}
+
 int det_reduce(const float* part, int nparts, long n, long stride, float* out, int accumulate, hipStream_t st) {
   if (n <= 0 || !out) return 0;
+  if (n == 1 && nparts > 64) {
+    hipLaunchKernelGGL(det_sum1_kernel, dim3(1), dim3(256), 0, st, part, nparts, stride, out, accumulate);
+    SLX_LAUNCH_CHECK("det_reduce");
+    return 0;
+  }
   hipLaunchKernelGGL(det_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, part, nparts, n, stride, out,
                      accumulate);
   SLX_LAUNCH_CHECK("det_reduce");

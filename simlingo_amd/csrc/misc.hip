@@ -556,17 +556,36 @@ __global__ void pack_scaled_kernel(const long long* tab, int n) {
   const long rows = t[4], cols = t[5];
   const float sc = __int_as_float((int)t[6]);
   const int mode = (int)t[7];
-  // 32-bit index arithmetic (an entry is at most 4864 x 32 elements): the 64-bit division per element this loop used
-  // to do was most of the launch's time (engine._build_lora_cat refuses an entry of 2^31 elements or more)
-  const int nel = (int)(rows * cols), ncol = (int)cols;
+  // The loop walks the DESTINATION in order, so every mode's stores are contiguous; the transposed (4) and fragment-
+  // ordered (2, 3) modes used to walk the source and scatter 2-byte stores (167 us per step for ~12 MB). Sources are
+  // the small f32 LoRA matrices (L2-resident). 32-bit index arithmetic: the host (engine._build_lora_cat) refuses an
+  // entry of 2^31 elements or more, and modes 2 / 3 need rows == 32 (the packed-fragment layouts of common.h).
+  const int nel = (int)(rows * cols), ncol = (int)cols, nrow = (int)rows;
   for (int i = blockIdx.y * blockDim.x + threadIdx.x; i < nel; i += gridDim.y * blockDim.x) {
-    const int r = i / ncol, c = i - r * ncol;
+    int r, c;
+    long dst;
+    if (mode == 2) {  // inverse of lora_frag_index
+      const int lane = (i >> 3) & 63, q = i >> 9;
+      r = lane & 31;
+      c = 32 * (q >> 1) + 16 * (q & 1) + 8 * (lane >> 5) + (i & 7);
+      dst = i;
+    } else if (mode == 3) {  // inverse of lora_dxfrag_index
+      const int lane = (i >> 3) & 63, q = i >> 9;
+      r = 16 * (q & 1) + 8 * (lane >> 5) + (i & 7);
+      c = 32 * (q >> 1) + (lane & 31);
+      dst = i;
+    } else if (mode == 4) {  // transposed: dst[c][r]
+      c = i / nrow;
+      r = i - c * nrow;
+      dst = (long)c * ldd + r;
+    } else {
+      r = i / ncol;
+      c = i - r * ncol;
+      dst = (long)r * ldd + c;
+    }
     const float v = src[(long)r * lds + c] * sc;
-    if (mode == 1) reinterpret_cast<float*>(t[2])[(long)r * ldd + c] = v;
-    else if (mode == 2) reinterpret_cast<bf16*>(t[2])[lora_frag_index((int)r, (int)c)] = (bf16)v;
-    else if (mode == 3) reinterpret_cast<bf16*>(t[2])[lora_dxfrag_index((int)r, (int)c)] = (bf16)v;
-    else if (mode == 4) reinterpret_cast<bf16*>(t[2])[(long)c * ldd + r] = (bf16)v;
-    else reinterpret_cast<bf16*>(t[2])[(long)r * ldd + c] = (bf16)v;
+    if (mode == 1) reinterpret_cast<float*>(t[2])[dst] = v;
+    else reinterpret_cast<bf16*>(t[2])[dst] = (bf16)v;
   }
 }
 

@@ -216,3 +216,27 @@ def test_layernorm_bwd_1024_many_rows_vs_torch(dev, dy_bf16, fused_ls):
         assert torch.equal(g, (dx * ls).bfloat16())
         torch.testing.assert_close(dls.double(), (dx.double() * yb.double()).sum(0), rtol=1e-4, atol=5e-3)
         torch.testing.assert_close(dbias.double(), (dx.double() * ls.double()).sum(0), rtol=1e-4, atol=5e-3)
+
+
+@pytest.mark.parametrize("rows,D,rms", [(16401, 1024, False), (6384, 896, True), (4097, 512, False)])
+def test_norm_fwd_many_rows(dev, rows, D, rms):
+    """The norm forward on the step's long row streams (one row per wave, every load unconditional) against a
+    float64 reference: bf16 y within its rounding, mean / rstd within f32 rounding."""
+    gen = torch.Generator(device=dev).manual_seed(rows)
+    x = torch.randn(rows, D, device=dev, generator=gen) * 2 + 0.5
+    g = torch.rand(D, device=dev, generator=gen) + 0.5
+    b = torch.randn(D, device=dev, generator=gen)
+    y = torch.empty(rows, D, device=dev, dtype=torch.bfloat16)
+    mean, rstd = torch.empty(rows, device=dev), torch.empty(rows, device=dev)
+    d = K.norm_desc(x, g, None if rms else b, y, None if rms else mean, rstd, rows, D, 1e-6, rms=rms)
+    K.norm_fwd(d)
+    torch.cuda.synchronize()
+    xd = x.double()
+    mu = torch.zeros(rows, 1, device=dev, dtype=torch.float64) if rms else xd.mean(1, keepdim=True)
+    rs = torch.rsqrt(((xd - mu) ** 2).mean(1, keepdim=True) + 1e-6)
+    xh = (xd - mu) * rs
+    ref = g.double() * (xh.float().bfloat16().double() if rms else xh) + (0 if rms else b.double())
+    torch.testing.assert_close(rstd.double(), rs[:, 0], rtol=2e-6, atol=0)
+    if not rms:
+        torch.testing.assert_close(mean.double(), mu[:, 0], rtol=0, atol=2e-6)
+    torch.testing.assert_close(y.double(), ref, rtol=8e-3, atol=8e-3)
