@@ -104,6 +104,26 @@ typedef struct slx_gemm_desc {
                        in directly (the backward epilogue then evaluates no transcendental)                           */
 } slx_gemm_desc;
 int slx_gemm_bf16(const slx_gemm_desc* d, slx_stream_t stream);
+
+/* Plain GEMM through hipBLASLt (round 6): D[M][N] = alpha * A[M][K] . B[N][K]^T + beta * C[M][N], row-major, A / B
+   bf16, C / D both f32 (out_f32) or both bf16, f32 accumulation. The step's plain GEMMs where the vendor library's
+   tiles beat slx_gemm_bf16 (measured per shape): the Qwen2 gate/up data gradient ([dx | dt] = dgu . W_cat, no
+   epilogue) and the Qwen2 o / down projections with their residual (C = the f32 residual stream, beta = 1: Qwen2's
+   `hidden_states = residual + mlp(...)`, modeling_qwen2 decoder layer, reached through llm.py:88-119). Replaces the
+   same torch.nn.Linear calls as slx_gemm_bf16. The plan (descriptors + the heuristic's algorithm) is cached per
+   shape; workspace: caller-owned, ws_bytes (0 allowed). Not bitwise reproducible against slx_gemm_bf16 (another
+   summation order); callers in deterministic-reduction mode keep slx_gemm_bf16. */
+typedef struct slx_gemm_lt_desc {
+  int64_t M, N, K;
+  const void* A; int64_t lda;   /* bf16 [M][K] */
+  const void* B; int64_t ldb;   /* bf16 [N][K] */
+  const void* C; int64_t ldc;   /* [M][N], read when beta != 0 (may equal D) */
+  void* D; int64_t ldd;         /* [M][N] */
+  float alpha, beta;
+  int out_f32;                  /* C and D f32 (1) or bf16 (0) */
+  void* ws; int64_t ws_bytes;
+} slx_gemm_lt_desc;
+int slx_gemm_lt(const slx_gemm_lt_desc* d, slx_stream_t stream);
 /* Two independent accumulating f32 STORE GEMMs (same layout and K, no bias / colsum / batch) in one launch:
  * the InternViT weight-gradient pairs (fc2.w + fc1.w, proj.w + qkv.w; the torch autograd wgrad GEMMs of
  * internvl2 InternMLP / InternAttention, K = tokens) share one round of 256 split-K blocks.

@@ -52,7 +52,8 @@ def build(verbose: bool = True, jobs: int | None = None, extra: list[str] | None
     with cf.ThreadPoolExecutor(jobs) as ex:
         objs = list(ex.map(lambda s: _compile(s, extra or []), srcs))
     if _needs(OUT, objs):
-        cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *map(str, objs), "-o", str(OUT)]
+        # hipBLASLt: slx_gemm_lt (csrc/blaslt.hip), the vendor library for the plain GEMMs it runs faster
+        cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *map(str, objs), "-lhipblaslt", "-o", str(OUT)]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")

@@ -47,8 +47,19 @@ class GemmDesc(ctypes.Structure):
     ]
 
 
+class GemmLtDesc(ctypes.Structure):  # slx_gemm_lt_desc
+    _fields_ = [
+        ("M", c_i64), ("N", c_i64), ("K", c_i64),
+        ("A", c_vp), ("lda", c_i64), ("B", c_vp), ("ldb", c_i64),
+        ("C", c_vp), ("ldc", c_i64), ("D", c_vp), ("ldd", c_i64),
+        ("alpha", c_float), ("beta", c_float), ("out_f32", c_int),
+        ("ws", c_vp), ("ws_bytes", c_i64),
+    ]
+
+
 # name -> argtypes (restype int unless listed in _RESTYPE)
 _SIGS: dict[str, list] = {
+    "slx_gemm_lt": [ctypes.POINTER(GemmLtDesc), c_vp],
     "slx_abi_version": [],
     "slx_device_sync": [],
     "slx_gemm_bf16": [ctypes.POINTER(GemmDesc), c_vp],
@@ -814,6 +825,38 @@ def _mm_dims(A, B, C, ta, tb):
     layout = {(False, True): GEMM_NT, (False, False): GEMM_NN, (True, False): GEMM_TN, (True, True): GEMM_TT}[(ta, tb)]
     assert C.shape[0] >= M and C.shape[1] >= N, (C.shape, M, N)
     return M, N, Kd, layout
+
+
+LT_WS_BYTES = 32 << 20
+_lt_ws: dict = {}
+
+
+def mm_lt(A, B, D, *, C=None, alpha=1.0, beta=0.0, ws=None):
+    """D = alpha * A @ B^T + beta * C through hipBLASLt (slx_gemm_lt): A [M,K] and B [N,K] bf16 row-major views with
+    unit inner stride, C / D [M,N] both f32 or both bf16 (C may be D). The plain GEMMs it runs faster than
+    slx_gemm_bf16 (csrc/blaslt.hip); ws: a >= LT_WS_BYTES uint8 device buffer (one per device by default)."""
+    _require_cuda(A, B, D)
+    M, Kd = A.shape
+    N = B.shape[0]
+    if A.dtype != torch.bfloat16 or B.dtype != torch.bfloat16 or B.shape[1] != Kd:
+        raise RuntimeError("slx_gemm_lt: bf16 A [M,K] and B [N,K]")
+    if D.dtype not in (torch.float32, torch.bfloat16) or D.shape[0] < M or D.shape[1] < N:
+        raise RuntimeError("slx_gemm_lt: D [M,N] f32 or bf16")
+    if beta != 0.0 and (C is None or C.dtype != D.dtype):
+        raise RuntimeError("slx_gemm_lt: beta != 0 needs C of D's dtype")
+    if ws is None:
+        ws = _lt_ws.get(D.device)
+        if ws is None:
+            ws = _lt_ws[D.device] = torch.empty(LT_WS_BYTES, dtype=torch.uint8, device=D.device)
+    d = GemmLtDesc()
+    d.M, d.N, d.K = int(M), int(N), int(Kd)
+    d.A, d.lda, d.B, d.ldb = A.data_ptr(), int(A.stride(0)), B.data_ptr(), int(B.stride(0))
+    d.C, d.ldc = (C.data_ptr(), int(C.stride(0))) if C is not None else (0, 0)
+    d.D, d.ldd = D.data_ptr(), int(D.stride(0))
+    d.alpha, d.beta, d.out_f32 = float(alpha), float(beta), int(D.dtype == torch.float32)
+    d.ws, d.ws_bytes = ws.data_ptr(), int(ws.numel())
+    check(lib().slx_gemm_lt(ctypes.byref(d), stream_ptr()), "slx_gemm_lt")
+    return D
 
 
 def mm_pair(g1, g2, *, ta=True, tb=False, alpha=1.0, ksplit_max=0, variant=None):

@@ -53,7 +53,8 @@ def test_struct_layouts_match_header(tmp_path):
     import subprocess
     if shutil.which("gcc") is None:
         pytest.skip("gcc not available")
-    structs = {"slx_gemm_desc": K.GemmDesc, "slx_attn_desc": K.AttnDesc, "slx_attn_bwd_desc": K.AttnBwdDesc,
+    structs = {"slx_gemm_desc": K.GemmDesc, "slx_gemm_lt_desc": K.GemmLtDesc, "slx_attn_desc": K.AttnDesc,
+               "slx_attn_bwd_desc": K.AttnBwdDesc,
                "slx_norm_desc": K.NormDesc, "slx_sgemm_desc": K.SgemmDesc,
                "slx_lora_down_desc": K.LoraDownDesc,
                "slx_lora_bwd_desc": K.LoraBwdDesc, "slx_dropout_bits_desc": K.DropoutBitsDesc,

@@ -550,3 +550,42 @@ def test_gelu_aux_grad(dev, M, v):
         torch.testing.assert_close(d1.float(), dv * gpre.float(), atol=3e-2, rtol=2e-2)
         # against the h-aux path: the only difference is the bf16 rounding of act'(h)
         torch.testing.assert_close(d1.float(), d0.float(), atol=3e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("M,N,Kd,f32,beta", [(6384, 960, 9728, True, 0.0), (6384, 896, 4928, True, 1.0),
+                                             (6384, 896, 960, True, 1.0), (777, 200, 136, False, 0.0),
+                                             (130, 64, 64, True, 1.0)])
+def test_gemm_lt_vs_torch(dev, M, N, Kd, f32, beta):
+    """slx_gemm_lt (hipBLASLt) on the step's plain Qwen2 shapes (gate/up data gradient; o / down projections with the
+    f32 residual as C, beta = 1) and ragged ones, on strided row views, against a float64 reference."""
+    gen = torch.Generator(device=dev).manual_seed(M + N)
+    Ab = torch.randn(M, Kd + 8, device=dev, generator=gen).bfloat16()
+    Bb = torch.randn(N, Kd + 16, device=dev, generator=gen).bfloat16()
+    A, B = Ab[:, :Kd], Bb[:, :Kd]
+    dt = torch.float32 if f32 else torch.bfloat16
+    Dfull = torch.full((M, N + 24), 7.0, device=dev, dtype=dt)
+    D = Dfull[:, :N]
+    C = torch.randn(M, N, device=dev, generator=gen).to(dt) if beta else None
+    K.mm_lt(A, B, D, C=C, beta=beta)
+    torch.cuda.synchronize()
+    ref = A.double() @ B.double().t() + (beta * C.double() if beta else 0)
+    tol = 2e-5 * Kd ** 0.5 * 4 if f32 else 2e-2
+    err = ((D.double() - ref).abs().max() / ref.abs().max()).item()
+    assert err < tol, err
+    assert torch.all(Dfull[:, N:] == 7.0)  # nothing written past N
+
+
+def test_gemm_lt_in_place_residual(dev):
+    """C == D (the residual updated in place) and a second call with the same shape reusing the cached plan."""
+    gen = torch.Generator(device=dev).manual_seed(3)
+    A = torch.randn(640, 256, device=dev, generator=gen).bfloat16()
+    B = torch.randn(128, 256, device=dev, generator=gen).bfloat16()
+    X = torch.randn(640, 128, device=dev, generator=gen)
+    ref = X.double() + A.double() @ B.double().t()
+    K.mm_lt(A, B, X, C=X, beta=1.0)
+    torch.cuda.synchronize()
+    assert ((X.double() - ref).abs().max() / ref.abs().max()).item() < 1e-5
+    Y = torch.zeros(640, 128, device=dev)
+    K.mm_lt(A, B, Y, C=Y, beta=1.0)
+    torch.cuda.synchronize()
+    assert ((Y.double() - A.double() @ B.double().t()).abs().max()).item() < 1e-2

@@ -25,6 +25,7 @@ SHAPES = {  # name: (M, N, K, layout)
     "llm_gateup": (6384, 9728, 896, K.GEMM_NT),
     "llm_down": (6384, 896, 4864, K.GEMM_NT),
     "llm_gu_dgrad": (6384, 896, 9728, K.GEMM_NN),
+    "llm_gu_dgrad_nt": (6384, 960, 9728, K.GEMM_NT),   # the step's form: [dx | dt] over the transposed W_cat copy
     "sq8192": (8192, 8192, 8192, K.GEMM_NT),
     "tn8192": (8192, 8192, 8192, K.GEMM_TN),   # both operands MN-contiguous (tr-reads), no split-K
     "nn8192": (8192, 8192, 8192, K.GEMM_NN),
