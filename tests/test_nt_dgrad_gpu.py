@@ -67,6 +67,7 @@ def _step(monkeypatch, nt, case):
     import simlingo_amd.engine as E
     from simlingo_amd.plan import plan_from_example
     monkeypatch.setattr(E, "NT_DGRAD", nt)
+    monkeypatch.setattr(E, "GEMM_LT", False)  # slx_gemm_bf16 on both sides: the NT / NN main loops are the subject
     cfg, P, ex, _ = load_case(case)
     dev = torch.device("cuda")
     eng = E.VLAEngine(cfg, dev, P)
