@@ -438,6 +438,11 @@ int slx_llava_merge_bwd(const float* dout, int C, int64_t n_img, int npatch_h, i
  * Packs LoRA B (scaled by lora_alpha/r) into the fused
  * [W | s*B] operands and LoRA A into the packed copies slx_lora_down / slx_lora_bwd read, once per optimizer step. */
 int slx_pack_scaled(const int64_t* table, int n, slx_stream_t s);
+/* The same packing over a flat grid of equal chunks (round 6): block b packs chunk block_map[b] >> 16 (SLX_PACK_CHUNK
+   elements) of entry block_map[b] & 0xFFFF (n <= 65536); block_map: nblocks device int32 built by the caller. One
+   block per 2048 elements instead of 32 blocks per entry whatever its size. */
+#define SLX_PACK_CHUNK 2048
+int slx_pack_scaled_flat(const int64_t* table, int n, const int* block_map, int nblocks, slx_stream_t s);
 /* table: n device-resident entries {src bf16*, lds, dst bf16*, ldd, rows, cols}: dst[c][r] = src[r][c].
  * max_tiles >= the largest ceil(rows/64)*ceil(cols/64) of the entries. Refreshes the [in][out] copies of the
  * weights whose data-gradient GEMM then runs in the NT layout (no reference counterpart: a layout choice of

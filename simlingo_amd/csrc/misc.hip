@@ -547,45 +547,82 @@ __global__ void cast_rows_kernel(const float* src, long lds, bf16* dst, long ldd
 // {src, lds, dst, ldd, rows, cols, scale(bits), mode}, mode 0 bf16 [rows][ldd], 1 f32 [rows][ldd], 2 / 3 bf16 in the
 // packed LoRA-A fragment orders of slx_lora_down / slx_lora_bwd's dx term (rows == 32, ldd unused). Packs every LoRA B (times alpha/r) into the
 // fused [W | s*B] GEMM operands and every LoRA A into its fragment copy in one launch.
+// destination index d of a pack entry -> source (r, c) and destination offset (the loop walks the DESTINATION in order,
+// so every mode's stores are contiguous; the transposed (4) and fragment-ordered (2, 3) modes used to walk the source
+// and scatter 2-byte stores). 32-bit index arithmetic: the host (engine._build_lora_cat) refuses an entry of 2^31
+// elements or more, and modes 2 / 3 need rows == 32 (the packed-fragment layouts of common.h).
+__device__ __forceinline__ void pack_at(int mode, int i, int nrow, int ncol, long ldd, int& r, int& c, long& dst) {
+  if (mode == 2) {  // inverse of lora_frag_index
+    const int lane = (i >> 3) & 63, q = i >> 9;
+    r = lane & 31;
+    c = 32 * (q >> 1) + 16 * (q & 1) + 8 * (lane >> 5) + (i & 7);
+    dst = i;
+  } else if (mode == 3) {  // inverse of lora_dxfrag_index
+    const int lane = (i >> 3) & 63, q = i >> 9;
+    r = 16 * (q & 1) + 8 * (lane >> 5) + (i & 7);
+    c = 32 * (q >> 1) + (lane & 31);
+    dst = i;
+  } else if (mode == 4) {  // transposed: dst[c][r]
+    c = i / nrow;
+    r = i - c * nrow;
+    dst = (long)c * ldd + r;
+  } else {
+    r = i / ncol;
+    c = i - r * ncol;
+    dst = (long)r * ldd + c;
+  }
+}
+
 __global__ void pack_scaled_kernel(const long long* tab, int n) {
   const int e = blockIdx.x;
   const long long* t = tab + 8 * (long)e;
   const float* src = reinterpret_cast<const float*>(t[0]);
   const long lds = t[1];
   const long ldd = t[3];
-  const long rows = t[4], cols = t[5];
+  const int nrow = (int)t[4], ncol = (int)t[5];
   const float sc = __int_as_float((int)t[6]);
   const int mode = (int)t[7];
-  // The loop walks the DESTINATION in order, so every mode's stores are contiguous; the transposed (4) and fragment-
-  // ordered (2, 3) modes used to walk the source and scatter 2-byte stores (167 us per step for ~12 MB). Sources are
-  // the small f32 LoRA matrices (L2-resident). 32-bit index arithmetic: the host (engine._build_lora_cat) refuses an
-  // entry of 2^31 elements or more, and modes 2 / 3 need rows == 32 (the packed-fragment layouts of common.h).
-  const int nel = (int)(rows * cols), ncol = (int)cols, nrow = (int)rows;
+  const int nel = nrow * ncol;
   for (int i = blockIdx.y * blockDim.x + threadIdx.x; i < nel; i += gridDim.y * blockDim.x) {
     int r, c;
     long dst;
-    if (mode == 2) {  // inverse of lora_frag_index
-      const int lane = (i >> 3) & 63, q = i >> 9;
-      r = lane & 31;
-      c = 32 * (q >> 1) + 16 * (q & 1) + 8 * (lane >> 5) + (i & 7);
-      dst = i;
-    } else if (mode == 3) {  // inverse of lora_dxfrag_index
-      const int lane = (i >> 3) & 63, q = i >> 9;
-      r = 16 * (q & 1) + 8 * (lane >> 5) + (i & 7);
-      c = 32 * (q >> 1) + (lane & 31);
-      dst = i;
-    } else if (mode == 4) {  // transposed: dst[c][r]
-      c = i / nrow;
-      r = i - c * nrow;
-      dst = (long)c * ldd + r;
-    } else {
-      r = i / ncol;
-      c = i - r * ncol;
-      dst = (long)r * ldd + c;
-    }
+    pack_at(mode, i, nrow, ncol, ldd, r, c, dst);
     const float v = src[(long)r * lds + c] * sc;
     if (mode == 1) reinterpret_cast<float*>(t[2])[dst] = v;
     else reinterpret_cast<bf16*>(t[2])[dst] = (bf16)v;
+  }
+}
+
+// flat grid (slx_pack_scaled_flat): block b packs chunk block_map[b] >> 16 (SLX_PACK_CHUNK elements, 8 per thread: 8
+// loads in flight per thread, one round trip per block) of entry block_map[b] & 0xFFFF
+__global__ __launch_bounds__(256) void pack_scaled_flat_kernel(const long long* tab, int n, const int* bmap) {
+  const int bm = bmap[blockIdx.x];
+  const int lo = bm & 0xFFFF, chunk = bm >> 16;
+  const long long* t = tab + 8 * (long)lo;
+  const float* src = reinterpret_cast<const float*>(t[0]);
+  const long lds = t[1];
+  const long ldd = t[3];
+  const int nrow = (int)t[4], ncol = (int)t[5];
+  const float sc = __int_as_float((int)t[6]);
+  const int mode = (int)t[7];
+  const int nel = nrow * ncol;
+  const int i0 = chunk * SLX_PACK_CHUNK + threadIdx.x;
+  constexpr int PER = SLX_PACK_CHUNK / 256;
+  float v[PER];
+  long dst[PER];
+#pragma unroll
+  for (int u = 0; u < PER; ++u) {
+    const int i = min(i0 + 256 * u, nel - 1);
+    int r, c;
+    pack_at(mode, i, nrow, ncol, ldd, r, c, dst[u]);
+    v[u] = src[(long)r * lds + c] * sc;
+  }
+#pragma unroll
+  for (int u = 0; u < PER; ++u) {
+    if (i0 + 256 * u < nel) {
+      if (mode == 1) reinterpret_cast<float*>(t[2])[dst[u]] = v[u];
+      else reinterpret_cast<bf16*>(t[2])[dst[u]] = (bf16)v[u];
+    }
   }
 }
 
@@ -1043,6 +1080,16 @@ int slx_pack_scaled(const int64_t* table, int n, slx_stream_t s) {
   if (n <= 0) return 0;
   hipLaunchKernelGGL(pack_scaled_kernel, dim3(n, 32), dim3(256), 0, (hipStream_t)s, (const long long*)table, n);
   SLX_LAUNCH_CHECK("slx_pack_scaled");
+  return 0;
+}
+
+int slx_pack_scaled_flat(const int64_t* table, int n, const int* block_map, int nblocks, slx_stream_t s) {
+  SLX_CHECK_ARG(n >= 0 && n <= 65536 && nblocks >= 0 && (n == 0 || (table && block_map)),
+                "slx_pack_scaled_flat: table, block_map, n <= 65536");
+  if (n <= 0 || nblocks == 0) return 0;
+  hipLaunchKernelGGL(pack_scaled_flat_kernel, dim3(nblocks), dim3(256), 0, (hipStream_t)s, (const long long*)table, n,
+                     block_map);
+  SLX_LAUNCH_CHECK("slx_pack_scaled_flat");
   return 0;
 }
 

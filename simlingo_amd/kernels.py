@@ -363,6 +363,7 @@ for _n, _a in {
     "slx_swiglu_bwd": [_vp, _I, _vp, _I, _vp, _I, _I, _i, _vp],
     "slx_cast_rows": [_vp, _I, _vp, _I, _I, _i, _vp],
     "slx_pack_scaled": [_vp, _i, _vp],
+    "slx_pack_scaled_flat": [_vp, _i, _vp, _i, _vp],
     "slx_transpose_bf16": [_vp, _i, _I, _vp],
     "slx_cast_f32_bf16": [_vp, _vp, _I, _vp],
     # fp32 parity mode (csrc/precise.hip)

@@ -117,3 +117,40 @@ def test_base_engine_copies_follow_optimizer(dev):
     torch.cuda.synchronize()
     for n, wt in eng.WT.items():
         assert torch.equal(wt, eng.W[n].t()), n
+
+
+def test_pack_scaled_flat_equals_per_entry_grid(dev):
+    """slx_pack_scaled_flat (one block per 2048 elements through a block map) writes exactly what slx_pack_scaled
+    (32 blocks per entry) writes, for every mode: 0 / 1 row-major bf16 / f32, 2 / 3 the LoRA fragment orders (32 rows),
+    4 transposed; entries from a few elements to more than one chunk per thread."""
+    g = torch.Generator(device=dev).manual_seed(8)
+    specs = [(0, 96, 32), (1, 40, 32), (2, 32, 896), (3, 32, 4864), (4, 4864, 32), (0, 3, 5), (4, 130, 7), (2, 32, 64)]
+    srcs, outs = [], {True: [], False: []}
+    for mode, r, c in specs:
+        srcs.append(torch.randn(r, c + 3, device=dev, generator=g)[:, :c])
+    for flat in (False, True):
+        rows = []
+        for (mode, r, c), src in zip(specs, srcs):
+            if mode in (2, 3):
+                dst = torch.zeros(r * c, device=dev, dtype=torch.bfloat16)
+                ld = 0
+            elif mode == 4:
+                dst = torch.zeros(c, r + 6, device=dev, dtype=torch.bfloat16)
+                ld = dst.stride(0)
+            else:
+                dst = torch.zeros(r, c + 6, device=dev, dtype=torch.float32 if mode == 1 else torch.bfloat16)
+                ld = dst.stride(0)
+            outs[flat].append(dst)
+            rows.append([src.data_ptr(), src.stride(0), dst.data_ptr(), ld, r, c,
+                         int(np.float32(0.75).view(np.int32)), mode])
+        tab = torch.tensor(rows, dtype=torch.int64, device=dev)
+        if flat:
+            bmap = [e | (k << 16) for e, row in enumerate(rows) for k in range((row[4] * row[5] + 2047) // 2048)]
+            bm = torch.tensor(bmap, dtype=torch.int32, device=dev)
+            K.call("slx_pack_scaled_flat", K.P(tab), len(rows), K.P(bm), len(bmap), K.stream_ptr())
+        else:
+            K.call("slx_pack_scaled", K.P(tab), len(rows), K.stream_ptr())
+        torch.cuda.synchronize()
+    for a, b in zip(outs[False], outs[True]):
+        assert torch.equal(a, b)
+    assert bool((outs[True][4][:, 4864:] == 0).all())  # nothing past the transposed rows
