@@ -97,10 +97,11 @@ __device__ __forceinline__ float gelu_erf_grad(float x) {
   const GeluTerms g = gelu_terms(x);
   return __builtin_fmaf(x * 0.39894228040143268f, g.e, g.cdf);
 }
-__device__ __forceinline__ float silu(float x) { return x / (1.0f + __expf(-x)); }
-// the derivative takes sigmoid(x) from the hardware reciprocal (v_rcp_f32, 1 ulp) instead of an IEEE division (~10
-// instructions): it only feeds gradients (bf16-rounded dgu), while silu itself keeps the division so the activations
-// recomputed in the backward equal the forward's bit for bit
+// x * sigmoid(x) with the sigmoid from the hardware reciprocal (v_rcp_f32, 1 ulp) instead of an IEEE division: every
+// forward and backward kernel of the bf16 engine (SwiGLU forward, its LoRA-fused forms, the backward's recomputation,
+// the decode GEMV) shares this one definition, so recomputed activations still equal the forward's bit for bit
+__device__ __forceinline__ float silu(float x) { return x * __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
+// the derivative likewise (it only feeds gradients, bf16-rounded dgu)
 __device__ __forceinline__ float silu_grad(float x) {
   const float s = __builtin_amdgcn_rcpf(1.0f + __expf(-x));
   return s * (1.0f + x * (1.0f - s));
